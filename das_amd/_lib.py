@@ -1,0 +1,348 @@
+"""ctypes binding of libdas_mi355x.so (include/das_mi355x.h).
+
+The product path has no CPU fallback: if the shared library is missing or no
+gfx950 device is present, importing works but every call that needs the GPU
+raises `DasNativeError` (or `ImportError` for a missing library) loudly.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DAS_MI355X_LIB", os.path.join(_HERE, "libdas_mi355x.so"))
+
+DAS_NONE = 0xFFFFFFFF
+TABLE_ORDERED = 0
+TABLE_UNORDERED = 1
+
+ERR_INVALID, ERR_HIP, ERR_NOT_BUILT, ERR_UNSUPPORTED, ERR_INTERNAL = -1, -2, -3, -4, -5
+
+
+class DasNativeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[das_mi355x {code}] {msg}")
+        self.code = code
+
+
+class das_atoms_t(C.Structure):
+    _fields_ = [
+        ("n_leaf", C.c_uint64),
+        ("leaf_bytes", C.c_void_p),
+        ("leaf_off", C.c_void_p),
+        ("leaf_kind", C.c_void_p),
+        ("leaf_ctype", C.c_void_p),
+        ("leaf_type_id", C.c_void_p),
+        ("n_expr", C.c_uint64),
+        ("expr_off", C.c_void_p),
+        ("expr_child", C.c_void_p),
+        ("expr_kind", C.c_void_p),
+        ("expr_ctype_leaf", C.c_void_p),
+        ("n_levels", C.c_uint32),
+        ("level_off", C.c_void_p),
+        ("n_types", C.c_uint32),
+    ]
+
+
+class das_index_stats_t(C.Structure):
+    _fields_ = [
+        ("n_atoms", C.c_uint64), ("n_nodes", C.c_uint64), ("n_links", C.c_uint64),
+        ("n_types", C.c_uint64), ("n_ctypes", C.c_uint64), ("device_bytes", C.c_uint64),
+        ("links_by_arity", C.c_uint64 * 9),
+    ]
+
+
+class das_link_scan_t(C.Structure):
+    _fields_ = [
+        ("arity", C.c_uint32), ("type_id", C.c_uint32), ("target", C.c_uint32 * 8),
+        ("var", C.c_int32 * 8), ("n_vars", C.c_uint32), ("ordered", C.c_uint32),
+        ("no_overload", C.c_uint32), ("emit_link", C.c_uint32),
+    ]
+
+
+class das_template_scan_t(C.Structure):
+    _fields_ = [
+        ("ctype_id", C.c_uint32), ("arity", C.c_uint32), ("var", C.c_int32 * 8),
+        ("ordered", C.c_uint32), ("no_overload", C.c_uint32), ("emit_link", C.c_uint32),
+    ]
+
+
+P = C.c_void_p
+U32P = C.POINTER(C.c_uint32)
+
+# name -> (restype, argtypes); every function returns int status unless noted.
+_SIGS = {
+    "das_version": (C.c_int, []),
+    "das_ctx_create": (C.c_int, [C.c_int, P, C.POINTER(P)]),
+    "das_ctx_destroy": (C.c_int, [P]),
+    "das_last_error": (C.c_char_p, [P]),
+    "das_ctx_sync": (C.c_int, [P]),
+    "das_md5": (C.c_int, [P, C.c_uint64, P]),
+    "das_composite_digest": (C.c_int, [P, C.c_uint32, P]),
+    "das_hash_strings_dev": (C.c_int, [P, P, P, C.c_uint64, P]),
+    "das_hash_fixed_dev": (C.c_int, [P, P, C.c_uint32, C.c_uint64, P]),
+    "das_build_index": (C.c_int, [P, C.POINTER(das_atoms_t)]),
+    "das_index_stats": (C.c_int, [P, C.POINTER(das_index_stats_t)]),
+    "das_lookup": (C.c_int, [P, P, C.c_uint64, P, P, P, P]),
+    "das_atoms_info": (C.c_int, [P, P, C.c_uint64, P, P, P, P, P]),
+    "das_link_targets": (C.c_int, [P, C.c_uint32, P, C.c_uint32, P]),
+    "das_ctype_lookup": (C.c_int, [P, P, P]),
+    "das_scan_link": (C.c_int, [P, C.POINTER(das_link_scan_t), C.POINTER(P)]),
+    "das_scan_template": (C.c_int, [P, C.POINTER(das_template_scan_t), C.POINTER(P)]),
+    "das_scan_type": (C.c_int, [P, C.c_uint32, P]),
+    "das_join": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
+    "das_antijoin": (C.c_int, [P, P, P, C.POINTER(P)]),
+    "das_dedup": (C.c_int, [P, P, C.POINTER(P)]),
+    "das_concat": (C.c_int, [P, P, C.c_uint32, C.POINTER(P)]),
+    "das_table_info": (C.c_int, [P, P, P, P, P]),
+    "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
+    "das_table_column": (C.c_int, [P, C.c_int32, P]),
+    "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
+    "das_table_free": (C.c_int, [P]),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded shared library (raises ImportError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libdas_mi355x.so not found at {LIB_PATH}: run __graft_entry__.build() "
+                              "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, ctx=None):
+    if rc != 0:
+        msg = lib().das_last_error(ctx)
+        msg = msg.decode(errors="replace") if msg else ""
+        if rc == ERR_INVALID:
+            raise ValueError(msg)
+        if rc == ERR_UNSUPPORTED:
+            raise NotImplementedError(msg)
+        raise DasNativeError(rc, msg)
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ---------------------------------------------------------------------------
+# host hashing helpers (query planning); bulk hashing happens on the GPU
+# ---------------------------------------------------------------------------
+
+def md5_digest(text):
+    b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+    buf = C.create_string_buffer(b, len(b)) if b else None
+    out = np.zeros(4, dtype=np.uint32)
+    check(lib().das_md5(buf, len(b), ptr(out)))
+    return out
+
+
+def composite_digest(digests):
+    d = np.ascontiguousarray(np.asarray(digests, dtype=np.uint32).reshape(-1, 4))
+    out = np.zeros(4, dtype=np.uint32)
+    check(lib().das_composite_digest(ptr(d), d.shape[0], ptr(out)))
+    return out
+
+
+def digest_to_hex(d):
+    return np.asarray(d, dtype="<u4").tobytes().hex()
+
+
+def digests_to_hex(arr):
+    """(n,4) uint32 little-endian words -> list of 32-char hex handles."""
+    raw = np.ascontiguousarray(np.asarray(arr, dtype="<u4")).tobytes()
+    h = raw.hex()
+    return [h[i:i + 32] for i in range(0, len(h), 32)]
+
+
+def hex_to_digest(h):
+    if not isinstance(h, str) or len(h) != 32:
+        raise ValueError(f"Invalid handle: {h}")
+    try:
+        return np.frombuffer(bytes.fromhex(h), dtype="<u4").astype(np.uint32)
+    except ValueError:
+        raise ValueError(f"Invalid handle: {h}")
+
+
+class Table:
+    """Owning wrapper of a das_table_t* (a device binding table)."""
+
+    __slots__ = ("ctx", "h", "kind", "vars", "nrows")
+
+    def __init__(self, ctx, handle):
+        self.ctx = ctx
+        self.h = handle
+        kind = C.c_int32()
+        ncols = C.c_int32()
+        vars_ = (C.c_int32 * 16)()
+        nrows = C.c_uint64()
+        check(lib().das_table_info(handle, C.byref(kind), C.byref(ncols), vars_, C.byref(nrows)))
+        self.kind = kind.value
+        self.vars = tuple(vars_[i] for i in range(ncols.value))
+        self.nrows = nrows.value
+
+    @property
+    def schema(self):
+        return (self.kind, self.vars)
+
+    def fetch(self):
+        n, k = self.nrows, len(self.vars)
+        out = np.zeros((k, n), dtype=np.uint32)
+        if n and k:
+            check(lib().das_table_fetch(self.ctx.h, self.h, 0, n, ptr(out)), self.ctx.h)
+        return out
+
+    def free(self):
+        if self.h is not None:
+            lib().das_table_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """A device context: one HBM index + the stream every kernel runs on."""
+
+    def __init__(self, device=0, stream=None):
+        h = P()
+        check(lib().das_ctx_create(int(device), stream, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().das_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _table(self, fn, *args):
+        out = P()
+        check(fn(self.h, *args, C.byref(out)), self.h)
+        return Table(self, out)
+
+    def build_index(self, arrays):
+        a = arrays
+        keep = [a.leaf_bytes, a.leaf_off, a.leaf_kind, a.leaf_ctype, a.leaf_type_id, a.expr_off,
+                a.expr_child, a.expr_kind, a.expr_ctype_leaf, a.level_off]
+        s = das_atoms_t(
+            n_leaf=a.n_leaf, leaf_bytes=ptr(a.leaf_bytes), leaf_off=ptr(a.leaf_off), leaf_kind=ptr(a.leaf_kind),
+            leaf_ctype=ptr(a.leaf_ctype), leaf_type_id=ptr(a.leaf_type_id), n_expr=a.n_expr,
+            expr_off=ptr(a.expr_off), expr_child=ptr(a.expr_child), expr_kind=ptr(a.expr_kind),
+            expr_ctype_leaf=ptr(a.expr_ctype_leaf), n_levels=len(a.level_off) - 1, level_off=ptr(a.level_off),
+            n_types=len(a.type_names))
+        check(lib().das_build_index(self.h, C.byref(s)), self.h)
+        del keep
+
+    def stats(self):
+        st = das_index_stats_t()
+        check(lib().das_index_stats(self.h, C.byref(st)), self.h)
+        return st
+
+    def lookup(self, digests):
+        d = np.ascontiguousarray(np.asarray(digests, dtype=np.uint32).reshape(-1, 4))
+        n = d.shape[0]
+        ids = np.zeros(n, dtype=np.int64)
+        cat = np.zeros(n, dtype=np.uint8)
+        ar = np.zeros(n, dtype=np.uint32)
+        ty = np.zeros(n, dtype=np.uint32)
+        if n:
+            check(lib().das_lookup(self.h, ptr(d), n, ptr(ids), ptr(cat), ptr(ar), ptr(ty)), self.h)
+        return ids, cat, ar, ty
+
+    def atoms_info(self, ids):
+        ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint32))
+        n = ids.shape[0]
+        dig = np.zeros((n, 4), dtype=np.uint32)
+        cat = np.zeros(n, dtype=np.uint8)
+        ar = np.zeros(n, dtype=np.uint32)
+        ty = np.zeros(n, dtype=np.uint32)
+        nl = np.zeros(n, dtype=np.uint32)
+        if n:
+            check(lib().das_atoms_info(self.h, ptr(ids), n, ptr(dig), ptr(cat), ptr(ar), ptr(ty), ptr(nl)), self.h)
+        return dig, cat, ar, ty, nl
+
+    def link_targets(self, atom_id):
+        buf = np.zeros(64, dtype=np.uint32)
+        n = C.c_uint32()
+        check(lib().das_link_targets(self.h, int(atom_id), ptr(buf), 64, C.byref(n)), self.h)
+        return buf[:n.value].copy()
+
+    def ctype_lookup(self, digest):
+        d = np.ascontiguousarray(np.asarray(digest, dtype=np.uint32))
+        out = C.c_int64()
+        check(lib().das_ctype_lookup(self.h, ptr(d), C.byref(out)), self.h)
+        return out.value
+
+    def scan_link(self, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False):
+        q = das_link_scan_t()
+        q.arity = arity
+        q.type_id = DAS_NONE if type_id is None else type_id
+        for i in range(8):
+            q.target[i] = targets[i] if i < len(targets) else DAS_NONE
+            q.var[i] = var[i] if i < len(var) else -1
+        q.n_vars = n_vars
+        q.ordered = 1 if ordered else 0
+        q.no_overload = 1 if no_overload else 0
+        q.emit_link = 1 if emit_link else 0
+        return self._table(lib().das_scan_link, C.byref(q))
+
+    def scan_template(self, ctype_id, arity, var, ordered, no_overload=False, emit_link=False):
+        q = das_template_scan_t()
+        q.ctype_id = ctype_id
+        q.arity = arity
+        for i in range(8):
+            q.var[i] = var[i] if i < len(var) else -1
+        q.ordered = 1 if ordered else 0
+        q.no_overload = 1 if no_overload else 0
+        q.emit_link = 1 if emit_link else 0
+        return self._table(lib().das_scan_template, C.byref(q))
+
+    def scan_type(self, type_id):
+        arr = (P * 9)()
+        check(lib().das_scan_type(self.h, int(type_id), arr), self.h)
+        return [Table(self, arr[a]) if arr[a] else None for a in range(9)]
+
+    def join(self, a, b, no_overload=False):
+        return self._table(lib().das_join, a.h, b.h, 1 if no_overload else 0)
+
+    def antijoin(self, a, t):
+        return self._table(lib().das_antijoin, a.h, t.h)
+
+    def dedup(self, a):
+        return self._table(lib().das_dedup, a.h)
+
+    def concat(self, tables):
+        arr = (P * len(tables))(*[t.h for t in tables])
+        return self._table(lib().das_concat, arr, len(tables))
+
+    def table_from_host(self, kind, vars_, cols):
+        cols = np.ascontiguousarray(np.asarray(cols, dtype=np.uint32))
+        v = (C.c_int32 * len(vars_))(*vars_)
+        n = cols.shape[1] if cols.ndim == 2 else 0
+        return self._table(lib().das_table_from_host, kind, len(vars_), v, ptr(cols), n)
+
+    def sync(self):
+        check(lib().das_ctx_sync(self.h), self.h)

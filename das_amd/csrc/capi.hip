@@ -1,0 +1,353 @@
+// extern "C" boundary (include/das_mi355x.h).  Every entry point catches
+// das::Error / std::exception and returns a status; the message is kept per
+// context for das_last_error.
+#include <cstring>
+
+#include "das_internal.h"
+#include "md5.h"
+
+using das::Ctx;
+using das::Digest;
+using das::Error;
+using das::Table;
+
+struct das_ctx {
+  Ctx c;
+};
+struct das_table {
+  Table t;
+};
+
+namespace {
+
+thread_local std::string g_err;   // errors without a context
+
+int fail(das_ctx_t* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->c.err = msg;
+  g_err = msg;
+  return code;
+}
+
+template <typename F>
+int guarded(das_ctx_t* ctx, F&& f) {
+  try {
+    if (ctx) {
+      std::lock_guard<std::mutex> lk(ctx->c.mu);
+      DAS_HIP(hipSetDevice(ctx->c.device));
+      f();
+    } else {
+      f();
+    }
+    return DAS_OK;
+  } catch (const Error& e) {
+    return fail(ctx, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(ctx, DAS_ERR_INTERNAL, e.what());
+  } catch (...) {
+    return fail(ctx, DAS_ERR_INTERNAL, "unknown error");
+  }
+}
+
+das_table_t* wrap(std::unique_ptr<Table> t) {
+  // das_table is layout-identical to Table; move the object into a wrapper.
+  auto* w = new das_table;
+  w->t.kind = t->kind;
+  w->t.ncols = t->ncols;
+  std::memcpy(w->t.vars, t->vars, sizeof(t->vars));
+  w->t.nrows = t->nrows;
+  w->t.cap = t->cap;
+  w->t.data = t->data;
+  w->t.s = t->s;
+  t->data = nullptr;
+  return w;
+}
+
+__global__ void k_atom_info(const uint32_t* ids, uint64_t n, const Digest* dig, const uint8_t* cat,
+                            const uint32_t* arity, const uint32_t* type, const uint32_t* name_leaf, Digest* o_dig,
+                            uint8_t* o_cat, uint32_t* o_arity, uint32_t* o_type, uint32_t* o_name) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = ids[i];
+    if (o_dig) o_dig[i] = dig[id];
+    if (o_cat) o_cat[i] = cat[id];
+    if (o_arity) o_arity[i] = arity[id];
+    if (o_type) o_type[i] = type[id];
+    if (o_name) o_name[i] = name_leaf[id];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int das_version(void) { return 1; }
+
+int das_ctx_create(int device, void* stream, das_ctx_t** out) {
+  if (!out) return fail(nullptr, DAS_ERR_INVALID, "null out");
+  das_ctx_t* ctx = nullptr;
+  int rc = guarded(nullptr, [&] {
+    int n = 0;
+    DAS_HIP(hipGetDeviceCount(&n));
+    DAS_CHECK(device >= 0 && device < n, das::DAS_E_INVALID, "no such HIP device");
+    DAS_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    DAS_HIP(hipGetDeviceProperties(&prop, device));
+    DAS_CHECK(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, das::DAS_E_UNSUPPORTED,
+              std::string("this build targets gfx950 (MI355X), device is ") + prop.gcnArchName);
+    ctx = new das_ctx_t;
+    ctx->c.device = device;
+    if (stream) {
+      ctx->c.s = (hipStream_t)stream;
+    } else {
+      DAS_HIP(hipStreamCreateWithFlags(&ctx->c.s, hipStreamNonBlocking));
+      ctx->c.own_stream = true;
+    }
+  });
+  if (rc) {
+    delete ctx;
+    return rc;
+  }
+  *out = ctx;
+  return DAS_OK;
+}
+
+int das_ctx_destroy(das_ctx_t* ctx) {
+  if (!ctx) return DAS_OK;
+  int rc = guarded(ctx, [&] {
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    das::free_index(ctx->c.idx);
+    if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
+  });
+  delete ctx;
+  return rc;
+}
+
+const char* das_last_error(const das_ctx_t* ctx) { return ctx ? ctx->c.err.c_str() : g_err.c_str(); }
+
+int das_ctx_sync(das_ctx_t* ctx) {
+  return guarded(ctx, [&] { DAS_HIP(hipStreamSynchronize(ctx->c.s)); });
+}
+
+int das_md5(const uint8_t* bytes, uint64_t n, uint32_t out[4]) {
+  das::md5::digest_bytes(bytes, n, out);
+  return DAS_OK;
+}
+
+int das_composite_digest(const uint32_t* digests, uint32_t k, uint32_t out[4]) {
+  if (k == 0) return fail(nullptr, DAS_ERR_INVALID, "composite of nothing");
+  if (k == 1) {
+    std::memcpy(out, digests, 16);
+    return DAS_OK;
+  }
+  std::string msg;
+  msg.reserve(33 * k);
+  for (uint32_t i = 0; i < k; ++i) {
+    char hex[32];
+    das::md5::to_hex(digests + 4 * i, hex);
+    if (i) msg.push_back(' ');
+    msg.append(hex, 32);
+  }
+  das::md5::digest_bytes((const uint8_t*)msg.data(), msg.size(), out);
+  return DAS_OK;
+}
+
+int das_hash_strings_dev(das_ctx_t* ctx, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_out) {
+  return guarded(ctx, [&] { das::hash_strings(d_bytes, d_off, n, (Digest*)d_out, ctx->c.s); });
+}
+
+int das_hash_fixed_dev(das_ctx_t* ctx, const uint32_t* d_elems, uint32_t k, uint64_t n, uint32_t* d_out) {
+  return guarded(ctx, [&] { das::hash_fixed((const Digest*)d_elems, k, n, (Digest*)d_out, ctx->c.s); });
+}
+
+int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms) {
+  if (!ctx || !atoms) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] { das::build_index(ctx->c, *atoms); });
+}
+
+int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out) {
+  return guarded(ctx, [&] {
+    const das::Index& x = ctx->c.idx;
+    std::memset(out, 0, sizeof(*out));
+    out->n_atoms = x.n_atoms;
+    out->n_nodes = x.n_nodes;
+    out->n_links = x.n_links;
+    out->n_types = x.n_types;
+    out->n_ctypes = x.ctype_digest.size();
+    out->device_bytes = x.device_bytes;
+    for (int a = 1; a <= das::kMaxArity; ++a) out->links_by_arity[a] = x.ttab[a].rows;
+  });
+}
+
+int das_lookup(das_ctx_t* ctx, const uint32_t* digests, uint64_t n, int64_t* ids, uint8_t* cat, uint32_t* arity,
+               uint32_t* type) {
+  int rc = guarded(ctx, [&] { das::lookup_digests(ctx->c, (const Digest*)digests, n, ids); });
+  if (rc || (!cat && !arity && !type)) return rc;
+  std::vector<uint32_t> valid;
+  std::vector<uint64_t> where;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (cat) cat[i] = 0;
+    if (arity) arity[i] = 0;
+    if (type) type[i] = das::kNone;
+    if (ids[i] >= 0) { valid.push_back((uint32_t)ids[i]); where.push_back(i); }
+  }
+  if (valid.empty()) return DAS_OK;
+  std::vector<uint8_t> c(valid.size());
+  std::vector<uint32_t> a(valid.size()), t(valid.size());
+  rc = das_atoms_info(ctx, valid.data(), valid.size(), nullptr, c.data(), a.data(), t.data(), nullptr);
+  if (rc) return rc;
+  for (size_t k = 0; k < valid.size(); ++k) {
+    if (cat) cat[where[k]] = c[k];
+    if (arity) arity[where[k]] = a[k];
+    if (type) type[where[k]] = t[k];
+  }
+  return DAS_OK;
+}
+
+int das_atoms_info(das_ctx_t* ctx, const uint32_t* ids, uint64_t n, uint32_t* digests, uint8_t* cat, uint32_t* arity,
+                   uint32_t* type, uint32_t* name_leaf) {
+  return guarded(ctx, [&] {
+    const das::Index& x = ctx->c.idx;
+    DAS_CHECK(x.built, das::DAS_E_NOT_BUILT, "index not built");
+    if (!n) return;
+    for (uint64_t i = 0; i < n; ++i) DAS_CHECK(ids[i] < x.n_atoms, das::DAS_E_INVALID, "atom id out of range");
+    hipStream_t s = ctx->c.s;
+    das::DBuf<uint32_t> d_ids(n, s);
+    DAS_HIP(hipMemcpyAsync(d_ids.p, ids, 4 * n, hipMemcpyHostToDevice, s));
+    das::DBuf<Digest> dg(digests ? n : 0, s);
+    das::DBuf<uint8_t> dc(cat ? n : 0, s);
+    das::DBuf<uint32_t> da(arity ? n : 0, s), dt(type ? n : 0, s), dn(name_leaf ? n : 0, s);
+    hipLaunchKernelGGL(k_atom_info, dim3(das::grid_for(n, 256)), dim3(256), 0, s, (const uint32_t*)d_ids.p, n,
+                       (const Digest*)x.digest, (const uint8_t*)x.cat, (const uint32_t*)x.arity,
+                       (const uint32_t*)x.type, (const uint32_t*)x.name_leaf, dg.p, dc.p, da.p, dt.p, dn.p);
+    DAS_HIP(hipGetLastError());
+    if (digests) DAS_HIP(hipMemcpyAsync(digests, dg.p, 16 * n, hipMemcpyDeviceToHost, s));
+    if (cat) DAS_HIP(hipMemcpyAsync(cat, dc.p, n, hipMemcpyDeviceToHost, s));
+    if (arity) DAS_HIP(hipMemcpyAsync(arity, da.p, 4 * n, hipMemcpyDeviceToHost, s));
+    if (type) DAS_HIP(hipMemcpyAsync(type, dt.p, 4 * n, hipMemcpyDeviceToHost, s));
+    if (name_leaf) DAS_HIP(hipMemcpyAsync(name_leaf, dn.p, 4 * n, hipMemcpyDeviceToHost, s));
+    DAS_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, uint32_t* n) {
+  return guarded(ctx, [&] {
+    const das::Index& x = ctx->c.idx;
+    DAS_CHECK(x.built, das::DAS_E_NOT_BUILT, "index not built");
+    DAS_CHECK(id < x.n_atoms, das::DAS_E_INVALID, "atom id out of range");
+    uint64_t off[2];
+    DAS_HIP(hipMemcpyAsync(off, x.tgt_off + id, 16, hipMemcpyDeviceToHost, ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    const uint64_t k = off[1] - off[0];
+    *n = (uint32_t)k;
+    DAS_CHECK(k <= cap, das::DAS_E_INVALID, "target buffer too small");
+    if (k) {
+      DAS_HIP(hipMemcpyAsync(out, x.tgt + off[0], 4 * k, hipMemcpyDeviceToHost, ctx->c.s));
+      DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    }
+  });
+}
+
+int das_ctype_lookup(das_ctx_t* ctx, const uint32_t digest[4], int64_t* ctype_id) {
+  return guarded(ctx, [&] {
+    const auto& v = ctx->c.idx.ctype_digest;
+    Digest q{{digest[0], digest[1], digest[2], digest[3]}};
+    auto it = std::lower_bound(v.begin(), v.end(), q, [](const Digest& a, const Digest& b) {
+      return a.hi() < b.hi() || (a.hi() == b.hi() && a.lo() < b.lo());
+    });
+    *ctype_id = (it != v.end() && it->hi() == q.hi() && it->lo() == q.lo()) ? (int64_t)(it - v.begin()) : -1;
+  });
+}
+
+int das_scan_link(das_ctx_t* ctx, const das_link_scan_t* q, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::scan_link(ctx->c, *q)); });
+}
+
+int das_scan_template(das_ctx_t* ctx, const das_template_scan_t* q, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::scan_template(ctx->c, *q)); });
+}
+
+int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9) {
+  return guarded(ctx, [&] {
+    for (int a = 0; a <= 8; ++a) out9[a] = nullptr;
+    const das::Index& x = ctx->c.idx;
+    DAS_CHECK(x.built, das::DAS_E_NOT_BUILT, "index not built");
+    if (type_id >= x.n_types) return;
+    for (int a = 1; a <= das::kMaxArity; ++a) {
+      const das::RowTable& rt = x.ttab[a];
+      if (!rt.rows) continue;
+      const uint64_t b = x.type_off[a][type_id], e = x.type_off[a][type_id + 1];
+      if (e <= b) continue;
+      int32_t vars[das::kMaxCols];
+      for (int k = 0; k <= a; ++k) vars[k] = k - 1;
+      auto t = das::new_table(ctx->c, DAS_TABLE_ORDERED, a + 1, vars, e - b);
+      t->nrows = e - b;
+      for (int k = 0; k <= a; ++k)
+        DAS_HIP(hipMemcpyAsync(t->col(k), rt.col(k) + b, 4 * (e - b), hipMemcpyDeviceToDevice, ctx->c.s));
+      out9[a] = wrap(std::move(t));
+    }
+  });
+}
+
+int das_join(das_ctx_t* ctx, const das_table_t* a, const das_table_t* b, uint32_t no_overload, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::join(ctx->c, a->t, b->t, (int)no_overload)); });
+}
+
+int das_antijoin(das_ctx_t* ctx, const das_table_t* a, const das_table_t* t, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::antijoin(ctx->c, a->t, t->t)); });
+}
+
+int das_dedup(das_ctx_t* ctx, const das_table_t* a, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::dedup(ctx->c, a->t)); });
+}
+
+int das_concat(das_ctx_t* ctx, const das_table_t* const* ts, uint32_t n, das_table_t** out) {
+  return guarded(ctx, [&] {
+    std::vector<const Table*> v(n);
+    for (uint32_t i = 0; i < n; ++i) v[i] = &ts[i]->t;
+    *out = wrap(das::concat(ctx->c, v.data(), (int)n));
+  });
+}
+
+int das_table_info(const das_table_t* t, int32_t* kind, int32_t* ncols, int32_t* vars, uint64_t* nrows) {
+  if (!t) return fail(nullptr, DAS_ERR_INVALID, "null table");
+  if (kind) *kind = t->t.kind;
+  if (ncols) *ncols = t->t.ncols;
+  if (vars) std::memcpy(vars, t->t.vars, sizeof(int32_t) * t->t.ncols);
+  if (nrows) *nrows = t->t.nrows;
+  return DAS_OK;
+}
+
+int das_table_fetch(das_ctx_t* ctx, const das_table_t* t, uint64_t row0, uint64_t nrows, uint32_t* out) {
+  return guarded(ctx, [&] {
+    DAS_CHECK(row0 + nrows <= t->t.nrows, das::DAS_E_INVALID, "fetch out of range");
+    for (int c = 0; c < t->t.ncols; ++c)
+      if (nrows)
+        DAS_HIP(hipMemcpyAsync(out + (uint64_t)c * nrows, t->t.col(c) + row0, 4 * nrows, hipMemcpyDeviceToHost,
+                               ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+  });
+}
+
+int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr) {
+  if (!t || c < 0 || c >= t->t.ncols) return fail(nullptr, DAS_ERR_INVALID, "bad column");
+  *dptr = t->t.col(c);
+  return DAS_OK;
+}
+
+int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const uint32_t* cols,
+                        uint64_t nrows, das_table_t** out) {
+  return guarded(ctx, [&] {
+    auto t = das::new_table(ctx->c, kind, ncols, vars, nrows);
+    t->nrows = nrows;
+    for (int c = 0; c < ncols; ++c)
+      if (nrows) DAS_HIP(hipMemcpyAsync(t->col(c), cols + (uint64_t)c * nrows, 4 * nrows, hipMemcpyHostToDevice, ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    *out = wrap(std::move(t));
+  });
+}
+
+int das_table_free(das_table_t* t) {
+  delete t;
+  return DAS_OK;
+}
+
+}  // extern "C"

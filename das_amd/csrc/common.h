@@ -1,0 +1,116 @@
+// Shared host/device plumbing for the DAS MI355X library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace das {
+
+constexpr int kWave = 64;          // CDNA wavefront width
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+enum Status : int {
+  DAS_S_OK = 0,
+  DAS_E_INVALID = -1,     // bad argument / misuse          -> ValueError
+  DAS_E_HIP = -2,         // HIP runtime failure            -> RuntimeError
+  DAS_E_NOT_BUILT = -3,   // index not built                -> RuntimeError
+  DAS_E_UNSUPPORTED = -4, // shape outside this build       -> NotImplementedError
+  DAS_E_INTERNAL = -5,
+};
+
+#define DAS_HIP(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      throw ::das::Error(::das::DAS_E_HIP, std::string(#expr) + ": " +             \
+                                               hipGetErrorString(_e) + " at " +    \
+                                               __FILE__ + ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+#define DAS_CHECK(cond, code, msg)                 \
+  do {                                             \
+    if (!(cond)) throw ::das::Error((code), (msg)); \
+  } while (0)
+
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 8u) {
+  uint64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// Stream-ordered device buffer (hipMallocAsync / hipFreeAsync on the ctx stream).
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  uint64_t n = 0;
+  hipStream_t s = nullptr;
+  DBuf() = default;
+  DBuf(uint64_t count, hipStream_t st) { alloc(count, st); }
+  void alloc(uint64_t count, hipStream_t st) {
+    release();
+    s = st;
+    n = count;
+    if (count) DAS_HIP(hipMallocAsync((void**)&p, sizeof(T) * count, st));
+  }
+  void release() {
+    if (p) (void)hipFreeAsync(p, s);
+    p = nullptr;
+    n = 0;
+  }
+  T* release_ownership() {
+    T* q = p;
+    p = nullptr;
+    n = 0;
+    return q;
+  }
+  ~DBuf() { release(); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept { *this = std::move(o); }
+  DBuf& operator=(DBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p; n = o.n; s = o.s;
+      o.p = nullptr; o.n = 0;
+    }
+    return *this;
+  }
+  uint64_t bytes() const { return sizeof(T) * n; }
+};
+
+// Pinned host scratch for small D2H reads that the planner needs (row counts).
+struct HostScalar {
+  uint64_t* h = nullptr;
+  HostScalar() { DAS_HIP(hipHostMalloc((void**)&h, sizeof(uint64_t) * 64, hipHostMallocDefault)); }
+  ~HostScalar() { if (h) (void)hipHostFree(h); }
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// A 128-bit MD5 digest, stored as the four little-endian state words a..d
+// (byte i of the digest is byte (i&3) of word i>>2).  `hi()/lo()` give the
+// big-endian 64-bit halves, so (hi, lo) order == lexicographic order of the
+// 32-char hex handle (the order Python's sorted() gives handles).
+struct Digest {
+  uint32_t w[4];
+  __host__ __device__ uint64_t hi() const {
+    return ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+  }
+  __host__ __device__ uint64_t lo() const {
+    return ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
+  }
+};
+
+}  // namespace das

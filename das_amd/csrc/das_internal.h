@@ -1,0 +1,114 @@
+// Internal types of the DAS MI355X library: the HBM-resident atom index and
+// device binding tables.  Layout rationale is in DESIGN.md §3.
+#pragma once
+#include <array>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/das_mi355x.h"
+#include "common.h"
+#include "prims.h"
+
+namespace das {
+
+constexpr int kMaxArity = 8;      // index tables exist for arity 1..kMaxArity
+constexpr int kMaxPosArity = 3;   // per-position (pattern) index: arity 1..3, as the reference
+constexpr int kMaxCols = 16;      // columns in a binding table
+constexpr int kTypeBits = 24;     // P-index key = target << 24 | named-type id
+
+enum AtomCat : uint8_t { CAT_OTHER = 0, CAT_NODE = 1, CAT_LINK = 2 };
+
+// Rows (link id, t0 .. t_{a-1}) stored column-major: column c at data + c*rows.
+struct RowTable {
+  int arity = 0;
+  uint64_t rows = 0;
+  uint32_t* data = nullptr;
+  uint32_t* col(int c) const { return data + (uint64_t)c * rows; }
+};
+
+// P_{a,p}: RowTable sorted by (t_p, type, link id) + unique keys -> row offsets.
+struct PosIndex {
+  RowTable t;
+  uint64_t nkeys = 0;
+  uint64_t* ukey = nullptr;   // sorted unique (t_p << 24 | type)
+  uint64_t* uoff = nullptr;   // nkeys + 1 row offsets
+};
+
+struct CtypeRange {
+  uint32_t arity;
+  uint64_t begin, end;        // rows of ctab[arity]
+};
+
+struct Index {
+  bool built = false;
+  uint64_t n_atoms = 0, n_nodes = 0, n_links = 0, n_types = 0;
+  Digest* digest = nullptr;    // [n_atoms], sorted by (hi, lo)
+  uint8_t* cat = nullptr;      // [n_atoms]
+  uint32_t* type = nullptr;    // [n_atoms] named type id (kNone for CAT_OTHER)
+  uint32_t* arity = nullptr;   // [n_atoms]
+  uint64_t* tgt_off = nullptr; // [n_atoms + 1]
+  uint32_t* tgt = nullptr;     // [sum arity]
+  uint32_t* ctype = nullptr;   // [n_atoms] composite-type id of links, kNone otherwise
+  uint32_t* name_leaf = nullptr; // [n_atoms] loader leaf index of nodes (kNone otherwise)
+  // T_a: links of arity a sorted by (type, id);   C_a: by (ctype, id)
+  std::array<RowTable, kMaxArity + 1> ttab{};
+  std::array<RowTable, kMaxArity + 1> ctab{};
+  std::array<std::array<PosIndex, kMaxPosArity>, kMaxPosArity + 1> pidx{};
+  std::array<std::vector<uint64_t>, kMaxArity + 1> type_off;   // host: n_types + 1 per arity
+  std::vector<Digest> ctype_digest;                            // host: sorted ctype digests
+  std::vector<CtypeRange> ctype_range;                         // host
+  std::vector<void*> owned;                                    // device allocations
+  uint64_t device_bytes = 0;
+};
+
+struct Table {
+  int kind = DAS_TABLE_ORDERED;
+  int ncols = 0;
+  int32_t vars[kMaxCols] = {0};
+  uint64_t nrows = 0, cap = 0;
+  uint32_t* data = nullptr;   // ncols columns of `cap` u32 each
+  hipStream_t s = nullptr;
+  uint32_t* col(int c) const { return data + (uint64_t)c * cap; }
+  ~Table() {
+    if (data) (void)hipFreeAsync(data, s);
+  }
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t s = nullptr;
+  bool own_stream = false;
+  std::string err;
+  std::mutex mu;
+  Index idx;
+  HostScalar scratch;
+  // loader-side host copies kept for metadata calls
+  std::vector<uint8_t> leaf_bytes;
+  std::vector<uint64_t> leaf_off;
+};
+
+// hash.hip
+void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, Digest* out, hipStream_t s);
+void hash_group(Digest* table, Digest* ctab, const uint32_t* child, const uint64_t* child_off,
+                const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n, uint32_t K,
+                hipStream_t s);
+void hash_fixed(const Digest* elems, uint32_t k, uint64_t n, Digest* out, hipStream_t s);
+
+// index.hip
+void build_index(Ctx& c, const das_atoms_t& a);
+void free_index(Index& idx);
+void lookup_digests(Ctx& c, const Digest* h_digests, uint64_t n, int64_t* h_ids);
+
+// query.hip
+std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q);
+std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q);
+std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
+std::unique_ptr<Table> antijoin(Ctx& c, const Table& a, const Table& t);
+std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
+std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);
+std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap);
+
+}  // namespace das

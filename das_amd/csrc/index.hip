@@ -1,0 +1,606 @@
+// HBM index build: hashing, handle interning and the CSR-style tables the
+// query operators read.  Replaces the reference's load path
+//   CanonicalParser.parse/_add_* + Mongo insert_many         canonical_parser.py:48-124, 185-206
+//   _build_key_value_files + sort(1) + Redis SADD              canonical_parser.py:132-240
+// (same families as parser_threads.py:141-253 for the MettaYacc loader).
+//
+// Layout:
+//   atoms        sorted by digest (== sorted hex handle): id order == handle order
+//   T_a          links of arity a, rows (link, t0..t_{a-1}) sorted by (type, id)
+//   C_a          same rows sorted by (composite type, id)       -> templates:*
+//   P_{a,p}      same rows sorted by (t_p, type, id), a <= 3     -> patterns:* with a
+//                grounded target at p; unique (t_p<<24|type) keys + row offsets
+//   tgt_off/tgt  outgoing sets (stored target order)
+// Pattern keys with only wildcard targets are served by T_a (typed) or all of
+// T_a ('*' type); a '*' type with grounded targets by the untyped key range of
+// P_{a,p}.  This covers exactly the families the reference writes for arity
+// 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
+#include "das_internal.h"
+
+namespace das {
+
+__global__ void k_iota(uint32_t* p, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)i;
+}
+__global__ void k_gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t* dst, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
+}
+
+uint64_t read_u64(const uint64_t* d, hipStream_t s) {
+  uint64_t v = 0;
+  DAS_HIP(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  return v;
+}
+uint32_t read_u32(const uint32_t* d, hipStream_t s) {
+  uint32_t v = 0;
+  DAS_HIP(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  return v;
+}
+
+namespace {
+
+template <typename T>
+T* dalloc(Index& idx, uint64_t count) {
+  T* p = nullptr;
+  if (!count) count = 1;
+  DAS_HIP(hipMalloc((void**)&p, sizeof(T) * count));
+  idx.owned.push_back(p);
+  idx.device_bytes += sizeof(T) * count;
+  return p;
+}
+
+template <typename T>
+DBuf<T> upload(const T* h, uint64_t n, hipStream_t s) {
+  DBuf<T> d(n ? n : 1, s);
+  if (n) DAS_HIP(hipMemcpyAsync(d.p, h, sizeof(T) * n, hipMemcpyHostToDevice, s));
+  return d;
+}
+
+__global__ void k_leaf_ctype(const Digest* dig, const uint32_t* leaf_ctype, Digest* ct, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    ct[i] = dig[leaf_ctype[i]];
+}
+
+// flag/catl over unified indices: nodes, links, and anything a link targets.
+__global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, uint64_t n_leaf, uint64_t n_expr,
+                           uint8_t* catl, uint32_t* flag) {
+  const uint64_t n = n_leaf + n_expr;
+  for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t c = CAT_OTHER;
+    uint32_t f = 0;
+    if (u < n_leaf) {
+      if (leaf_kind[u] == 1) { c = CAT_NODE; f = 1; }
+    } else if (expr_kind[u - n_leaf] == 1) {
+      c = CAT_LINK;
+      f = 1;
+    }
+    catl[u] = c;
+    flag[u] = f;
+  }
+}
+
+__global__ void k_mark_targets(const uint8_t* expr_kind, const uint64_t* off, const uint32_t* child, uint64_t n_expr,
+                               uint32_t* flag) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_expr; j += (uint64_t)gridDim.x * blockDim.x) {
+    if (expr_kind[j] != 1) continue;
+    for (uint64_t k = off[j] + 1; k < off[j + 1]; ++k) flag[child[k]] = 1;
+  }
+}
+
+// Compaction: out[scan[i]] = i for flagged i.
+__global__ void k_compact_index(const uint32_t* flag, const uint32_t* scan, uint64_t n, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[i]) out[scan[i]] = (uint32_t)i;
+}
+
+__global__ void k_digest_key(const Digest* dig, const uint32_t* idx, uint64_t n, uint64_t* key, bool hi) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Digest d = dig[idx[i]];
+    key[i] = hi ? d.hi() : d.lo();
+  }
+}
+
+// Counts adjacent entries whose 64-bit high halves tie but whose digests differ
+// (then the hi-only sort is not a full 128-bit order and we redo it).
+__global__ void k_hi_ties(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Digest a = dig[idx[i - 1]], b = dig[idx[i]];
+    if (a.hi() == b.hi() && a.lo() != b.lo()) atomicAdd(bad, 1u);
+  }
+}
+
+__global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t f = 1;
+    if (i > 0) {
+      const Digest a = dig[idx[i - 1]], b = dig[idx[i]];
+      f = (a.w[0] != b.w[0]) | (a.w[1] != b.w[1]) | (a.w[2] != b.w[2]) | (a.w[3] != b.w[3]);
+    }
+    first[i] = f;
+  }
+}
+
+// id = inclusive run index; catmax = max category over the run.
+__global__ void k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan, uint64_t n,
+                             const uint8_t* catl, uint32_t* local2id, uint32_t* catmax) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = scan[i] + first[i] - 1;
+    const uint32_t u = idx[i];
+    local2id[u] = id;
+    atomicMax(&catmax[id], (uint32_t)catl[u]);
+  }
+}
+
+__global__ void k_pick_rep(const uint32_t* idx, uint64_t n, const uint32_t* local2id, const uint8_t* catl,
+                           const uint32_t* catmax, uint32_t* rep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = idx[i];
+    const uint32_t id = local2id[u];
+    if ((uint32_t)catl[u] == catmax[id]) atomicMin(&rep[id], u);
+  }
+}
+
+__global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, const Digest* dig,
+                             const Digest* ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
+                             const uint32_t* leaf_type_id, const uint64_t* expr_off, const uint32_t* expr_child,
+                             Digest* a_dig, uint8_t* a_cat, uint32_t* a_type, uint32_t* a_arity, Digest* a_ct,
+                             uint32_t* a_name_leaf) {
+  for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = rep[id];
+    const uint32_t c = catmax[id];
+    a_dig[id] = dig[u];
+    a_ct[id] = ct[u];
+    a_cat[id] = (uint8_t)c;
+    uint32_t ty = kNone, ar = 0, nl = kNone;
+    if (u < n_leaf) {
+      ty = leaf_type_id[leaf_ctype[u]];
+      if (c == CAT_NODE) nl = u;
+    } else {
+      const uint64_t j = u - n_leaf;
+      if (c == CAT_LINK) {
+        ty = leaf_type_id[expr_child[expr_off[j]]];
+        ar = (uint32_t)(expr_off[j + 1] - expr_off[j] - 1);
+      }
+    }
+    a_type[id] = ty;
+    a_arity[id] = ar;
+    a_name_leaf[id] = nl;
+  }
+}
+
+__global__ void k_fill_targets(uint64_t n_atoms, const uint32_t* rep, const uint8_t* a_cat, const uint64_t* tgt_off,
+                               uint64_t n_leaf, const uint64_t* expr_off, const uint32_t* expr_child,
+                               const uint32_t* local2id, uint32_t* tgt) {
+  for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    if (a_cat[id] != CAT_LINK) continue;
+    const uint64_t j = rep[id] - n_leaf;
+    const uint64_t b = expr_off[j] + 1, e = expr_off[j + 1];
+    uint64_t o = tgt_off[id];
+    for (uint64_t k = b; k < e; ++k) tgt[o++] = local2id[expr_child[k]];
+  }
+}
+
+__global__ void k_link_flags(const uint8_t* cat, const uint32_t* arity, uint64_t n, uint32_t want_arity, uint32_t* f) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    f[i] = (cat[i] == CAT_LINK) && (want_arity == kNone || arity[i] == want_arity);
+}
+
+__global__ void k_arity_hist(const uint8_t* cat, const uint32_t* arity, uint64_t n, unsigned long long* h) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (cat[i] == CAT_NODE) atomicAdd(&h[63], 1ull);
+    if (cat[i] != CAT_LINK) continue;
+    uint32_t a = arity[i] > 62 ? 62 : arity[i];
+    atomicAdd(&h[a], 1ull);
+  }
+}
+
+__global__ void k_ct_key(const Digest* a_ct, const uint32_t* ids, uint64_t n, uint64_t* key, bool hi) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Digest d = a_ct[ids[i]];
+    key[i] = hi ? d.hi() : d.lo();
+  }
+}
+
+__global__ void k_set_ctype(const uint32_t* ids, const uint32_t* first, const uint32_t* scan, uint64_t n,
+                            uint32_t* a_ctype) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    a_ctype[ids[i]] = scan[i] + first[i] - 1;
+}
+
+__global__ void k_ct_unique(const Digest* a_ct, const uint32_t* ids, const uint32_t* first, const uint32_t* scan,
+                            uint64_t n, Digest* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (first[i]) out[scan[i]] = a_ct[ids[i]];
+}
+
+__global__ void k_u32_key(const uint32_t* src, const uint32_t* ids, uint64_t n, uint32_t* key) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    key[i] = src[ids[i]];
+}
+
+__global__ void k_pos_key(const uint32_t* type, const uint64_t* tgt_off, const uint32_t* tgt, const uint32_t* ids,
+                          uint64_t n, uint32_t p, uint64_t* key) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = ids[i];
+    key[i] = ((uint64_t)tgt[tgt_off[id] + p] << kTypeBits) | (uint64_t)type[id];
+  }
+}
+
+// rows: col 0 = link id, col 1+k = target k
+__global__ void k_gather_rows(const uint32_t* ids, uint64_t R, uint32_t arity, const uint64_t* tgt_off,
+                              const uint32_t* tgt, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = ids[i];
+    out[i] = id;
+    const uint64_t o = tgt_off[id];
+    for (uint32_t k = 0; k < arity; ++k) out[(uint64_t)(k + 1) * R + i] = tgt[o + k];
+  }
+}
+
+template <typename K>
+__global__ void k_run_flags(const K* key, uint64_t n, uint32_t* f) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    f[i] = (i == 0) || key[i] != key[i - 1];
+}
+
+template <typename K>
+__global__ void k_run_emit(const K* key, const uint32_t* f, const uint32_t* scan, uint64_t n, K* ukey, uint64_t* uoff) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (f[i]) {
+      ukey[scan[i]] = key[i];
+      uoff[scan[i]] = i;
+    }
+}
+
+__global__ void k_lookup(const Digest* dig, uint64_t n_atoms, const Digest* q, uint64_t nq, int64_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t qh = q[i].hi(), ql = q[i].lo();
+    uint64_t lo = 0, hi = n_atoms;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const Digest d = dig[mid];
+      const uint64_t dh = d.hi(), dl = d.lo();
+      if (dh < qh || (dh == qh && dl < ql)) lo = mid + 1;
+      else hi = mid;
+    }
+    int64_t r = -1;
+    if (lo < n_atoms) {
+      const Digest d = dig[lo];
+      if (d.hi() == qh && d.lo() == ql) r = (int64_t)lo;
+    }
+    out[i] = r;
+  }
+}
+
+struct WidenU32 {
+  const uint32_t* a;
+  uint64_t n;
+  __device__ uint64_t operator()(uint64_t i) const { return i < n ? (uint64_t)a[i] : 0ull; }
+};
+
+inline dim3 G(uint64_t n) { return dim3(grid_for(n, 256)); }
+constexpr unsigned B = 256;
+
+// Indices 0..n) of `flag` set -> compacted list (device) + count.
+uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hipStream_t s) {
+  if (!n) { out.alloc(1, s); return 0; }
+  DBuf<uint32_t> scan(n, s);
+  exclusive_scan<uint32_t>(flag, n, scan.p, s);
+  uint32_t last_scan = 0, last_flag = 0;
+  DAS_HIP(hipMemcpyAsync(&last_scan, scan.p + n - 1, 4, hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipMemcpyAsync(&last_flag, flag + n - 1, 4, hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  const uint64_t m = (uint64_t)last_scan + last_flag;
+  out.alloc(m ? m : 1, s);
+  hipLaunchKernelGGL(k_compact_index, G(n), dim3(B), 0, s, flag, (const uint32_t*)scan.p, n, out.p);
+  DAS_HIP(hipGetLastError());
+  return m;
+}
+
+// Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact fallback).
+void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s) {
+  if (n <= 1) return;
+  DBuf<uint64_t> key(n, s);
+  hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
+  radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+  DBuf<uint32_t> bad(1, s);
+  DAS_HIP(hipMemsetAsync(bad.p, 0, 4, s));
+  hipLaunchKernelGGL(k_hi_ties, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, bad.p);
+  if (read_u32(bad.p, s) == 0) return;
+  // exact: LSD over (lo, hi)
+  hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, false);
+  radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+  hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
+  radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+}
+
+// Run-length encoding of sorted keys: unique keys + n_runs+1 offsets (device).
+template <typename K>
+uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hipStream_t s) {
+  DBuf<uint32_t> f(n ? n : 1, s), scan(n ? n : 1, s);
+  uint64_t m = 0;
+  if (n) {
+    hipLaunchKernelGGL((k_run_flags<K>), G(n), dim3(B), 0, s, key, n, f.p);
+    exclusive_scan<uint32_t>(f.p, n, scan.p, s);
+    m = (uint64_t)read_u32(scan.p + n - 1, s) + 1;
+  }
+  *ukey = dalloc<K>(idx, m);
+  *uoff = dalloc<uint64_t>(idx, m + 1);
+  if (n) {
+    hipLaunchKernelGGL((k_run_emit<K>), G(n), dim3(B), 0, s, key, (const uint32_t*)f.p, (const uint32_t*)scan.p, n,
+                       *ukey, *uoff);
+    DAS_HIP(hipGetLastError());
+  }
+  DAS_HIP(hipMemcpyAsync(*uoff + m, &n, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  DAS_HIP(hipStreamSynchronize(s));   // &n is a host stack value
+  return m;
+}
+
+}  // namespace
+
+void free_index(Index& idx) {
+  for (void* p : idx.owned) (void)hipFree(p);
+  idx = Index();
+}
+
+void build_index(Ctx& c, const das_atoms_t& a) {
+  hipStream_t s = c.s;
+  free_index(c.idx);
+  Index& idx = c.idx;
+  const uint64_t nl = a.n_leaf, ne = a.n_expr, nu = nl + ne;
+  DAS_CHECK(nu > 0 && nu < 0xFFFFFFF0ull, DAS_E_INVALID, "atom count out of range");
+  DAS_CHECK(a.n_types < (1u << kTypeBits), DAS_E_UNSUPPORTED, "too many named types");
+  const uint64_t n_bytes = a.leaf_off[nl];
+  const uint64_t n_child = a.expr_off[ne];
+
+  // host copies for metadata (node names)
+  c.leaf_bytes.assign(a.leaf_bytes, a.leaf_bytes + n_bytes);
+  c.leaf_off.assign(a.leaf_off, a.leaf_off + nl + 1);
+
+  auto d_bytes = upload(a.leaf_bytes, n_bytes, s);
+  auto d_loff = upload(a.leaf_off, nl + 1, s);
+  auto d_lkind = upload(a.leaf_kind, nl, s);
+  auto d_lct = upload(a.leaf_ctype, nl, s);
+  auto d_ltype = upload(a.leaf_type_id, nl, s);
+  auto d_eoff = upload(a.expr_off, ne + 1, s);
+  auto d_child = upload(a.expr_child, n_child, s);
+  auto d_ekind = upload(a.expr_kind, ne, s);
+  auto d_ectl = upload(a.expr_ctype_leaf, ne, s);
+
+  // 1. digests + composite types of every unified index
+  DBuf<Digest> dig(nu, s), ct(nu, s);
+  hash_strings(d_bytes.p, d_loff.p, nl, dig.p, s);
+  if (nl) hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)d_lct.p, ct.p, nl);
+  for (uint32_t g = 0; g < a.n_levels; ++g) {
+    const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
+    if (e <= b) continue;
+    const uint32_t K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
+    hash_group(dig.p, ct.p, d_child.p, d_eoff.p, d_ectl.p, nl, b, e - b, K, s);
+  }
+
+  // 2. which unified indices are atoms (nodes, links, link targets)
+  DBuf<uint8_t> catl(nu, s);
+  DBuf<uint32_t> flag(nu, s);
+  hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)d_ekind.p, nl, ne,
+                     catl.p, flag.p);
+  if (ne) hipLaunchKernelGGL(k_mark_targets, G(ne), dim3(B), 0, s, (const uint8_t*)d_ekind.p, (const uint64_t*)d_eoff.p,
+                             (const uint32_t*)d_child.p, ne, flag.p);
+  DAS_HIP(hipGetLastError());
+  DBuf<uint32_t> list;
+  const uint64_t nc = compact_flags(flag.p, nu, list, s);
+  flag.release();
+
+  // 3. intern: sort by digest, one id per distinct digest
+  sort_by_digest(dig.p, list.p, nc, s);
+  DBuf<uint32_t> first(nc ? nc : 1, s), scan(nc ? nc : 1, s);
+  uint64_t n_atoms = 0;
+  if (nc) {
+    hipLaunchKernelGGL(k_first_flags, G(nc), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)list.p, nc, first.p);
+    exclusive_scan<uint32_t>(first.p, nc, scan.p, s);
+    n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
+  }
+  DBuf<uint32_t> local2id(nu, s), catmax(n_atoms ? n_atoms : 1, s), rep(n_atoms ? n_atoms : 1, s);
+  DAS_HIP(hipMemsetAsync(catmax.p, 0, 4 * catmax.n, s));
+  DAS_HIP(hipMemsetAsync(rep.p, 0xFF, 4 * rep.n, s));
+  if (nc) {
+    hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
+                       (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p);
+    hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, nc, (const uint32_t*)local2id.p,
+                       (const uint8_t*)catl.p, (const uint32_t*)catmax.p, rep.p);
+    DAS_HIP(hipGetLastError());
+  }
+  first.release(); scan.release(); list.release();
+
+  // 4. atom arrays (id order == handle order)
+  idx.n_atoms = n_atoms;
+  idx.n_types = a.n_types;
+  idx.digest = dalloc<Digest>(idx, n_atoms);
+  idx.cat = dalloc<uint8_t>(idx, n_atoms);
+  idx.type = dalloc<uint32_t>(idx, n_atoms);
+  idx.arity = dalloc<uint32_t>(idx, n_atoms);
+  idx.tgt_off = dalloc<uint64_t>(idx, n_atoms + 1);
+  idx.ctype = dalloc<uint32_t>(idx, n_atoms);
+  idx.name_leaf = dalloc<uint32_t>(idx, n_atoms);
+  DBuf<Digest> a_ct(n_atoms ? n_atoms : 1, s);
+  if (n_atoms) {
+    hipLaunchKernelGGL(k_fill_atoms, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
+                       (const uint32_t*)catmax.p, (const Digest*)dig.p, (const Digest*)ct.p, nl,
+                       (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)d_eoff.p,
+                       (const uint32_t*)d_child.p, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf);
+    DAS_HIP(hipGetLastError());
+  }
+  DAS_HIP(hipMemsetAsync(idx.ctype, 0xFF, 4 * (n_atoms ? n_atoms : 1), s));
+  // outgoing CSR
+  {
+    // widen arity to u64 for the scan (sum of arities may exceed 2^32 at 1B links)
+    exclusive_scan_fn<uint64_t>(WidenU32{idx.arity, n_atoms}, n_atoms + 1, idx.tgt_off, s);
+    const uint64_t total = read_u64(idx.tgt_off + n_atoms, s);
+    idx.tgt = dalloc<uint32_t>(idx, total);
+    if (n_atoms)
+      hipLaunchKernelGGL(k_fill_targets, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
+                         (const uint8_t*)idx.cat, (const uint64_t*)idx.tgt_off, nl, (const uint64_t*)d_eoff.p,
+                         (const uint32_t*)d_child.p, (const uint32_t*)local2id.p, idx.tgt);
+    DAS_HIP(hipGetLastError());
+  }
+  dig.release(); ct.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
+  d_child.release(); d_bytes.release();
+
+  // 5. counts per arity, node count
+  {
+    DBuf<unsigned long long> h(64, s);
+    DAS_HIP(hipMemsetAsync(h.p, 0, 64 * 8, s));
+    if (n_atoms) hipLaunchKernelGGL(k_arity_hist, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+                                    (const uint32_t*)idx.arity, n_atoms, h.p);
+    unsigned long long hh[64];
+    DAS_HIP(hipMemcpyAsync(hh, h.p, sizeof(hh), hipMemcpyDeviceToHost, s));
+    DAS_HIP(hipStreamSynchronize(s));
+    idx.n_nodes = hh[63];
+    idx.n_links = 0;
+    for (int i = 0; i < 63; ++i) idx.n_links += hh[i];
+    for (int i = kMaxArity + 1; i < 63; ++i)
+      DAS_CHECK(hh[i] == 0, DAS_E_UNSUPPORTED, "links with arity > 8 are not indexed by this build");
+  }
+
+  // 6. composite-type ids over links
+  uint64_t n_ctypes = 0;
+  {
+    DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), lids;
+    if (n_atoms) hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+                                    (const uint32_t*)idx.arity, n_atoms, kNone, lf.p);
+    const uint64_t nlk = compact_flags(lf.p, n_atoms, lids, s);
+    if (nlk) {
+      // sort link ids by ctype digest (hi, exact fallback)
+      DBuf<uint64_t> key(nlk, s);
+      hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
+      radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
+      DBuf<uint32_t> bad(1, s);
+      DAS_HIP(hipMemsetAsync(bad.p, 0, 4, s));
+      hipLaunchKernelGGL(k_hi_ties, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, bad.p);
+      if (read_u32(bad.p, s)) {
+        hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, false);
+        radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
+        hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
+        radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
+      }
+      DBuf<uint32_t> f(nlk, s), sc(nlk, s);
+      hipLaunchKernelGGL(k_first_flags, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, f.p);
+      exclusive_scan<uint32_t>(f.p, nlk, sc.p, s);
+      n_ctypes = (uint64_t)read_u32(sc.p + nlk - 1, s) + read_u32(f.p + nlk - 1, s);
+      hipLaunchKernelGGL(k_set_ctype, G(nlk), dim3(B), 0, s, (const uint32_t*)lids.p, (const uint32_t*)f.p,
+                         (const uint32_t*)sc.p, nlk, idx.ctype);
+      DBuf<Digest> u(n_ctypes, s);
+      hipLaunchKernelGGL(k_ct_unique, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p,
+                         (const uint32_t*)f.p, (const uint32_t*)sc.p, nlk, u.p);
+      idx.ctype_digest.resize(n_ctypes);
+      DAS_HIP(hipMemcpyAsync(idx.ctype_digest.data(), u.p, sizeof(Digest) * n_ctypes, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipStreamSynchronize(s));
+      DAS_HIP(hipGetLastError());
+    }
+  }
+  a_ct.release();
+  idx.ctype_range.assign(n_ctypes, CtypeRange{0, 0, 0});
+
+  // 7. per-arity tables
+  for (uint32_t ar = 1; ar <= (uint32_t)kMaxArity; ++ar) {
+    DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), ids;
+    if (n_atoms) hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+                                    (const uint32_t*)idx.arity, n_atoms, ar, lf.p);
+    const uint64_t R = compact_flags(lf.p, n_atoms, ids, s);
+    lf.release();
+    if (!R) continue;
+    const int tbits = bits_for(a.n_types ? a.n_types - 1 : 0);
+    // T_a by (type, id)
+    {
+      DBuf<uint32_t> key(R, s), perm(R, s);
+      DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint32_t*)perm.p, R, key.p);
+      radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, tbits > 0 ? tbits : 1, s);
+      RowTable& t = idx.ttab[ar];
+      t.arity = (int)ar;
+      t.rows = R;
+      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
+      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+                         (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      // host type offsets
+      uint32_t* ukey; uint64_t* uoff;
+      const uint64_t m = rle<uint32_t>(key.p, R, &ukey, &uoff, idx, s);
+      std::vector<uint32_t> hk(m);
+      std::vector<uint64_t> ho(m + 1);
+      DAS_HIP(hipMemcpyAsync(hk.data(), ukey, 4 * m, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipMemcpyAsync(ho.data(), uoff, 8 * (m + 1), hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipStreamSynchronize(s));
+      auto& to = idx.type_off[ar];
+      to.assign(a.n_types + 1, 0);
+      // to[t] = first row with type >= t
+      uint64_t r = 0;
+      for (uint32_t ty = 0; ty <= a.n_types; ++ty) {
+        while (r < m && hk[r] < ty) ++r;
+        to[ty] = r < m ? ho[r] : R;
+      }
+    }
+    // C_a by (ctype, id)
+    {
+      DBuf<uint32_t> key(R, s), perm(R, s);
+      DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.ctype, (const uint32_t*)perm.p, R, key.p);
+      const int cbits = bits_for(n_ctypes ? n_ctypes - 1 : 0);
+      radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, cbits > 0 ? cbits : 1, s);
+      RowTable& t = idx.ctab[ar];
+      t.arity = (int)ar;
+      t.rows = R;
+      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
+      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+                         (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      uint32_t* ukey; uint64_t* uoff;
+      const uint64_t m = rle<uint32_t>(key.p, R, &ukey, &uoff, idx, s);
+      std::vector<uint32_t> hk(m);
+      std::vector<uint64_t> ho(m + 1);
+      DAS_HIP(hipMemcpyAsync(hk.data(), ukey, 4 * m, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipMemcpyAsync(ho.data(), uoff, 8 * (m + 1), hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipStreamSynchronize(s));
+      for (uint64_t r = 0; r < m; ++r) idx.ctype_range[hk[r]] = CtypeRange{ar, ho[r], ho[r + 1]};
+    }
+    // P_{a,p}
+    if (ar <= (uint32_t)kMaxPosArity) {
+      for (uint32_t p = 0; p < ar; ++p) {
+        DBuf<uint64_t> key(R, s);
+        DBuf<uint32_t> perm(R, s);
+        DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,
+                           (const uint32_t*)idx.tgt, (const uint32_t*)perm.p, R, p, key.p);
+        const int kb = kTypeBits + bits_for(n_atoms ? n_atoms - 1 : 0);
+        radix_sort_pairs<uint64_t>(key.p, perm.p, R, 0, kb, s);
+        PosIndex& P = idx.pidx[ar][p];
+        P.t.arity = (int)ar;
+        P.t.rows = R;
+        P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
+        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+                           (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, P.t.data);
+        P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
+      }
+    }
+    DAS_HIP(hipGetLastError());
+  }
+  DAS_HIP(hipStreamSynchronize(s));
+  idx.built = true;
+}
+
+void lookup_digests(Ctx& c, const Digest* h, uint64_t n, int64_t* out) {
+  DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
+  if (!n) return;
+  auto q = upload(h, n, c.s);
+  DBuf<int64_t> r(n, c.s);
+  hipLaunchKernelGGL(k_lookup, G(n), dim3(B), 0, c.s, (const Digest*)c.idx.digest, c.idx.n_atoms, (const Digest*)q.p,
+                     n, r.p);
+  DAS_HIP(hipGetLastError());
+  DAS_HIP(hipMemcpyAsync(out, r.p, 8 * n, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipStreamSynchronize(c.s));
+}
+
+}  // namespace das

@@ -1,0 +1,249 @@
+// Device primitives shared by the index build and the query kernels:
+// exclusive scan, stable LSD radix sort (pairs), gather/iota/compaction.
+// All launches go on the caller's stream; nothing here synchronises except
+// the explicit `read_scalar` helper.
+#pragma once
+#include "common.h"
+
+namespace das {
+
+// ---------------------------------------------------------------------------
+// Exclusive scan (wave-level shuffles, 2048 items per 256-thread block)
+// ---------------------------------------------------------------------------
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_scan(T x) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_reduce_sum(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// Per-tile sums.
+template <typename T, typename In>
+__global__ void __launch_bounds__(kScanBlock) k_scan_reduce(In in, uint64_t n, T* tile_sums) {
+  __shared__ T s[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  T acc = 0;
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    if (i < n) acc += (T)in(i);
+  }
+  acc = wave_reduce_sum(acc);
+  if (__lane_id() == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T t = 0;
+    for (int w = 0; w < kScanBlock / 64; ++w) t += s[w];
+    tile_sums[blockIdx.x] = t;
+  }
+}
+
+// Scan each tile with its (already scanned) tile offset.
+template <typename T, typename In>
+__global__ void __launch_bounds__(kScanBlock) k_scan_tiles(In in, uint64_t n, const T* tile_off, T* out) {
+  __shared__ T s_wave[kScanBlock / 64];
+  __shared__ T s_carry;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  const int wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = tile_off ? tile_off[blockIdx.x] : (T)0;
+  __syncthreads();
+  for (int r = 0; r < kScanItems; ++r) {
+    uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    T x = (i < n) ? (T)in(i) : (T)0;
+    T inc = wave_inclusive_scan(x);
+    if (__lane_id() == 63) s_wave[wave] = inc;
+    __syncthreads();
+    T pre = s_carry;
+    for (int w = 0; w < wave; ++w) pre += s_wave[w];
+    if (i < n) out[i] = pre + inc - x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      T t = 0;
+      for (int w = 0; w < kScanBlock / 64; ++w) t += s_wave[w];
+      s_carry += t;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+struct PtrIn {
+  const T* p;
+  __device__ __forceinline__ T operator()(uint64_t i) const { return p[i]; }
+};
+
+// out[i] = sum_{j<i} in(j).  Returns nothing; total = out[n-1] + in(n-1).
+template <typename T, typename In>
+void exclusive_scan_fn(In in, uint64_t n, T* out, hipStream_t s) {
+  if (n == 0) return;
+  uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles == 1) {
+    hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3(1), dim3(kScanBlock), 0, s, in, n, (const T*)nullptr, out);
+    DAS_HIP(hipGetLastError());
+    return;
+  }
+  DBuf<T> sums(tiles, s), offs(tiles, s);
+  hipLaunchKernelGGL((k_scan_reduce<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n, sums.p);
+  DAS_HIP(hipGetLastError());
+  exclusive_scan_fn<T>(PtrIn<T>{sums.p}, tiles, offs.p, s);
+  hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n,
+                     (const T*)offs.p, out);
+  DAS_HIP(hipGetLastError());
+}
+
+template <typename T>
+void exclusive_scan(const T* in, uint64_t n, T* out, hipStream_t s) {
+  exclusive_scan_fn<T>(PtrIn<T>{in}, n, out, s);
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (key, u32 value) pairs, 8-bit digits.
+// Upsweep: per-tile LDS histogram -> digit-major table -> exclusive scan.
+// Downsweep: per 256-key round, lanes with equal digits are matched with
+// 8 wave ballots (rank = popcount of lower peers), waves are prefixed through
+// LDS, so the scatter keeps input order inside each digit (stable).
+// ---------------------------------------------------------------------------
+constexpr int kSortBlock = 256;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kSortBlock * kSortItems;
+
+template <typename K>
+__global__ void __launch_bounds__(kSortBlock) k_radix_hist(const K* keys, uint64_t n, int shift,
+                                                          uint32_t* hist, uint32_t n_tiles) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+#pragma unroll 4
+  for (int r = 0; r < kSortItems; ++r) {
+    uint64_t i = base + (uint64_t)r * kSortBlock + threadIdx.x;
+    if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
+}
+
+template <typename K, bool kHasVals>
+__global__ void __launch_bounds__(kSortBlock) k_radix_scatter(const K* kin, const uint32_t* vin, K* kout,
+                                                             uint32_t* vout, uint64_t n, int shift,
+                                                             const uint32_t* offs, uint32_t n_tiles) {
+  __shared__ uint32_t s_base[256];
+  __shared__ uint32_t s_cnt[kSortBlock / 64][256];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  s_base[tid] = offs[(uint64_t)tid * n_tiles + blockIdx.x];
+#pragma unroll
+  for (int w = 0; w < kSortBlock / 64; ++w) s_cnt[w][tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+  const uint64_t lt = __lanemask_lt();
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
+    const bool valid = i < n;
+    K k = valid ? kin[i] : (K)0;
+    uint32_t v = 0;
+    if (kHasVals && valid) v = vin[i];
+    const uint32_t d = (uint32_t)(k >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = __popcll(peers & lt);
+    if (valid && rank == 0) s_cnt[wave][d] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = s_base[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += s_cnt[w][d];
+      kout[pos] = k;
+      if (kHasVals) vout[pos] = v;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < kSortBlock / 64; ++w) {
+      add += s_cnt[w][tid];
+      s_cnt[w][tid] = 0;
+    }
+    s_base[tid] += add;
+    __syncthreads();
+  }
+}
+
+// Sorts keys[0..n) (and vals alongside, if given) by bits [begin_bit, end_bit).
+// Result lands back in keys/vals.
+template <typename K>
+void radix_sort_pairs(K* keys, uint32_t* vals, uint64_t n, int begin_bit, int end_bit, hipStream_t s) {
+  if (n <= 1 || end_bit <= begin_bit) return;
+  DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "radix sort: more than 2^32 keys");
+  const uint32_t tiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
+  DBuf<K> k2(n, s);
+  DBuf<uint32_t> v2(vals ? n : 0, s);
+  DBuf<uint32_t> hist((uint64_t)tiles * 256, s), offs((uint64_t)tiles * 256, s);
+  K* ka = keys; K* kb = k2.p;
+  uint32_t* va = vals; uint32_t* vb = v2.p;
+  int passes = 0;
+  for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
+    hipLaunchKernelGGL((k_radix_hist<K>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka, n, shift, hist.p, tiles);
+    DAS_HIP(hipGetLastError());
+    exclusive_scan<uint32_t>(hist.p, (uint64_t)tiles * 256, offs.p, s);
+    if (vals)
+      hipLaunchKernelGGL((k_radix_scatter<K, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                         (const uint32_t*)va, kb, vb, n, shift, (const uint32_t*)offs.p, tiles);
+    else
+      hipLaunchKernelGGL((k_radix_scatter<K, false>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                         (const uint32_t*)nullptr, kb, (uint32_t*)nullptr, n, shift, (const uint32_t*)offs.p, tiles);
+    DAS_HIP(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  if (passes & 1) {
+    DAS_HIP(hipMemcpyAsync(keys, ka, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
+    if (vals) DAS_HIP(hipMemcpyAsync(vals, va, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+  }
+}
+
+inline int bits_for(uint64_t max_value) {
+  int b = 0;
+  while (b < 64 && (max_value >> b) != 0) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------------------
+// Small element-wise helpers
+// ---------------------------------------------------------------------------
+__global__ void k_iota(uint32_t* p, uint64_t n);
+__global__ void k_gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t* dst, uint64_t n);
+
+inline void iota(uint32_t* p, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n);
+  DAS_HIP(hipGetLastError());
+}
+inline void gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t* dst, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_gather_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, src, idx, dst, n);
+  DAS_HIP(hipGetLastError());
+}
+
+// Reads one device u64 (or u32) back to the host; synchronises the stream.
+uint64_t read_u64(const uint64_t* d, hipStream_t s);
+uint32_t read_u32(const uint32_t* d, hipStream_t s);
+
+}  // namespace das

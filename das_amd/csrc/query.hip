@@ -1,0 +1,667 @@
+// Query operators over the HBM index: Link / LinkTemplate scans with fused
+// variable assignment, ordered natural join, anti-join, set dedup.
+//
+// Reference semantics (das/pattern_matcher/pattern_matcher.py):
+//   scan      Link.matched :502-538 -> RedisMongoDB.get_matched_links
+//             (redis_mongo_db.py:235-252) -> Link._assign_variables :466-489
+//   template  LinkTemplate.matched :603-614 / _assign_variables :591-601
+//   join      OrderedAssignment.join/_join_ordered/evaluate_compatibility
+//             :105-153 == natural join on the shared variables
+//   antijoin  And.matched :741-746 with OrderedAssignment.check_negation
+//             :112-117 (a row is dropped iff a forbidden mapping is a subset)
+//   dedup     Python set semantics of PatternMatchingAnswer.assignments
+//
+// Kernels are wave64 ballot/popcount compactions; counts go through a
+// per-block two-pass (count -> scan -> write) so output order is the input
+// order (deterministic) and no global atomics sit on the hot path.
+#include <algorithm>
+
+#include "das_internal.h"
+
+namespace das {
+
+__global__ void k_compact_index_q(const uint32_t* flag, const uint32_t* scan, uint64_t n, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[i]) out[scan[i]] = (uint32_t)i;
+}
+
+namespace {
+
+struct WidenCnt {
+  const uint32_t* a;
+  uint64_t n;
+  __device__ uint64_t operator()(uint64_t i) const { return i < n ? (uint64_t)a[i] : 0ull; }
+};
+
+constexpr unsigned B = 256;
+constexpr int kChunkIters = 16;                 // rows per thread per block chunk
+constexpr uint64_t kChunk = (uint64_t)B * kChunkIters;
+inline dim3 G(uint64_t n) { return dim3(grid_for(n, B)); }
+
+struct ColSet {
+  const uint32_t* c[kMaxCols];
+  int n;
+};
+
+// ---------------------------------------------------------------------------
+// Scan spec (device, by value)
+// ---------------------------------------------------------------------------
+struct ScanSpec {
+  const uint32_t* col[kMaxArity + 1];  // col[0] = link id, col[1+k] = target k
+  uint32_t arity;
+  uint32_t fixed[kMaxArity];           // kNone = no filter
+  int32_t outpos[kMaxCols];            // ordered: source position of out col (-1 link)
+  uint32_t nout;
+  uint32_t eq_a[kMaxArity], eq_b[kMaxArity], neq;
+  uint32_t no_overload;
+  uint32_t unordered;
+  uint32_t upos[kMaxArity], nupos;     // unordered: wildcard positions
+  uint32_t emit_link;
+  uint32_t all_keep;                   // no predicate at all (pure projection)
+};
+
+__device__ __forceinline__ bool scan_keep(const ScanSpec& sp, uint64_t r) {
+  if (sp.all_keep) return true;
+  for (uint32_t p = 0; p < sp.arity; ++p)
+    if (sp.fixed[p] != kNone && sp.col[1 + p][r] != sp.fixed[p]) return false;
+  for (uint32_t e = 0; e < sp.neq; ++e)
+    if (sp.col[1 + sp.eq_a[e]][r] != sp.col[1 + sp.eq_b[e]][r]) return false;
+  if (sp.unordered) {
+    for (uint32_t i = 0; i < sp.nupos; ++i)
+      for (uint32_t j = i + 1; j < sp.nupos; ++j)
+        if (sp.col[1 + sp.upos[i]][r] == sp.col[1 + sp.upos[j]][r]) return false;
+  } else if (sp.no_overload) {
+    const uint32_t base = sp.emit_link ? 1 : 0;
+    for (uint32_t i = base; i < sp.nout; ++i)
+      for (uint32_t j = i + 1; j < sp.nout; ++j)
+        if (sp.col[1 + sp.outpos[i]][r] == sp.col[1 + sp.outpos[j]][r]) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ void scan_emit(const ScanSpec& sp, uint64_t r, uint32_t* out, uint64_t cap, uint64_t pos) {
+  if (!sp.unordered) {
+    for (uint32_t c = 0; c < sp.nout; ++c) out[c * cap + pos] = sp.col[1 + sp.outpos[c]][r];
+    return;
+  }
+  uint32_t c0 = 0;
+  if (sp.emit_link) { out[pos] = sp.col[0][r]; c0 = 1; }
+  uint32_t v[kMaxArity];
+  for (uint32_t i = 0; i < sp.nupos; ++i) v[i] = sp.col[1 + sp.upos[i]][r];
+  for (uint32_t i = 1; i < sp.nupos; ++i) {       // insertion sort, <= 8 values
+    uint32_t x = v[i];
+    int j = (int)i - 1;
+    while (j >= 0 && v[j] > x) { v[j + 1] = v[j]; --j; }
+    v[j + 1] = x;
+  }
+  for (uint32_t i = 0; i < sp.nupos; ++i) out[(c0 + i) * cap + pos] = v[i];
+}
+
+__global__ void __launch_bounds__(B) k_scan_count(ScanSpec sp, uint64_t begin, uint64_t end, uint32_t* chunk_cnt) {
+  __shared__ uint32_t s_w[B / 64];
+  const uint64_t cb = begin + (uint64_t)blockIdx.x * kChunk;
+  uint32_t cnt = 0;
+  for (int it = 0; it < kChunkIters; ++it) {
+    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
+    if (r < end && scan_keep(sp, r)) ++cnt;
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (__lane_id() == 0) s_w[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ void __launch_bounds__(B) k_scan_write(ScanSpec sp, uint64_t begin, uint64_t end, const uint32_t* chunk_off,
+                                                  uint32_t* out, uint64_t cap) {
+  __shared__ uint32_t s_w[B / 64];
+  __shared__ uint32_t s_run;
+  const uint64_t cb = begin + (uint64_t)blockIdx.x * kChunk;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t lt = __lanemask_lt();
+  if (threadIdx.x == 0) s_run = chunk_off ? chunk_off[blockIdx.x] : (uint32_t)(cb - begin);
+  __syncthreads();
+  for (int it = 0; it < kChunkIters; ++it) {
+    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
+    const bool keep = r < end && scan_keep(sp, r);
+    const uint64_t m = __ballot(keep);
+    if (__lane_id() == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t pos = s_run + __popcll(m & lt);
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+    if (keep) scan_emit(sp, r, out, cap, pos);
+    __syncthreads();
+    if (threadIdx.x == 0) s_run += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+}
+
+// Range lookup in a P_{a,p} key array: [lower_bound(lo), lower_bound(hi)) -> rows.
+__global__ void k_key_ranges(const uint64_t* ukey, const uint64_t* uoff, uint64_t nkeys, const uint64_t* qlo,
+                             const uint64_t* qhi, uint32_t nq, uint64_t* out) {
+  const uint32_t i = threadIdx.x;
+  if (i >= 2 * nq) return;
+  const uint64_t q = (i & 1) ? qhi[i >> 1] : qlo[i >> 1];
+  uint64_t lo = 0, hi = nkeys;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (ukey[mid] < q) lo = mid + 1; else hi = mid;
+  }
+  out[i] = uoff[lo];
+}
+
+// ---------------------------------------------------------------------------
+// Join / antijoin / dedup helpers
+// ---------------------------------------------------------------------------
+
+// Lexicographic compare of row i of A-cols against row j of B-cols.
+__device__ __forceinline__ int cmp_rows(const ColSet& a, uint64_t i, const ColSet& b, uint64_t j) {
+  for (int c = 0; c < a.n; ++c) {
+    const uint32_t x = a.c[c][i], y = b.c[c][j];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ uint64_t lower_bound_rows(const ColSet& probe, uint64_t i, const ColSet& sorted, uint64_t n) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (cmp_rows(sorted, mid, probe, i) < 0) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint64_t upper_bound_rows(const ColSet& probe, uint64_t i, const ColSet& sorted, uint64_t n) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (cmp_rows(sorted, mid, probe, i) <= 0) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_join_count(ColSet probe_key, uint64_t np, ColSet build_key, uint64_t nb, uint32_t* lo_out,
+                             uint32_t* cnt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t lo = lower_bound_rows(probe_key, i, build_key, nb);
+    uint64_t hi = lo;
+    if (lo < nb && cmp_rows(build_key, lo, probe_key, i) == 0) hi = upper_bound_rows(probe_key, i, build_key, nb);
+    lo_out[i] = (uint32_t)lo;
+    cnt[i] = (uint32_t)(hi - lo);
+  }
+}
+
+// Output column sources: src[c] = (side, column) ; side 0 probe, 1 build
+struct OutMap {
+  const uint32_t* col[kMaxCols];
+  uint8_t side[kMaxCols];
+  int n;
+};
+
+__global__ void k_join_expand(const uint64_t* offs, uint64_t np, const uint32_t* lo, OutMap om, uint64_t total,
+                              uint32_t* out, uint64_t cap) {
+  for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < total; o += (uint64_t)gridDim.x * blockDim.x) {
+    // i = upper_bound(offs, o) - 1
+    uint64_t a = 0, b = np;
+    while (a < b) {
+      const uint64_t mid = (a + b) >> 1;
+      if (offs[mid] <= o) a = mid + 1; else b = mid;
+    }
+    const uint64_t i = a - 1;
+    const uint64_t j = lo[i] + (o - offs[i]);
+    for (int c = 0; c < om.n; ++c) out[(uint64_t)c * cap + o] = om.side[c] ? om.col[c][j] : om.col[c][i];
+  }
+}
+
+__global__ void k_cartesian(OutMap om, uint64_t nb, uint64_t total, uint32_t* out, uint64_t cap) {
+  for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < total; o += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = o / nb, j = o - i * nb;
+    for (int c = 0; c < om.n; ++c) out[(uint64_t)c * cap + o] = om.side[c] ? om.col[c][j] : om.col[c][i];
+  }
+}
+
+// keep[i] = 0 if a matching row exists in `sorted`
+__global__ void k_anti_flags(ColSet probe, uint64_t np, ColSet sorted, uint64_t ns, uint32_t* keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t lo = lower_bound_rows(probe, i, sorted, ns);
+    keep[i] = !(lo < ns && cmp_rows(sorted, lo, probe, i) == 0);
+  }
+}
+
+__global__ void k_distinct_flags(ColSet sorted, uint64_t n, uint32_t* keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    keep[i] = (i == 0) || cmp_rows(sorted, i - 1, sorted, i) != 0;
+}
+
+// no_overload filter on join output: distinct vars must have distinct values
+__global__ void k_overload_flags(ColSet t, uint64_t n, uint32_t* keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t k = 1;
+    for (int a = 0; a < t.n && k; ++a)
+      for (int b = a + 1; b < t.n; ++b)
+        if (t.c[a][i] == t.c[b][i]) { k = 0; break; }
+    keep[i] = k;
+  }
+}
+
+__global__ void k_gather_cols(ColSet src, const uint32_t* idx, uint64_t n, uint32_t* out, uint64_t cap) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = idx[i];
+    for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + i] = src.c[c][r];
+  }
+}
+
+ColSet cols_of(const Table& t) {
+  ColSet s{};
+  s.n = t.ncols;
+  for (int c = 0; c < t.ncols; ++c) s.c[c] = t.col(c);
+  return s;
+}
+
+// perm sorted by the given columns (LSD, stable).
+void sort_perm(const ColSet& cs, uint64_t n, uint32_t* perm, int bits, hipStream_t s) {
+  iota(perm, n, s);
+  if (n <= 1) return;
+  DBuf<uint32_t> key(n, s);
+  for (int c = cs.n - 1; c >= 0; --c) {
+    gather_u32(cs.c[c], perm, key.p, n, s);
+    radix_sort_pairs<uint32_t>(key.p, perm, n, 0, bits > 0 ? bits : 1, s);
+  }
+}
+
+int id_bits(const Ctx& c) { return bits_for(c.idx.n_atoms ? c.idx.n_atoms - 1 : 0); }
+
+// Gathers rows idx[0..m) of table `a` into a new table (same schema).
+std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx, uint64_t m) {
+  auto t = new_table(c, a.kind, a.ncols, a.vars, m);
+  t->nrows = m;
+  if (m && a.ncols) {
+    hipLaunchKernelGGL(k_gather_cols, G(m), dim3(B), 0, c.s, cols_of(a), idx, m, t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return t;
+}
+
+// keep flags -> compacted table
+std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep) {
+  const uint64_t n = a.nrows;
+  if (!n) return gather_table(c, a, nullptr, 0);
+  DBuf<uint32_t> scan(n, c.s);
+  exclusive_scan<uint32_t>(keep, n, scan.p, c.s);
+  uint32_t h[2];
+  DAS_HIP(hipMemcpyAsync(&h[0], scan.p + n - 1, 4, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipMemcpyAsync(&h[1], keep + n - 1, 4, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipStreamSynchronize(c.s));
+  const uint64_t m = (uint64_t)h[0] + h[1];
+  if (m == n) {   // nothing dropped: copy
+    auto t = new_table(c, a.kind, a.ncols, a.vars, n);
+    t->nrows = n;
+    for (int k = 0; k < a.ncols; ++k)
+      DAS_HIP(hipMemcpyAsync(t->col(k), a.col(k), 4 * n, hipMemcpyDeviceToDevice, c.s));
+    return t;
+  }
+  DBuf<uint32_t> idx(m ? m : 1, c.s);
+  hipLaunchKernelGGL(k_compact_index_q, G(n), dim3(B), 0, c.s, keep, (const uint32_t*)scan.p, n, idx.p);
+  DAS_HIP(hipGetLastError());
+  return gather_table(c, a, idx.p, m);
+}
+
+}  // namespace
+
+std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap) {
+  DAS_CHECK(ncols >= 0 && ncols <= kMaxCols, DAS_E_UNSUPPORTED, "too many columns in a binding table");
+  auto t = std::make_unique<Table>();
+  t->kind = kind;
+  t->ncols = ncols;
+  for (int i = 0; i < ncols; ++i) t->vars[i] = vars ? vars[i] : 0;
+  t->s = c.s;
+  t->cap = cap ? cap : 1;
+  if (ncols) DAS_HIP(hipMallocAsync((void**)&t->data, 4ull * ncols * t->cap, c.s));
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Scans
+// ---------------------------------------------------------------------------
+namespace {
+
+std::unique_ptr<Table> run_scan(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t end, int kind, int ncols,
+                                const int32_t* vars) {
+  const uint64_t n = end > begin ? end - begin : 0;
+  if (!n) return new_table(c, kind, ncols, vars, 0);
+  const uint64_t chunks = (n + kChunk - 1) / kChunk;
+  DAS_CHECK(chunks < (1ull << 31), DAS_E_UNSUPPORTED, "scan range too large");
+  if (sp.all_keep) {
+    auto t = new_table(c, kind, ncols, vars, n);
+    t->nrows = n;
+    if (!sp.unordered) {   // pure projection: column copies
+      for (uint32_t k = 0; k < sp.nout; ++k)
+        DAS_HIP(hipMemcpyAsync(t->col(k), sp.col[1 + sp.outpos[k]] + begin, 4 * n, hipMemcpyDeviceToDevice, c.s));
+      return t;
+    }
+    hipLaunchKernelGGL(k_scan_write, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, (const uint32_t*)nullptr,
+                       t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+    return t;
+  }
+  DBuf<uint32_t> cnt(chunks, c.s), off(chunks, c.s);
+  hipLaunchKernelGGL(k_scan_count, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, cnt.p);
+  DAS_HIP(hipGetLastError());
+  exclusive_scan<uint32_t>(cnt.p, chunks, off.p, c.s);
+  uint32_t h[2];
+  DAS_HIP(hipMemcpyAsync(&h[0], off.p + chunks - 1, 4, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipMemcpyAsync(&h[1], cnt.p + chunks - 1, 4, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipStreamSynchronize(c.s));
+  const uint64_t m = (uint64_t)h[0] + h[1];
+  auto t = new_table(c, kind, ncols, vars, m);
+  t->nrows = m;
+  if (m) {
+    hipLaunchKernelGGL(k_scan_write, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, (const uint32_t*)off.p,
+                       t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return t;
+}
+
+void set_cols(ScanSpec& sp, const RowTable& rt) {
+  for (int k = 0; k <= rt.arity; ++k) sp.col[k] = rt.col(k);
+  // ScanSpec reads col[1 + p]; col[0] is the link id
+}
+
+}  // namespace
+
+std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
+  Index& idx = c.idx;
+  DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
+  const uint32_t ar = q.arity;
+  DAS_CHECK(ar <= 8, DAS_E_INVALID, "arity > 8");
+  // output schema
+  int32_t vars[kMaxCols];
+  int ncols = 0;
+  ScanSpec sp{};
+  sp.arity = ar;
+  sp.no_overload = q.no_overload;
+  sp.emit_link = q.emit_link;
+  sp.unordered = q.ordered ? 0 : 1;
+  int kind = q.ordered ? DAS_TABLE_ORDERED : DAS_TABLE_UNORDERED;
+  bool any_wild = false;
+  for (uint32_t p = 0; p < ar; ++p) {
+    sp.fixed[p] = q.target[p];
+    if (q.target[p] == kNone) any_wild = true;
+  }
+  if (q.emit_link) { vars[ncols] = -1; sp.outpos[ncols] = -1; ++ncols; }
+  if (q.ordered) {
+    // distinct variables in ascending id order; repeated ones -> equality constraints
+    int32_t first_pos[64];
+    for (int i = 0; i < 64; ++i) first_pos[i] = -1;
+    std::vector<std::pair<int32_t, uint32_t>> vp;
+    for (uint32_t p = 0; p < ar; ++p)
+      if (q.var[p] >= 0) vp.push_back({q.var[p], p});
+    std::sort(vp.begin(), vp.end());
+    for (size_t i = 0; i < vp.size(); ++i) {
+      if (i > 0 && vp[i].first == vp[i - 1].first) {
+        sp.eq_a[sp.neq] = vp[i - 1].second;
+        sp.eq_b[sp.neq] = vp[i].second;
+        ++sp.neq;
+        continue;
+      }
+      DAS_CHECK(ncols < kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
+      vars[ncols] = vp[i].first;
+      sp.outpos[ncols] = (int32_t)vp[i].second;
+      ++ncols;
+    }
+    sp.nout = ncols;
+  } else {
+    for (uint32_t p = 0; p < ar; ++p)
+      if (q.target[p] == kNone) sp.upos[sp.nupos++] = p;
+    std::vector<int32_t> vs(q.var, q.var + q.n_vars);
+    std::sort(vs.begin(), vs.end());
+    for (int32_t v : vs) vars[ncols++] = v;
+    DAS_CHECK(sp.nupos == q.n_vars, DAS_E_INVALID, "unordered scan: variables != wildcard positions");
+    sp.nout = ncols;
+  }
+  auto empty = [&]() { return new_table(c, kind, ncols, vars, 0); };
+  if (ar == 0 || ar > (uint32_t)kMaxArity || idx.ttab[ar].rows == 0) return empty();
+  if (q.type_id != kNone && q.type_id >= idx.n_types) return empty();
+  // Families the reference indexes (canonical_parser.py:144-178)
+  if (ar > (uint32_t)kMaxPosArity) {
+    if (q.type_id != kNone || any_wild) return empty();   // only [*, e0..en]
+  }
+  uint64_t begin = 0, end = 0;
+  const RowTable* rt = nullptr;
+  std::vector<uint32_t> grounded;
+  for (uint32_t p = 0; p < ar; ++p)
+    if (q.target[p] != kNone) grounded.push_back(p);
+  if (grounded.empty() || ar > (uint32_t)kMaxPosArity) {
+    rt = &idx.ttab[ar];
+    if (q.type_id == kNone) { begin = 0; end = rt->rows; }
+    else { begin = idx.type_off[ar][q.type_id]; end = idx.type_off[ar][q.type_id + 1]; }
+  } else {
+    // smallest P_{a,p} range among the grounded positions
+    uint64_t best = ~0ull;
+    for (uint32_t p : grounded) {
+      const PosIndex& P = idx.pidx[ar][p];
+      if (!P.nkeys) return empty();
+      const uint64_t t = q.target[p];
+      uint64_t qlo = (t << kTypeBits) | (q.type_id == kNone ? 0 : q.type_id);
+      uint64_t qhi = q.type_id == kNone ? ((t + 1) << kTypeBits) : qlo + 1;
+      DBuf<uint64_t> dq(2, c.s), dr(2, c.s);
+      uint64_t hq[2] = {qlo, qhi};
+      DAS_HIP(hipMemcpyAsync(dq.p, hq, 16, hipMemcpyHostToDevice, c.s));
+      hipLaunchKernelGGL(k_key_ranges, dim3(1), dim3(64), 0, c.s, (const uint64_t*)P.ukey, (const uint64_t*)P.uoff,
+                         P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + 1, 1u, dr.p);
+      DAS_HIP(hipGetLastError());
+      uint64_t hr[2];
+      DAS_HIP(hipMemcpyAsync(hr, dr.p, 16, hipMemcpyDeviceToHost, c.s));
+      DAS_HIP(hipStreamSynchronize(c.s));
+      if (hr[1] - hr[0] < best) {
+        best = hr[1] - hr[0];
+        begin = hr[0];
+        end = hr[1];
+        rt = &P.t;
+        // this position's filter is implied by the range
+        for (uint32_t pp = 0; pp < ar; ++pp) sp.fixed[pp] = q.target[pp];
+        sp.fixed[p] = kNone;
+      }
+      if (best == 0) return empty();
+    }
+  }
+  set_cols(sp, *rt);
+  bool filt = false;
+  for (uint32_t p = 0; p < ar; ++p) filt |= sp.fixed[p] != kNone;
+  sp.all_keep = !filt && sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
+  return run_scan(c, sp, begin, end, kind, ncols, vars);
+}
+
+std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
+  Index& idx = c.idx;
+  DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
+  DAS_CHECK(q.ctype_id < idx.ctype_range.size(), DAS_E_INVALID, "bad ctype id");
+  const CtypeRange& cr = idx.ctype_range[q.ctype_id];
+  DAS_CHECK(q.arity == cr.arity, DAS_E_INVALID, "template arity mismatch");
+  ScanSpec sp{};
+  sp.arity = cr.arity;
+  for (uint32_t p = 0; p < cr.arity; ++p) sp.fixed[p] = kNone;
+  sp.no_overload = q.no_overload;
+  sp.emit_link = q.emit_link;
+  sp.unordered = q.ordered ? 0 : 1;
+  int32_t vars[kMaxCols];
+  int ncols = 0;
+  if (q.emit_link) { vars[ncols] = -1; sp.outpos[ncols] = -1; ++ncols; }
+  if (q.ordered) {
+    std::vector<std::pair<int32_t, uint32_t>> vp;
+    for (uint32_t p = 0; p < cr.arity; ++p) vp.push_back({q.var[p], p});
+    std::sort(vp.begin(), vp.end());
+    for (size_t i = 0; i < vp.size(); ++i) {
+      if (i > 0 && vp[i].first == vp[i - 1].first) {
+        sp.eq_a[sp.neq] = vp[i - 1].second;
+        sp.eq_b[sp.neq] = vp[i].second;
+        ++sp.neq;
+        continue;
+      }
+      vars[ncols] = vp[i].first;
+      sp.outpos[ncols] = (int32_t)vp[i].second;
+      ++ncols;
+    }
+  } else {
+    std::vector<int32_t> vs(q.var, q.var + cr.arity);
+    std::sort(vs.begin(), vs.end());
+    for (int32_t v : vs) vars[ncols++] = v;
+    for (uint32_t p = 0; p < cr.arity; ++p) sp.upos[sp.nupos++] = p;
+  }
+  sp.nout = ncols;
+  const int kind = q.ordered ? DAS_TABLE_ORDERED : DAS_TABLE_UNORDERED;
+  set_cols(sp, idx.ctab[cr.arity]);
+  sp.all_keep = sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
+  return run_scan(c, sp, cr.begin, cr.end, kind, ncols, vars);
+}
+
+// ---------------------------------------------------------------------------
+// Join, antijoin, dedup, concat
+// ---------------------------------------------------------------------------
+std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {
+  DAS_CHECK(A.kind == DAS_TABLE_ORDERED && Bt.kind == DAS_TABLE_ORDERED, DAS_E_UNSUPPORTED,
+            "join: unordered operands are not supported by this build");
+  // schemas
+  std::vector<int32_t> va(A.vars, A.vars + A.ncols), vb(Bt.vars, Bt.vars + Bt.ncols), shared, uni;
+  std::set_intersection(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(shared));
+  std::set_union(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(uni));
+  DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
+  auto colof = [](const Table& t, int32_t v) {
+    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+    return -1;
+  };
+  const int nu = (int)uni.size();
+  if (A.nrows == 0 || Bt.nrows == 0) return new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), 0);
+  // probe = larger side, build = smaller (sorted)
+  const bool a_probe = A.nrows >= Bt.nrows;
+  const Table& P = a_probe ? A : Bt;
+  const Table& Q = a_probe ? Bt : A;
+  std::unique_ptr<Table> out;
+  if (shared.empty()) {
+    const uint64_t total = P.nrows * Q.nrows;
+    out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
+    out->nrows = total;
+    OutMap om{};
+    om.n = nu;
+    for (int k = 0; k < nu; ++k) {
+      int ip = colof(P, uni[k]);
+      if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
+      else { om.col[k] = Q.col(colof(Q, uni[k])); om.side[k] = 1; }
+    }
+    hipLaunchKernelGGL(k_cartesian, G(total), dim3(B), 0, c.s, om, Q.nrows, total, out->data, out->cap);
+    DAS_HIP(hipGetLastError());
+  } else {
+    // sort build rows by the shared columns
+    ColSet qk{};
+    qk.n = (int)shared.size();
+    for (int k = 0; k < qk.n; ++k) qk.c[k] = Q.col(colof(Q, shared[k]));
+    DBuf<uint32_t> perm(Q.nrows, c.s);
+    sort_perm(qk, Q.nrows, perm.p, id_bits(c), c.s);
+    auto Qs = gather_table(c, Q, perm.p, Q.nrows);
+    perm.release();
+    ColSet qks{}, pk{};
+    qks.n = pk.n = (int)shared.size();
+    for (int k = 0; k < qks.n; ++k) {
+      qks.c[k] = Qs->col(colof(*Qs, shared[k]));
+      pk.c[k] = P.col(colof(P, shared[k]));
+    }
+    DBuf<uint32_t> lo(P.nrows, c.s), cnt(P.nrows, c.s);
+    DBuf<uint64_t> offs(P.nrows + 1, c.s);
+    hipLaunchKernelGGL(k_join_count, G(P.nrows), dim3(B), 0, c.s, pk, P.nrows, qks, Qs->nrows, lo.p, cnt.p);
+    DAS_HIP(hipGetLastError());
+    exclusive_scan_fn<uint64_t>(WidenCnt{cnt.p, P.nrows}, P.nrows + 1, offs.p, c.s);
+    const uint64_t total = read_u64(offs.p + P.nrows, c.s);
+    out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
+    out->nrows = total;
+    if (total) {
+      OutMap om{};
+      om.n = nu;
+      for (int k = 0; k < nu; ++k) {
+        int ip = colof(P, uni[k]);
+        if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
+        else { om.col[k] = Qs->col(colof(*Qs, uni[k])); om.side[k] = 1; }
+      }
+      hipLaunchKernelGGL(k_join_expand, G(total), dim3(B), 0, c.s, (const uint64_t*)offs.p, P.nrows,
+                         (const uint32_t*)lo.p, om, total, out->data, out->cap);
+      DAS_HIP(hipGetLastError());
+    }
+  }
+  if (no_overload && out->nrows) {
+    // _join_ordered NO_COVERING path re-assigns every value (pattern_matcher.py:128-137);
+    // covering joins return an operand unchanged.
+    const bool a_sub = std::includes(vb.begin(), vb.end(), va.begin(), va.end());
+    const bool b_sub = std::includes(va.begin(), va.end(), vb.begin(), vb.end());
+    if (!a_sub && !b_sub) {
+      DBuf<uint32_t> keep(out->nrows, c.s);
+      hipLaunchKernelGGL(k_overload_flags, G(out->nrows), dim3(B), 0, c.s, cols_of(*out), out->nrows, keep.p);
+      DAS_HIP(hipGetLastError());
+      out = compact_table(c, *out, keep.p);
+    }
+  }
+  return out;
+}
+
+std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
+  DAS_CHECK(A.kind == T.kind, DAS_E_UNSUPPORTED, "antijoin: mixed ordered/unordered operands");
+  std::vector<int32_t> va(A.vars, A.vars + A.ncols), vt(T.vars, T.vars + T.ncols);
+  const bool covered = std::includes(va.begin(), va.end(), vt.begin(), vt.end());
+  if (A.kind == DAS_TABLE_UNORDERED) DAS_CHECK(va == vt, DAS_E_UNSUPPORTED, "antijoin: unordered containment");
+  if (!covered || T.nrows == 0 || A.nrows == 0) {
+    DBuf<uint32_t> idx(A.nrows ? A.nrows : 1, c.s);
+    iota(idx.p, A.nrows, c.s);
+    return gather_table(c, A, idx.p, A.nrows);
+  }
+  auto colof = [](const Table& t, int32_t v) {
+    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+    return -1;
+  };
+  ColSet tk = cols_of(T);
+  DBuf<uint32_t> perm(T.nrows, c.s);
+  sort_perm(tk, T.nrows, perm.p, id_bits(c), c.s);
+  auto Ts = gather_table(c, T, perm.p, T.nrows);
+  ColSet tks = cols_of(*Ts), ak{};
+  ak.n = T.ncols;
+  for (int k = 0; k < T.ncols; ++k) ak.c[k] = A.col(A.kind == DAS_TABLE_ORDERED ? colof(A, T.vars[k]) : k);
+  DBuf<uint32_t> keep(A.nrows, c.s);
+  hipLaunchKernelGGL(k_anti_flags, G(A.nrows), dim3(B), 0, c.s, ak, A.nrows, tks, Ts->nrows, keep.p);
+  DAS_HIP(hipGetLastError());
+  return compact_table(c, A, keep.p);
+}
+
+std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
+  if (A.nrows <= 1) {
+    DBuf<uint32_t> idx(A.nrows ? A.nrows : 1, c.s);
+    iota(idx.p, A.nrows, c.s);
+    return gather_table(c, A, idx.p, A.nrows);
+  }
+  DBuf<uint32_t> perm(A.nrows, c.s);
+  sort_perm(cols_of(A), A.nrows, perm.p, id_bits(c), c.s);
+  auto S = gather_table(c, A, perm.p, A.nrows);
+  DBuf<uint32_t> keep(A.nrows, c.s);
+  hipLaunchKernelGGL(k_distinct_flags, G(A.nrows), dim3(B), 0, c.s, cols_of(*S), A.nrows, keep.p);
+  DAS_HIP(hipGetLastError());
+  return compact_table(c, *S, keep.p);
+}
+
+std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {
+  DAS_CHECK(n >= 1, DAS_E_INVALID, "concat of nothing");
+  const Table& f = *ts[0];
+  uint64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    DAS_CHECK(ts[i]->kind == f.kind && ts[i]->ncols == f.ncols, DAS_E_INVALID, "concat: schema mismatch");
+    for (int k = 0; k < f.ncols; ++k) DAS_CHECK(ts[i]->vars[k] == f.vars[k], DAS_E_INVALID, "concat: schema mismatch");
+    total += ts[i]->nrows;
+  }
+  auto t = new_table(c, f.kind, f.ncols, f.vars, total);
+  t->nrows = total;
+  uint64_t o = 0;
+  for (int i = 0; i < n; ++i) {
+    for (int k = 0; k < f.ncols; ++k)
+      if (ts[i]->nrows)
+        DAS_HIP(hipMemcpyAsync(t->col(k) + o, ts[i]->col(k), 4 * ts[i]->nrows, hipMemcpyDeviceToDevice, c.s));
+    o += ts[i]->nrows;
+  }
+  return t;
+}
+
+}  // namespace das

@@ -1,0 +1,394 @@
+"""HipDB — the DBInterface backed by the MI355X HBM index.
+
+Drop-in for the reference's production adapter `RedisMongoDB`
+(das/database/redis_mongo_db.py:49-335): the same methods, argument meaning,
+return formats and exceptions, with the Redis pattern/template sets and the
+Mongo collections replaced by the device index that `das_build_index` builds
+(include/das_mi355x.h).  Method docstrings cite the reference method each one
+replaces.
+
+Two extra, non-reference entry points feed the pattern matcher without
+materialising Python tuples: `match_link` and `match_template` return device
+binding tables (`Relation`).
+"""
+import re
+from typing import Any, List, Tuple
+
+import numpy as np
+
+from .. import _lib
+from .. import loader as _loader
+from ..expression_hasher import ExpressionHasher
+from .db_interface import UNORDERED_LINK_TYPES, WILDCARD, DBInterface
+
+
+class Relation:
+    """A set of assignments held on the GPU: device tables, one per schema
+    (kind, variable ids).  Rows of one table are distinct."""
+
+    __slots__ = ("tables",)
+
+    def __init__(self, tables=()):
+        self.tables = [t for t in tables if t is not None and t.nrows > 0]
+
+    @property
+    def nrows(self):
+        return sum(t.nrows for t in self.tables)
+
+    def __bool__(self):
+        return self.nrows > 0
+
+    def __len__(self):
+        return self.nrows
+
+
+class HipDB(DBInterface):
+
+    def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False):
+        """`tuple_targets=True` reproduces the reference DB path exactly,
+        including returning targets as tuples from get_matched_links, which
+        makes `Link._assign_variables` raise AttributeError for unordered links
+        with a grounded target.  The default returns lists (the
+        semantics StubDB and service/README.md:356-363 show)."""
+        if stream is None:
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    torch.cuda.set_device(device)
+                    stream = torch.cuda.current_stream(device).cuda_stream
+            except ImportError:
+                stream = None
+        self.ctx = _lib.Context(device, stream)
+        self.tuple_targets = tuple_targets
+        self.arrays = None
+        self.type_id = {}
+        self._hex_cache = {}
+        self._mirror = None
+        self.pattern_black_list = []
+
+    def __repr__(self):
+        return "<HipDB>"
+
+    # ------------------------------------------------------------------ load
+    def load_arrays(self, arrays: "_loader.AtomArrays"):
+        """Hash + intern + index every atom on the GPU (replaces the Mongo
+        insert / key-value files / Redis SADD of canonical_parser.py:111-240)."""
+        self.ctx.build_index(arrays)
+        self.arrays = arrays
+        self.type_id = dict(arrays.type_id)
+        self._hex_cache = {}
+        self._mirror = None
+
+    def load_metta(self, texts):
+        self.load_arrays(_loader.parse_metta(texts).finish())
+
+    def load_canonical(self, texts):
+        self.load_arrays(_loader.parse_canonical(texts).finish())
+
+    def clear(self):
+        b = _loader.AtomBuilder()
+        self.load_arrays(b.finish())
+
+    def stats(self):
+        return self.ctx.stats()
+
+    # --------------------------------------------------------------- helpers
+    def ids_of(self, handles: List[str]) -> np.ndarray:
+        if not handles:
+            return np.zeros(0, dtype=np.int64)
+        dig = np.stack([_lib.hex_to_digest(h) for h in handles])
+        ids, _, _, _ = self.ctx.lookup(dig)
+        return ids
+
+    def _lookup(self, handle):
+        try:
+            dig = _lib.hex_to_digest(handle)
+        except ValueError:
+            return -1, 0, 0
+        ids, cat, ar, _ = self.ctx.lookup(dig.reshape(1, 4))
+        return int(ids[0]), int(cat[0]), int(ar[0])
+
+    def hex_of(self, ids) -> List[str]:
+        ids = np.asarray(ids, dtype=np.uint32).ravel()
+        if ids.size == 0:
+            return []
+        uniq = np.unique(ids)
+        missing = [int(i) for i in uniq if int(i) not in self._hex_cache]
+        if missing:
+            dig, _, _, _, _ = self.ctx.atoms_info(np.array(missing, dtype=np.uint32))
+            for i, h in zip(missing, _lib.digests_to_hex(dig)):
+                self._hex_cache[i] = h
+        return [self._hex_cache[int(i)] for i in ids]
+
+    def _host_mirror(self):
+        """Host copy of per-atom category/type/name leaf (metadata calls only)."""
+        if self._mirror is None:
+            n = int(self.ctx.stats().n_atoms)
+            ids = np.arange(n, dtype=np.uint32)
+            dig, cat, ar, ty, nl = self.ctx.atoms_info(ids)
+            self._mirror = (dig, cat, ar, ty, nl)
+        return self._mirror
+
+    def _atom_type_ok(self, name):
+        return name in self.type_id
+
+    def _exists(self, handle, arity):
+        """_retrieve_mongo_document(handle, arity) is not None (redis_mongo_db.py:129-145)."""
+        aid, cat, ar = self._lookup(handle)
+        if aid < 0:
+            return False
+        if arity == 0:
+            return cat == 1
+        if cat != 2:
+            return False
+        if arity == 1:
+            return ar == 1
+        if arity == 2:
+            return ar == 2
+        return ar not in (1, 2)
+
+    def _fmt_targets(self, targets):
+        return tuple(targets) if self.tuple_targets else list(targets)
+
+    # ------------------------------------------------- DBInterface (reference)
+    def node_exists(self, node_type: str, node_name: str) -> bool:
+        """redis_mongo_db.py:204-208"""
+        return self._exists(ExpressionHasher.terminal_hash(node_type, node_name), 0)
+
+    def link_exists(self, link_type: str, target_handles: List[str]) -> bool:
+        """redis_mongo_db.py:210-213 (no sorting for unordered types, as the reference)"""
+        h = ExpressionHasher.expression_hash(ExpressionHasher.named_type_hash(link_type), target_handles)
+        return self._exists(h, len(target_handles))
+
+    def get_node_handle(self, node_type: str, node_name: str) -> str:
+        """redis_mongo_db.py:215-216"""
+        return ExpressionHasher.terminal_hash(node_type, node_name)
+
+    def get_link_handle(self, link_type: str, target_handles: List[str]) -> str:
+        """redis_mongo_db.py:218-220"""
+        return ExpressionHasher.expression_hash(ExpressionHasher.named_type_hash(link_type), target_handles)
+
+    def get_link_targets(self, link_handle: str) -> List[str]:
+        """redis_mongo_db.py:222-227: the outgoing set.  Redis returns a set, so
+        order and repeats are not preserved there; here the stored order is
+        returned (a superset of what the reference guarantees)."""
+        aid, cat, _ = self._lookup(link_handle)
+        if aid < 0 or cat != 2:
+            raise ValueError(f"Invalid handle: {link_handle}")
+        return self.hex_of(self.ctx.link_targets(aid))
+
+    def is_ordered(self, link_handle: str) -> bool:
+        """redis_mongo_db.py:229-233"""
+        aid, cat, _ = self._lookup(link_handle)
+        if aid < 0 or cat != 2:
+            raise ValueError(f"Invalid handle: {link_handle}")
+        return True
+
+    def get_matched_links(self, link_type: str, target_handles: List[str]):
+        """redis_mongo_db.py:235-252: grounded -> [handle] / []; otherwise the
+        pattern key (sorted targets for Similarity/Set) -> [(handle, targets)]."""
+        if link_type != WILDCARD and WILDCARD not in target_handles:
+            h = self.get_link_handle(link_type, target_handles)
+            return [h] if self._exists(h, len(target_handles)) else []
+        if link_type in UNORDERED_LINK_TYPES:
+            target_handles = sorted(target_handles)
+        arity = len(target_handles)
+        ttype = self._type_or_empty(link_type)
+        if ttype is False:
+            return []
+        tids = self._target_ids(target_handles)
+        if tids is None:
+            return []
+        t = self.ctx.scan_link(arity, ttype, tids, list(range(arity)), 0, True, False, True)
+        return self._pairs(t, arity)
+
+    def _pairs(self, t, arity):
+        cols = t.fetch()
+        if cols.shape[1] == 0:
+            return []
+        links = self.hex_of(cols[0])
+        tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
+        return [(links[i], self._fmt_targets([tg[k][i] for k in range(arity)])) for i in range(cols.shape[1])]
+
+    def get_all_nodes(self, node_type: str, names: bool = False) -> List[str]:
+        """redis_mongo_db.py:254-267"""
+        tid = self.type_id.get(node_type)
+        if tid is None:
+            return []
+        dig, cat, _, ty, nl = self._host_mirror()
+        sel = np.nonzero((cat == 1) & (ty == tid))[0]
+        if names:
+            return [self.arrays.node_name(int(nl[i])) for i in sel]
+        return _lib.digests_to_hex(dig[sel]) if sel.size else []
+
+    def _template_ctype(self, template):
+        hashed = []
+        for t in template:
+            if not isinstance(t, str):
+                raise TypeError("sequence item: expected str instance, list found")
+            hashed.append(_lib.md5_digest(t))
+        if len(hashed) == 1:
+            return None, hashed[0]
+        return self.ctx.ctype_lookup(_lib.composite_digest(hashed)), None
+
+    def get_matched_type_template(self, template: List[Any]) -> List[str]:
+        """redis_mongo_db.py:269-275 (templates:<composite_type_hash>)"""
+        ct, named = self._template_ctype(template)
+        if named is not None:
+            return self.get_matched_type(template[0])
+        if ct < 0:
+            return []
+        arity = len(template) - 1
+        t = self.ctx.scan_template(ct, arity, list(range(arity)), True, False, True)
+        return self._pairs(t, arity)
+
+    def get_matched_type(self, link_type: str) -> List[str]:
+        """redis_mongo_db.py:277-279 (templates:<named_type_hash>)"""
+        tid = self.type_id.get(link_type)
+        if tid is None:
+            return []
+        out = []
+        for a, t in enumerate(self.ctx.scan_type(tid)):
+            if t is not None:
+                out += self._pairs(t, a)
+        return out
+
+    def get_node_name(self, node_handle: str) -> str:
+        """redis_mongo_db.py:281-285 (names:<handle>)"""
+        aid, cat, _ = self._lookup(node_handle)
+        if aid < 0 or cat != 1:
+            raise ValueError(f"Invalid handle: {node_handle}")
+        _, _, _, _, nl = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        return self.arrays.node_name(int(nl[0]))
+
+    def get_matched_node_name(self, node_type: str, substring: str) -> str:
+        """redis_mongo_db.py:287-293 (Mongo $regex on names of that type)"""
+        tid = self.type_id.get(node_type)
+        if tid is None:
+            return []
+        dig, cat, _, ty, nl = self._host_mirror()
+        sel = np.nonzero((cat == 1) & (ty == tid))[0]
+        rx = re.compile(substring)
+        hits = [i for i in sel if rx.search(self.arrays.node_name(int(nl[i])))]
+        return _lib.digests_to_hex(dig[hits]) if hits else []
+
+    def get_atom_as_dict(self, handle, arity=-1) -> dict:
+        """redis_mongo_db.py:297-311"""
+        aid, cat, ar = self._lookup(handle)
+        if aid < 0 or cat == 0:
+            return {}
+        _, _, _, ty, nl = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        tname = self.arrays.type_names[int(ty[0])]
+        if cat == 1:
+            return {"handle": handle, "type": tname, "name": self.arrays.node_name(int(nl[0]))}
+        targets = self.hex_of(self.ctx.link_targets(aid))
+        return {"handle": handle, "type": tname, "template": self._template_of(aid), "targets": targets}
+
+    def _template_of(self, aid):
+        _, cat, _, ty, _ = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        tname = self.arrays.type_names[int(ty[0])]
+        if cat[0] != 2:
+            return tname
+        return [tname] + [self._template_of(int(x)) for x in self.ctx.link_targets(aid)]
+
+    def get_atom_as_deep_representation(self, handle: str, arity=-1) -> str:
+        """redis_mongo_db.py:187-199, 313-314"""
+        aid, cat, _ = self._lookup(handle)
+        if aid < 0:
+            raise ValueError(f"Invalid handle: {handle}")
+        return self._deep(aid)
+
+    def _deep(self, aid):
+        _, cat, _, ty, nl = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        tname = self.arrays.type_names[int(ty[0])] if ty[0] != _lib.DAS_NONE else None
+        if cat[0] == 1:
+            return {"type": tname, "name": self.arrays.node_name(int(nl[0]))}
+        return {"type": tname, "targets": [self._deep(int(x)) for x in self.ctx.link_targets(aid)]}
+
+    def get_link_type(self, link_handle: str) -> str:
+        aid, cat, _ = self._lookup(link_handle)
+        if aid < 0 or cat != 2:
+            raise KeyError(link_handle)
+        _, _, _, ty, _ = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        return self.arrays.type_names[int(ty[0])]
+
+    def get_node_type(self, node_handle: str) -> str:
+        aid, cat, _ = self._lookup(node_handle)
+        if aid < 0 or cat != 1:
+            raise KeyError(node_handle)
+        _, _, _, ty, _ = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
+        return self.arrays.type_names[int(ty[0])]
+
+    def count_atoms(self) -> Tuple[int, int]:
+        """redis_mongo_db.py:330-335"""
+        st = self.ctx.stats()
+        return (int(st.n_nodes), int(st.n_links))
+
+    def prefetch(self) -> None:
+        """redis_mongo_db.py:89-127 — the index is already resident in HBM."""
+        return None
+
+    # ------------------------------------------------ matcher entry points
+    def _type_or_empty(self, link_type):
+        """type id, None for '*', False for a type the KB never saw (no match)."""
+        if link_type == WILDCARD:
+            return None
+        tid = self.type_id.get(link_type)
+        return False if tid is None else tid
+
+    def _target_ids(self, handles):
+        """ids for grounded handles (DAS_NONE for '*'); None if one is unknown."""
+        grounded = [h for h in handles if h != WILDCARD]
+        ids = self.ids_of(grounded) if grounded else np.zeros(0, np.int64)
+        if (ids < 0).any():
+            return None
+        it = iter(ids.tolist())
+        return [_lib.DAS_NONE if h == WILDCARD else next(it) for h in handles]
+
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+        """Link.matched's wildcard branch fused with _assign_variables
+        (pattern_matcher.py:515-535 over redis_mongo_db.py:235-252).
+        handles: reference-order target handles ('*' for variables);
+        var_ids: variable id per position in the Link's own target order."""
+        if link_type in UNORDERED_LINK_TYPES:
+            order = sorted(range(len(handles)), key=lambda i: handles[i])
+            key_handles = [handles[i] for i in order]
+        else:
+            key_handles = list(handles)
+        arity = len(handles)
+        ttype = self._type_or_empty(link_type)
+        tids = self._target_ids(key_handles)
+        if ttype is False or tids is None or arity == 0 or arity > 8:
+            return Relation()
+        names = [v for v in var_ids if v is not None]
+        repeated = len(set(names)) != len(names)
+        if ordered:
+            var = [v if v is not None else -1 for v in var_ids]
+            t = self.ctx.scan_link(arity, ttype, tids, var, 0, True, no_overload)
+        else:
+            if repeated:
+                return Relation()       # UnorderedAssignment.assign rejects a repeat (:196-197)
+            t = self.ctx.scan_link(arity, ttype, tids, names, len(names), False, no_overload)
+        # rows are distinct links of one type unless a '*' type, a repeated
+        # variable, an unordered value set or the sorted-key quirk of ordered
+        # Similarity/Set queries can make two links bind the same values
+        if ttype is None or repeated or not ordered or link_type in UNORDERED_LINK_TYPES:
+            t = self.ctx.dedup(t)
+        return Relation([t])
+
+    def match_template(self, link_type, target_types, var_ids, ordered, no_overload=False):
+        """LinkTemplate.matched (pattern_matcher.py:603-614) over
+        get_matched_type_template (redis_mongo_db.py:269-275)."""
+        ct, named = self._template_ctype([link_type, *target_types])
+        if named is not None:
+            if self.get_matched_type(link_type):
+                raise AssertionError("LinkTemplate without targets matched links with targets")
+            return Relation()
+        if ct < 0:
+            return Relation()
+        if not ordered and len(set(var_ids)) != len(var_ids):
+            return Relation()
+        t = self.ctx.scan_template(ct, len(target_types), list(var_ids), ordered, no_overload)
+        if not ordered or len(set(var_ids)) != len(var_ids):
+            t = self.ctx.dedup(t)
+        return Relation([t])

@@ -1,0 +1,402 @@
+"""Host-side ingestion: MeTTa text -> AtomArrays (the das_atoms_t layout).
+
+Parsing is host work; what it hands the GPU is the
+expression DAG: string leaves (type names, terminals) and expressions whose
+first child is the link type.  Hashing, interning and every index are built
+on the device (`das_build_index`).  Two readers reproduce the reference's two
+loaders:
+
+* `parse_metta`      general MeTTa with deferred typedef resolution, as
+                     MettaYacc/BaseYacc (das/base_yacc.py:83-161,
+                     das/metta_yacc.py:38-172): nodes are the terminals that
+                     appear inside expressions; a symbol used as a target is
+                     its typedef expression (md5(":"), md5(name), md5(type)).
+* `parse_canonical`  one expression per line, typed terminals "Type name", as
+                     CanonicalParser (das/canonical_parser.py:242-365): nodes
+                     are the terminals declared by `(: "name" Type)` lines.
+"""
+import re
+
+import numpy as np
+
+NONE = 0xFFFFFFFF
+LEAF_TYPE, LEAF_NODE, LEAF_OTHER = 0, 1, 2
+EXPR_LINK, EXPR_TYPEDEF = 1, 2
+BASIC_TYPE = "Type"          # metta_lex.py:4
+TYPEDEF_MARK = ":"
+
+
+class AtomArrays:
+    """Flat arrays in the das_atoms_t layout (include/das_mi355x.h)."""
+
+    def __init__(self, leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start,
+                 expr_off, expr_child, expr_kind, expr_ctype_leaf, level_off, type_names):
+        self.leaf_bytes = np.ascontiguousarray(leaf_bytes, dtype=np.uint8)
+        self.leaf_off = np.ascontiguousarray(leaf_off, dtype=np.uint64)
+        self.leaf_kind = np.ascontiguousarray(leaf_kind, dtype=np.uint8)
+        self.leaf_ctype = np.ascontiguousarray(leaf_ctype, dtype=np.uint32)
+        self.leaf_type_id = np.ascontiguousarray(leaf_type_id, dtype=np.uint32)
+        self.name_start = np.ascontiguousarray(name_start, dtype=np.uint32)
+        self.expr_off = np.ascontiguousarray(expr_off, dtype=np.uint64)
+        self.expr_child = np.ascontiguousarray(expr_child, dtype=np.uint32)
+        self.expr_kind = np.ascontiguousarray(expr_kind, dtype=np.uint8)
+        self.expr_ctype_leaf = np.ascontiguousarray(expr_ctype_leaf, dtype=np.int32)
+        self.level_off = np.ascontiguousarray(level_off, dtype=np.uint64)
+        self.type_names = list(type_names)
+        self.type_id = {n: i for i, n in enumerate(self.type_names)}
+
+    @property
+    def n_leaf(self):
+        return len(self.leaf_off) - 1
+
+    @property
+    def n_expr(self):
+        return len(self.expr_off) - 1
+
+    # --- accessors used by tests / the oracle -------------------------------
+    @property
+    def expr_level(self):
+        lv = np.zeros(self.n_expr, dtype=np.int64)
+        for g in range(len(self.level_off) - 1):
+            lv[int(self.level_off[g]):int(self.level_off[g + 1])] = g
+        return lv
+
+    def leaf_string(self, i):
+        return bytes(self.leaf_bytes[int(self.leaf_off[i]):int(self.leaf_off[i + 1])]).decode("utf-8")
+
+    def leaf_strings(self):
+        return [self.leaf_string(i) for i in range(self.n_leaf)]
+
+    def node_name(self, i):
+        b = int(self.leaf_off[i]) + int(self.name_start[i])
+        return bytes(self.leaf_bytes[b:int(self.leaf_off[i + 1])]).decode("utf-8")
+
+    def children(self, j):
+        return [int(x) for x in self.expr_child[int(self.expr_off[j]):int(self.expr_off[j + 1])]]
+
+
+class AtomBuilder:
+    """Incremental builder; `finish()` groups expressions by (level, arity)."""
+
+    def __init__(self):
+        self.leaf_index = {}
+        self.leaf_str = []
+        self.leaf_kind = []
+        self.leaf_ctype = []
+        self.name_start = []
+        self.type_names = []
+        self.type_of_leaf = {}
+        self.e_children = []      # child refs: leaf i -> i, expr j -> -(j + 1)
+        self.e_kind = []
+        self.e_ctype_leaf = []
+        self.e_level = []
+
+    def type_leaf(self, name):
+        i = self.leaf_index.get(name)
+        if i is None:
+            i = len(self.leaf_str)
+            self.leaf_index[name] = i
+            self.leaf_str.append(name)
+            self.leaf_kind.append(LEAF_TYPE)
+            self.leaf_ctype.append(i)
+            self.name_start.append(0)
+        if i not in self.type_of_leaf:
+            if self.leaf_kind[i] != LEAF_TYPE:
+                raise ValueError(f"'{name}' is both a terminal string and a type name")
+            self.type_of_leaf[i] = len(self.type_names)
+            self.type_names.append(name)
+        return i
+
+    def terminal(self, named_type, name, node):
+        """Leaf hashed as terminal_hash(named_type, name) (expression_hasher.py:17-19)."""
+        t = self.type_leaf(named_type)
+        s = " ".join([named_type, name])
+        i = self.leaf_index.get(s)
+        if i is None:
+            i = len(self.leaf_str)
+            self.leaf_index[s] = i
+            self.leaf_str.append(s)
+            self.leaf_kind.append(LEAF_NODE if node else LEAF_OTHER)
+            self.leaf_ctype.append(t)
+            self.name_start.append(len(named_type.encode("utf-8")) + 1)
+        elif node and self.leaf_kind[i] == LEAF_OTHER:
+            self.leaf_kind[i] = LEAF_NODE
+        return i
+
+    def expr(self, type_name, children, kind=EXPR_LINK, ctype_leaf=-1):
+        """children: refs returned by terminal()/expr()/type_leaf(); returns a ref."""
+        t = self.type_leaf(type_name)
+        refs = [t] + list(children)
+        lv = 1 + max([self.e_level[-r - 1] if r < 0 else 0 for r in refs])
+        self.e_children.append(refs)
+        self.e_kind.append(kind)
+        self.e_ctype_leaf.append(ctype_leaf)
+        self.e_level.append(lv)
+        return -len(self.e_children)
+
+    def typedef_expr(self, name, type_name):
+        """The typedef atom (: name type) — expression_hash(md5(':'), [md5(name), md5(type)])
+        (canonical_parser.py:48-59, base_yacc.py:108-130).  Used as a target it is
+        the symbol's handle; its composite type is md5(name) (base_yacc.py:147-161)."""
+        n = self.type_leaf(name)
+        t = self.type_leaf(type_name)
+        return self.expr(TYPEDEF_MARK, [n, t], kind=EXPR_TYPEDEF, ctype_leaf=n)
+
+    def finish(self):
+        n_leaf = len(self.leaf_str)
+        n_expr = len(self.e_children)
+        enc = [s.encode("utf-8") for s in self.leaf_str]
+        lens = np.array([len(b) for b in enc], dtype=np.uint64)
+        leaf_off = np.zeros(n_leaf + 1, dtype=np.uint64)
+        np.cumsum(lens, out=leaf_off[1:])
+        leaf_bytes = np.frombuffer(b"".join(enc), dtype=np.uint8) if n_leaf else np.zeros(0, np.uint8)
+        leaf_type_id = np.full(n_leaf, NONE, dtype=np.uint32)
+        for i, tid in self.type_of_leaf.items():
+            leaf_type_id[i] = tid
+        # group expressions by (level, number of children)
+        nch = np.array([len(c) for c in self.e_children], dtype=np.int64)
+        lev = np.array(self.e_level, dtype=np.int64)
+        order = np.lexsort((np.arange(n_expr), nch, lev)) if n_expr else np.zeros(0, np.int64)
+        newpos = np.empty(n_expr, dtype=np.int64)
+        newpos[order] = np.arange(n_expr)
+        expr_off = np.zeros(n_expr + 1, dtype=np.uint64)
+        np.cumsum(nch[order], out=expr_off[1:])
+        child = np.empty(int(expr_off[-1]) if n_expr else 0, dtype=np.uint32)
+        pos = 0
+        for j in order:
+            for r in self.e_children[j]:
+                child[pos] = r if r >= 0 else n_leaf + newpos[-r - 1]
+                pos += 1
+        kinds = np.array(self.e_kind, dtype=np.uint8)[order] if n_expr else np.zeros(0, np.uint8)
+        ctl = np.array(self.e_ctype_leaf, dtype=np.int32)[order] if n_expr else np.zeros(0, np.int32)
+        groups = [0]
+        for k in range(1, n_expr):
+            a, b = order[k - 1], order[k]
+            if lev[a] != lev[b] or nch[a] != nch[b]:
+                groups.append(k)
+        groups.append(n_expr)
+        if n_expr == 0:
+            groups = [0]
+        self._newpos = newpos
+        return AtomArrays(leaf_bytes, leaf_off, np.array(self.leaf_kind, np.uint8),
+                          np.array(self.leaf_ctype, np.uint32), leaf_type_id,
+                          np.array(self.name_start, np.uint32), expr_off, child, kinds, ctl,
+                          np.array(groups, dtype=np.uint64), self.type_names)
+
+    def unified(self, ref):
+        """Unified index (after finish()) of a builder ref."""
+        return ref if ref >= 0 else len(self.leaf_str) + int(self._newpos[-ref - 1])
+
+
+# ---------------------------------------------------------------------------
+# General MeTTa (MettaYacc semantics)
+# ---------------------------------------------------------------------------
+_TOKEN = re.compile(r'\s*(?:(\()|(\))|(:)|"([^"]+)"|([^\W0-9]\w*)|(\S))')
+
+
+def _tokens(text):
+    pos = 0
+    n = len(text)
+    while pos < n:
+        m = _TOKEN.match(text, pos)
+        if not m or m.end() == pos:
+            break
+        pos = m.end()
+        if m.group(1):
+            yield ("(", None)
+        elif m.group(2):
+            yield (")", None)
+        elif m.group(3):
+            yield (":", None)
+        elif m.group(4) is not None:
+            yield ("T", m.group(4))
+        elif m.group(5) is not None:
+            yield ("S", m.group(5))
+        elif m.group(6) is not None:
+            if m.group(6).strip():
+                raise SyntaxError(f"illegal character {m.group(6)!r} (metta_lex.py:58-63)")
+
+
+def _read_sexprs(text):
+    stack = [[]]
+    for kind, val in _tokens(text):
+        if kind == "(":
+            stack.append([])
+        elif kind == ")":
+            if len(stack) < 2:
+                raise SyntaxError("unbalanced ')'")
+            e = stack.pop()
+            stack[-1].append(("E", e))
+        else:
+            stack[-1].append((kind, val))
+    if len(stack) != 1:
+        raise SyntaxError("unbalanced '('")
+    return stack[0]
+
+
+def parse_metta(texts, builder=None):
+    """MeTTa source(s) -> AtomBuilder, MettaYacc semantics."""
+    if isinstance(texts, str):
+        texts = [texts]
+    b = builder or AtomBuilder()
+    tops = []
+    named_types = {BASIC_TYPE: BASIC_TYPE}
+    typedefs = []
+    for text in texts:
+        for item in _read_sexprs(text):
+            if item[0] != "E":
+                raise SyntaxError("top level must be expressions")
+            body = item[1]
+            if body and body[0][0] == ":":
+                if len(body) != 3 or body[1][0] not in ("S", "T") or body[2][0] != "S":
+                    raise SyntaxError(f"bad typedef {body}")
+                named_types[body[1][1]] = body[2][1]
+                typedefs.append((body[1][1], body[2][1]))
+            else:
+                tops.append(body)
+    symbol_ref = {}
+
+    def sym(name):
+        if name not in named_types:
+            raise NameError(f"undefined symbol {name} (UndefinedSymbolError, exceptions.py:19-22)")
+        r = symbol_ref.get(name)
+        if r is None:
+            r = b.typedef_expr(name, named_types[name])
+            symbol_ref[name] = r
+        return r
+
+    def build(body):
+        if not body:
+            raise SyntaxError("empty expression")
+        head = body[0]
+        if head[0] != "S":
+            raise NotImplementedError("only symbol-headed expressions are typed (base_yacc.py:101-105)")
+        if head[1] not in named_types:
+            raise NameError(f"undefined symbol {head[1]}")
+        kids = []
+        for kind, val in body[1:]:
+            if kind == "E":
+                if val and val[0][0] == ":":
+                    raise SyntaxError("nested type definition (metta_yacc.py:145-156)")
+                kids.append(build(val))
+            elif kind == "T":
+                if val not in named_types:
+                    raise NameError(f"undefined terminal {val}")
+                kids.append(b.terminal(named_types[val], val, node=True))
+            elif kind == "S":
+                kids.append(sym(val))
+            else:
+                raise SyntaxError(f"unexpected token {kind}")
+        return b.expr(head[1], kids)
+
+    for body in tops:
+        build(body)
+    return b
+
+
+# ---------------------------------------------------------------------------
+# Canonical MeTTa (CanonicalParser semantics)
+# ---------------------------------------------------------------------------
+
+def _canonical_expression(line, b):
+    stack = []            # refs, or ("sym", name) for raw symbols
+    cur = []
+    i, n = 0, len(line)
+    while i < n:
+        c = line[i]
+        if c == '"':
+            j = line.index('"', i + 1)
+            parts = line[i + 1:j].split()
+            stype, name = parts[0], " ".join(parts[1:])
+            stack.append(b.terminal(stype, name, node=False))
+            i = j + 1
+            continue
+        if c == "(":
+            stack.append("(")
+        elif c == " ":
+            if cur:
+                stack.append(("sym", "".join(cur)))
+                cur = []
+        elif c == ")":
+            if cur:
+                stack.append(("sym", "".join(cur)))
+                cur = []
+            items = []
+            while stack and stack[-1] != "(":
+                items.append(stack.pop())
+            stack.pop()
+            items.reverse()
+            if not items or not isinstance(items[0], tuple):
+                raise NotImplementedError("canonical expression without a type symbol")
+            kids = []
+            for x in items[1:]:
+                if isinstance(x, tuple):
+                    raise NotImplementedError("bare symbols as link targets (canonical_parser.py:253-261)")
+                kids.append(x)
+            stack.append(b.expr(items[0][1], kids))
+        else:
+            cur.append(c)
+        i += 1
+    if len(stack) != 1:
+        raise SyntaxError(f"unbalanced canonical line: {line[:80]}")
+
+
+def parse_canonical(texts, builder=None):
+    """Canonical MeTTa -> AtomBuilder (canonical_parser.py:315-365)."""
+    if isinstance(texts, str):
+        texts = [texts]
+    b = builder or AtomBuilder()
+    for text in texts:
+        state = 0
+        for raw in text.splitlines():
+            line = raw.strip()
+            if not line:
+                continue
+            words = line.split()
+            if state == 0:
+                if words[0] != "(:":
+                    raise SyntaxError(f"expected a typedef: {line[:80]}")
+                if words[1].startswith('"'):
+                    state = 1
+                else:
+                    b.type_leaf(words[1])
+                    b.type_leaf(words[-1].rstrip(")"))
+            if state == 1:
+                if words[0] == "(:":
+                    name = " ".join(words[1:-1]).strip('"')
+                    b.terminal(words[-1].rstrip(")"), name, node=True)
+                    continue
+                state = 2
+            if state == 2:
+                if words[0] == "(:" or not line.startswith("(") or not line.endswith(")"):
+                    raise SyntaxError(f"bad canonical expression line: {line[:80]}")
+                _canonical_expression(line, b)
+    return b
+
+
+# ---------------------------------------------------------------------------
+# From stored-atom tables (golden fixtures: what the reference put in Mongo)
+# ---------------------------------------------------------------------------
+
+def from_tables(nodes, links):
+    """nodes: [handle, type, name]; links: [handle, type, [target handles], ctype].
+    Rebuilds the DAG; the GPU then recomputes every handle."""
+    b = AtomBuilder()
+    ref = {}
+    for h, t, name in nodes:
+        ref[h] = b.terminal(t, name, node=True)
+    pending = {h: (t, tg) for h, t, tg, _ in links}
+
+    def make(h, depth=0):
+        if h in ref:
+            return ref[h]
+        if h not in pending or depth > 10000:
+            raise KeyError(f"target {h} is neither a stored node nor a stored link")
+        t, tg = pending[h]
+        r = b.expr(t, [make(x, depth + 1) for x in tg])
+        ref[h] = r
+        return r
+
+    for h, _, _, _ in links:
+        make(h)
+    return b

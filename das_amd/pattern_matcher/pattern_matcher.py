@@ -1,0 +1,700 @@
+"""Pattern matcher with the reference's API (das/pattern_matcher/pattern_matcher.py).
+
+Same classes, constructor signatures and `matched(db, answer) -> bool`
+contract; `answer.assignments` is the reference's set of `Assignment`
+objects.  Evaluation is different: every term produces a *device* binding
+relation (HipDB.match_link / match_template -> scan kernels), `And` folds
+them with GPU natural joins and anti-joins, `Or` with GPU union/dedup and set
+difference.  Python `Assignment` objects are only built when a caller reads
+`answer.assignments`.
+
+Semantics kept from the reference: reset-on-empty in
+And (:725-729), skipped empty terms (:717-719), negated terms collected as a
+forbidden set (:720-724, :741-746), Or with Not terms = And(negated) minus the
+positive union with negation=True (:674-683), top-level Not flips the flag
+(:627-631), `_typed_variable_matched` last-writer-wins (:491-500).
+
+Ordered assignments are evaluated entirely on the GPU.  Joins or negations
+that mix in unordered (Similarity/Set) assignments — the reference's
+CompositeAssignment algebra (:264-368) — raise NotImplementedError in this
+build rather than silently running on the host.
+"""
+from abc import ABC, abstractmethod
+from collections import Counter
+from copy import deepcopy
+from enum import Enum, auto
+from functools import cmp_to_key
+from typing import Dict, FrozenSet, List, Optional, Set, Union
+
+import numpy as np
+
+from .. import _lib
+from ..database.db_interface import WILDCARD, DBInterface
+from ..database.hip_db import HipDB, Relation
+
+DEBUG_AND = False
+DEBUG_OR = False
+DEBUG_NOT = False
+DEBUG_LINK = False
+DEBUG_LINK_TEMPLATE = False
+
+CONFIG = {
+    'no_overload': False,   # distinct variables must take distinct values (ordered)
+}
+
+
+class CompatibilityStatus(int, Enum):
+    INCOMPATIBLE = auto()
+    NO_COVERING = auto()
+    FIRST_COVERS_SECOND = auto()
+    SECOND_COVERS_FIRST = auto()
+    EQUAL = auto()
+
+
+# ---------------------------------------------------------------------------
+# variable ids (device tables carry small integer variable ids)
+# ---------------------------------------------------------------------------
+_VAR_ID: Dict[str, int] = {}
+_VAR_NAME: List[str] = []
+
+
+def _vid(name: str) -> int:
+    v = _VAR_ID.get(name)
+    if v is None:
+        v = len(_VAR_NAME)
+        _VAR_ID[name] = v
+        _VAR_NAME.append(name)
+    return v
+
+
+def _var_name(v: int) -> str:
+    return _VAR_NAME[v]
+
+
+# ---------------------------------------------------------------------------
+# Assignments: the reference's value objects (identity = hash equality)
+# ---------------------------------------------------------------------------
+class Assignment(ABC):
+
+    def __init__(self):
+        self.variables: Union[Set[str], FrozenSet] = set()
+        self.hash: int = 0
+        self.frozen = False
+
+    def __hash__(self) -> int:
+        assert self.hash
+        return self.hash
+
+    def __eq__(self, other) -> bool:
+        assert self.hash and other.hash
+        return self.hash == other.hash
+
+    def __lt__(self, other) -> bool:
+        assert self.hash and other.hash
+        return self.hash < other.hash
+
+    def freeze(self) -> bool:
+        if self.frozen:
+            return False
+        self.frozen = True
+        self.variables = frozenset(self.variables)
+        return True
+
+    @abstractmethod
+    def assign(self, variable: str, value: str) -> bool: ...
+
+    @abstractmethod
+    def join(self, other: 'Assignment') -> 'Assignment': ...
+
+    @abstractmethod
+    def check_negation(self, negation: 'Assignment') -> bool: ...
+
+
+def _bad_assign(variable, value, frozen):
+    if variable is None or value is None or frozen:
+        raise ValueError(f'Invalid assignment: variable = {variable} value = {value} frozen = {frozen}')
+
+
+class OrderedAssignment(Assignment):
+
+    def __init__(self):
+        super().__init__()
+        self.mapping: Dict[str, str] = {}
+        self.values: Union[Set[str], FrozenSet] = set()
+
+    def __repr__(self):
+        return repr(self.mapping)
+
+    def freeze(self):
+        assert super().freeze()
+        self.values = frozenset(self.values)
+        self.hash = hash(frozenset(self.mapping.items()))
+        return True
+
+    def assign(self, variable: str, value: str) -> bool:
+        _bad_assign(variable, value, self.frozen)
+        if variable in self.variables:
+            return self.mapping[variable] == value
+        if CONFIG['no_overload'] and value in self.values:
+            return False
+        self.variables.add(variable)
+        self.values.add(value)
+        self.mapping[variable] = value
+        return True
+
+    def evaluate_compatibility(self, other) -> CompatibilityStatus:
+        assert other is not None
+        if self.hash == other.hash:
+            return CompatibilityStatus.EQUAL
+        if any(self.mapping[v] != other.mapping[v] for v in self.variables & other.variables):
+            return CompatibilityStatus.INCOMPATIBLE
+        if other.variables < self.variables:
+            return CompatibilityStatus.FIRST_COVERS_SECOND
+        if self.variables < other.variables:
+            return CompatibilityStatus.SECOND_COVERS_FIRST
+        return CompatibilityStatus.NO_COVERING
+
+    def compatible(self, other) -> bool:
+        return self.evaluate_compatibility(other) != CompatibilityStatus.INCOMPATIBLE
+
+    def _join_ordered(self, other):
+        status = self.evaluate_compatibility(other)
+        if status == CompatibilityStatus.INCOMPATIBLE:
+            return None
+        if status in (CompatibilityStatus.EQUAL, CompatibilityStatus.FIRST_COVERS_SECOND):
+            return self
+        if status == CompatibilityStatus.SECOND_COVERS_FIRST:
+            return other
+        merged = OrderedAssignment()
+        for var, val in list(self.mapping.items()) + list(other.mapping.items()):
+            if not merged.assign(var, val):
+                return None
+        merged.freeze()
+        return merged
+
+    def join(self, other: Assignment) -> Assignment:
+        assert self.frozen and other.frozen
+        return self._join_ordered(other) if isinstance(other, OrderedAssignment) else other.join(self)
+
+    def check_negation(self, negation: Assignment) -> bool:
+        if isinstance(negation, OrderedAssignment):
+            return self.evaluate_compatibility(negation) not in (
+                CompatibilityStatus.EQUAL, CompatibilityStatus.FIRST_COVERS_SECOND)
+        return not negation.is_covered_by_ordered(self)
+
+
+class UnorderedAssignment(Assignment):
+
+    def __init__(self):
+        super().__init__()
+        self.symbols: Dict[str, int] = {}
+        self.values: Dict[str, int] = {}
+
+    def __repr__(self):
+        syms = [s for s, c in self.symbols.items() for _ in range(c)]
+        vals = [v for v, c in self.values.items() for _ in range(c)]
+        return '*' + repr(dict(zip(syms, vals)))
+
+    def freeze(self):
+        assert super().freeze()
+        if sorted(self.symbols.values()) != sorted(self.values.values()):
+            return False
+        self.hash = hash((hash(frozenset(self.symbols.items())), hash(frozenset(self.values.items()))))
+        return True
+
+    def assign(self, variable: str, value: str) -> bool:
+        _bad_assign(variable, value, self.frozen)
+        if variable in self.variables:
+            return False
+        self.symbols[variable] = self.symbols.get(variable, 0) + 1
+        self.values[value] = self.values.get(value, 0) + 1
+        self.variables.add(variable)
+        return True
+
+    def join(self, other: Assignment) -> Assignment:
+        assert self.frozen and other.frozen
+        if isinstance(other, CompositeAssignment):
+            return other.join(self)
+        return CompositeAssignment(self).join(other)
+
+    def check_negation(self, negation: Assignment) -> bool:
+        if isinstance(negation, OrderedAssignment):
+            return not self.contains_ordered(negation)
+        if isinstance(negation, UnorderedAssignment):
+            return not self.contains_unordered(negation)
+        return all(not self.contains_unordered(u) for u in negation.unordered_mappings)
+
+    def contains_ordered(self, ordered_assignment) -> bool:
+        if not set(ordered_assignment.mapping) <= set(self.variables):
+            return False
+        need = Counter(ordered_assignment.mapping.values())
+        return all(self.values.get(v, 0) >= c for v, c in need.items())
+
+    def is_covered_by_ordered(self, ordered_assignment) -> bool:
+        sym = Counter(self.symbols)
+        val = Counter(self.values)
+        sym.subtract(Counter(ordered_assignment.mapping.keys()))
+        val.subtract(Counter(ordered_assignment.mapping.values()))
+        return all(c <= 0 for c in sym.values()) and all(c <= 0 for c in val.values())
+
+    def contains_unordered(self, unordered_assignment) -> bool:
+        return all(self.symbols.get(s, 0) >= c for s, c in unordered_assignment.symbols.items()) and \
+            all(self.values.get(v, 0) >= c for v, c in unordered_assignment.values.items())
+
+    def compatible(self, other) -> bool:
+        common_syms = set(self.variables) & set(other.variables)
+        common_vals = set(self.values) & set(other.values)
+        s_self = sum(self.symbols[s] for s in common_syms)
+        s_other = sum(other.symbols[s] for s in common_syms)
+        v_self = sum(self.values[v] for v in common_vals)
+        v_other = sum(other.values[v] for v in common_vals)
+        return v_other >= s_self and v_self >= s_other
+
+
+class CompositeAssignment(Assignment):
+
+    def __init__(self, assignment: UnorderedAssignment):
+        super().__init__()
+        self.unordered_mappings: List[UnorderedAssignment] = [assignment]
+        self.ordered_mapping: Optional[OrderedAssignment] = None
+        self.variables = deepcopy(assignment.variables)
+        assert self._freeze()
+
+    def __repr__(self):
+        return f'Ordered = {self.ordered_mapping} | Unordered = {self.unordered_mappings}'
+
+    def _freeze(self):
+        assert super().freeze()
+        self._recompute_hash()
+        return True
+
+    def freeze(self):
+        assert False
+
+    def assign(self, variable: str, value: str) -> bool:
+        assert False
+
+    def _recompute_hash(self) -> None:
+        h = self.ordered_mapping.hash if self.ordered_mapping else 1
+        for u in self.unordered_mappings:
+            h ^= u.hash
+        self.hash = h
+
+    def _viable(self) -> bool:
+        if not self.ordered_mapping:
+            return bool(self.unordered_mappings)
+        return all(u.contains_ordered(self.ordered_mapping) or u.is_covered_by_ordered(self.ordered_mapping)
+                   for u in self.unordered_mappings)
+
+    def _add_ordered_mapping(self, other: OrderedAssignment) -> bool:
+        if self.ordered_mapping is None:
+            self.ordered_mapping = other
+        else:
+            self.ordered_mapping = self.ordered_mapping.join(other)
+            if self.ordered_mapping is None:
+                return False
+        if not self._viable():
+            return False
+        self._recompute_hash()
+        return True
+
+    def _add_unordered_mapping(self, u) -> bool:
+        if self.ordered_mapping and not u.contains_ordered(self.ordered_mapping):
+            return False
+        if not all(x.compatible(u) for x in self.unordered_mappings):
+            return False
+        self.unordered_mappings.append(u)
+        self._recompute_hash()
+        return True
+
+    def join(self, other: Assignment) -> Assignment:
+        assert self.frozen and other.frozen
+        out = deepcopy(self)
+        if isinstance(other, OrderedAssignment):
+            ok = out._add_ordered_mapping(other)
+        elif isinstance(other, UnorderedAssignment):
+            ok = out._add_unordered_mapping(other)
+        else:
+            ok = out._add_ordered_mapping(other.ordered_mapping) and \
+                all(out._add_unordered_mapping(u) for u in other.unordered_mappings)
+        return out if ok else None
+
+    def check_negation(self, negation: Assignment) -> bool:
+        if isinstance(negation, OrderedAssignment):
+            return all(not u.contains_ordered(negation) for u in self.unordered_mappings)
+        if isinstance(negation, UnorderedAssignment):
+            return all(not u.contains_unordered(negation) for u in self.unordered_mappings)
+        raise AttributeError("'CompositeAssignment' object has no attribute 'unordered_assignments'")
+
+    def contains_ordered(self, ordered_assignment) -> bool:
+        return all(u.contains_ordered(ordered_assignment) for u in self.unordered_mappings)
+
+    def contains_unordered(self, unordered_assignment) -> bool:
+        return all(u.contains_unordered(unordered_assignment) for u in self.unordered_mappings)
+
+
+# ---------------------------------------------------------------------------
+# Device relation algebra
+# ---------------------------------------------------------------------------
+
+def _hip(db) -> HipDB:
+    if not isinstance(db, HipDB):
+        raise TypeError(f"das_amd evaluates patterns on the MI355X index; got {db!r} (use HipDB)")
+    return db
+
+
+def _group(tables):
+    g = {}
+    for t in tables:
+        g.setdefault(t.schema, []).append(t)
+    return g
+
+
+def _normalize(db, rel):
+    """One table per schema, rows distinct (Python set semantics)."""
+    out = []
+    for schema, ts in _group(rel.tables).items():
+        out.append(ts[0] if len(ts) == 1 else db.ctx.dedup(db.ctx.concat(ts)))
+    return Relation(out)
+
+
+def _union(db, a, b):
+    return _normalize(db, Relation(a.tables + b.tables))
+
+
+def _unsupported(what):
+    raise NotImplementedError(
+        f"{what} involving unordered (Similarity/Set) assignments — the reference's "
+        "CompositeAssignment algebra (pattern_matcher.py:264-368) — is not implemented on the GPU in this build")
+
+
+def _join(db, a, b):
+    out = []
+    for ta in a.tables:
+        for tb in b.tables:
+            if ta.kind != _lib.TABLE_ORDERED or tb.kind != _lib.TABLE_ORDERED:
+                _unsupported("join")
+            out.append(db.ctx.join(ta, tb, CONFIG['no_overload']))
+    return Relation(out)
+
+
+def _without_forbidden(db, rel, forbidden):
+    """check_negation of every row against every forbidden row (:741-746)."""
+    tables = rel.tables
+    for f in forbidden.tables:
+        nxt = []
+        for t in tables:
+            if t.kind != _lib.TABLE_ORDERED or f.kind != _lib.TABLE_ORDERED:
+                _unsupported("negation")
+            nxt.append(db.ctx.antijoin(t, f))
+        tables = nxt
+    return Relation(tables)
+
+
+def _minus(db, a, b):
+    """Set difference a - b by identity (same kind and variables, equal values)."""
+    groups = _group(b.tables)
+    out = []
+    for t in a.tables:
+        for f in groups.get(t.schema, []):
+            t = db.ctx.antijoin(t, f)
+        out.append(t)
+    return Relation(out)
+
+
+# ---------------------------------------------------------------------------
+# Answers
+# ---------------------------------------------------------------------------
+class PatternMatchingAnswer:
+
+    def __init__(self):
+        self._rel: Optional[Relation] = None
+        self._db: Optional[HipDB] = None
+        self._py = None
+        self.negation: bool = False
+
+    def __repr__(self):
+        s = 'NOT\n' if self.negation else ''
+        for a in self.assignments:
+            s += str(a) + '\n'
+        return s
+
+    def _set(self, db, rel):
+        self._db = db
+        self._rel = rel
+        self._py = None
+
+    def _relation(self) -> Relation:
+        if self._py is not None and self._rel is None:
+            if self._py:
+                raise NotImplementedError("host-built assignments cannot feed the device matcher")
+            return Relation()
+        return self._rel if self._rel is not None else Relation()
+
+    def __len__(self):
+        return len(self.assignments)
+
+    @property
+    def assignments(self):
+        if self._py is None:
+            self._py = _materialize(self._db, self._rel)
+        return self._py
+
+    @assignments.setter
+    def assignments(self, value):
+        self._py = set(value)
+        self._rel = None
+
+    def count(self) -> int:
+        """Number of distinct assignments, without building Python objects."""
+        if self._py is not None and self._rel is None:
+            return len(self._py)
+        return self._relation().nrows
+
+
+def _materialize(db, rel):
+    out = set()
+    if rel is None or not rel:
+        return out
+    for t in rel.tables:
+        cols = t.fetch()
+        names = [_var_name(v) for v in t.vars]
+        hexcols = [db.hex_of(c) for c in cols]
+        for i in range(t.nrows):
+            if t.kind == _lib.TABLE_ORDERED:
+                a = OrderedAssignment()
+                for k, name in enumerate(names):
+                    a.assign(name, hexcols[k][i])
+            else:
+                a = UnorderedAssignment()
+                for k, name in enumerate(names):
+                    a.assign(name, hexcols[k][i])
+            a.freeze()
+            out.add(a)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Expressions
+# ---------------------------------------------------------------------------
+class LogicalExpression(ABC):
+
+    @abstractmethod
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool: ...
+
+    def __repr__(self):
+        return '<LogicalExpression>'
+
+
+class Atom(LogicalExpression, ABC):
+
+    def __init__(self, atom_type: str):
+        self.atom_type = atom_type
+        self.handle = None
+
+    def __repr__(self):
+        return f'{self.atom_type}'
+
+    @abstractmethod
+    def get_handle(self, db: DBInterface) -> str: ...
+
+
+class Node(Atom):
+
+    def __init__(self, node_type: str, node_name: str):
+        super().__init__(node_type)
+        self.name = node_name
+
+    def __repr__(self):
+        return f'<{super().__repr__()}: {self.name}>'
+
+    def get_handle(self, db: DBInterface) -> str:
+        if not self.handle:
+            self.handle = db.get_node_handle(self.atom_type, self.name)
+        return self.handle
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        return db.node_exists(self.atom_type, self.name)
+
+
+def _variables_last(t1, t2):
+    """Link.__init__'s comparator for unordered links (pattern_matcher.py:442-448)."""
+    if isinstance(t1, Variable):
+        return 1
+    if isinstance(t2, Variable):
+        return -1
+    return 0
+
+
+class Link(Atom):
+
+    def __init__(self, link_type: str, targets: List[Atom], ordered: bool):
+        assert not any(isinstance(target, TypedVariable) for target in targets)
+        super().__init__(link_type)
+        self.ordered = ordered
+        self.targets = targets if ordered else sorted(targets, key=cmp_to_key(_variables_last))
+
+    def __repr__(self):
+        return f'<{super().__repr__()}: {self.targets}>'
+
+    def get_handle(self, db: DBInterface) -> str:
+        if not self.handle:
+            hs = [t.get_handle(db) for t in self.targets]
+            if any(h is None for h in hs):
+                return None
+            self.handle = db.get_link_handle(self.atom_type, hs)
+        return self.handle
+
+    def _typed_variable_matched(self, db, answer) -> bool:
+        if any(isinstance(t, Variable) for t in self.targets):
+            return False
+        return all(t.matched(db, answer) for t in self.targets)
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        db = _hip(db)
+        if any(isinstance(t, LinkTemplate) for t in self.targets):
+            return self._typed_variable_matched(db, answer)
+        if not all(t.matched(db, answer) for t in self.targets):
+            return False
+        handles = [t.get_handle(db) for t in self.targets]
+        if WILDCARD not in handles:
+            return db.link_exists(self.atom_type, handles)
+        var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in self.targets]
+        rel = db.match_link(self.atom_type, handles, var_ids, self.ordered, CONFIG['no_overload'])
+        if db.tuple_targets and not self.ordered and rel and any(v is None for v in var_ids):
+            # reference DB path: list.remove on a tuple (pattern_matcher.py:484)
+            raise AttributeError("'tuple' object has no attribute 'remove'")
+        answer._set(db, rel)
+        return bool(rel)
+
+
+class Variable(Atom):
+
+    def __init__(self, variable_name: str):
+        super().__init__('ANY')
+        self.name = variable_name
+
+    def __repr__(self):
+        return f'{self.name}'
+
+    def get_handle(self, db: DBInterface) -> str:
+        return WILDCARD
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        return True
+
+
+class TypedVariable(Variable):
+
+    def __init__(self, variable_name: str, variable_type: str):
+        super().__init__(variable_name)
+        self.type = variable_type
+
+    def __repr__(self):
+        return f'{self.name}: {self.type}'
+
+
+class LinkTemplate(LogicalExpression):
+
+    def __init__(self, link_type: str, targets: List[TypedVariable], ordered: bool):
+        assert all(isinstance(target, TypedVariable) for target in targets)
+        self.link_type = link_type
+        self.targets = targets
+        self.ordered = ordered
+        self.handle = None
+
+    def __repr__(self):
+        return f'<{self.link_type}: {self.targets}>'
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        db = _hip(db)
+        rel = db.match_template(self.link_type, [v.type for v in self.targets],
+                                [_vid(v.name) for v in self.targets], self.ordered, CONFIG['no_overload'])
+        answer._set(db, rel)
+        return bool(rel)
+
+
+class Not(LogicalExpression):
+
+    def __init__(self, term: LogicalExpression):
+        self.term = term
+
+    def __repr__(self):
+        return f'NOT({self.term})'
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        self.term.matched(db, answer)
+        answer.negation = not answer.negation
+        return True
+
+
+class Or(LogicalExpression):
+
+    def __init__(self, terms: List[LogicalExpression]):
+        self.terms = terms
+
+    def __repr__(self):
+        return f'OR({self.terms})'
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        db = _hip(db)
+        if not self.terms:
+            return False
+        assert not answer._relation()
+        union = Relation()
+        any_matched = False
+        negated = [t for t in self.terms if isinstance(t, Not)]
+        for term in self.terms:
+            if isinstance(term, Not):
+                continue
+            sub = PatternMatchingAnswer()
+            if not term.matched(db, sub):
+                continue
+            any_matched = True
+            rel = sub._relation()
+            if rel:
+                union = rel if not union else _union(db, union, rel)
+        if negated:
+            sub = PatternMatchingAnswer()
+            And([t.term for t in negated]).matched(db, sub)
+            answer._set(db, _minus(db, sub._relation(), union))
+            answer.negation = True
+        else:
+            answer._set(db, union)
+        return any_matched
+
+
+class And(LogicalExpression):
+
+    def __init__(self, terms: List[LogicalExpression]):
+        self.terms = terms
+
+    def __repr__(self):
+        return f'AND({self.terms})'
+
+    def post_process(self, assignment) -> Assignment:
+        return assignment
+
+    def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        db = _hip(db)
+        if not self.terms:
+            return False
+        assert not answer._relation()
+        acc = Relation()
+        forbidden = Relation()
+        for term in self.terms:
+            sub = PatternMatchingAnswer()
+            if not term.matched(db, sub):
+                return False
+            rel = sub._relation()
+            if not rel:
+                continue
+            if sub.negation:
+                forbidden = Relation(forbidden.tables + rel.tables)
+                continue
+            acc = rel if not acc else _join(db, acc, rel)
+        if acc and forbidden:
+            acc = _without_forbidden(db, acc, forbidden)
+        acc = _normalize(db, acc)
+        answer._set(db, acc)
+        return bool(acc)

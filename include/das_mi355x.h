@@ -1,0 +1,181 @@
+/*
+ * das_mi355x.h — C ABI of the MI355X-native DAS query hot path.
+ *
+ * This library replaces, behind the reference's own Python API, the storage
+ * and evaluation layers of tanksha/das (reference snapshot 2025-02-09):
+ *   - the Redis pattern/template index + Mongo link/node collections that
+ *     `RedisMongoDB` reads          (das/database/redis_mongo_db.py:204-279)
+ *   - their construction            (das/canonical_parser.py:132-183,
+ *                                    das/parser_threads.py:141-253)
+ *   - the ExpressionHasher handles  (das/expression_hasher.py:9-35)
+ *   - the binding algebra of the pattern matcher for ordered assignments
+ *                                   (das/pattern_matcher/pattern_matcher.py:73-156,
+ *                                    :466-538, :591-614, :705-748)
+ * The Python host package `das_amd` binds it with ctypes.
+ *
+ * Conventions: every entry point returns int (0 = DAS_OK, < 0 = error; the
+ * message is in das_last_error(ctx)); no C++ exception crosses the ABI;
+ * plain pointers and sizes only.  Device buffers are owned by the context
+ * (index) or by a table handle (results) until das_table_free.  A digest is
+ * the 16 raw MD5 bytes as 4 little-endian uint32 words (the reference handle
+ * is its 32-char lowercase hex).  Atom ids are dense uint32 in handle order.
+ */
+#ifndef DAS_MI355X_H
+#define DAS_MI355X_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct das_ctx das_ctx_t;
+typedef struct das_table das_table_t;
+
+#define DAS_OK 0
+#define DAS_ERR_INVALID (-1)
+#define DAS_ERR_HIP (-2)
+#define DAS_ERR_NOT_BUILT (-3)
+#define DAS_ERR_UNSUPPORTED (-4)
+#define DAS_ERR_INTERNAL (-5)
+
+#define DAS_NONE 0xFFFFFFFFu   /* "no atom / wildcard" id */
+
+#define DAS_TABLE_ORDERED 0    /* column c binds vars[c] (OrderedAssignment.mapping) */
+#define DAS_TABLE_UNORDERED 1  /* vars = variable set, columns = sorted value set
+                                  (UnorderedAssignment.symbols / .values)           */
+
+/* ---- context ------------------------------------------------------------ */
+/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or NULL
+ * for a private stream. */
+int das_ctx_create(int device, void* stream, das_ctx_t** out);
+int das_ctx_destroy(das_ctx_t* ctx);
+const char* das_last_error(const das_ctx_t* ctx);
+int das_ctx_sync(das_ctx_t* ctx);
+int das_version(void);
+
+/* ---- ExpressionHasher (expression_hasher.py:9-35) ------------------------ */
+/* Host-side md5 of one UTF-8 string -> digest (query planning). */
+int das_md5(const uint8_t* bytes, uint64_t n, uint32_t out_digest[4]);
+/* Host-side composite_hash: md5(" ".join(hex(d_0), ..., hex(d_{k-1}))), k>=2;
+ * k==1 returns d_0 (composite_hash([x]) == x). */
+int das_composite_digest(const uint32_t* digests, uint32_t k, uint32_t out_digest[4]);
+/* Device bulk: n strings (device bytes + n+1 offsets) -> n device digests. */
+int das_hash_strings_dev(das_ctx_t* ctx, const uint8_t* d_bytes, const uint64_t* d_off,
+                         uint64_t n, uint32_t* d_out);
+/* Device bulk: n messages, message i = composite of elems[i*k .. i*k+k) (device
+ * digests) -> n device digests.  This is the one-link-per-lane kernel the index
+ * build uses, exposed for the bulk-hash benchmark. */
+int das_hash_fixed_dev(das_ctx_t* ctx, const uint32_t* d_elems, uint32_t k, uint64_t n,
+                       uint32_t* d_out);
+
+/* ---- knowledge-base load + index build ----------------------------------- */
+/* Parsed atoms, host arrays (das_amd.loader.AtomArrays).  "Leaves" are strings
+ * hashed as md5(string): type names (md5(name), named_type_hash) and terminals
+ * ("Type name", terminal_hash).  "Expressions" are composite_hash of their
+ * children (child 0 = the type leaf), listed level by level (children first).
+ * Indices are unified: < n_leaf is a leaf, otherwise n_leaf + expression. */
+typedef struct {
+  uint64_t n_leaf;
+  const uint8_t* leaf_bytes;
+  const uint64_t* leaf_off;        /* n_leaf + 1 */
+  const uint8_t* leaf_kind;        /* 0 type name, 1 node (terminal in `nodes`), 2 other terminal */
+  const uint32_t* leaf_ctype;      /* leaf whose digest is this leaf's composite type */
+  const uint32_t* leaf_type_id;    /* named-type id of a type leaf, DAS_NONE otherwise */
+  uint64_t n_expr;
+  const uint64_t* expr_off;        /* n_expr + 1 */
+  const uint32_t* expr_child;
+  const uint8_t* expr_kind;        /* 1 link (`links_*` collections), 2 typedef (`atom_types`) */
+  const int32_t* expr_ctype_leaf;  /* -1: composite type from children; else that leaf's digest */
+  uint32_t n_levels;
+  const uint64_t* level_off;       /* n_levels + 1, expression ranges per nesting level */
+  uint32_t n_types;
+} das_atoms_t;
+
+typedef struct {
+  uint64_t n_atoms, n_nodes, n_links, n_types, n_ctypes;
+  uint64_t device_bytes;
+  uint64_t links_by_arity[9];
+} das_index_stats_t;
+
+/* Loads + hashes every atom on the GPU and builds the HBM index (replaces the
+ * Mongo insert + key-value files + sort + Redis SADD of canonical_parser.py:
+ * 111-240).  Rebuilds from scratch if called again. */
+int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms);
+int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out);
+
+/* digests -> atom ids (-1 if absent); cat: 0 other, 1 node, 2 link. */
+int das_lookup(das_ctx_t* ctx, const uint32_t* digests, uint64_t n, int64_t* ids,
+               uint8_t* cat, uint32_t* arity, uint32_t* type);
+/* ids -> digests / category / arity / named type id / loader leaf of nodes */
+int das_atoms_info(das_ctx_t* ctx, const uint32_t* ids, uint64_t n, uint32_t* digests,
+                   uint8_t* cat, uint32_t* arity, uint32_t* type, uint32_t* name_leaf);
+/* outgoing set of a link: targets in stored order (get_link_targets) */
+int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, uint32_t* n);
+/* composite-type digest -> ctype id, or -1 (templates:<composite_type_hash>) */
+int das_ctype_lookup(das_ctx_t* ctx, const uint32_t digest[4], int64_t* ctype_id);
+
+/* ---- query operators ----------------------------------------------------- */
+/* One Link with >= 1 wildcard, evaluated against the pattern index
+ * (RedisMongoDB.get_matched_links :235-252 + Link._assign_variables :466-489).
+ * `target[i]`: atom id or DAS_NONE for '*', in the position order the
+ * reference builds its pattern key (sorted for Similarity/Set).  type_id
+ * DAS_NONE means the '*' link type.
+ * ordered: var[i] is the variable id bound at position i (-1 = grounded).
+ * unordered: the variable set is var[0..n_vars) and values are the targets at
+ * wildcard positions (sorted, must be distinct).
+ * emit_link: prepend the link id column (var id -1) for get_matched_links. */
+typedef struct {
+  uint32_t arity;
+  uint32_t type_id;
+  uint32_t target[8];
+  int32_t var[8];
+  uint32_t n_vars;
+  uint32_t ordered;
+  uint32_t no_overload;
+  uint32_t emit_link;
+} das_link_scan_t;
+
+/* LinkTemplate (get_matched_type_template :269-275 + LinkTemplate._assign_variables
+ * :591-601): all links of composite type `ctype_id`, var[i] bound at position i. */
+typedef struct {
+  uint32_t ctype_id;
+  uint32_t arity;
+  int32_t var[8];
+  uint32_t ordered;
+  uint32_t no_overload;
+  uint32_t emit_link;
+} das_template_scan_t;
+
+int das_scan_link(das_ctx_t* ctx, const das_link_scan_t* q, das_table_t** out);
+int das_scan_template(das_ctx_t* ctx, const das_template_scan_t* q, das_table_t** out);
+/* All links of a named type, any arity (get_matched_type :277-279), as
+ * (link id) tables per arity: out[a] for a in 0..8 (NULL where empty). */
+int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9);
+
+/* Ordered natural join (OrderedAssignment.join/_join_ordered :105-139). */
+int das_join(das_ctx_t* ctx, const das_table_t* a, const das_table_t* b, uint32_t no_overload,
+             das_table_t** out);
+/* Rows of `a` that no row of `t` is covered by (check_negation :112-117 over the
+ * forbidden set, And.matched :741-746); also set difference when vars equal. */
+int das_antijoin(das_ctx_t* ctx, const das_table_t* a, const das_table_t* t, das_table_t** out);
+/* Set semantics (Python set of assignments): unique rows. */
+int das_dedup(das_ctx_t* ctx, const das_table_t* a, das_table_t** out);
+/* Concatenate same-schema tables. */
+int das_concat(das_ctx_t* ctx, const das_table_t* const* ts, uint32_t n, das_table_t** out);
+
+int das_table_info(const das_table_t* t, int32_t* kind, int32_t* ncols, int32_t* vars,
+                   uint64_t* nrows);
+/* Copies rows [row0, row0+nrows) column-major into host `out` (ncols*nrows). */
+int das_table_fetch(das_ctx_t* ctx, const das_table_t* t, uint64_t row0, uint64_t nrows,
+                    uint32_t* out);
+/* Device pointer of column c (valid until das_table_free). */
+int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
+/* New ordered table from device/host columns (multi-GPU exchange import). */
+int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,
+                        const uint32_t* cols, uint64_t nrows, das_table_t** out);
+int das_table_free(das_table_t* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DAS_MI355X_H */

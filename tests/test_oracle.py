@@ -1,0 +1,108 @@
+"""The CPU oracle against the reference's own outputs (golden fixtures made by
+running the reference here, tests/golden/make_golden.py) and the handles the
+reference prints (scripts/service_regression_test.sh, service/README.md)."""
+import hashlib
+
+import pytest
+
+from oracle import das_oracle as O
+
+KB_FIXTURES = ["kb_animals.json", "kb_toy_mining.json", "kb_stub_like.json"]
+
+# Appendix C of SURVEY.md; printed by the reference at
+# scripts/service_regression_test.sh:34,43 and service/README.md:290-378
+KNOWN = {
+    ("Concept", "human"): "af12f10f9ae2002a1607ba0b47ba8407",
+    ("Concept", "mammal"): "bdfe4e7a431f73386f37c6448afe5840",
+    ("Concept", "monkey"): "1cdffc6b0b89ff41d68bec237481d1e1",
+    ("Concept", "chimp"): "5b34c54bee150c04f9fa584b899dc030",
+    ("Concept", "snake"): "c1db9b517073e51eb7ef6fed608ec204",
+    ("Concept", "earthworm"): "bb34ce95f161a6b37ff54b3d4c817857",
+    ("Concept", "rhino"): "99d18c702e813b07260baf577c60c455",
+    ("Concept", "triceratops"): "d03e59654221c1e8fcda404fd5c8d6cb",
+    ("Concept", "vine"): "b94941d8cd1c0ee4ad3dd3dcab52b964",
+    ("Concept", "ent"): "4e8e26e3276af8a5c2ac2cc2dc95c6d2",
+    ("Concept", "animal"): "0a32b476852eeb954979b87f5f6cb7af",
+    ("Concept", "reptile"): "b99ae727c787f1b13b452fd4c9ce1b9a",
+    ("Concept", "dinosaur"): "08126b066d32ee37743e255a2558cccd",
+}
+INH_HUMAN_MAMMAL = "c93e1e758c53912638438e2a7d7f7b7f"
+
+
+def test_known_handles():
+    for (t, n), h in KNOWN.items():
+        assert O.terminal_hash(t, n) == h
+    assert O.expression_hash(O.named_type_hash("Inheritance"),
+                             [KNOWN[("Concept", "human")], KNOWN[("Concept", "mammal")]]) == INH_HUMAN_MAMMAL
+
+
+def test_hash_vectors(golden):
+    hv = golden("hash_vectors.json")
+    for s, h in hv["md5"]:
+        assert O.md5hex(s) == h
+    for parts, h in hv["composite"]:
+        assert O.composite_hash(parts) == h
+    for t, n, h in hv["terminal"]:
+        assert O.terminal_hash(t, n) == h
+
+
+def _check(rec, want):
+    if want.get("error"):
+        return rec.get("error") == want["error"]
+    return rec.get("error") is None and all(rec[k] == want[k] for k in ("matched", "negation", "n", "sha256"))
+
+
+@pytest.mark.parametrize("fixture", KB_FIXTURES)
+def test_oracle_matches_reference_db_path(golden, fixture):
+    d = golden(fixture)
+    kb = O.KB.from_tables(d["nodes"], d["links"])
+    db = O.RedisMongoSemantics(kb, tuple_targets=True)
+    assert list(db.count_atoms()) == d["count_atoms"]
+    bad = [q["query"] for q in d["queries"] if not _check(O.evaluate(q["query"], db), q)]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("fixture", KB_FIXTURES)
+def test_oracle_list_targets_agree_where_reference_succeeds(golden, fixture):
+    d = golden(fixture)
+    db = O.RedisMongoSemantics(O.KB.from_tables(d["nodes"], d["links"]), tuple_targets=False)
+    for q in d["queries"]:
+        if not q.get("error"):
+            assert _check(O.evaluate(q["query"], db), q), q["query"]
+
+
+def test_oracle_index_probes(golden):
+    d = golden("kb_animals.json")
+    db = O.RedisMongoSemantics(O.KB.from_tables(d["nodes"], d["links"]))
+    for p in d["index"]:
+        if p["kind"] == "links":
+            r = db.get_matched_links(*p["args"])
+        elif p["kind"] == "template":
+            r = db.get_matched_type_template(p["args"])
+        else:
+            r = db.get_matched_type(p["args"])
+        assert sorted(x if isinstance(x, str) else x[0] for x in r) == p["handles"], p["args"]
+
+
+def test_oracle_matches_reference_stubdb(golden):
+    d = golden("stubdb.json")
+    db = O.StubSemantics(d["nodes"], d["links"])
+    bad = [q["query"] for q in d["queries"] if not _check(O.evaluate(q["query"], db), q)]
+    assert not bad, bad
+
+
+def test_readme_examples(golden):
+    """service/README.md:286-378 answer sizes (query strings -> expressions)."""
+    d = golden("kb_animals.json")
+    db = O.RedisMongoSemantics(O.KB.from_tables(d["nodes"], d["links"]))
+    V = lambda n: ["Var", n]  # noqa: E731
+    inh = lambda a, b: ["Link", "Inheritance", True, [a, b]]  # noqa: E731
+    mammal, human = ["Node", "Concept", "mammal"], ["Node", "Concept", "human"]
+    q1 = ["And", [inh(V("$1"), V("$2")), inh(V("$2"), V("$3"))]]
+    q2 = ["And", [["Not", inh(V("$1"), mammal)], inh(V("$1"), V("$2")), inh(V("$2"), V("$3"))]]
+    q3 = ["Or", [["And", [inh(V("$1"), V("$2")), inh(V("$2"), V("$3")), ["Not", inh(V("$1"), mammal)]]],
+                 inh(human, V("$2"))]]
+    assert O.evaluate(q1, db)["n"] == 7
+    assert O.evaluate(q2, db)["n"] == 3
+    assert O.evaluate(q3, db)["n"] == 4
+    assert O.evaluate(["Link", "Similarity", False, [V("$1"), V("$2")]], db)["n"] == 7
