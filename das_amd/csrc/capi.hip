@@ -1,6 +1,7 @@
 // extern "C" boundary (include/das_mi355x.h).  Every entry point catches
 // das::Error / std::exception and returns a status; the message is kept per
 // context for das_last_error.
+#include <cstdlib>
 #include <cstring>
 
 #include "das_internal.h"
@@ -28,6 +29,16 @@ int fail(das_ctx_t* ctx, int code, const std::string& msg) {
   return code;
 }
 
+// DAS_SYNC_CHECK=1: synchronise after every entry point so an asynchronous
+// kernel fault is reported by the call that launched it (debug builds of a run).
+bool sync_check() {
+  static const bool on = [] {
+    const char* e = std::getenv("DAS_SYNC_CHECK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 template <typename F>
 int guarded(das_ctx_t* ctx, F&& f) {
   try {
@@ -35,6 +46,10 @@ int guarded(das_ctx_t* ctx, F&& f) {
       std::lock_guard<std::mutex> lk(ctx->c.mu);
       DAS_HIP(hipSetDevice(ctx->c.device));
       f();
+      if (sync_check()) {
+        DAS_HIP(hipStreamSynchronize(ctx->c.s));
+        DAS_HIP(hipGetLastError());
+      }
     } else {
       f();
     }

@@ -328,7 +328,7 @@ uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hi
   if (n) {
     hipLaunchKernelGGL((k_run_flags<K>), G(n), dim3(B), 0, s, key, n, f.p);
     exclusive_scan<uint32_t>(f.p, n, scan.p, s);
-    m = (uint64_t)read_u32(scan.p + n - 1, s) + 1;
+    m = (uint64_t)read_u32(scan.p + n - 1, s) + read_u32(f.p + n - 1, s);
   }
   *ukey = dalloc<K>(idx, m);
   *uoff = dalloc<uint64_t>(idx, m + 1);

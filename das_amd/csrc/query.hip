@@ -465,6 +465,7 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
       if (best == 0) return empty();
     }
   }
+  DAS_CHECK(rt && begin <= end && end <= rt->rows, DAS_E_INTERNAL, "scan range outside its table");
   set_cols(sp, *rt);
   bool filt = false;
   for (uint32_t p = 0; p < ar; ++p) filt |= sp.fixed[p] != kNone;
@@ -510,6 +511,7 @@ std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
   }
   sp.nout = ncols;
   const int kind = q.ordered ? DAS_TABLE_ORDERED : DAS_TABLE_UNORDERED;
+  DAS_CHECK(cr.begin <= cr.end && cr.end <= idx.ctab[cr.arity].rows, DAS_E_INTERNAL, "template range outside its table");
   set_cols(sp, idx.ctab[cr.arity]);
   sp.all_keep = sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
   return run_scan(c, sp, cr.begin, cr.end, kind, ncols, vars);
