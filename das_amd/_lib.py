@@ -99,6 +99,10 @@ _SIGS = {
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
     "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
     "das_table_free": (C.c_int, [P]),
+    "das_prof_enable": (C.c_int, [P, C.c_int]),
+    "das_prof_reset": (C.c_int, [P]),
+    "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
+    "das_prof_names": (C.c_int, [P, P, C.c_uint64]),
 }
 
 _lib = None
@@ -343,6 +347,24 @@ class Context:
         v = (C.c_int32 * len(vars_))(*vars_)
         n = cols.shape[1] if cols.ndim == 2 else 0
         return self._table(lib().das_table_from_host, kind, len(vars_), v, ptr(cols), n)
+
+    def prof_enable(self, on=True):
+        check(lib().das_prof_enable(self.h, 1 if on else 0), self.h)
+
+    def prof_reset(self):
+        check(lib().das_prof_reset(self.h), self.h)
+
+    def prof_stats(self):
+        buf = C.create_string_buffer(1 << 16)
+        check(lib().das_prof_names(self.h, buf, len(buf)), self.h)
+        out = {}
+        for name in buf.value.decode().split("\n"):
+            if not name:
+                continue
+            ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+            check(lib().das_prof_read(self.h, name.encode(), C.byref(ms), C.byref(n), C.byref(b)), self.h)
+            out[name] = {"ms": ms.value, "launches": n.value, "bytes": b.value}
+        return out
 
     def sync(self):
         check(lib().das_ctx_sync(self.h), self.h)

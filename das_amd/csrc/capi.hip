@@ -365,4 +365,58 @@ int das_table_free(das_table_t* t) {
   return DAS_OK;
 }
 
+int das_prof_enable(das_ctx_t* ctx, int on) {
+  return guarded(ctx, [&] {
+    das::prof_collect(ctx->c);
+    ctx->c.prof = on != 0;
+  });
+}
+
+int das_prof_reset(das_ctx_t* ctx) {
+  return guarded(ctx, [&] {
+    das::prof_collect(ctx->c);
+    ctx->c.kstats.clear();
+  });
+}
+
+int das_prof_read(das_ctx_t* ctx, const char* name, double* ms, uint64_t* launches, double* bytes) {
+  return guarded(ctx, [&] {
+    das::prof_collect(ctx->c);
+    auto it = ctx->c.kstats.find(name);
+    das::KStat z;
+    const das::KStat& k = it == ctx->c.kstats.end() ? z : it->second;
+    *ms = k.ms;
+    *launches = k.launches;
+    *bytes = k.bytes;
+  });
+}
+
+int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap) {
+  return guarded(ctx, [&] {
+    das::prof_collect(ctx->c);
+    std::string all;
+    for (auto& kv : ctx->c.kstats) all += kv.first + "\n";
+    DAS_CHECK(all.size() + 1 <= cap, das::DAS_E_INVALID, "buffer too small");
+    std::memcpy(buf, all.c_str(), all.size() + 1);
+  });
+}
+
 }  // extern "C"
+
+namespace das {
+void prof_collect(Ctx& c) {
+  if (c.pending.empty()) return;
+  DAS_HIP(hipStreamSynchronize(c.s));
+  for (auto& p : c.pending) {
+    float ms = 0;
+    DAS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    KStat& k = c.kstats[p.name];
+    k.ms += ms;
+    k.bytes += p.bytes;
+    k.launches += 1;
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  c.pending.clear();
+}
+}  // namespace das

@@ -77,7 +77,22 @@ struct Table {
   }
 };
 
+// Per-kernel timing with HIP events on the ctx stream (das_prof_*): what
+// bench.py's roofline figures are computed from.
+struct KStat {
+  double ms = 0, bytes = 0;
+  uint64_t launches = 0;
+};
+struct PendingEv {
+  std::string name;
+  hipEvent_t a, b;
+  double bytes;
+};
+
 struct Ctx {
+  bool prof = false;
+  std::vector<PendingEv> pending;
+  std::map<std::string, KStat> kstats;
   int device = 0;
   hipStream_t s = nullptr;
   bool own_stream = false;
@@ -89,6 +104,25 @@ struct Ctx {
   std::vector<uint8_t> leaf_bytes;
   std::vector<uint64_t> leaf_off;
 };
+
+struct ProfScope {
+  Ctx& c;
+  const char* name;
+  double bytes;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(Ctx& ctx, const char* n, double algorithmic_bytes) : c(ctx), name(n), bytes(algorithmic_bytes) {
+    if (!c.prof) return;
+    DAS_HIP(hipEventCreate(&a));
+    DAS_HIP(hipEventCreate(&b));
+    DAS_HIP(hipEventRecord(a, c.s));
+  }
+  ~ProfScope() {
+    if (!c.prof || !a) return;
+    (void)hipEventRecord(b, c.s);
+    c.pending.push_back(PendingEv{name, a, b, bytes});
+  }
+};
+void prof_collect(Ctx& c);
 
 // hash.hip
 void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, Digest* out, hipStream_t s);

@@ -135,6 +135,27 @@ __global__ void __launch_bounds__(B) k_scan_write(ScanSpec sp, uint64_t begin, u
   }
 }
 
+// Pure projection (a scan with no predicate): out column c = source column
+// outpos[c] over [begin, end).  16-byte loads/stores where alignment allows.
+__global__ void __launch_bounds__(B) k_project(ScanSpec sp, uint64_t begin, uint64_t n, uint32_t* out, uint64_t cap) {
+  const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint32_t c = 0; c < sp.nout; ++c) {
+    const uint32_t* src = sp.col[1 + sp.outpos[c]] + begin;
+    uint32_t* dst = out + c * cap;
+    const bool vec = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+    if (vec) {
+      const uint64_t n4 = n >> 2;
+      const uint4* s4 = reinterpret_cast<const uint4*>(src);
+      uint4* d4 = reinterpret_cast<uint4*>(dst);
+      for (uint64_t i = tid; i < n4; i += stride) d4[i] = s4[i];
+      for (uint64_t i = (n4 << 2) + tid; i < n; i += stride) dst[i] = src[i];
+    } else {
+      for (uint64_t i = tid; i < n; i += stride) dst[i] = src[i];
+    }
+  }
+}
+
 // Range lookup in a P_{a,p} key array: [lower_bound(lo), lower_bound(hi)) -> rows.
 __global__ void k_key_ranges(const uint64_t* ukey, const uint64_t* uoff, uint64_t nkeys, const uint64_t* qlo,
                              const uint64_t* qhi, uint32_t nq, uint64_t* out) {
@@ -250,6 +271,119 @@ __global__ void k_gather_cols(ColSet src, const uint32_t* idx, uint64_t n, uint3
   }
 }
 
+// ---------------------------------------------------------------------------
+// Direct-address join on one shared variable (atom ids are dense):
+//   build  k_key_minmax -> k_key_hist -> scan -> k_key_scatter   (counting sort)
+//   probe  k_dj_count (per-tile output totals) -> scan -> k_dj_write
+// k_dj_write processes 256 probe rows per round: their bucket sizes are
+// prefix-summed in LDS and the round's outputs are written by all 256 threads
+// (output o -> row by an 8-step LDS search), so fan-out is balanced inside the
+// round and every output column is stored coalesced.
+// ---------------------------------------------------------------------------
+constexpr int kDjItems = 16;
+constexpr uint64_t kDjTile = (uint64_t)B * kDjItems;
+
+__global__ void k_key_minmax(const uint32_t* key, uint64_t n, uint32_t* mm) {
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = key[i];
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if (__lane_id() == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+__global__ void k_key_hist(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cnt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[key[i] - kmin], 1u);
+}
+
+__global__ void k_key_scatter(ColSet src, const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cursor,
+                              uint32_t* out, uint64_t cap) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t pos = atomicAdd(&cursor[key[i] - kmin], 1u);
+    for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
+  }
+}
+
+__device__ __forceinline__ uint32_t dj_bucket(const uint32_t* off, uint32_t range, uint32_t kmin, uint32_t k,
+                                              uint32_t& lo) {
+  const uint32_t d = k - kmin;             // wraps for k < kmin
+  if (d >= range) { lo = 0; return 0; }
+  lo = off[d];
+  return off[d + 1] - lo;
+}
+
+__global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
+                                                const uint32_t* off, uint64_t* tile_tot) {
+  __shared__ uint64_t s_w[B / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
+  uint64_t acc = 0;
+  for (int it = 0; it < kDjItems; ++it) {
+    const uint64_t r = t0 + (uint64_t)it * B + threadIdx.x;
+    if (r < np) {
+      uint32_t lo;
+      acc += dj_bucket(off, range, kmin, pkey[r], lo);
+    }
+  }
+  acc = wave_reduce_sum(acc);
+  if (__lane_id() == 0) s_w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_tot[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// om.side[c]: 0 = probe column (staged in LDS), 1 = build column (bucket rows)
+__global__ void __launch_bounds__(B) k_dj_write(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
+                                                const uint32_t* off, const uint64_t* tile_off, OutMap om,
+                                                uint32_t* out, uint64_t cap) {
+  __shared__ uint64_t s_pref[B + 1];
+  __shared__ uint32_t s_lo[B];
+  __shared__ uint32_t s_pv[kMaxCols][B];
+  __shared__ uint64_t s_wave[B / 64];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
+  uint64_t base = tile_off[blockIdx.x];
+  for (int it = 0; it < kDjItems; ++it) {
+    const uint64_t r = t0 + (uint64_t)it * B + tid;
+    uint32_t lo = 0, cnt = 0;
+    if (r < np) cnt = dj_bucket(off, range, kmin, pkey[r], lo);
+    s_lo[tid] = lo;
+    for (int c = 0; c < om.n; ++c)
+      if (!om.side[c]) s_pv[c][tid] = (r < np && cnt) ? om.col[c][r] : 0u;
+    const uint64_t inc = wave_inclusive_scan((uint64_t)cnt);
+    if (__lane_id() == 63) s_wave[wave] = inc;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (int w = 0; w < wave; ++w) pre += s_wave[w];
+    s_pref[tid] = pre + inc - cnt;
+    if (tid == B - 1) s_pref[B] = pre + inc;
+    __syncthreads();
+    const uint64_t total = s_pref[B];
+    for (uint64_t o = tid; o < total; o += B) {
+      int a = 0, b = B;                      // last t with s_pref[t] <= o
+      while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (s_pref[m] <= o) a = m; else b = m;
+      }
+      const uint64_t j = o - s_pref[a];
+      const uint64_t pos = base + o;
+      for (int c = 0; c < om.n; ++c)
+        out[(uint64_t)c * cap + pos] = om.side[c] ? om.col[c][s_lo[a] + j] : s_pv[c][a];
+    }
+    base += total;
+    __syncthreads();
+  }
+}
+
 ColSet cols_of(const Table& t) {
   ColSet s{};
   s.n = t.ncols;
@@ -333,19 +467,24 @@ std::unique_ptr<Table> run_scan(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t e
   if (sp.all_keep) {
     auto t = new_table(c, kind, ncols, vars, n);
     t->nrows = n;
-    if (!sp.unordered) {   // pure projection: column copies
-      for (uint32_t k = 0; k < sp.nout; ++k)
-        DAS_HIP(hipMemcpyAsync(t->col(k), sp.col[1 + sp.outpos[k]] + begin, 4 * n, hipMemcpyDeviceToDevice, c.s));
+    if (!sp.unordered) {   // pure projection
+      ProfScope ps(c, "k_project", 8.0 * sp.nout * n);
+      hipLaunchKernelGGL(k_project, dim3(grid_for(n / 4 + 1, B, 2048)), dim3(B), 0, c.s, sp, begin, n, t->data, t->cap);
+      DAS_HIP(hipGetLastError());
       return t;
     }
+    ProfScope ps(c, "k_scan_write", 4.0 * n * (sp.arity + 1) + 4.0 * n * sp.nout);
     hipLaunchKernelGGL(k_scan_write, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, (const uint32_t*)nullptr,
                        t->data, t->cap);
     DAS_HIP(hipGetLastError());
     return t;
   }
   DBuf<uint32_t> cnt(chunks, c.s), off(chunks, c.s);
-  hipLaunchKernelGGL(k_scan_count, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, cnt.p);
-  DAS_HIP(hipGetLastError());
+  {
+    ProfScope ps(c, "k_scan_count", 4.0 * n * sp.arity);
+    hipLaunchKernelGGL(k_scan_count, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, cnt.p);
+    DAS_HIP(hipGetLastError());
+  }
   exclusive_scan<uint32_t>(cnt.p, chunks, off.p, c.s);
   uint32_t h[2];
   DAS_HIP(hipMemcpyAsync(&h[0], off.p + chunks - 1, 4, hipMemcpyDeviceToHost, c.s));
@@ -355,6 +494,7 @@ std::unique_ptr<Table> run_scan(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t e
   auto t = new_table(c, kind, ncols, vars, m);
   t->nrows = m;
   if (m) {
+    ProfScope ps(c, "k_scan_write", 4.0 * n * (sp.arity + 1) + 4.0 * m * sp.nout);
     hipLaunchKernelGGL(k_scan_write, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, (const uint32_t*)off.p,
                        t->data, t->cap);
     DAS_HIP(hipGetLastError());
@@ -520,6 +660,75 @@ std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
 // ---------------------------------------------------------------------------
 // Join, antijoin, dedup, concat
 // ---------------------------------------------------------------------------
+// Direct-address join on a single shared variable; nullptr if the build key
+// range is too sparse for a dense offsets array (caller falls back to sort +
+// binary search).
+std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32_t var,
+                                   const std::vector<int32_t>& uni) {
+  auto colof = [](const Table& t, int32_t v) {
+    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+    return -1;
+  };
+  const uint32_t* qkey = Q.col(colof(Q, var));
+  const uint32_t* pkey = P.col(colof(P, var));
+  DBuf<uint32_t> mm(2, c.s);
+  const uint32_t init[2] = {0xFFFFFFFFu, 0u};
+  DAS_HIP(hipMemcpyAsync(mm.p, init, 8, hipMemcpyHostToDevice, c.s));
+  hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(Q.nrows, B, 1024)), dim3(B), 0, c.s, qkey, Q.nrows, mm.p);
+  uint32_t h[2];
+  DAS_HIP(hipMemcpyAsync(h, mm.p, 8, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipStreamSynchronize(c.s));
+  const uint64_t range = (uint64_t)h[1] - h[0] + 1;
+  if (range > std::max<uint64_t>(8 * Q.nrows, 1ull << 26) || range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
+    return nullptr;
+  const uint32_t kmin = h[0];
+  // counting sort of the build side by key
+  DBuf<uint32_t> cnt(range + 1, c.s), off(range + 1, c.s);
+  std::unique_ptr<Table> Qs;
+  {
+    ProfScope ps(c, "join_build", 4.0 * Q.nrows * (Q.ncols + 1) + 8.0 * range);
+    DAS_HIP(hipMemsetAsync(cnt.p, 0, 4 * (range + 1), c.s));
+    hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, cnt.p);
+    exclusive_scan<uint32_t>(cnt.p, range + 1, off.p, c.s);
+    DAS_HIP(hipMemcpyAsync(cnt.p, off.p, 4 * (range + 1), hipMemcpyDeviceToDevice, c.s));
+    Qs = new_table(c, Q.kind, Q.ncols, Q.vars, Q.nrows);
+    Qs->nrows = Q.nrows;
+    hipLaunchKernelGGL(k_key_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin, cnt.p, Qs->data,
+                       Qs->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  // probe: per-tile totals -> scan -> fused write
+  const uint64_t tiles = (P.nrows + kDjTile - 1) / kDjTile;
+  DBuf<uint64_t> tot(tiles + 1, c.s), toff(tiles + 1, c.s);
+  {
+    ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
+    hipLaunchKernelGGL(k_dj_count, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
+                       (const uint32_t*)off.p, tot.p);
+    DAS_HIP(hipGetLastError());
+  }
+  DAS_HIP(hipMemsetAsync(tot.p + tiles, 0, 8, c.s));
+  exclusive_scan<uint64_t>(tot.p, tiles + 1, toff.p, c.s);
+  const uint64_t total = read_u64(toff.p + tiles, c.s);
+  const int nu = (int)uni.size();
+  auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
+  out->nrows = total;
+  if (total) {
+    OutMap om{};
+    om.n = nu;
+    for (int k = 0; k < nu; ++k) {
+      int ip = colof(P, uni[k]);
+      if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
+      else { om.col[k] = Qs->col(colof(*Qs, uni[k])); om.side[k] = 1; }
+    }
+    // algorithmic bytes: probe payload + build payload + output
+    ProfScope ps(c, "k_dj_write", 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
+    hipLaunchKernelGGL(k_dj_write, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
+                       (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return out;
+}
+
 std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {
   DAS_CHECK(A.kind == DAS_TABLE_ORDERED && Bt.kind == DAS_TABLE_ORDERED, DAS_E_UNSUPPORTED,
             "join: unordered operands are not supported by this build");
@@ -550,15 +759,21 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
       else { om.col[k] = Q.col(colof(Q, uni[k])); om.side[k] = 1; }
     }
+    ProfScope ps(c, "k_cartesian", 4.0 * nu * total);
     hipLaunchKernelGGL(k_cartesian, G(total), dim3(B), 0, c.s, om, Q.nrows, total, out->data, out->cap);
     DAS_HIP(hipGetLastError());
+  } else if (shared.size() == 1 && (out = direct_join(c, P, Q, shared[0], uni))) {
+    // direct-address path taken
   } else {
     // sort build rows by the shared columns
     ColSet qk{};
     qk.n = (int)shared.size();
     for (int k = 0; k < qk.n; ++k) qk.c[k] = Q.col(colof(Q, shared[k]));
     DBuf<uint32_t> perm(Q.nrows, c.s);
-    sort_perm(qk, Q.nrows, perm.p, id_bits(c), c.s);
+    {
+      ProfScope ps(c, "join_build_sort", 4.0 * Q.nrows * (Q.ncols + 2));
+      sort_perm(qk, Q.nrows, perm.p, id_bits(c), c.s);
+    }
     auto Qs = gather_table(c, Q, perm.p, Q.nrows);
     perm.release();
     ColSet qks{}, pk{};
@@ -569,8 +784,11 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
     }
     DBuf<uint32_t> lo(P.nrows, c.s), cnt(P.nrows, c.s);
     DBuf<uint64_t> offs(P.nrows + 1, c.s);
-    hipLaunchKernelGGL(k_join_count, G(P.nrows), dim3(B), 0, c.s, pk, P.nrows, qks, Qs->nrows, lo.p, cnt.p);
-    DAS_HIP(hipGetLastError());
+    {
+      ProfScope ps(c, "k_join_count", 4.0 * P.nrows * (pk.n + 2));
+      hipLaunchKernelGGL(k_join_count, G(P.nrows), dim3(B), 0, c.s, pk, P.nrows, qks, Qs->nrows, lo.p, cnt.p);
+      DAS_HIP(hipGetLastError());
+    }
     exclusive_scan_fn<uint64_t>(WidenCnt{cnt.p, P.nrows}, P.nrows + 1, offs.p, c.s);
     const uint64_t total = read_u64(offs.p + P.nrows, c.s);
     out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
@@ -583,6 +801,8 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
         if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
         else { om.col[k] = Qs->col(colof(*Qs, uni[k])); om.side[k] = 1; }
       }
+      // algorithmic: the join's output, |O| x 4 B x k_out
+      ProfScope ps(c, "k_join_expand", 4.0 * nu * total);
       hipLaunchKernelGGL(k_join_expand, G(total), dim3(B), 0, c.s, (const uint64_t*)offs.p, P.nrows,
                          (const uint32_t*)lo.p, om, total, out->data, out->cap);
       DAS_HIP(hipGetLastError());
@@ -625,7 +845,10 @@ std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
   ak.n = T.ncols;
   for (int k = 0; k < T.ncols; ++k) ak.c[k] = A.col(A.kind == DAS_TABLE_ORDERED ? colof(A, T.vars[k]) : k);
   DBuf<uint32_t> keep(A.nrows, c.s);
-  hipLaunchKernelGGL(k_anti_flags, G(A.nrows), dim3(B), 0, c.s, ak, A.nrows, tks, Ts->nrows, keep.p);
+  {
+    ProfScope ps(c, "k_anti_flags", 4.0 * A.nrows * (T.ncols + 1));
+    hipLaunchKernelGGL(k_anti_flags, G(A.nrows), dim3(B), 0, c.s, ak, A.nrows, tks, Ts->nrows, keep.p);
+  }
   DAS_HIP(hipGetLastError());
   return compact_table(c, A, keep.p);
 }

@@ -175,6 +175,14 @@ int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32
                         const uint32_t* cols, uint64_t nrows, das_table_t** out);
 int das_table_free(das_table_t* t);
 
+/* ---- measurement ---------------------------------------------------------- */
+/* Per-kernel HIP-event timing on the context stream (bench.py roofline):
+ * totals of elapsed ms, launches and algorithmic bytes since the last reset. */
+int das_prof_enable(das_ctx_t* ctx, int on);
+int das_prof_reset(das_ctx_t* ctx);
+int das_prof_read(das_ctx_t* ctx, const char* name, double* ms, uint64_t* launches, double* bytes);
+int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif
