@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--inheritance", type=int, default=100_000)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
     return ap.parse_args()
 
 
@@ -99,11 +100,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
+    # DAS_BENCH_SAME_DEVICE=1 + DAS_DIST_BACKEND=gloo rehearse N ranks on one GPU
+    if os.environ.get("DAS_BENCH_SAME_DEVICE") == "1":
+        local_rank = 0
+    backend = os.environ.get("DAS_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
@@ -123,7 +131,7 @@ def main():
     qs = queries(pm, rank_genes, args.bps, seed=17)
     if world > 1:
         from das_amd import parallel
-        engine = parallel.ShardedMatcher(db, dist)
+        engine = parallel.ShardedMatcher(db, dist, cpu_staging=(backend != "nccl"))
 
         def run(q):
             return engine.count(q)
@@ -154,11 +162,21 @@ def main():
     elapsed = time.perf_counter() - t0
     db.ctx.prof_enable(False)
     stats = db.ctx.prof_stats()
+    if args.cprofile and rank == 0:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(3):
+            step()
+        pr.disable()
+        with open(args.cprofile, "w") as f:
+            pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        b = torch.tensor([bindings], dtype=torch.float64, device="cuda")
+        b = torch.tensor([bindings], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(b)
         bindings = float(b.item())
     value = bindings / elapsed

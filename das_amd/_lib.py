@@ -99,6 +99,9 @@ _SIGS = {
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
     "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
     "das_table_free": (C.c_int, [P]),
+    "das_partition": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P), P]),
+    "das_table_export_rows": (C.c_int, [P, P, P]),
+    "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
@@ -347,6 +350,20 @@ class Context:
         v = (C.c_int32 * len(vars_))(*vars_)
         n = cols.shape[1] if cols.ndim == 2 else 0
         return self._table(lib().das_table_from_host, kind, len(vars_), v, ptr(cols), n)
+
+    def partition(self, t, key_vars, nparts):
+        kv = (C.c_int32 * max(len(key_vars), 1))(*key_vars)
+        counts = np.zeros(nparts, dtype=np.uint64)
+        out = P()
+        check(lib().das_partition(self.h, t.h, kv, len(key_vars), nparts, C.byref(out), ptr(counts)), self.h)
+        return Table(self, out), counts
+
+    def export_rows(self, t, dptr):
+        check(lib().das_table_export_rows(self.h, t.h, dptr), self.h)
+
+    def import_rows(self, kind, vars_, dptr, nrows):
+        v = (C.c_int32 * max(len(vars_), 1))(*vars_)
+        return self._table(lib().das_table_import_rows, kind, len(vars_), v, dptr, nrows)
 
     def prof_enable(self, on=True):
         check(lib().das_prof_enable(self.h, 1 if on else 0), self.h)

@@ -108,6 +108,14 @@ int das_ctx_create(int device, void* stream, das_ctx_t** out) {
     DAS_HIP(hipGetDeviceProperties(&prop, device));
     DAS_CHECK(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, das::DAS_E_UNSUPPORTED,
               std::string("this build targets gfx950 (MI355X), device is ") + prop.gcnArchName);
+    // keep freed stream-ordered allocations in the pool: the query operators
+    // allocate per call, and returning memory to the OS at each sync costs more
+    // than the kernels on small queries
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     ctx = new das_ctx_t;
     ctx->c.device = device;
     if (stream) {
@@ -363,6 +371,20 @@ int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32
 int das_table_free(das_table_t* t) {
   delete t;
   return DAS_OK;
+}
+
+int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
+                  das_table_t** out, uint64_t* counts) {
+  return guarded(ctx, [&] { *out = wrap(das::partition(ctx->c, t->t, key_vars, nkey, nparts, counts)); });
+}
+
+int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst) {
+  return guarded(ctx, [&] { das::export_rows(ctx->c, t->t, d_dst); });
+}
+
+int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const uint32_t* d_src,
+                          uint64_t nrows, das_table_t** out) {
+  return guarded(ctx, [&] { *out = wrap(das::import_rows(ctx->c, kind, ncols, vars, d_src, nrows)); });
 }
 
 int das_prof_enable(das_ctx_t* ctx, int on) {

@@ -19,7 +19,14 @@ constexpr int kMaxPosArity = 3;   // per-position (pattern) index: arity 1..3, a
 constexpr int kMaxCols = 16;      // columns in a binding table
 constexpr int kTypeBits = 24;     // P-index key = target << 24 | named-type id
 
-enum AtomCat : uint8_t { CAT_OTHER = 0, CAT_NODE = 1, CAT_LINK = 2 };
+// External category codes (das_lookup): a remote link is an atom of the global
+// id space whose index rows live on another shard (multi-GPU).
+enum AtomCat : uint8_t { CAT_OTHER = 0, CAT_NODE = 1, CAT_LINK = 2, CAT_LINK_REMOTE = 3 };
+// Priority when several loader entries share a digest (a local link wins).
+enum CatPrio : uint8_t { PRIO_OTHER = 0, PRIO_NODE = 1, PRIO_REMOTE = 2, PRIO_LINK = 3 };
+__host__ __device__ inline uint8_t cat_of_prio(uint32_t p) {
+  return p == PRIO_LINK ? CAT_LINK : p == PRIO_REMOTE ? CAT_LINK_REMOTE : p == PRIO_NODE ? CAT_NODE : CAT_OTHER;
+}
 
 // Rows (link id, t0 .. t_{a-1}) stored column-major: column c at data + c*rows.
 struct RowTable {
@@ -61,6 +68,7 @@ struct Index {
   std::vector<Digest> ctype_digest;                            // host: sorted ctype digests
   std::vector<CtypeRange> ctype_range;                         // host
   std::vector<void*> owned;                                    // device allocations
+  std::map<std::array<uint64_t, 4>, std::pair<uint64_t, uint64_t>> range_cache;   // P lookups
   uint64_t device_bytes = 0;
 };
 
@@ -144,5 +152,9 @@ std::unique_ptr<Table> antijoin(Ctx& c, const Table& a, const Table& t);
 std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);
 std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap);
+std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
+                                 uint64_t* counts);
+void export_rows(Ctx& c, const Table& t, uint32_t* dst);
+std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const uint32_t* src, uint64_t n);
 
 }  // namespace das

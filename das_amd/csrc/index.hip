@@ -70,12 +70,15 @@ __global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, u
                            uint8_t* catl, uint32_t* flag) {
   const uint64_t n = n_leaf + n_expr;
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x) {
-    uint8_t c = CAT_OTHER;
+    uint8_t c = PRIO_OTHER;
     uint32_t f = 0;
     if (u < n_leaf) {
-      if (leaf_kind[u] == 1) { c = CAT_NODE; f = 1; }
+      if (leaf_kind[u] == 1) { c = PRIO_NODE; f = 1; }
     } else if (expr_kind[u - n_leaf] == 1) {
-      c = CAT_LINK;
+      c = PRIO_LINK;
+      f = 1;
+    } else if (expr_kind[u - n_leaf] == 3) {
+      c = PRIO_REMOTE;
       f = 1;
     }
     catl[u] = c;
@@ -86,7 +89,7 @@ __global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, u
 __global__ void k_mark_targets(const uint8_t* expr_kind, const uint64_t* off, const uint32_t* child, uint64_t n_expr,
                                uint32_t* flag) {
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_expr; j += (uint64_t)gridDim.x * blockDim.x) {
-    if (expr_kind[j] != 1) continue;
+    if (expr_kind[j] != 1 && expr_kind[j] != 3) continue;
     for (uint64_t k = off[j] + 1; k < off[j + 1]; ++k) flag[child[k]] = 1;
   }
 }
@@ -152,17 +155,17 @@ __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32
   for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
        id += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = rep[id];
-    const uint32_t c = catmax[id];
+    const uint8_t c = cat_of_prio(catmax[id]);
     a_dig[id] = dig[u];
     a_ct[id] = ct[u];
-    a_cat[id] = (uint8_t)c;
+    a_cat[id] = c;
     uint32_t ty = kNone, ar = 0, nl = kNone;
     if (u < n_leaf) {
       ty = leaf_type_id[leaf_ctype[u]];
       if (c == CAT_NODE) nl = u;
     } else {
       const uint64_t j = u - n_leaf;
-      if (c == CAT_LINK) {
+      if (c == CAT_LINK || c == CAT_LINK_REMOTE) {
         ty = leaf_type_id[expr_child[expr_off[j]]];
         ar = (uint32_t)(expr_off[j + 1] - expr_off[j] - 1);
       }
@@ -178,7 +181,7 @@ __global__ void k_fill_targets(uint64_t n_atoms, const uint32_t* rep, const uint
                                const uint32_t* local2id, uint32_t* tgt) {
   for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
        id += (uint64_t)gridDim.x * blockDim.x) {
-    if (a_cat[id] != CAT_LINK) continue;
+    if (a_cat[id] != CAT_LINK && a_cat[id] != CAT_LINK_REMOTE) continue;
     const uint64_t j = rep[id] - n_leaf;
     const uint64_t b = expr_off[j] + 1, e = expr_off[j + 1];
     uint64_t o = tgt_off[id];
@@ -346,6 +349,7 @@ uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hi
 
 void free_index(Index& idx) {
   for (void* p : idx.owned) (void)hipFree(p);
+  idx.owned.clear();
   idx = Index();
 }
 

@@ -584,15 +584,24 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
       const uint64_t t = q.target[p];
       uint64_t qlo = (t << kTypeBits) | (q.type_id == kNone ? 0 : q.type_id);
       uint64_t qhi = q.type_id == kNone ? ((t + 1) << kTypeBits) : qlo + 1;
-      DBuf<uint64_t> dq(2, c.s), dr(2, c.s);
-      uint64_t hq[2] = {qlo, qhi};
-      DAS_HIP(hipMemcpyAsync(dq.p, hq, 16, hipMemcpyHostToDevice, c.s));
-      hipLaunchKernelGGL(k_key_ranges, dim3(1), dim3(64), 0, c.s, (const uint64_t*)P.ukey, (const uint64_t*)P.uoff,
-                         P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + 1, 1u, dr.p);
-      DAS_HIP(hipGetLastError());
       uint64_t hr[2];
-      DAS_HIP(hipMemcpyAsync(hr, dr.p, 16, hipMemcpyDeviceToHost, c.s));
-      DAS_HIP(hipStreamSynchronize(c.s));
+      const std::array<uint64_t, 4> ck{ar, p, qlo, qhi};
+      auto hit = idx.range_cache.find(ck);
+      if (hit != idx.range_cache.end()) {
+        hr[0] = hit->second.first;
+        hr[1] = hit->second.second;
+      } else {
+        DBuf<uint64_t> dq(2, c.s), dr(2, c.s);
+        uint64_t hq[2] = {qlo, qhi};
+        DAS_HIP(hipMemcpyAsync(dq.p, hq, 16, hipMemcpyHostToDevice, c.s));
+        hipLaunchKernelGGL(k_key_ranges, dim3(1), dim3(64), 0, c.s, (const uint64_t*)P.ukey, (const uint64_t*)P.uoff,
+                           P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + 1, 1u, dr.p);
+        DAS_HIP(hipGetLastError());
+        DAS_HIP(hipMemcpyAsync(hr, dr.p, 16, hipMemcpyDeviceToHost, c.s));
+        DAS_HIP(hipStreamSynchronize(c.s));
+        if (idx.range_cache.size() > (1u << 20)) idx.range_cache.clear();
+        idx.range_cache[ck] = {hr[0], hr[1]};
+      }
       if (hr[1] - hr[0] < best) {
         best = hr[1] - hr[0];
         begin = hr[0];
@@ -671,13 +680,16 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   };
   const uint32_t* qkey = Q.col(colof(Q, var));
   const uint32_t* pkey = P.col(colof(P, var));
-  DBuf<uint32_t> mm(2, c.s);
-  const uint32_t init[2] = {0xFFFFFFFFu, 0u};
-  DAS_HIP(hipMemcpyAsync(mm.p, init, 8, hipMemcpyHostToDevice, c.s));
-  hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(Q.nrows, B, 1024)), dim3(B), 0, c.s, qkey, Q.nrows, mm.p);
-  uint32_t h[2];
-  DAS_HIP(hipMemcpyAsync(h, mm.p, 8, hipMemcpyDeviceToHost, c.s));
-  DAS_HIP(hipStreamSynchronize(c.s));
+  uint32_t h[2] = {0u, (uint32_t)(c.idx.n_atoms ? c.idx.n_atoms - 1 : 0)};
+  if (c.idx.n_atoms > std::max<uint64_t>(8 * Q.nrows, 1ull << 22)) {
+    // large id space: bound the offsets array by the build keys' actual range
+    DBuf<uint32_t> mm(2, c.s);
+    const uint32_t init[2] = {0xFFFFFFFFu, 0u};
+    DAS_HIP(hipMemcpyAsync(mm.p, init, 8, hipMemcpyHostToDevice, c.s));
+    hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(Q.nrows, B, 1024)), dim3(B), 0, c.s, qkey, Q.nrows, mm.p);
+    DAS_HIP(hipMemcpyAsync(h, mm.p, 8, hipMemcpyDeviceToHost, c.s));
+    DAS_HIP(hipStreamSynchronize(c.s));
+  }
   const uint64_t range = (uint64_t)h[1] - h[0] + 1;
   if (range > std::max<uint64_t>(8 * Q.nrows, 1ull << 26) || range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
@@ -866,6 +878,84 @@ std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
   hipLaunchKernelGGL(k_distinct_flags, G(A.nrows), dim3(B), 0, c.s, cols_of(*S), A.nrows, keep.p);
   DAS_HIP(hipGetLastError());
   return compact_table(c, *S, keep.p);
+}
+
+// ---------------------------------------------------------------------------
+// Exchange helpers (multi-GPU): destination by key hash, row-major staging
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {   // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__global__ void k_dest(ColSet key, uint64_t n, uint32_t nparts, uint32_t* dest) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t h = 0x9e3779b9u;
+    for (int c = 0; c < key.n; ++c) h = mix32(h ^ (key.c[c][i] + 0x7f4a7c15u * (uint32_t)(c + 1)));
+    dest[i] = h % nparts;
+  }
+}
+__global__ void k_rows_out(ColSet src, uint64_t n, uint32_t* dst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    for (int c = 0; c < src.n; ++c) dst[i * src.n + c] = src.c[c][i];
+}
+__global__ void k_rows_in(const uint32_t* src, uint64_t n, int ncols, uint32_t* out, uint64_t cap) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    for (int c = 0; c < ncols; ++c) out[(uint64_t)c * cap + i] = src[i * ncols + c];
+}
+__global__ void k_dest_hist(const uint32_t* dest, uint64_t n, unsigned long long* cnt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[dest[i]], 1ull);
+}
+}  // namespace
+
+std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
+                                 uint64_t* counts) {
+  DAS_CHECK(nparts >= 1 && nparts <= 4096, DAS_E_INVALID, "bad partition count");
+  ColSet key{};
+  if (nkey == 0) {
+    key = cols_of(t);
+  } else {
+    key.n = (int)nkey;
+    for (uint32_t k = 0; k < nkey; ++k) {
+      int ci = -1;
+      for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == key_vars[k]) ci = i;
+      DAS_CHECK(ci >= 0, DAS_E_INVALID, "partition key is not a column of the table");
+      key.c[k] = t.col(ci);
+    }
+  }
+  for (uint32_t d = 0; d < nparts; ++d) counts[d] = 0;
+  if (t.nrows == 0) return gather_table(c, t, nullptr, 0);
+  DBuf<uint32_t> dest(t.nrows, c.s), perm(t.nrows, c.s);
+  DBuf<unsigned long long> h(nparts, c.s);
+  DAS_HIP(hipMemsetAsync(h.p, 0, 8 * nparts, c.s));
+  hipLaunchKernelGGL(k_dest, G(t.nrows), dim3(B), 0, c.s, key, t.nrows, nparts, dest.p);
+  hipLaunchKernelGGL(k_dest_hist, G(t.nrows), dim3(B), 0, c.s, (const uint32_t*)dest.p, t.nrows, h.p);
+  DAS_HIP(hipGetLastError());
+  iota(perm.p, t.nrows, c.s);
+  radix_sort_pairs<uint32_t>(dest.p, perm.p, t.nrows, 0, std::max(1, bits_for(nparts - 1)), c.s);
+  std::vector<unsigned long long> hh(nparts);
+  DAS_HIP(hipMemcpyAsync(hh.data(), h.p, 8 * nparts, hipMemcpyDeviceToHost, c.s));
+  DAS_HIP(hipStreamSynchronize(c.s));
+  for (uint32_t d = 0; d < nparts; ++d) counts[d] = hh[d];
+  return gather_table(c, t, perm.p, t.nrows);
+}
+
+void export_rows(Ctx& c, const Table& t, uint32_t* dst) {
+  if (!t.nrows || !t.ncols) return;
+  hipLaunchKernelGGL(k_rows_out, G(t.nrows), dim3(B), 0, c.s, cols_of(t), t.nrows, dst);
+  DAS_HIP(hipGetLastError());
+}
+
+std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const uint32_t* src,
+                                   uint64_t n) {
+  auto t = new_table(c, kind, ncols, vars, n);
+  t->nrows = n;
+  if (n && ncols) {
+    hipLaunchKernelGGL(k_rows_in, G(n), dim3(B), 0, c.s, src, n, ncols, t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return t;
 }
 
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {

@@ -26,10 +26,11 @@ class Relation:
     """A set of assignments held on the GPU: device tables, one per schema
     (kind, variable ids).  Rows of one table are distinct."""
 
-    __slots__ = ("tables",)
+    __slots__ = ("tables", "_global")
 
     def __init__(self, tables=()):
         self.tables = [t for t in tables if t is not None and t.nrows > 0]
+        self._global = None
 
     @property
     def nrows(self):
@@ -42,7 +43,39 @@ class Relation:
         return self.nrows
 
 
-class HipDB(DBInterface):
+class RelationalDB(DBInterface):
+    """A DBInterface whose pattern-matcher entry points return device
+    relations, plus the relation algebra the matcher folds them with."""
+
+    tuple_targets = False
+
+    def rel_empty(self):
+        return Relation()
+
+    def rel_nonempty(self, rel) -> bool:
+        return bool(rel)
+
+    def rel_count(self, rel) -> int:
+        return rel.nrows
+
+    def rel_local_tables(self, rel):
+        return rel.tables
+
+
+def _group(tables):
+    g = {}
+    for t in tables:
+        g.setdefault(t.schema, []).append(t)
+    return g
+
+
+def _unsupported(what):
+    raise NotImplementedError(
+        f"{what} involving unordered (Similarity/Set) assignments — the reference's "
+        "CompositeAssignment algebra (pattern_matcher.py:264-368) — is not implemented on the GPU in this build")
+
+
+class HipDB(RelationalDB):
 
     def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False):
         """`tuple_targets=True` reproduces the reference DB path exactly,
@@ -63,6 +96,7 @@ class HipDB(DBInterface):
         self.arrays = None
         self.type_id = {}
         self._hex_cache = {}
+        self._handle_cache = {}
         self._mirror = None
         self.pattern_black_list = []
 
@@ -77,6 +111,7 @@ class HipDB(DBInterface):
         self.arrays = arrays
         self.type_id = dict(arrays.type_id)
         self._hex_cache = {}
+        self._handle_cache = {}
         self._mirror = None
 
     def load_metta(self, texts):
@@ -93,20 +128,30 @@ class HipDB(DBInterface):
         return self.ctx.stats()
 
     # --------------------------------------------------------------- helpers
+    def _resolve(self, handles):
+        """handle -> (id, category, arity) through a host cache of the device
+        index (handles are immutable once the index is built)."""
+        miss = [h for h in dict.fromkeys(handles) if h not in self._handle_cache]
+        if miss:
+            good = []
+            for h in miss:
+                try:
+                    good.append((h, _lib.hex_to_digest(h)))
+                except ValueError:
+                    self._handle_cache[h] = (-1, 0, 0)
+            if good:
+                ids, cat, ar, _ = self.ctx.lookup(np.stack([d for _, d in good]))
+                for (h, _), i, c, a in zip(good, ids.tolist(), cat.tolist(), ar.tolist()):
+                    self._handle_cache[h] = (i, c, a)
+        return [self._handle_cache[h] for h in handles]
+
     def ids_of(self, handles: List[str]) -> np.ndarray:
         if not handles:
             return np.zeros(0, dtype=np.int64)
-        dig = np.stack([_lib.hex_to_digest(h) for h in handles])
-        ids, _, _, _ = self.ctx.lookup(dig)
-        return ids
+        return np.array([r[0] for r in self._resolve(handles)], dtype=np.int64)
 
     def _lookup(self, handle):
-        try:
-            dig = _lib.hex_to_digest(handle)
-        except ValueError:
-            return -1, 0, 0
-        ids, cat, ar, _ = self.ctx.lookup(dig.reshape(1, 4))
-        return int(ids[0]), int(cat[0]), int(ar[0])
+        return self._resolve([handle])[0]
 
     def hex_of(self, ids) -> List[str]:
         ids = np.asarray(ids, dtype=np.uint32).ravel()
@@ -139,7 +184,7 @@ class HipDB(DBInterface):
             return False
         if arity == 0:
             return cat == 1
-        if cat != 2:
+        if cat not in (2, 3):          # 3: a link whose index rows live on another shard
             return False
         if arity == 1:
             return ar == 1
@@ -173,7 +218,7 @@ class HipDB(DBInterface):
         order and repeats are not preserved there; here the stored order is
         returned (a superset of what the reference guarantees)."""
         aid, cat, _ = self._lookup(link_handle)
-        if aid < 0 or cat != 2:
+        if aid < 0 or cat not in (2, 3):
             raise ValueError(f"Invalid handle: {link_handle}")
         return self.hex_of(self.ctx.link_targets(aid))
 
@@ -392,3 +437,47 @@ class HipDB(DBInterface):
         if not ordered or len(set(var_ids)) != len(var_ids):
             t = self.ctx.dedup(t)
         return Relation([t])
+
+    # ------------------------------------------------ relation algebra (1 GPU)
+    def rel_normalize(self, rel):
+        """One table per schema, rows distinct (Python set semantics)."""
+        out = []
+        for schema, ts in _group(rel.tables).items():
+            out.append(ts[0] if len(ts) == 1 else self.ctx.dedup(self.ctx.concat(ts)))
+        return Relation(out)
+
+    def rel_union(self, a, b):
+        return self.rel_normalize(Relation(a.tables + b.tables))
+
+    def rel_join(self, a, b):
+        """And's join step (pattern_matcher.py:732-738) for every schema pair."""
+        from ..pattern_matcher.pattern_matcher import CONFIG
+        out = []
+        for ta in a.tables:
+            for tb in b.tables:
+                if ta.kind != _lib.TABLE_ORDERED or tb.kind != _lib.TABLE_ORDERED:
+                    _unsupported("join")
+                out.append(self.ctx.join(ta, tb, CONFIG['no_overload']))
+        return Relation(out)
+
+    def rel_antijoin(self, rel, forbidden):
+        """check_negation of every row against every forbidden row (:741-746)."""
+        tables = rel.tables
+        for f in forbidden.tables:
+            nxt = []
+            for t in tables:
+                if t.kind != _lib.TABLE_ORDERED or f.kind != _lib.TABLE_ORDERED:
+                    _unsupported("negation")
+                nxt.append(self.ctx.antijoin(t, f))
+            tables = nxt
+        return Relation(tables)
+
+    def rel_minus(self, a, b):
+        """Set difference a - b by identity (same kind and variables, equal values)."""
+        groups = _group(b.tables)
+        out = []
+        for t in a.tables:
+            for f in groups.get(t.schema, []):
+                t = self.ctx.antijoin(t, f)
+            out.append(t)
+        return Relation(out)

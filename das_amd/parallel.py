@@ -1,0 +1,392 @@
+"""Multi-GPU query evaluation: links hash-partitioned across ranks, binding
+tables exchanged with all-to-all only where a join needs co-location.
+
+Layout.  Every rank holds the *atom directory* of the whole KB
+(all handles -> global ids, outgoing sets), so ids agree across ranks and
+node/link existence needs no collective; the *pattern index* rows (T_a, C_a,
+P_{a,p}) of a link live only on its owner shard.  The reference's only
+"distribution" is Redis Cluster key sharding plus one Mongo
+(das/distributed_atom_space.py:48-61); there is no counterpart of this
+exchange in the reference.
+
+Relational algebra of pattern_matcher over sharded relations:
+  scan        local (each rank scans its own links); rows of different links
+              are distinct, so no exchange unless the scan can duplicate
+              bindings ('*' type, repeated variable, unordered sets) -> global
+              dedup (repartition by every column)
+  join        repartition both sides by hash(shared variables) (all-to-all),
+              local join; no shared variable -> all-gather the smaller side
+  antijoin    repartition by hash(forbidden variables)
+  union/minus repartition by hash(all columns), local dedup / antijoin
+  nonempty    all-reduce of local row counts (so control flow is identical
+              on every rank and every rank issues the same collectives)
+
+The collectives go through torch.distributed ("nccl" = RCCL on ROCm, over
+xGMI; "gloo" in the CPU tests).  `local` is a HipDB (or, in tests, a CPU
+double with the same surface).
+"""
+import zlib
+
+import numpy as np
+
+from .database.db_interface import UNORDERED_LINK_TYPES, WILDCARD
+from .database.hip_db import RelationalDB
+
+ORDERED, UNORDERED = 0, 1
+
+
+class DRel:
+    """A sharded relation: one local table per schema, empty tables kept so the
+    schema list (and so the collective sequence) is the same on every rank."""
+
+    __slots__ = ("tables", "_global")
+
+    def __init__(self, tables):
+        self.tables = list(tables)
+        self._global = None
+
+
+class ShardedDB(RelationalDB):
+
+    def __init__(self, local, dist, group=None):
+        self.local = local
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.tuple_targets = local.tuple_targets
+
+    # ------------------------------------------------------------ collectives
+    def _allreduce_sum(self, values):
+        t = self.local.xfer_tensor(np.asarray(values, dtype=np.int64))
+        self.dist.all_reduce(t, group=self.group)
+        return self.local.xfer_numpy(t)
+
+    def _exchange(self, table, key_vars):
+        """Repartition `table` by hash(key_vars) (every column if empty)."""
+        if self.world == 1:
+            return table
+        part, counts = self.local.partition(table, list(key_vars), self.world)
+        send_counts = self.local.xfer_tensor(counts.astype(np.int64))
+        recv_counts = self.local.xfer_tensor(np.zeros(self.world, dtype=np.int64))
+        self.dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        rc = self.local.xfer_numpy(recv_counts).tolist()
+        ncols = len(table.vars)
+        send = self.local.rows_out(part)
+        recv = self.local.rows_buffer(int(sum(rc)), ncols)
+        self.dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=counts.tolist(),
+                                    group=self.group)
+        return self.local.rows_in(table.kind, table.vars, recv, int(sum(rc)))
+
+    def _gather_all(self, table):
+        """Every rank gets the whole relation (all-gather of row blocks)."""
+        if self.world == 1:
+            return table
+        n = self._allgather_counts(table.nrows)
+        ncols = len(table.vars)
+        send = self.local.rows_out(table)
+        width = int(max(n)) if len(n) else 0
+        padded = self.local.rows_pad(send, width, ncols)
+        outs = [self.local.rows_buffer(width, ncols) for _ in range(self.world)]
+        self.dist.all_gather(outs, padded, group=self.group)
+        return self.local.rows_in_many(table.kind, table.vars, outs, [int(x) for x in n])
+
+    def _allgather_counts(self, n):
+        t = self.local.xfer_tensor(np.array([n], dtype=np.int64))
+        outs = [self.local.xfer_tensor(np.zeros(1, dtype=np.int64)) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return np.array([int(self.local.xfer_numpy(o)[0]) for o in outs], dtype=np.int64)
+
+    # ----------------------------------------------------- DBInterface (global)
+    def node_exists(self, node_type, node_name):
+        return self.local.node_exists(node_type, node_name)
+
+    def link_exists(self, link_type, targets):
+        return self.local.link_exists(link_type, targets)
+
+    def get_node_handle(self, node_type, node_name):
+        return self.local.get_node_handle(node_type, node_name)
+
+    def get_link_handle(self, link_type, targets):
+        return self.local.get_link_handle(link_type, targets)
+
+    def get_link_targets(self, handle):
+        return self.local.get_link_targets(handle)
+
+    def is_ordered(self, handle):
+        return self.local.is_ordered(handle)
+
+    def get_matched_links(self, link_type, target_handles):
+        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+
+    def get_all_nodes(self, node_type, names=False):
+        return self.local.get_all_nodes(node_type, names)
+
+    def get_matched_type_template(self, template):
+        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+
+    def get_matched_type(self, link_named_type):
+        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+
+    def get_node_name(self, node_handle):
+        return self.local.get_node_name(node_handle)
+
+    def get_matched_node_name(self, node_type, substring):
+        return self.local.get_matched_node_name(node_type, substring)
+
+    def count_atoms(self):
+        nodes, links = self.local.count_atoms()
+        return (nodes, int(self._allreduce_sum([links])[0]))
+
+    def hex_of(self, ids):
+        return self.local.hex_of(ids)
+
+    # ------------------------------------------------------- matcher entries
+    @staticmethod
+    def _schema(var_ids, ordered):
+        names = [v for v in var_ids if v is not None]
+        return (ORDERED if ordered else UNORDERED), tuple(sorted(set(names)) if ordered else sorted(names))
+
+    def _ensure(self, rel, kind, vars_):
+        tables = self.local.rel_local_tables(rel)
+        if tables:
+            return tables[0]
+        return self.local.empty_table(kind, list(vars_))
+
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+        kind, vars_ = self._schema(var_ids, ordered)
+        names = [v for v in var_ids if v is not None]
+        if not ordered and len(set(names)) != len(names):
+            return DRel([])
+        t = self._ensure(self.local.match_link(link_type, handles, var_ids, ordered, no_overload), kind, vars_)
+        dup = link_type == WILDCARD or len(set(names)) != len(names) or not ordered or \
+            link_type in UNORDERED_LINK_TYPES
+        if dup:
+            t = self.local.dedup(self._exchange(t, []))
+        return DRel([t])
+
+    def match_template(self, link_type, target_types, var_ids, ordered, no_overload=False):
+        kind = ORDERED if ordered else UNORDERED
+        vars_ = tuple(sorted(set(var_ids))) if ordered else tuple(sorted(var_ids))
+        if not ordered and len(set(var_ids)) != len(var_ids):
+            return DRel([])
+        t = self._ensure(self.local.match_template(link_type, target_types, var_ids, ordered, no_overload),
+                         kind, vars_)
+        if not ordered or len(set(var_ids)) != len(var_ids):
+            t = self.local.dedup(self._exchange(t, []))
+        return DRel([t])
+
+    # ------------------------------------------------------- relation algebra
+    def rel_empty(self):
+        return DRel([])
+
+    def _global_rows(self, rel):
+        if rel._global is None:
+            rel._global = int(self._allreduce_sum([sum(t.nrows for t in rel.tables)])[0])
+        return rel._global
+
+    def rel_nonempty(self, rel):
+        return self._global_rows(rel) > 0
+
+    def rel_count(self, rel):
+        return self._global_rows(rel)
+
+    def rel_local_count(self, rel):
+        return sum(t.nrows for t in rel.tables)
+
+    def rel_local_tables(self, rel):
+        return [self._gather_all(t) for t in rel.tables]
+
+    def _group(self, tables):
+        g = {}
+        for t in tables:
+            g.setdefault((t.kind, tuple(t.vars)), []).append(t)
+        return g
+
+    def rel_normalize(self, rel):
+        out = []
+        for _, ts in self._group(rel.tables).items():
+            if len(ts) == 1:
+                out.append(ts[0])
+            else:
+                out.append(self.local.dedup(self._exchange(self.local.concat(ts), [])))
+        return DRel(out)
+
+    def rel_union(self, a, b):
+        return self.rel_normalize(DRel(a.tables + b.tables))
+
+    def rel_join(self, a, b):
+        from .pattern_matcher.pattern_matcher import CONFIG
+        out = []
+        for ta in a.tables:
+            for tb in b.tables:
+                if ta.kind != ORDERED or tb.kind != ORDERED:
+                    raise NotImplementedError("join involving unordered (Similarity/Set) assignments "
+                                              "(CompositeAssignment algebra) is not implemented on the GPU")
+                shared = sorted(set(ta.vars) & set(tb.vars))
+                if shared:
+                    out.append(self.local.join(self._exchange(ta, shared), self._exchange(tb, shared),
+                                               CONFIG['no_overload']))
+                else:
+                    na = self._allreduce_sum([ta.nrows])[0]
+                    nb = self._allreduce_sum([tb.nrows])[0]
+                    if na <= nb:
+                        out.append(self.local.join(self._gather_all(ta), tb, CONFIG['no_overload']))
+                    else:
+                        out.append(self.local.join(ta, self._gather_all(tb), CONFIG['no_overload']))
+        return DRel(out)
+
+    def rel_antijoin(self, rel, forbidden):
+        tables = rel.tables
+        for f in forbidden.tables:
+            nxt = []
+            for t in tables:
+                if t.kind != ORDERED or f.kind != ORDERED:
+                    raise NotImplementedError("negation involving unordered (Similarity/Set) assignments "
+                                              "is not implemented on the GPU")
+                if set(f.vars) <= set(t.vars):
+                    key = sorted(f.vars)
+                    nxt.append(self.local.antijoin(self._exchange(t, key), self._exchange(f, key)))
+                else:
+                    nxt.append(t)
+            tables = nxt
+        return DRel(tables)
+
+    def rel_minus(self, a, b):
+        groups = self._group(b.tables)
+        out = []
+        for t in a.tables:
+            fs = groups.get((t.kind, tuple(t.vars)), [])
+            if fs:
+                t = self._exchange(t, [])
+                for f in fs:
+                    t = self.local.antijoin(t, self._exchange(f, []))
+            out.append(t)
+        return DRel(out)
+
+
+# ---------------------------------------------------------------------------
+# The GPU local engine surface ShardedDB needs (HipDB + torch buffers)
+# ---------------------------------------------------------------------------
+class HipLocal:
+    """Adapts a HipDB for ShardedDB: device tables, torch CUDA staging buffers
+    for the RCCL collectives."""
+
+    def __init__(self, db, cpu_staging=False):
+        """cpu_staging: collective buffers on the host (gloo backend; used to
+        rehearse several ranks on one GPU).  Default: device buffers (RCCL)."""
+        import torch
+        self.db = db
+        self.torch = torch
+        self.gpu = torch.device("cuda", torch.cuda.current_device())
+        self.dev = torch.device("cpu") if cpu_staging else self.gpu
+        self.tuple_targets = db.tuple_targets
+
+    def __getattr__(self, name):     # DBInterface passthrough
+        return getattr(self.db, name)
+
+    def rel_local_tables(self, rel):
+        return rel.tables
+
+    def empty_table(self, kind, vars_):
+        return self.db.ctx.import_rows(kind, vars_, None, 0)
+
+    def partition(self, t, key_vars, nparts):
+        return self.db.ctx.partition(t, key_vars, nparts)
+
+    def dedup(self, t):
+        return self.db.ctx.dedup(t)
+
+    def concat(self, ts):
+        return self.db.ctx.concat(ts)
+
+    def join(self, a, b, no_overload):
+        return self.db.ctx.join(a, b, no_overload)
+
+    def antijoin(self, a, t):
+        return self.db.ctx.antijoin(a, t)
+
+    def xfer_tensor(self, arr):
+        return self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.dev)
+
+    def xfer_numpy(self, t):
+        return t.cpu().numpy()
+
+    def rows_buffer(self, n, ncols):
+        return self.torch.empty((max(n, 0), max(ncols, 1)), dtype=self.torch.int32, device=self.dev)
+
+    def rows_out(self, t):
+        buf = self.torch.empty((t.nrows, max(len(t.vars), 1)), dtype=self.torch.int32, device=self.gpu)
+        if t.nrows:
+            self.db.ctx.export_rows(t, buf.data_ptr())
+        return buf if self.dev == self.gpu else buf.cpu()
+
+    def rows_pad(self, buf, width, ncols):
+        if buf.shape[0] == width:
+            return buf
+        out = self.rows_buffer(width, ncols)
+        out[:buf.shape[0]] = buf
+        return out
+
+    def rows_in(self, kind, vars_, buf, n):
+        buf = buf.to(self.gpu).contiguous()
+        return self.db.ctx.import_rows(kind, list(vars_), buf.data_ptr() if n else None, n)
+
+    def rows_in_many(self, kind, vars_, bufs, counts):
+        parts = [b[:c] for b, c in zip(bufs, counts)]
+        cat = self.torch.cat(parts) if parts else self.rows_buffer(0, len(vars_))
+        return self.rows_in(kind, vars_, cat, int(sum(counts)))
+
+
+class ShardedMatcher:
+    """bench.py helper: evaluates one expression on the sharded DB and returns
+    the number of distinct bindings held by this rank (sum over ranks = the
+    answer's size)."""
+
+    def __init__(self, db, dist, cpu_staging=False):
+        self.sdb = ShardedDB(HipLocal(db, cpu_staging), dist)
+
+    def count(self, expr):
+        from .pattern_matcher.pattern_matcher import PatternMatchingAnswer
+        ans = PatternMatchingAnswer()
+        expr.matched(self.sdb, ans)
+        return self.sdb.rel_local_count(ans._relation()) if ans._rel is not None else 0
+
+
+# ---------------------------------------------------------------------------
+# Sharded synthetic KB for the benchmark (every rank builds the directory of
+# the whole KB; index rows only for the links it owns)
+# ---------------------------------------------------------------------------
+
+def owner_of(children, world):
+    """Content hash of a link (its type + targets) -> owning rank."""
+    h = np.zeros(children.shape[0], dtype=np.uint64)
+    for c in range(children.shape[1]):
+        x = children[:, c].astype(np.uint64)
+        h = (h * np.uint64(0x100000001B3)) ^ (x * np.uint64(0x9E3779B97F4A7C15))
+    h ^= h >> np.uint64(29)
+    return (h % np.uint64(world)).astype(np.int64)
+
+
+def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
+    """Weak scaling: rank r owns the Member links of its own n_genes genes
+    (gene range r*n_genes..), the Inheritance links are shared and owned by
+    content hash.  Returns (AtomArrays for this rank, this rank's gene ids)."""
+    from . import synthetic
+    blocks = []
+    total_genes = n_genes * world
+    for r in range(world):
+        rng = np.random.default_rng(seed + 1000 * (r + 1))
+        genes = r * n_genes + rng.integers(0, n_genes, n_members)
+        bps = synthetic.zipf_indices(rng, n_bps, n_members)
+        ch = np.stack([genes, total_genes + bps], 1)
+        blocks.append(("Member", ch, np.full(n_members, 1 if r == rank else 3, np.uint8)))
+    rng = np.random.default_rng(seed)
+    child = rng.integers(1, n_bps, n_inh)
+    parent = (rng.random(n_inh) * child).astype(np.int64)
+    ich = np.stack([total_genes + child, total_genes + parent], 1)
+    own = owner_of(ich, world)
+    blocks.append(("Inheritance", ich, np.where(own == rank, 1, 3).astype(np.uint8)))
+    arrays, _ = synthetic.build_arrays(["Member", "Inheritance"],
+                                       [("Gene", "g", total_genes), ("BiologicalProcess", "bp", n_bps)], blocks)
+    return arrays, np.arange(rank * n_genes, (rank + 1) * n_genes)

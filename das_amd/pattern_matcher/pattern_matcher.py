@@ -30,7 +30,7 @@ import numpy as np
 
 from .. import _lib
 from ..database.db_interface import WILDCARD, DBInterface
-from ..database.hip_db import HipDB, Relation
+from ..database.hip_db import HipDB, Relation, RelationalDB
 
 DEBUG_AND = False
 DEBUG_OR = False
@@ -334,72 +334,14 @@ class CompositeAssignment(Assignment):
 
 
 # ---------------------------------------------------------------------------
-# Device relation algebra
+# Relational evaluation: the DB owns the device relation algebra
+# (HipDB on one GPU, parallel.ShardedDB across ranks)
 # ---------------------------------------------------------------------------
 
-def _hip(db) -> HipDB:
-    if not isinstance(db, HipDB):
+def _hip(db):
+    if not isinstance(db, RelationalDB):
         raise TypeError(f"das_amd evaluates patterns on the MI355X index; got {db!r} (use HipDB)")
     return db
-
-
-def _group(tables):
-    g = {}
-    for t in tables:
-        g.setdefault(t.schema, []).append(t)
-    return g
-
-
-def _normalize(db, rel):
-    """One table per schema, rows distinct (Python set semantics)."""
-    out = []
-    for schema, ts in _group(rel.tables).items():
-        out.append(ts[0] if len(ts) == 1 else db.ctx.dedup(db.ctx.concat(ts)))
-    return Relation(out)
-
-
-def _union(db, a, b):
-    return _normalize(db, Relation(a.tables + b.tables))
-
-
-def _unsupported(what):
-    raise NotImplementedError(
-        f"{what} involving unordered (Similarity/Set) assignments — the reference's "
-        "CompositeAssignment algebra (pattern_matcher.py:264-368) — is not implemented on the GPU in this build")
-
-
-def _join(db, a, b):
-    out = []
-    for ta in a.tables:
-        for tb in b.tables:
-            if ta.kind != _lib.TABLE_ORDERED or tb.kind != _lib.TABLE_ORDERED:
-                _unsupported("join")
-            out.append(db.ctx.join(ta, tb, CONFIG['no_overload']))
-    return Relation(out)
-
-
-def _without_forbidden(db, rel, forbidden):
-    """check_negation of every row against every forbidden row (:741-746)."""
-    tables = rel.tables
-    for f in forbidden.tables:
-        nxt = []
-        for t in tables:
-            if t.kind != _lib.TABLE_ORDERED or f.kind != _lib.TABLE_ORDERED:
-                _unsupported("negation")
-            nxt.append(db.ctx.antijoin(t, f))
-        tables = nxt
-    return Relation(tables)
-
-
-def _minus(db, a, b):
-    """Set difference a - b by identity (same kind and variables, equal values)."""
-    groups = _group(b.tables)
-    out = []
-    for t in a.tables:
-        for f in groups.get(t.schema, []):
-            t = db.ctx.antijoin(t, f)
-        out.append(t)
-    return Relation(out)
 
 
 # ---------------------------------------------------------------------------
@@ -424,7 +366,7 @@ class PatternMatchingAnswer:
         self._rel = rel
         self._py = None
 
-    def _relation(self) -> Relation:
+    def _relation(self):
         if self._py is not None and self._rel is None:
             if self._py:
                 raise NotImplementedError("host-built assignments cannot feed the device matcher")
@@ -446,17 +388,20 @@ class PatternMatchingAnswer:
         self._rel = None
 
     def count(self) -> int:
-        """Number of distinct assignments, without building Python objects."""
+        """Number of distinct assignments, without building Python objects
+        (summed over ranks for a sharded DB)."""
         if self._py is not None and self._rel is None:
             return len(self._py)
-        return self._relation().nrows
+        if self._db is None:
+            return 0
+        return self._db.rel_count(self._relation())
 
 
 def _materialize(db, rel):
     out = set()
     if rel is None or not rel:
         return out
-    for t in rel.tables:
+    for t in db.rel_local_tables(rel):
         cols = t.fetch()
         names = [_var_name(v) for v in t.vars]
         hexcols = [db.hex_of(c) for c in cols]
@@ -561,11 +506,12 @@ class Link(Atom):
             return db.link_exists(self.atom_type, handles)
         var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in self.targets]
         rel = db.match_link(self.atom_type, handles, var_ids, self.ordered, CONFIG['no_overload'])
-        if db.tuple_targets and not self.ordered and rel and any(v is None for v in var_ids):
+        found = db.rel_nonempty(rel)
+        if db.tuple_targets and not self.ordered and found and any(v is None for v in var_ids):
             # reference DB path: list.remove on a tuple (pattern_matcher.py:484)
             raise AttributeError("'tuple' object has no attribute 'remove'")
         answer._set(db, rel)
-        return bool(rel)
+        return found
 
 
 class Variable(Atom):
@@ -611,7 +557,7 @@ class LinkTemplate(LogicalExpression):
         rel = db.match_template(self.link_type, [v.type for v in self.targets],
                                 [_vid(v.name) for v in self.targets], self.ordered, CONFIG['no_overload'])
         answer._set(db, rel)
-        return bool(rel)
+        return db.rel_nonempty(rel)
 
 
 class Not(LogicalExpression):
@@ -640,8 +586,7 @@ class Or(LogicalExpression):
         db = _hip(db)
         if not self.terms:
             return False
-        assert not answer._relation()
-        union = Relation()
+        union = None
         any_matched = False
         negated = [t for t in self.terms if isinstance(t, Not)]
         for term in self.terms:
@@ -652,12 +597,13 @@ class Or(LogicalExpression):
                 continue
             any_matched = True
             rel = sub._relation()
-            if rel:
-                union = rel if not union else _union(db, union, rel)
+            if db.rel_nonempty(rel):
+                union = rel if union is None else db.rel_union(union, rel)
+        union = union if union is not None else db.rel_empty()
         if negated:
             sub = PatternMatchingAnswer()
             And([t.term for t in negated]).matched(db, sub)
-            answer._set(db, _minus(db, sub._relation(), union))
+            answer._set(db, db.rel_minus(sub._relation(), union))
             answer.negation = True
         else:
             answer._set(db, union)
@@ -679,22 +625,26 @@ class And(LogicalExpression):
         db = _hip(db)
         if not self.terms:
             return False
-        assert not answer._relation()
-        acc = Relation()
-        forbidden = Relation()
+        acc = None
+        forbidden = []
         for term in self.terms:
             sub = PatternMatchingAnswer()
             if not term.matched(db, sub):
                 return False
             rel = sub._relation()
-            if not rel:
+            if not db.rel_nonempty(rel):
                 continue
             if sub.negation:
-                forbidden = Relation(forbidden.tables + rel.tables)
+                forbidden.append(rel)
                 continue
-            acc = rel if not acc else _join(db, acc, rel)
-        if acc and forbidden:
-            acc = _without_forbidden(db, acc, forbidden)
-        acc = _normalize(db, acc)
+            # reset-on-empty (pattern_matcher.py:725-729): an empty running
+            # result takes the next term's assignments as they are
+            acc = rel if acc is None or not db.rel_nonempty(acc) else db.rel_join(acc, rel)
+        if acc is None:
+            acc = db.rel_empty()
+        for f in forbidden:
+            if db.rel_nonempty(acc):
+                acc = db.rel_antijoin(acc, f)
+        acc = db.rel_normalize(acc)
         answer._set(db, acc)
-        return bool(acc)
+        return db.rel_nonempty(acc)

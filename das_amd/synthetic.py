@@ -30,7 +30,8 @@ def zipf_indices(rng, n_items, size, s=1.1):
 def build_arrays(type_names, node_blocks, link_blocks):
     """node_blocks: [(type_name, prefix, count)] -> node g of block b is the
     terminal "type prefix<g>"; global node index = block offset + g.
-    link_blocks: [(type_name, children int array (n, k))] of global node indices.
+    link_blocks: [(type_name, children int array (n, k)[, expr kinds (n,)])] of
+    global node indices; kind 1 = local link, 3 = link owned by another shard.
     Returns AtomArrays plus the per-block node offsets."""
     types = list(type_names)
     tid = {t: i for i, t in enumerate(types)}
@@ -38,7 +39,8 @@ def build_arrays(type_names, node_blocks, link_blocks):
         if t not in tid:
             tid[t] = len(types)
             types.append(t)
-    for t, _ in link_blocks:
+    for blk in link_blocks:
+        t = blk[0]
         if t not in tid:
             tid[t] = len(types)
             types.append(t)
@@ -65,27 +67,31 @@ def build_arrays(type_names, node_blocks, link_blocks):
     name_start = np.concatenate([np.zeros(n_types, np.uint32)] +
                                 [np.full(c, len(t.encode()) + 1 + 0, np.uint32) for t, _, c in node_blocks])
     # expressions: one group per arity (all at level 1)
-    by_k = {}
-    for t, ch in link_blocks:
-        ch = np.asarray(ch, dtype=np.int64)
+    by_k, kinds_k = {}, {}
+    for blk in link_blocks:
+        t, ch = blk[0], np.asarray(blk[1], dtype=np.int64)
+        kinds = np.asarray(blk[2], np.uint8) if len(blk) > 2 else np.ones(ch.shape[0], np.uint8)
         k = ch.shape[1] + 1
         full = np.concatenate([np.full((ch.shape[0], 1), tid[t], np.int64), ch + n_types], axis=1)
         by_k.setdefault(k, []).append(full)
-    offs, childs, groups = [0], [], [0]
+        kinds_k.setdefault(k, []).append(kinds)
+    childs, groups, nchs, ekinds = [], [0], [], []
     total = 0
     for k in sorted(by_k):
         blk = np.concatenate(by_k[k])
         childs.append(blk.reshape(-1).astype(np.uint32))
+        nchs.append(np.full(blk.shape[0], k, np.uint64))
+        ekinds.append(np.concatenate(kinds_k[k]))
         total += blk.shape[0]
         groups.append(total)
     n_expr = total
-    nch = np.concatenate([np.full(np.concatenate(by_k[k]).shape[0], k, np.uint64) for k in sorted(by_k)]) \
-        if by_k else np.zeros(0, np.uint64)
+    nch = np.concatenate(nchs) if nchs else np.zeros(0, np.uint64)
     expr_off = np.zeros(n_expr + 1, dtype=np.uint64)
     np.cumsum(nch, out=expr_off[1:])
     expr_child = np.concatenate(childs) if childs else np.zeros(0, np.uint32)
+    expr_kind = np.concatenate(ekinds) if ekinds else np.zeros(0, np.uint8)
     arrays = AtomArrays(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start, expr_off,
-                        expr_child, np.ones(n_expr, np.uint8), np.full(n_expr, -1, np.int32),
+                        expr_child, expr_kind, np.full(n_expr, -1, np.int32),
                         np.array(groups, np.uint64), types)
     return arrays, node_off
 

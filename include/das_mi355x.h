@@ -84,7 +84,9 @@ typedef struct {
   uint64_t n_expr;
   const uint64_t* expr_off;        /* n_expr + 1 */
   const uint32_t* expr_child;
-  const uint8_t* expr_kind;        /* 1 link (`links_*` collections), 2 typedef (`atom_types`) */
+  const uint8_t* expr_kind;        /* 1 link (`links_*` collections), 2 typedef (`atom_types`),
+                                      3 link whose index rows live on another shard (multi-GPU:
+                                      it gets its global id and outgoing set, no pattern rows) */
   const int32_t* expr_ctype_leaf;  /* -1: composite type from children; else that leaf's digest */
   uint32_t n_levels;
   const uint64_t* level_off;       /* n_levels + 1, expression ranges per nesting level */
@@ -174,6 +176,17 @@ int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
 int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,
                         const uint32_t* cols, uint64_t nrows, das_table_t** out);
 int das_table_free(das_table_t* t);
+
+/* ---- multi-GPU exchange (RCCL all-to-all of binding rows) ----- */
+/* Rows of `t` regrouped by destination = mix(key columns) % nparts (stable
+ * inside a destination); counts[nparts] receives the group sizes.  nkey == 0
+ * keys on every column (global dedup / set difference). */
+int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars, uint32_t nkey,
+                  uint32_t nparts, das_table_t** out, uint64_t* counts);
+/* Row-major (n x ncols u32) device copies for the collective buffers. */
+int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst);
+int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,
+                          const uint32_t* d_src, uint64_t nrows, das_table_t** out);
 
 /* ---- measurement ---------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the context stream (bench.py roofline):

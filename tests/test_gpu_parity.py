@@ -215,3 +215,67 @@ def test_gpu_facade_readme_examples():
     assert sorted(das.get_links("Inheritance", None, ["*", "bdfe4e7a431f73386f37c6448afe5840"])) == sorted(
         das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"]) and
         [h for h, _ in das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"])])
+
+
+def _sharded_worker(rank, world, port, out_path):
+    import os as _os
+    import torch
+    import torch.distributed as dist
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    from das_amd.parallel import HipLocal, ShardedDB, owner_of
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    from tests.test_parallel_gloo import _queries
+    arrays = synthetic.bio_kb(60, 25, 600, 80, seed=3)
+    # mark links not owned by this rank as remote (kind 3): same directory, split index
+    n_leaf = arrays.n_leaf
+    kinds = arrays.expr_kind.copy()
+    for j in range(arrays.n_expr):
+        ch = np.array(arrays.children(j)[1:], dtype=np.int64)[None, :]
+        if owner_of(ch, world)[0] != rank:
+            kinds[j] = 3
+    arrays.expr_kind = kinds
+    db = HipDB(device=0)
+    db.load_arrays(arrays)
+    sdb = ShardedDB(HipLocal(db, cpu_staging=True), dist)
+    res = []
+    for q in _queries():
+        ans = pm.PatternMatchingAnswer()
+        m = build(q).matched(sdb, ans)
+        rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
+        res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
+                    "local": sdb.rel_local_count(ans._relation())})
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_gpu_sharded_two_ranks_one_gpu():
+    """The multi-GPU path (partition / export / import kernels + exchange) with
+    two ranks sharing cuda:0 over gloo, against the single-process oracle."""
+    import socket
+    import tempfile
+    import torch.multiprocessing as mp
+    from das_amd import synthetic
+    from tests.test_parallel_gloo import _queries
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)))
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.spawn(_sharded_worker, args=(2, port, out), nprocs=2, join=True)
+        per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    for qi, q in enumerate(_queries()):
+        want = O.evaluate(q, odb)
+        want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])
+        assert sum(per_rank[r][qi]["local"] for r in range(2)) == want["n"], q
+        for r in range(2):
+            got = per_rank[r][qi]
+            assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
+            assert got["rows"] == want_rows, q

@@ -1,0 +1,275 @@
+"""Multi-rank evaluation (das_amd/parallel.py) on CPU: world_size 2 over gloo.
+
+The exchange logic (which rows go where, all-to-all / all-gather sequences,
+global emptiness, global dedup) is the product code; each rank's local engine
+here is a CPU test double with HipLocal's surface, built on the oracle's
+DB-path semantics over the rank's own link partition.  Answers must equal the
+single-process oracle over the whole KB."""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import das_oracle as O
+
+ORDERED, UNORDERED = 0, 1
+
+
+class NTable:
+    def __init__(self, kind, vars_, rows):
+        self.kind = kind
+        self.vars = tuple(vars_)
+        self.rows = np.asarray(rows, dtype=np.uint32).reshape(-1, len(vars_))
+
+    @property
+    def nrows(self):
+        return self.rows.shape[0]
+
+    @property
+    def schema(self):
+        return (self.kind, self.vars)
+
+    def fetch(self):
+        return self.rows.T.copy()
+
+
+class NRel:
+    def __init__(self, tables):
+        self.tables = [t for t in tables if t.nrows]
+        self._global = None
+
+
+class NumpyLocal:
+    """CPU double of parallel.HipLocal: global atom directory, local links."""
+
+    tuple_targets = False
+
+    def __init__(self, kb_full, rank, world):
+        handles = set(kb_full.nodes) | set(kb_full.links)
+        for _, (_, tg, _) in kb_full.links.items():
+            handles.update(tg)
+        self.hexes = sorted(handles)
+        self.id_of = {h: i for i, h in enumerate(self.hexes)}
+        local = O.KB()
+        local.nodes = dict(kb_full.nodes)
+        local.links = {h: v for h, v in kb_full.links.items() if int(h[:8], 16) % world == rank}
+        self.odb = O.RedisMongoSemantics(local)
+        self.full = O.RedisMongoSemantics(kb_full)
+
+    # DBInterface bits the matcher / ShardedDB use
+    def node_exists(self, t, n):
+        return self.full.node_exists(t, n)
+
+    def link_exists(self, t, tg):
+        return self.full.link_exists(t, tg)
+
+    def get_node_handle(self, t, n):
+        return self.full.get_node_handle(t, n)
+
+    def get_link_handle(self, t, tg):
+        return self.full.get_link_handle(t, tg)
+
+    def count_atoms(self):
+        return (len(self.odb.kb.nodes), len(self.odb.kb.links))
+
+    def hex_of(self, ids):
+        return [self.hexes[int(i)] for i in np.asarray(ids).ravel()]
+
+    def rel_local_tables(self, rel):
+        return rel.tables
+
+    # scans (oracle semantics, local links only)
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+        from das_amd.pattern_matcher.pattern_matcher import _var_name
+        pairs = self.odb.get_matched_links(link_type, handles)
+        names = [v for v in var_ids if v is not None]
+        rows = set()
+        for _, targets in pairs:
+            if ordered:
+                m = {}
+                ok = True
+                for v, h in zip(var_ids, targets):
+                    if v is None:
+                        continue
+                    if v in m and m[v] != h:
+                        ok = False
+                        break
+                    m[v] = h
+                if ok:
+                    rows.add(tuple(self.id_of[m[v]] for v in sorted(m)))
+            else:
+                rem = list(targets)
+                for h in handles:
+                    if h != "*":
+                        rem.remove(h)
+                if len(set(rem)) == len(rem):
+                    rows.add(tuple(sorted(self.id_of[h] for h in rem)))
+        vars_ = sorted(set(names)) if ordered else sorted(names)
+        return NRel([NTable(ORDERED if ordered else UNORDERED, vars_, sorted(rows))])
+
+    def match_template(self, link_type, target_types, var_ids, ordered, no_overload=False):
+        pairs = self.odb.get_matched_type_template([link_type, *target_types])
+        rows = set()
+        for _, targets in pairs:
+            if ordered:
+                m = {}
+                ok = True
+                for v, h in zip(var_ids, targets):
+                    if v in m and m[v] != h:
+                        ok = False
+                        break
+                    m[v] = h
+                if ok:
+                    rows.add(tuple(self.id_of[m[v]] for v in sorted(m)))
+            elif len(set(targets)) == len(targets):
+                rows.add(tuple(sorted(self.id_of[h] for h in targets)))
+        vars_ = sorted(set(var_ids)) if ordered else sorted(var_ids)
+        return NRel([NTable(ORDERED if ordered else UNORDERED, vars_, sorted(rows))])
+
+    # table ops
+    def empty_table(self, kind, vars_):
+        return NTable(kind, vars_, np.zeros((0, len(vars_)), np.uint32))
+
+    def partition(self, t, key_vars, nparts):
+        cols = [t.vars.index(v) for v in key_vars] if key_vars else list(range(len(t.vars)))
+        h = np.zeros(t.nrows, dtype=np.uint64)
+        for c in cols:
+            h = h * np.uint64(1000003) + t.rows[:, c].astype(np.uint64)
+        dest = (h % np.uint64(nparts)).astype(np.int64)
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=nparts).astype(np.uint64)
+        return NTable(t.kind, t.vars, t.rows[order]), counts
+
+    def dedup(self, t):
+        if t.nrows == 0:
+            return t
+        return NTable(t.kind, t.vars, np.unique(t.rows, axis=0))
+
+    def concat(self, ts):
+        return NTable(ts[0].kind, ts[0].vars, np.concatenate([t.rows for t in ts]))
+
+    def join(self, a, b, no_overload=False):
+        shared = sorted(set(a.vars) & set(b.vars))
+        uni = sorted(set(a.vars) | set(b.vars))
+        idx = {}
+        for r in b.rows:
+            idx.setdefault(tuple(r[b.vars.index(v)] for v in shared), []).append(r)
+        out = []
+        for r in a.rows:
+            for s in idx.get(tuple(r[a.vars.index(v)] for v in shared), []):
+                m = {v: r[a.vars.index(v)] for v in a.vars}
+                m.update({v: s[b.vars.index(v)] for v in b.vars})
+                out.append([m[v] for v in uni])
+        return NTable(ORDERED, uni, np.array(out, np.uint32).reshape(-1, len(uni)))
+
+    def antijoin(self, a, t):
+        if not set(t.vars) <= set(a.vars):
+            return a
+        bad = {tuple(r) for r in t.rows}
+        keep = [r for r in a.rows if tuple(r[a.vars.index(v)] for v in t.vars) not in bad]
+        return NTable(a.kind, a.vars, np.array(keep, np.uint32).reshape(-1, len(a.vars)))
+
+    # collective staging (CPU tensors for gloo)
+    def xfer_tensor(self, arr):
+        return torch.from_numpy(np.ascontiguousarray(arr))
+
+    def xfer_numpy(self, t):
+        return t.numpy()
+
+    def rows_buffer(self, n, ncols):
+        return torch.zeros((max(n, 0), max(ncols, 1)), dtype=torch.int32)
+
+    def rows_out(self, t):
+        return torch.from_numpy(t.rows.astype(np.int32).reshape(-1, max(len(t.vars), 1)).copy())
+
+    def rows_pad(self, buf, width, ncols):
+        out = self.rows_buffer(width, ncols)
+        out[:buf.shape[0]] = buf
+        return out
+
+    def rows_in(self, kind, vars_, buf, n):
+        return NTable(kind, vars_, buf[:n].numpy().astype(np.uint32).reshape(-1, len(vars_)))
+
+    def rows_in_many(self, kind, vars_, bufs, counts):
+        parts = [b[:c].numpy() for b, c in zip(bufs, counts)]
+        return NTable(kind, vars_, np.concatenate(parts).astype(np.uint32).reshape(-1, len(vars_)))
+
+
+def _queries():
+    V = lambda n: ["Var", n]  # noqa: E731
+    m = lambda a, b: ["Link", "Member", True, [a, b]]  # noqa: E731
+    i = lambda a, b: ["Link", "Inheritance", True, [a, b]]  # noqa: E731
+    g = lambda k: ["Node", "Gene", f"g{k}"]  # noqa: E731
+    bp = lambda k: ["Node", "BiologicalProcess", f"bp{k}"]  # noqa: E731
+    return [
+        m(V("G"), V("B")),
+        m(V("G"), bp(0)),
+        ["And", [m(V("G"), V("B")), i(V("B"), V("P"))]],
+        ["And", [m(g(3), V("B")), m(g(5), V("B"))]],
+        ["And", [m(V("G"), bp(0)), m(V("G"), V("B"))]],
+        ["And", [m(V("G"), V("B")), ["Not", m(V("G"), bp(1))]]],
+        ["Or", [m(V("G"), bp(0)), m(V("G"), bp(2))]],
+        ["Or", [i(V("B"), V("P")), ["Not", i(V("B"), bp(0))]]],
+        ["And", [i(V("A"), V("B")), i(V("B"), V("C")), i(V("C"), V("D"))]],
+        ["And", [m(g(7), V("B")), i(V("X"), V("Y"))]],           # no shared variable
+        ["Link", "*", True, [V("X"), bp(0)]],                     # global dedup path
+        ["Template", "Inheritance", True, [["TVar", "A", "BiologicalProcess"], ["TVar", "B", "BiologicalProcess"]]],
+    ]
+
+
+def _worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from das_amd import synthetic
+    from das_amd.parallel import ShardedDB
+    from tests.util import build, canon
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    kb = O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3))
+    sdb = ShardedDB(NumpyLocal(kb, rank, world), dist)
+    res = []
+    for q in _queries():
+        ans = pm.PatternMatchingAnswer()
+        m = build(q).matched(sdb, ans)
+        rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
+        res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
+                    "local": sdb.rel_local_count(ans._relation())})
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_matcher_equals_single_process_oracle(world):
+    from das_amd import synthetic
+    kb = O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3))
+    odb = O.RedisMongoSemantics(kb)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        per_rank = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    for qi, q in enumerate(_queries()):
+        want = O.evaluate(q, odb)
+        want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])
+        locals_ = 0
+        for r in range(world):
+            got = per_rank[r][qi]
+            assert got["matched"] == want["matched"] and got["negation"] == want["negation"], q
+            assert got["n"] == want["n"], (q, got["n"], want["n"])
+            assert got["rows"] == want_rows, q
+            locals_ += got["local"]
+        assert locals_ == want["n"], (q, locals_, want["n"])      # partitions are disjoint
