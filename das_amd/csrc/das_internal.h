@@ -52,7 +52,8 @@ struct CtypeRange {
 struct Index {
   bool built = false;
   uint64_t n_atoms = 0, n_nodes = 0, n_links = 0, n_types = 0;
-  Digest* digest = nullptr;    // [n_atoms], sorted by (hi, lo)
+  Digest* digest = nullptr;    // [n_atoms] by id (ids clustered by named type)
+  uint32_t* by_digest = nullptr; // [n_atoms] ids in handle (digest) order
   uint8_t* cat = nullptr;      // [n_atoms]
   uint32_t* type = nullptr;    // [n_atoms] named type id (kNone for CAT_OTHER)
   uint32_t* arity = nullptr;   // [n_atoms]

@@ -147,6 +147,38 @@ __global__ void k_pick_rep(const uint32_t* idx, uint64_t n, const uint32_t* loca
   }
 }
 
+// named-type cluster key of a temp (digest-order) id; kNone types last
+__global__ void k_temp_type(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, uint64_t n_leaf,
+                            const uint32_t* leaf_ctype, const uint32_t* leaf_type_id, const uint64_t* expr_off,
+                            const uint32_t* expr_child, uint32_t n_types, uint32_t* key) {
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n_atoms; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = rep[t];
+    uint32_t ty = kNone;
+    if (u < n_leaf) {
+      ty = leaf_type_id[leaf_ctype[u]];
+    } else if (catmax[t] == PRIO_LINK || catmax[t] == PRIO_REMOTE) {
+      ty = leaf_type_id[expr_child[expr_off[u - n_leaf]]];
+    }
+    key[t] = ty == kNone ? n_types : ty;
+  }
+}
+
+// final id f <- temp perm[f]; by_digest[temp] = f
+__global__ void k_apply_perm(uint64_t n, const uint32_t* perm, const uint32_t* rep, const uint32_t* catmax,
+                             uint32_t* rep2, uint32_t* cat2, uint32_t* by_digest) {
+  for (uint64_t f = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; f < n; f += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t t = perm[f];
+    rep2[f] = rep[t];
+    cat2[f] = catmax[t];
+    by_digest[t] = (uint32_t)f;
+  }
+}
+
+__global__ void k_remap_local(uint64_t n, const uint32_t* by_digest, uint32_t* local2id) {
+  for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x)
+    if (local2id[u] != kNone) local2id[u] = by_digest[local2id[u]];
+}
+
 __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, const Digest* dig,
                              const Digest* ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
                              const uint32_t* leaf_type_id, const uint64_t* expr_off, const uint32_t* expr_child,
@@ -195,12 +227,17 @@ __global__ void k_link_flags(const uint8_t* cat, const uint32_t* arity, uint64_t
 }
 
 __global__ void k_arity_hist(const uint8_t* cat, const uint32_t* arity, uint64_t n, unsigned long long* h) {
+  __shared__ unsigned int sh[64];
+  if (threadIdx.x < 64) sh[threadIdx.x] = 0;
+  __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (cat[i] == CAT_NODE) atomicAdd(&h[63], 1ull);
+    if (cat[i] == CAT_NODE) atomicAdd(&sh[63], 1u);
     if (cat[i] != CAT_LINK) continue;
     uint32_t a = arity[i] > 62 ? 62 : arity[i];
-    atomicAdd(&h[a], 1ull);
+    atomicAdd(&sh[a], 1u);
   }
+  __syncthreads();
+  if (threadIdx.x < 64 && sh[threadIdx.x]) atomicAdd(&h[threadIdx.x], (unsigned long long)sh[threadIdx.x]);
 }
 
 __global__ void k_ct_key(const Digest* a_ct, const uint32_t* ids, uint64_t n, uint64_t* key, bool hi) {
@@ -261,21 +298,23 @@ __global__ void k_run_emit(const K* key, const uint32_t* f, const uint32_t* scan
     }
 }
 
-__global__ void k_lookup(const Digest* dig, uint64_t n_atoms, const Digest* q, uint64_t nq, int64_t* out) {
+__global__ void k_lookup(const Digest* dig, const uint32_t* by_digest, uint64_t n_atoms, const Digest* q, uint64_t nq,
+                         int64_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t qh = q[i].hi(), ql = q[i].lo();
     uint64_t lo = 0, hi = n_atoms;
     while (lo < hi) {
       const uint64_t mid = (lo + hi) >> 1;
-      const Digest d = dig[mid];
+      const Digest d = dig[by_digest[mid]];
       const uint64_t dh = d.hi(), dl = d.lo();
       if (dh < qh || (dh == qh && dl < ql)) lo = mid + 1;
       else hi = mid;
     }
     int64_t r = -1;
     if (lo < n_atoms) {
-      const Digest d = dig[lo];
-      if (d.hi() == qh && d.lo() == ql) r = (int64_t)lo;
+      const uint32_t id = by_digest[lo];
+      const Digest d = dig[id];
+      if (d.hi() == qh && d.lo() == ql) r = (int64_t)id;
     }
     out[i] = r;
   }
@@ -410,6 +449,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
   }
   DBuf<uint32_t> local2id(nu, s), catmax(n_atoms ? n_atoms : 1, s), rep(n_atoms ? n_atoms : 1, s);
+  DAS_HIP(hipMemsetAsync(local2id.p, 0xFF, 4 * nu, s));
   DAS_HIP(hipMemsetAsync(catmax.p, 0, 4 * catmax.n, s));
   DAS_HIP(hipMemsetAsync(rep.p, 0xFF, 4 * rep.n, s));
   if (nc) {
@@ -421,7 +461,31 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   }
   first.release(); scan.release(); list.release();
 
-  // 4. atom arrays (id order == handle order)
+  // 3b. final ids clustered by named type (digest order inside a type), so a
+  // variable's bindings occupy a compact id range (direct-address joins);
+  // by_digest keeps the digest order for handle lookups.
+  {
+    DBuf<uint32_t> tkey(n_atoms ? n_atoms : 1, s), perm(n_atoms ? n_atoms : 1, s);
+    if (n_atoms) {
+      hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
+                         (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
+                         (const uint64_t*)d_eoff.p, (const uint32_t*)d_child.p, a.n_types, tkey.p);
+      iota(perm.p, n_atoms, s);
+      radix_sort_pairs<uint32_t>(tkey.p, perm.p, n_atoms, 0, std::max(1, bits_for(a.n_types)), s);
+    }
+    idx.by_digest = dalloc<uint32_t>(idx, n_atoms);
+    DBuf<uint32_t> rep2(n_atoms ? n_atoms : 1, s), cat2(n_atoms ? n_atoms : 1, s);
+    if (n_atoms) {
+      hipLaunchKernelGGL(k_apply_perm, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)perm.p,
+                         (const uint32_t*)rep.p, (const uint32_t*)catmax.p, rep2.p, cat2.p, idx.by_digest);
+      hipLaunchKernelGGL(k_remap_local, G(nu), dim3(B), 0, s, nu, (const uint32_t*)idx.by_digest, local2id.p);
+      DAS_HIP(hipGetLastError());
+    }
+    rep = std::move(rep2);
+    catmax = std::move(cat2);
+  }
+
+  // 4. atom arrays (id order: named type, then handle)
   idx.n_atoms = n_atoms;
   idx.n_types = a.n_types;
   idx.digest = dalloc<Digest>(idx, n_atoms);
@@ -600,7 +664,8 @@ void lookup_digests(Ctx& c, const Digest* h, uint64_t n, int64_t* out) {
   if (!n) return;
   auto q = upload(h, n, c.s);
   DBuf<int64_t> r(n, c.s);
-  hipLaunchKernelGGL(k_lookup, G(n), dim3(B), 0, c.s, (const Digest*)c.idx.digest, c.idx.n_atoms, (const Digest*)q.p,
+  hipLaunchKernelGGL(k_lookup, G(n), dim3(B), 0, c.s, (const Digest*)c.idx.digest, (const uint32_t*)c.idx.by_digest,
+                     c.idx.n_atoms, (const Digest*)q.p,
                      n, r.p);
   DAS_HIP(hipGetLastError());
   DAS_HIP(hipMemcpyAsync(out, r.p, 8 * n, hipMemcpyDeviceToHost, c.s));

@@ -14,15 +14,64 @@ constexpr int kScanBlock = 256;
 constexpr int kScanItems = 8;
 constexpr int kScanTile = kScanBlock * kScanItems;
 
+// 32-bit wave scans on DPP lane moves (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast 15/31 across rows): VALU-latency steps instead of
+// ds_bpermute round trips.  Invalid source lanes read 0, the identity of
+// both sum and unsigned max.
+#define DAS_DPP(x, ctrl, rmask) \
+  ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), (ctrl), (rmask), 0xf, false))
+
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+  x += DAS_DPP(x, 0x111, 0xf);
+  x += DAS_DPP(x, 0x112, 0xf);
+  x += DAS_DPP(x, 0x114, 0xf);
+  x += DAS_DPP(x, 0x118, 0xf);
+  x += DAS_DPP(x, 0x142, 0xa);
+  x += DAS_DPP(x, 0x143, 0xc);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t x) {
+  x = max(x, DAS_DPP(x, 0x111, 0xf));
+  x = max(x, DAS_DPP(x, 0x112, 0xf));
+  x = max(x, DAS_DPP(x, 0x114, 0xf));
+  x = max(x, DAS_DPP(x, 0x118, 0xf));
+  x = max(x, DAS_DPP(x, 0x142, 0xa));
+  x = max(x, DAS_DPP(x, 0x143, 0xc));
+  return x;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_scan(T x) {
-  const int lane = __lane_id();
+  if constexpr (sizeof(T) == 4) {
+    return (T)wave_incl_sum_u32((uint32_t)x);
+  } else {
+    const int lane = __lane_id();
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    T y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
+    for (int d = 1; d < 64; d <<= 1) {
+      T y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    return x;
   }
-  return x;
+}
+
+// One atomicAdd per lane on base[slot]; lanes sharing the first active lane's
+// slot are merged into a single atomic (Zipf hubs put many equal keys in one
+// wave).  Returns the lane's pre-increment value.  Call wave-uniformly.
+__device__ __forceinline__ uint32_t wave_agg_atomic_inc(uint32_t* base, uint32_t slot, bool active) {
+  const uint64_t act = __ballot(active);
+  if (!act) return 0;
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)act) - 1;
+  const uint32_t ls = __shfl(slot, leader, 64);
+  const bool same = active && slot == ls;
+  const uint64_t m = __ballot(same);
+  uint32_t b = 0;
+  if (lane == leader) b = atomicAdd(&base[ls], (uint32_t)__popcll(m));
+  b = __shfl(b, leader, 64);
+  if (same) return b + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  return active ? atomicAdd(&base[slot], 1u) : 0u;
 }
 
 template <typename T>

@@ -275,15 +275,21 @@ __global__ void k_gather_cols(ColSet src, const uint32_t* idx, uint64_t n, uint3
 // Direct-address join on one shared variable (atom ids are dense):
 //   build  k_key_minmax -> k_key_hist -> scan -> k_key_scatter   (counting sort)
 //   probe  k_dj_count (per-tile output totals) -> scan -> k_dj_write
-// k_dj_write processes 256 probe rows per round: their bucket sizes are
-// prefix-summed in LDS and the round's outputs are written by all 256 threads
-// (output o -> row by an 8-step LDS search), so fan-out is balanced inside the
-// round and every output column is stored coalesced.
+// Probe tiles are kDjTile rows.  k_dj_write first resolves the whole tile
+// (all key and bucket loads issued together), compacts the matching rows
+// into LDS with their output prefix, then each wave expands a contiguous
+// quarter of the tile's outputs 64 at a time: the rows starting inside a
+// 64-output window are scattered into a per-wave owner array and a wave
+// max-scan gives every lane its row, so stores are coalesced and no
+// per-output search is needed.
 // ---------------------------------------------------------------------------
-constexpr int kDjItems = 16;
+constexpr int kDjItems = 8;
 constexpr uint64_t kDjTile = (uint64_t)B * kDjItems;
+constexpr int kDjWaves = B / 64;
+constexpr int kDjSpan = 256;          // outputs a wave expands per step (4 per lane)
 
-__global__ void k_key_minmax(const uint32_t* key, uint64_t n, uint32_t* mm) {
+__global__ void __launch_bounds__(B) k_key_minmax(const uint32_t* key, uint64_t n, uint32_t* mm) {
+  __shared__ uint32_t s_lo[kDjWaves], s_hi[kDjWaves];
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t k = key[i];
@@ -297,90 +303,205 @@ __global__ void k_key_minmax(const uint32_t* key, uint64_t n, uint32_t* mm) {
     hi = b > hi ? b : hi;
   }
   if (__lane_id() == 0) {
+    s_lo[threadIdx.x >> 6] = lo;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kDjWaves; ++w) {
+      lo = s_lo[w] < lo ? s_lo[w] : lo;
+      hi = s_hi[w] > hi ? s_hi[w] : hi;
+    }
     atomicMin(&mm[0], lo);
     atomicMax(&mm[1], hi);
   }
 }
 
-__global__ void k_key_hist(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cnt) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[key[i] - kmin], 1u);
-}
-
-__global__ void k_key_scatter(ColSet src, const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cursor,
-                              uint32_t* out, uint64_t cap) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t pos = atomicAdd(&cursor[key[i] - kmin], 1u);
-    for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
+__global__ void __launch_bounds__(B) k_key_hist(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {   // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    const bool act = i < n;
+    wave_agg_atomic_inc(cnt, act ? key[i] - kmin : 0u, act);
   }
 }
 
-__device__ __forceinline__ uint32_t dj_bucket(const uint32_t* off, uint32_t range, uint32_t kmin, uint32_t k,
-                                              uint32_t& lo) {
-  const uint32_t d = k - kmin;             // wraps for k < kmin
-  if (d >= range) { lo = 0; return 0; }
-  lo = off[d];
-  return off[d + 1] - lo;
+__global__ void __launch_bounds__(B) k_key_scatter(ColSet src, const uint32_t* key, uint64_t n, uint32_t kmin,
+                                                   uint32_t* cursor, uint32_t* out, uint64_t cap) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool act = i < n;
+    const uint32_t pos = wave_agg_atomic_inc(cursor, act ? key[i] - kmin : 0u, act);
+    if (act)
+      for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
+  }
 }
 
 __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
                                                 const uint32_t* off, uint64_t* tile_tot) {
-  __shared__ uint64_t s_w[B / 64];
+  __shared__ uint64_t s_w[kDjWaves];
   const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
-  uint64_t acc = 0;
+  uint32_t d[kDjItems];
+#pragma unroll
   for (int it = 0; it < kDjItems; ++it) {
     const uint64_t r = t0 + (uint64_t)it * B + threadIdx.x;
-    if (r < np) {
-      uint32_t lo;
-      acc += dj_bucket(off, range, kmin, pkey[r], lo);
-    }
+    d[it] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;          // wraps for keys below kmin
   }
+  uint64_t acc = 0;
+#pragma unroll
+  for (int it = 0; it < kDjItems; ++it)
+    if (d[it] < range) acc += off[d[it] + 1] - off[d[it]];
   acc = wave_reduce_sum(acc);
   if (__lane_id() == 0) s_w[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) tile_tot[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kDjWaves; ++w) t += s_w[w];
+    tile_tot[blockIdx.x] = t;
+  }
 }
 
-// om.side[c]: 0 = probe column (staged in LDS), 1 = build column (bucket rows)
+// om.side[c]: 0 = probe column (row of the probe tile), 1 = build column
+// (bucket row).  T holds tile-local output offsets (uint32_t unless a tile
+// emits >= 2^32 rows).
+template <typename T>
 __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
                                                 const uint32_t* off, const uint64_t* tile_off, OutMap om,
                                                 uint32_t* out, uint64_t cap) {
-  __shared__ uint64_t s_pref[B + 1];
-  __shared__ uint32_t s_lo[B];
-  __shared__ uint32_t s_pv[kMaxCols][B];
-  __shared__ uint64_t s_wave[B / 64];
-  const int tid = threadIdx.x, wave = tid >> 6;
+  constexpr int E = kDjItems * kDjWaves;
+  static_assert(E <= 64, "one wave scans the per-(item, wave) totals");
+  __shared__ uint16_t s_row[kDjTile];
+  __shared__ uint32_t s_lo[kDjTile];
+  __shared__ T s_pre[kDjTile + 1];
+  __shared__ uint32_t s_nz[E];
+  __shared__ T s_sum[E];
+  __shared__ uint32_t s_own[kDjWaves][kDjSpan];
+  __shared__ uint32_t s_m;
+  __shared__ T s_tot;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
   const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
-  uint64_t base = tile_off[blockIdx.x];
+  const uint64_t lt = (1ull << lane) - 1;
+  // 1. resolve the tile: keys, then buckets (independent loads in flight)
+  uint32_t d[kDjItems], lo[kDjItems], cnt[kDjItems];
+  T inc[kDjItems];
+  uint64_t nzm[kDjItems];
+#pragma unroll
   for (int it = 0; it < kDjItems; ++it) {
     const uint64_t r = t0 + (uint64_t)it * B + tid;
-    uint32_t lo = 0, cnt = 0;
-    if (r < np) cnt = dj_bucket(off, range, kmin, pkey[r], lo);
-    s_lo[tid] = lo;
-    for (int c = 0; c < om.n; ++c)
-      if (!om.side[c]) s_pv[c][tid] = (r < np && cnt) ? om.col[c][r] : 0u;
-    const uint64_t inc = wave_inclusive_scan((uint64_t)cnt);
-    if (__lane_id() == 63) s_wave[wave] = inc;
-    __syncthreads();
-    uint64_t pre = 0;
-    for (int w = 0; w < wave; ++w) pre += s_wave[w];
-    s_pref[tid] = pre + inc - cnt;
-    if (tid == B - 1) s_pref[B] = pre + inc;
-    __syncthreads();
-    const uint64_t total = s_pref[B];
-    for (uint64_t o = tid; o < total; o += B) {
-      int a = 0, b = B;                      // last t with s_pref[t] <= o
-      while (b - a > 1) {
-        const int m = (a + b) >> 1;
-        if (s_pref[m] <= o) a = m; else b = m;
-      }
-      const uint64_t j = o - s_pref[a];
-      const uint64_t pos = base + o;
-      for (int c = 0; c < om.n; ++c)
-        out[(uint64_t)c * cap + pos] = om.side[c] ? om.col[c][s_lo[a] + j] : s_pv[c][a];
+    d[it] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int it = 0; it < kDjItems; ++it) {
+    lo[it] = 0;
+    cnt[it] = 0;
+    if (d[it] < range) {
+      lo[it] = off[d[it]];
+      cnt[it] = off[d[it] + 1] - lo[it];
     }
-    base += total;
-    __syncthreads();
+  }
+#pragma unroll
+  for (int it = 0; it < kDjItems; ++it) {
+    nzm[it] = __ballot(cnt[it] != 0);
+    inc[it] = wave_inclusive_scan((T)cnt[it]);
+    if (lane == 63) {
+      s_nz[it * kDjWaves + wave] = (uint32_t)__popcll(nzm[it]);
+      s_sum[it * kDjWaves + wave] = inc[it];
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t a = lane < E ? s_nz[lane] : 0u;
+    const T b = lane < E ? s_sum[lane] : (T)0;
+    const uint32_t ai = wave_inclusive_scan(a);
+    const T bi = wave_inclusive_scan(b);
+    if (lane < E) {
+      s_nz[lane] = ai - a;
+      s_sum[lane] = bi - b;
+    }
+    if (lane == E - 1) {
+      s_m = ai;
+      s_tot = bi;
+    }
+  }
+  __syncthreads();
+  // 2. compact matching rows (tile order) with their output prefix
+#pragma unroll
+  for (int it = 0; it < kDjItems; ++it) {
+    if (cnt[it]) {
+      const uint32_t k = s_nz[it * kDjWaves + wave] + (uint32_t)__popcll(nzm[it] & lt);
+      s_row[k] = (uint16_t)(it * B + tid);
+      s_lo[k] = lo[it];
+      s_pre[k] = s_sum[it * kDjWaves + wave] + inc[it] - (T)cnt[it];
+    }
+  }
+  const uint32_t m = s_m;
+  const T tot = s_tot;
+  if (tid == 0) s_pre[m] = tot;
+  __syncthreads();
+  if (tot == 0) return;
+  // 3. each wave expands a contiguous quarter of the tile's outputs
+  const uint64_t base = tile_off[blockIdx.x];
+  const T q = (tot + kDjWaves - 1) / kDjWaves;
+  T o0 = (T)wave * q < tot ? (T)wave * q : tot;
+  const T w1 = o0 + q < tot ? o0 + q : tot;
+  if (o0 >= w1) return;                                  // no block barrier below
+  uint32_t ka = 0, kb = m;                                // s_pre[ka] <= o0 < s_pre[kb]
+  while (kb - ka > 1) {
+    const uint32_t mid = (ka + kb) >> 1;
+    if (s_pre[mid] <= o0) ka = mid; else kb = mid;
+  }
+  uint32_t k0 = ka;
+  uint32_t* own = s_own[wave];
+  for (; o0 < w1; o0 += kDjSpan) {
+    // owner slots of the window [o0, o0 + 256): rows starting inside it
+#pragma unroll
+    for (int j = 0; j < kDjSpan / 64; ++j) own[j * 64 + lane] = 0;
+#pragma unroll
+    for (int j = 0; j < kDjSpan / 64; ++j) {
+      const uint32_t c = (uint32_t)(j * 64 + lane);
+      const uint32_t k = k0 + c;
+      if (c && k < m) {
+        const T p = s_pre[k];                              // > o0 for c >= 1
+        if (p < o0 + kDjSpan) own[(uint32_t)(p - o0)] = c;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t ow[kDjSpan / 64];
+#pragma unroll
+    for (int j = 0; j < kDjSpan / 64; ++j) ow[j] = wave_incl_max_u32(own[j * 64 + lane]);
+#pragma unroll
+    for (int j = 1; j < kDjSpan / 64; ++j) {
+      const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)ow[j - 1], 63);
+      ow[j] = ow[j] > carry ? ow[j] : carry;
+    }
+    uint64_t pr[kDjSpan / 64];
+    uint32_t br[kDjSpan / 64];
+#pragma unroll
+    for (int j = 0; j < kDjSpan / 64; ++j) {
+      const uint32_t kk = k0 + ow[j];
+      const T o = o0 + (T)(j * 64 + lane);
+      const T st = s_pre[kk];
+      pr[j] = t0 + s_row[kk];
+      br[j] = s_lo[kk] + (uint32_t)(o - st);
+    }
+    for (int c = 0; c < om.n; ++c) {
+      const uint32_t* col = om.col[c];
+      const bool bside = om.side[c];
+      uint32_t v[kDjSpan / 64];
+#pragma unroll
+      for (int j = 0; j < kDjSpan / 64; ++j)
+        if (o0 + (T)(j * 64 + lane) < w1) v[j] = col[bside ? (uint64_t)br[j] : pr[j]];
+#pragma unroll
+      for (int j = 0; j < kDjSpan / 64; ++j) {
+        const T o = o0 + (T)(j * 64 + lane);
+        if (o < w1) out[(uint64_t)c * cap + base + o] = v[j];
+      }
+    }
+    // row owning output o0 + 255, then the row owning o0 + 256
+    const uint32_t kl = k0 + (uint32_t)__builtin_amdgcn_readlane((int)ow[kDjSpan / 64 - 1], 63);
+    k0 = (kl + 1 < m && s_pre[kl + 1] <= o0 + kDjSpan) ? kl + 1 : kl;
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -686,7 +807,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     DBuf<uint32_t> mm(2, c.s);
     const uint32_t init[2] = {0xFFFFFFFFu, 0u};
     DAS_HIP(hipMemcpyAsync(mm.p, init, 8, hipMemcpyHostToDevice, c.s));
-    hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(Q.nrows, B, 1024)), dim3(B), 0, c.s, qkey, Q.nrows, mm.p);
+    hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(Q.nrows, B, 512)), dim3(B), 0, c.s, qkey, Q.nrows, mm.p);
     DAS_HIP(hipMemcpyAsync(h, mm.p, 8, hipMemcpyDeviceToHost, c.s));
     DAS_HIP(hipStreamSynchronize(c.s));
   }
@@ -734,8 +855,12 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     }
     // algorithmic bytes: probe payload + build payload + output
     ProfScope ps(c, "k_dj_write", 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
-    hipLaunchKernelGGL(k_dj_write, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
-                       (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
+    if (total < (1ull << 32) - (1ull << 16))
+      hipLaunchKernelGGL(k_dj_write<uint32_t>, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin,
+                         (uint32_t)range, (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
+    else
+      hipLaunchKernelGGL(k_dj_write<uint64_t>, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin,
+                         (uint32_t)range, (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
     DAS_HIP(hipGetLastError());
   }
   return out;

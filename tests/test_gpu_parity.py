@@ -77,7 +77,13 @@ def test_gpu_index_reproduces_reference_atoms(golden, fixture):
     dig, cat, ar, ty, nl = db._host_mirror()
     from das_amd import _lib
     hexes = _lib.digests_to_hex(dig)
-    assert hexes == sorted(hexes)                                  # id order == handle order
+    assert len(set(hexes)) == len(hexes)
+    named = [int(ty[i]) if cat[i] in (1, 2) else 1 << 32 for i in range(len(hexes))]
+    assert named == sorted(named)                                  # ids clustered by named type
+    for t in set(named):                                           # handle order inside a type
+        grp = [h for h, k in zip(hexes, named) if k == t]
+        assert grp == sorted(grp)
+    assert db.ids_of(hexes).tolist() == list(range(len(hexes)))
     nodes = sorted([h, db.arrays.type_names[int(ty[i])], db.arrays.node_name(int(nl[i]))]
                    for i, h in enumerate(hexes) if cat[i] == 1)
     assert nodes == sorted(d["nodes"])
