@@ -15,8 +15,9 @@ LIB_PATH = os.environ.get("DAS_MI355X_LIB", os.path.join(_HERE, "libdas_mi355x.s
 DAS_NONE = 0xFFFFFFFF
 TABLE_ORDERED = 0
 TABLE_UNORDERED = 1
+TABLE_COMPOSITE = 2
 
-ERR_INVALID, ERR_HIP, ERR_NOT_BUILT, ERR_UNSUPPORTED, ERR_INTERNAL = -1, -2, -3, -4, -5
+ERR_INVALID, ERR_HIP, ERR_NOT_BUILT, ERR_UNSUPPORTED, ERR_INTERNAL, ERR_ATTRIBUTE = -1, -2, -3, -4, -5, -6
 
 
 class DasNativeError(RuntimeError):
@@ -94,14 +95,17 @@ _SIGS = {
     "das_antijoin": (C.c_int, [P, P, P, C.POINTER(P)]),
     "das_dedup": (C.c_int, [P, P, C.POINTER(P)]),
     "das_concat": (C.c_int, [P, P, C.c_uint32, C.POINTER(P)]),
+    "das_set_dedup": (C.c_int, [P, P, C.c_uint32, P]),
+    "das_set_minus": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P]),
+    "das_table_members": (C.c_int, [P, P]),
     "das_table_info": (C.c_int, [P, P, P, P, P]),
     "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
-    "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
+    "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_table_free": (C.c_int, [P]),
     "das_partition": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P), P]),
     "das_table_export_rows": (C.c_int, [P, P, P]),
-    "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, C.c_uint64, C.POINTER(P)]),
+    "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
@@ -139,6 +143,8 @@ def check(rc, ctx=None):
             raise ValueError(msg)
         if rc == ERR_UNSUPPORTED:
             raise NotImplementedError(msg)
+        if rc == ERR_ATTRIBUTE:
+            raise AttributeError(msg)
         raise DasNativeError(rc, msg)
 
 
@@ -188,7 +194,7 @@ def hex_to_digest(h):
 class Table:
     """Owning wrapper of a das_table_t* (a device binding table)."""
 
-    __slots__ = ("ctx", "h", "kind", "vars", "nrows")
+    __slots__ = ("ctx", "h", "kind", "vars", "members", "nrows")
 
     def __init__(self, ctx, handle):
         self.ctx = ctx
@@ -201,10 +207,16 @@ class Table:
         self.kind = kind.value
         self.vars = tuple(vars_[i] for i in range(ncols.value))
         self.nrows = nrows.value
+        if self.kind == TABLE_COMPOSITE:
+            mem = (C.c_int32 * 16)()
+            check(lib().das_table_members(handle, mem))
+            self.members = tuple(mem[i] for i in range(ncols.value))
+        else:
+            self.members = None
 
     @property
     def schema(self):
-        return (self.kind, self.vars)
+        return (self.kind, self.vars, self.members)
 
     def fetch(self):
         n, k = self.nrows, len(self.vars)
@@ -345,11 +357,27 @@ class Context:
         arr = (P * len(tables))(*[t.h for t in tables])
         return self._table(lib().das_concat, arr, len(tables))
 
-    def table_from_host(self, kind, vars_, cols):
+    def set_dedup(self, tables):
+        """Python-set identity across tables of any kinds: first occurrence kept."""
+        arr = (P * len(tables))(*[t.h for t in tables])
+        out = (P * len(tables))()
+        check(lib().das_set_dedup(self.h, arr, len(tables), out), self.h)
+        return [Table(self, out[i]) for i in range(len(tables))]
+
+    def set_minus(self, a, b):
+        """Rows of each table of `a` whose identity is in no table of `b`."""
+        aa = (P * max(len(a), 1))(*[t.h for t in a])
+        bb = (P * max(len(b), 1))(*[t.h for t in b])
+        out = (P * max(len(a), 1))()
+        check(lib().das_set_minus(self.h, aa, len(a), bb, len(b), out), self.h)
+        return [Table(self, out[i]) for i in range(len(a))]
+
+    def table_from_host(self, kind, vars_, cols, members=None):
         cols = np.ascontiguousarray(np.asarray(cols, dtype=np.uint32))
-        v = (C.c_int32 * len(vars_))(*vars_)
+        v = (C.c_int32 * max(len(vars_), 1))(*vars_)
+        m = (C.c_int32 * max(len(vars_), 1))(*members) if members is not None else None
         n = cols.shape[1] if cols.ndim == 2 else 0
-        return self._table(lib().das_table_from_host, kind, len(vars_), v, ptr(cols), n)
+        return self._table(lib().das_table_from_host, kind, len(vars_), v, m, ptr(cols), n)
 
     def partition(self, t, key_vars, nparts):
         kv = (C.c_int32 * max(len(key_vars), 1))(*key_vars)
@@ -361,9 +389,10 @@ class Context:
     def export_rows(self, t, dptr):
         check(lib().das_table_export_rows(self.h, t.h, dptr), self.h)
 
-    def import_rows(self, kind, vars_, dptr, nrows):
+    def import_rows(self, kind, vars_, dptr, nrows, members=None):
         v = (C.c_int32 * max(len(vars_), 1))(*vars_)
-        return self._table(lib().das_table_import_rows, kind, len(vars_), v, dptr, nrows)
+        m = (C.c_int32 * max(len(vars_), 1))(*members) if members is not None else None
+        return self._table(lib().das_table_import_rows, kind, len(vars_), v, m, dptr, nrows)
 
     def prof_enable(self, on=True):
         check(lib().das_prof_enable(self.h, 1 if on else 0), self.h)

@@ -63,12 +63,29 @@ int guarded(das_ctx_t* ctx, F&& f) {
   }
 }
 
+// Schema of an imported table: composite member ids run 0, 1, .. in column
+// order after the ordered (-1) columns, each member's variables sorted.
+void check_schema(int32_t kind, int32_t ncols, const int32_t* vars, const int32_t* member) {
+  DAS_CHECK(kind >= DAS_TABLE_ORDERED && kind <= DAS_TABLE_COMPOSITE, das::DAS_E_INVALID, "bad table kind");
+  DAS_CHECK(ncols >= 0 && ncols <= das::kMaxCols, das::DAS_E_UNSUPPORTED, "too many columns");
+  if (kind != DAS_TABLE_COMPOSITE) return;
+  DAS_CHECK(member != nullptr, das::DAS_E_INVALID, "composite table without member ids");
+  int32_t prev = -1;
+  for (int c = 0; c < ncols; ++c) {
+    DAS_CHECK(member[c] == prev || member[c] == prev + 1, das::DAS_E_INVALID, "composite member ids out of order");
+    if (c > 0 && member[c] == member[c - 1])
+      DAS_CHECK(vars[c] > vars[c - 1], das::DAS_E_INVALID, "composite member variables not sorted");
+    prev = member[c];
+  }
+}
+
 das_table_t* wrap(std::unique_ptr<Table> t) {
   // das_table is layout-identical to Table; move the object into a wrapper.
   auto* w = new das_table;
   w->t.kind = t->kind;
   w->t.ncols = t->ncols;
   std::memcpy(w->t.vars, t->vars, sizeof(t->vars));
+  std::memcpy(w->t.member, t->member, sizeof(t->member));
   w->t.nrows = t->nrows;
   w->t.cap = t->cap;
   w->t.data = t->data;
@@ -121,7 +138,10 @@ int das_ctx_create(int device, void* stream, das_ctx_t** out) {
     if (stream) {
       ctx->c.s = (hipStream_t)stream;
     } else {
-      DAS_HIP(hipStreamCreateWithFlags(&ctx->c.s, hipStreamNonBlocking));
+      // a blocking stream: ordered against work on the legacy null stream
+      // (torch's default stream), so torch-side copies into buffers the
+      // library reads, and reads of buffers it wrote, need no extra fences
+      DAS_HIP(hipStreamCreateWithFlags(&ctx->c.s, hipStreamDefault));
       ctx->c.own_stream = true;
     }
   });
@@ -356,10 +376,11 @@ int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr) {
   return DAS_OK;
 }
 
-int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const uint32_t* cols,
-                        uint64_t nrows, das_table_t** out) {
+int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const int32_t* member,
+                        const uint32_t* cols, uint64_t nrows, das_table_t** out) {
   return guarded(ctx, [&] {
-    auto t = das::new_table(ctx->c, kind, ncols, vars, nrows);
+    check_schema(kind, ncols, vars, member);
+    auto t = das::new_table(ctx->c, kind, ncols, vars, nrows, member);
     t->nrows = nrows;
     for (int c = 0; c < ncols; ++c)
       if (nrows) DAS_HIP(hipMemcpyAsync(t->col(c), cols + (uint64_t)c * nrows, 4 * nrows, hipMemcpyHostToDevice, ctx->c.s));
@@ -382,9 +403,39 @@ int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst)
   return guarded(ctx, [&] { das::export_rows(ctx->c, t->t, d_dst); });
 }
 
-int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const uint32_t* d_src,
-                          uint64_t nrows, das_table_t** out) {
-  return guarded(ctx, [&] { *out = wrap(das::import_rows(ctx->c, kind, ncols, vars, d_src, nrows)); });
+int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars, const int32_t* member,
+                          const uint32_t* d_src, uint64_t nrows, das_table_t** out) {
+  return guarded(ctx, [&] {
+    check_schema(kind, ncols, vars, member);
+    *out = wrap(das::import_rows(ctx->c, kind, ncols, vars, member, d_src, nrows));
+  });
+}
+
+int das_table_members(const das_table_t* t, int32_t* member) {
+  if (!t) return fail(nullptr, DAS_ERR_INVALID, "null table");
+  for (int c = 0; c < t->t.ncols; ++c) member[c] = t->t.kind == DAS_TABLE_COMPOSITE ? t->t.member[c]
+                                                 : t->t.kind == DAS_TABLE_UNORDERED ? 0 : -1;
+  return DAS_OK;
+}
+
+int das_set_dedup(das_ctx_t* ctx, const das_table_t* const* ts, uint32_t n, das_table_t** out) {
+  return guarded(ctx, [&] {
+    std::vector<const Table*> v(n);
+    for (uint32_t i = 0; i < n; ++i) v[i] = &ts[i]->t;
+    auto r = das::set_dedup(ctx->c, v.data(), (int)n);
+    for (uint32_t i = 0; i < n; ++i) out[i] = wrap(std::move(r[i]));
+  });
+}
+
+int das_set_minus(das_ctx_t* ctx, const das_table_t* const* a, uint32_t na, const das_table_t* const* b, uint32_t nb,
+                  das_table_t** out) {
+  return guarded(ctx, [&] {
+    std::vector<const Table*> va(na), vb(nb);
+    for (uint32_t i = 0; i < na; ++i) va[i] = &a[i]->t;
+    for (uint32_t i = 0; i < nb; ++i) vb[i] = &b[i]->t;
+    auto r = das::set_minus(ctx->c, va.data(), (int)na, vb.data(), (int)nb);
+    for (uint32_t i = 0; i < na; ++i) out[i] = wrap(std::move(r[i]));
+  });
 }
 
 int das_prof_enable(das_ctx_t* ctx, int on) {

@@ -24,6 +24,7 @@ enum Status : int {
   DAS_E_NOT_BUILT = -3,   // index not built                -> RuntimeError
   DAS_E_UNSUPPORTED = -4, // shape outside this build       -> NotImplementedError
   DAS_E_INTERNAL = -5,
+  DAS_E_ATTRIBUTE = -6,   // the reference raises AttributeError here -> AttributeError
 };
 
 #define DAS_HIP(expr)                                                              \

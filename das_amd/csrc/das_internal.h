@@ -77,6 +77,7 @@ struct Table {
   int kind = DAS_TABLE_ORDERED;
   int ncols = 0;
   int32_t vars[kMaxCols] = {0};
+  int32_t member[kMaxCols] = {0};   // DAS_TABLE_COMPOSITE: -1 ordered column, else member index
   uint64_t nrows = 0, cap = 0;
   uint32_t* data = nullptr;   // ncols columns of `cap` u32 each
   hipStream_t s = nullptr;
@@ -145,17 +146,42 @@ void build_index(Ctx& c, const das_atoms_t& a);
 void free_index(Index& idx);
 void lookup_digests(Ctx& c, const Digest* h_digests, uint64_t n, int64_t* h_ids);
 
+// Column pointers of a table (kernel argument by value).
+struct ColSet {
+  const uint32_t* c[kMaxCols];
+  int n;
+};
+
 // query.hip
+ColSet cols_of(const Table& t);
+void sort_perm(const ColSet& cs, uint64_t n, uint32_t* perm, int bits, hipStream_t s);
+int id_bits(const Ctx& c);
+std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx, uint64_t m);
+std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep);
+// lo/cnt per probe row: the equal range of its key in the sorted build keys
+void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_sorted, uint64_t nb, uint32_t* lo,
+                 uint32_t* cnt);
 std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q);
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q);
 std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
 std::unique_ptr<Table> antijoin(Ctx& c, const Table& a, const Table& t);
 std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);
-std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap);
+std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap,
+                                 const int32_t* member = nullptr);
+inline std::unique_ptr<Table> new_table_like(Ctx& c, const Table& a, uint64_t cap) {
+  return new_table(c, a.kind, a.ncols, a.vars, cap, a.member);
+}
 std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
                                  uint64_t* counts);
 void export_rows(Ctx& c, const Table& t, uint32_t* dst);
-std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const uint32_t* src, uint64_t n);
+std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
+                                   const uint32_t* src, uint64_t n);
+
+// composite.hip: Unordered / Composite assignment algebra (pattern_matcher.py:158-368)
+std::unique_ptr<Table> theta_join(Ctx& c, const Table& a, const Table& b, int no_overload);
+std::unique_ptr<Table> theta_antijoin(Ctx& c, const Table& a, const Table& t);
+std::vector<std::unique_ptr<Table>> set_dedup(Ctx& c, const Table* const* ts, int n);
+std::vector<std::unique_ptr<Table>> set_minus(Ctx& c, const Table* const* a, int na, const Table* const* b, int nb);
 
 }  // namespace das

@@ -38,11 +38,6 @@ constexpr int kChunkIters = 16;                 // rows per thread per block chu
 constexpr uint64_t kChunk = (uint64_t)B * kChunkIters;
 inline dim3 G(uint64_t n) { return dim3(grid_for(n, B)); }
 
-struct ColSet {
-  const uint32_t* c[kMaxCols];
-  int n;
-};
-
 // ---------------------------------------------------------------------------
 // Scan spec (device, by value)
 // ---------------------------------------------------------------------------
@@ -505,6 +500,8 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* pkey, uint64_t n
   }
 }
 
+}  // namespace
+
 ColSet cols_of(const Table& t) {
   ColSet s{};
   s.n = t.ncols;
@@ -527,7 +524,7 @@ int id_bits(const Ctx& c) { return bits_for(c.idx.n_atoms ? c.idx.n_atoms - 1 : 
 
 // Gathers rows idx[0..m) of table `a` into a new table (same schema).
 std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx, uint64_t m) {
-  auto t = new_table(c, a.kind, a.ncols, a.vars, m);
+  auto t = new_table_like(c, a, m);
   t->nrows = m;
   if (m && a.ncols) {
     hipLaunchKernelGGL(k_gather_cols, G(m), dim3(B), 0, c.s, cols_of(a), idx, m, t->data, t->cap);
@@ -548,7 +545,7 @@ std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* kee
   DAS_HIP(hipStreamSynchronize(c.s));
   const uint64_t m = (uint64_t)h[0] + h[1];
   if (m == n) {   // nothing dropped: copy
-    auto t = new_table(c, a.kind, a.ncols, a.vars, n);
+    auto t = new_table_like(c, a, n);
     t->nrows = n;
     for (int k = 0; k < a.ncols; ++k)
       DAS_HIP(hipMemcpyAsync(t->col(k), a.col(k), 4 * n, hipMemcpyDeviceToDevice, c.s));
@@ -560,14 +557,21 @@ std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* kee
   return gather_table(c, a, idx.p, m);
 }
 
-}  // namespace
+void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_sorted, uint64_t nb, uint32_t* lo,
+                 uint32_t* cnt) {
+  if (!np) return;
+  hipLaunchKernelGGL(k_join_count, G(np), dim3(B), 0, c.s, probe, np, build_sorted, nb, lo, cnt);
+  DAS_HIP(hipGetLastError());
+}
 
-std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap) {
+std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap,
+                                 const int32_t* member) {
   DAS_CHECK(ncols >= 0 && ncols <= kMaxCols, DAS_E_UNSUPPORTED, "too many columns in a binding table");
   auto t = std::make_unique<Table>();
   t->kind = kind;
   t->ncols = ncols;
   for (int i = 0; i < ncols; ++i) t->vars[i] = vars ? vars[i] : 0;
+  for (int i = 0; i < ncols; ++i) t->member[i] = member ? member[i] : -1;
   t->s = c.s;
   t->cap = cap ? cap : 1;
   if (ncols) DAS_HIP(hipMallocAsync((void**)&t->data, 4ull * ncols * t->cap, c.s));
@@ -824,7 +828,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, cnt.p);
     exclusive_scan<uint32_t>(cnt.p, range + 1, off.p, c.s);
     DAS_HIP(hipMemcpyAsync(cnt.p, off.p, 4 * (range + 1), hipMemcpyDeviceToDevice, c.s));
-    Qs = new_table(c, Q.kind, Q.ncols, Q.vars, Q.nrows);
+    Qs = new_table_like(c, Q, Q.nrows);
     Qs->nrows = Q.nrows;
     hipLaunchKernelGGL(k_key_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin, cnt.p, Qs->data,
                        Qs->cap);
@@ -867,8 +871,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
 }
 
 std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {
-  DAS_CHECK(A.kind == DAS_TABLE_ORDERED && Bt.kind == DAS_TABLE_ORDERED, DAS_E_UNSUPPORTED,
-            "join: unordered operands are not supported by this build");
+  if (A.kind != DAS_TABLE_ORDERED || Bt.kind != DAS_TABLE_ORDERED) return theta_join(c, A, Bt, no_overload);
   // schemas
   std::vector<int32_t> va(A.vars, A.vars + A.ncols), vb(Bt.vars, Bt.vars + Bt.ncols), shared, uni;
   std::set_intersection(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(shared));
@@ -961,10 +964,9 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
 }
 
 std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
-  DAS_CHECK(A.kind == T.kind, DAS_E_UNSUPPORTED, "antijoin: mixed ordered/unordered operands");
+  if (A.kind != DAS_TABLE_ORDERED || T.kind != DAS_TABLE_ORDERED) return theta_antijoin(c, A, T);
   std::vector<int32_t> va(A.vars, A.vars + A.ncols), vt(T.vars, T.vars + T.ncols);
   const bool covered = std::includes(va.begin(), va.end(), vt.begin(), vt.end());
-  if (A.kind == DAS_TABLE_UNORDERED) DAS_CHECK(va == vt, DAS_E_UNSUPPORTED, "antijoin: unordered containment");
   if (!covered || T.nrows == 0 || A.nrows == 0) {
     DBuf<uint32_t> idx(A.nrows ? A.nrows : 1, c.s);
     iota(idx.p, A.nrows, c.s);
@@ -991,6 +993,10 @@ std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
 }
 
 std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
+  if (A.kind == DAS_TABLE_COMPOSITE) {
+    const Table* one = &A;
+    return std::move(set_dedup(c, &one, 1)[0]);
+  }
   if (A.nrows <= 1) {
     DBuf<uint32_t> idx(A.nrows ? A.nrows : 1, c.s);
     iota(idx.p, A.nrows, c.s);
@@ -1072,9 +1078,9 @@ void export_rows(Ctx& c, const Table& t, uint32_t* dst) {
   DAS_HIP(hipGetLastError());
 }
 
-std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const uint32_t* src,
-                                   uint64_t n) {
-  auto t = new_table(c, kind, ncols, vars, n);
+std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
+                                   const uint32_t* src, uint64_t n) {
+  auto t = new_table(c, kind, ncols, vars, n, member);
   t->nrows = n;
   if (n && ncols) {
     hipLaunchKernelGGL(k_rows_in, G(n), dim3(B), 0, c.s, src, n, ncols, t->data, t->cap);
@@ -1089,10 +1095,11 @@ std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {
   uint64_t total = 0;
   for (int i = 0; i < n; ++i) {
     DAS_CHECK(ts[i]->kind == f.kind && ts[i]->ncols == f.ncols, DAS_E_INVALID, "concat: schema mismatch");
-    for (int k = 0; k < f.ncols; ++k) DAS_CHECK(ts[i]->vars[k] == f.vars[k], DAS_E_INVALID, "concat: schema mismatch");
+    for (int k = 0; k < f.ncols; ++k)
+      DAS_CHECK(ts[i]->vars[k] == f.vars[k] && ts[i]->member[k] == f.member[k], DAS_E_INVALID, "concat: schema mismatch");
     total += ts[i]->nrows;
   }
-  auto t = new_table(c, f.kind, f.ncols, f.vars, total);
+  auto t = new_table_like(c, f, total);
   t->nrows = total;
   uint64_t o = 0;
   for (int i = 0; i < n; ++i) {

@@ -69,10 +69,8 @@ def _group(tables):
     return g
 
 
-def _unsupported(what):
-    raise NotImplementedError(
-        f"{what} involving unordered (Similarity/Set) assignments — the reference's "
-        "CompositeAssignment algebra (pattern_matcher.py:264-368) — is not implemented on the GPU in this build")
+def _has_composite(tables):
+    return any(t.kind == _lib.TABLE_COMPOSITE for t in tables)
 
 
 class HipDB(RelationalDB):
@@ -440,7 +438,14 @@ class HipDB(RelationalDB):
 
     # ------------------------------------------------ relation algebra (1 GPU)
     def rel_normalize(self, rel):
-        """One table per schema, rows distinct (Python set semantics)."""
+        """One table per schema, rows distinct (Python set semantics).  A
+        composite row can equal a row of another schema (XOR identity,
+        pattern_matcher.py:279-286), so relations holding composites are
+        deduplicated across all their tables by canonical identity."""
+        if _has_composite(rel.tables):
+            groups = _group(rel.tables)
+            merged = [ts[0] if len(ts) == 1 else self.ctx.concat(ts) for ts in groups.values()]
+            return Relation(self.ctx.set_dedup(merged))
         out = []
         for schema, ts in _group(rel.tables).items():
             out.append(ts[0] if len(ts) == 1 else self.ctx.dedup(self.ctx.concat(ts)))
@@ -455,8 +460,8 @@ class HipDB(RelationalDB):
         out = []
         for ta in a.tables:
             for tb in b.tables:
-                if ta.kind != _lib.TABLE_ORDERED or tb.kind != _lib.TABLE_ORDERED:
-                    _unsupported("join")
+                # ordered x ordered: natural join; any unordered operand: the
+                # CompositeAssignment algebra (:203-209, :316-351) on the GPU
                 out.append(self.ctx.join(ta, tb, CONFIG['no_overload']))
         return Relation(out)
 
@@ -466,14 +471,17 @@ class HipDB(RelationalDB):
         for f in forbidden.tables:
             nxt = []
             for t in tables:
-                if t.kind != _lib.TABLE_ORDERED or f.kind != _lib.TABLE_ORDERED:
-                    _unsupported("negation")
                 nxt.append(self.ctx.antijoin(t, f))
             tables = nxt
         return Relation(tables)
 
     def rel_minus(self, a, b):
-        """Set difference a - b by identity (same kind and variables, equal values)."""
+        """Set difference a - b by identity (same kind and variables, equal
+        values; canonical identity when composites are involved)."""
+        if _has_composite(a.tables) or _has_composite(b.tables):
+            if not a.tables or not b.tables:
+                return Relation(a.tables)
+            return Relation(self.ctx.set_minus(a.tables, b.tables))
         groups = _group(b.tables)
         out = []
         for t in a.tables:

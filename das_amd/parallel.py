@@ -32,7 +32,33 @@ import numpy as np
 from .database.db_interface import UNORDERED_LINK_TYPES, WILDCARD
 from .database.hip_db import RelationalDB
 
-ORDERED, UNORDERED = 0, 1
+ORDERED, UNORDERED, COMPOSITE = 0, 1, 2
+
+
+def _members(t):
+    return getattr(t, "members", None)
+
+
+def _has_o(t):
+    if t.kind == ORDERED:
+        return True
+    return t.kind == COMPOSITE and any(m < 0 for m in t.members)
+
+
+def _join_raises(ta, tb):
+    """The reference's AttributeError for a pair of non-empty relations
+    (pattern_matcher.py:106 via CompositeAssignment.join :348-349): the
+    absorbing composite has an ordered part and the other composite has none."""
+    if ta.kind == ORDERED or (ta.kind == UNORDERED and tb.kind == COMPOSITE):
+        x, y = tb, ta
+    else:
+        x, y = ta, tb
+    return y.kind == COMPOSITE and not _has_o(y) and _has_o(x)
+
+
+def _antijoin_raises(t, f):
+    """check_negation against a composite negation (:117, :359-360)."""
+    return f.kind == COMPOSITE and t.kind != UNORDERED
 
 
 class DRel:
@@ -76,7 +102,7 @@ class ShardedDB(RelationalDB):
         recv = self.local.rows_buffer(int(sum(rc)), ncols)
         self.dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=counts.tolist(),
                                     group=self.group)
-        return self.local.rows_in(table.kind, table.vars, recv, int(sum(rc)))
+        return self.local.rows_in(table.kind, table.vars, recv, int(sum(rc)), _members(table))
 
     def _gather_all(self, table):
         """Every rank gets the whole relation (all-gather of row blocks)."""
@@ -89,7 +115,15 @@ class ShardedDB(RelationalDB):
         padded = self.local.rows_pad(send, width, ncols)
         outs = [self.local.rows_buffer(width, ncols) for _ in range(self.world)]
         self.dist.all_gather(outs, padded, group=self.group)
-        return self.local.rows_in_many(table.kind, table.vars, outs, [int(x) for x in n])
+        return self.local.rows_in_many(table.kind, table.vars, outs, [int(x) for x in n], _members(table))
+
+    def _rank_slice(self, table):
+        """This rank's share of a table every rank holds identically."""
+        if self.world == 1:
+            return table
+        lo = table.nrows * self.rank // self.world
+        hi = table.nrows * (self.rank + 1) // self.world
+        return self.local.slice(table, lo, hi)
 
     def _allgather_counts(self, n):
         t = self.local.xfer_tensor(np.array([n], dtype=np.int64))
@@ -200,10 +234,16 @@ class ShardedDB(RelationalDB):
     def _group(self, tables):
         g = {}
         for t in tables:
-            g.setdefault((t.kind, tuple(t.vars)), []).append(t)
+            g.setdefault((t.kind, tuple(t.vars), _members(t)), []).append(t)
         return g
 
     def rel_normalize(self, rel):
+        if any(t.kind == COMPOSITE for t in rel.tables):
+            # composite identities cross schemas (XOR, :279-286): replicate,
+            # dedup identically on every rank, keep this rank's share
+            merged = [ts[0] if len(ts) == 1 else self.local.concat(ts) for ts in self._group(rel.tables).values()]
+            full = [self._gather_all(t) for t in merged]
+            return DRel([self._rank_slice(t) for t in self.local.set_dedup(full)])
         out = []
         for _, ts in self._group(rel.tables).items():
             if len(ts) == 1:
@@ -221,8 +261,16 @@ class ShardedDB(RelationalDB):
         for ta in a.tables:
             for tb in b.tables:
                 if ta.kind != ORDERED or tb.kind != ORDERED:
-                    raise NotImplementedError("join involving unordered (Similarity/Set) assignments "
-                                              "(CompositeAssignment algebra) is not implemented on the GPU")
+                    # CompositeAssignment algebra: no equality key in general;
+                    # replicate the smaller side, keep the operand order
+                    na, nb = (int(x) for x in self._allreduce_sum([ta.nrows, tb.nrows]))
+                    if na and nb and _join_raises(ta, tb):
+                        raise AttributeError("'NoneType' object has no attribute 'frozen'")
+                    if na <= nb:
+                        out.append(self.local.join(self._gather_all(ta), tb, CONFIG['no_overload']))
+                    else:
+                        out.append(self.local.join(ta, self._gather_all(tb), CONFIG['no_overload']))
+                    continue
                 shared = sorted(set(ta.vars) & set(tb.vars))
                 if shared:
                     out.append(self.local.join(self._exchange(ta, shared), self._exchange(tb, shared),
@@ -242,8 +290,13 @@ class ShardedDB(RelationalDB):
             nxt = []
             for t in tables:
                 if t.kind != ORDERED or f.kind != ORDERED:
-                    raise NotImplementedError("negation involving unordered (Similarity/Set) assignments "
-                                              "is not implemented on the GPU")
+                    nt, nf = (int(x) for x in self._allreduce_sum([t.nrows, f.nrows]))
+                    if nt and nf and _antijoin_raises(t, f):
+                        raise AttributeError("'CompositeAssignment' object has no attribute "
+                                             + ("'is_covered_by_ordered'" if t.kind == ORDERED
+                                                else "'unordered_assignments'"))
+                    nxt.append(self.local.antijoin(t, self._gather_all(f)) if nf else t)
+                    continue
                 if set(f.vars) <= set(t.vars):
                     key = sorted(f.vars)
                     nxt.append(self.local.antijoin(self._exchange(t, key), self._exchange(f, key)))
@@ -253,6 +306,12 @@ class ShardedDB(RelationalDB):
         return DRel(tables)
 
     def rel_minus(self, a, b):
+        if any(t.kind == COMPOSITE for t in a.tables + b.tables):
+            if not a.tables or not b.tables:
+                return DRel(a.tables)
+            fa = [self._gather_all(t) for t in a.tables]
+            fb = [self._gather_all(t) for t in b.tables]
+            return DRel([self._rank_slice(t) for t in self.local.set_minus(fa, fb)])
         groups = self._group(b.tables)
         out = []
         for t in a.tables:
@@ -288,8 +347,8 @@ class HipLocal:
     def rel_local_tables(self, rel):
         return rel.tables
 
-    def empty_table(self, kind, vars_):
-        return self.db.ctx.import_rows(kind, vars_, None, 0)
+    def empty_table(self, kind, vars_, members=None):
+        return self.db.ctx.import_rows(kind, vars_, None, 0, members)
 
     def partition(self, t, key_vars, nparts):
         return self.db.ctx.partition(t, key_vars, nparts)
@@ -306,6 +365,16 @@ class HipLocal:
     def antijoin(self, a, t):
         return self.db.ctx.antijoin(a, t)
 
+    def set_dedup(self, ts):
+        return self.db.ctx.set_dedup(ts)
+
+    def set_minus(self, a, b):
+        return self.db.ctx.set_minus(a, b)
+
+    def slice(self, t, lo, hi):
+        rows = self.rows_out(t)[lo:hi]
+        return self.rows_in(t.kind, t.vars, rows, hi - lo, t.members)
+
     def xfer_tensor(self, arr):
         return self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.dev)
 
@@ -317,8 +386,13 @@ class HipLocal:
 
     def rows_out(self, t):
         buf = self.torch.empty((t.nrows, max(len(t.vars), 1)), dtype=self.torch.int32, device=self.gpu)
+        # torch's allocation must be ready before the ctx stream writes it, and
+        # the ctx stream (its own, when torch runs on the null stream) must be
+        # done before torch / the collective reads it
+        self.torch.cuda.current_stream().synchronize()
         if t.nrows:
             self.db.ctx.export_rows(t, buf.data_ptr())
+        self.db.ctx.sync()
         return buf if self.dev == self.gpu else buf.cpu()
 
     def rows_pad(self, buf, width, ncols):
@@ -328,14 +402,17 @@ class HipLocal:
         out[:buf.shape[0]] = buf
         return out
 
-    def rows_in(self, kind, vars_, buf, n):
+    def rows_in(self, kind, vars_, buf, n, members=None):
         buf = buf.to(self.gpu).contiguous()
-        return self.db.ctx.import_rows(kind, list(vars_), buf.data_ptr() if n else None, n)
+        self.torch.cuda.current_stream().synchronize()     # copy / collective landed
+        t = self.db.ctx.import_rows(kind, list(vars_), buf.data_ptr() if n else None, n, members)
+        self.db.ctx.sync()                                  # before `buf` can be freed / reused
+        return t
 
-    def rows_in_many(self, kind, vars_, bufs, counts):
+    def rows_in_many(self, kind, vars_, bufs, counts, members=None):
         parts = [b[:c] for b, c in zip(bufs, counts)]
         cat = self.torch.cat(parts) if parts else self.rows_buffer(0, len(vars_))
-        return self.rows_in(kind, vars_, cat, int(sum(counts)))
+        return self.rows_in(kind, vars_, cat, int(sum(counts)), members)
 
 
 class ShardedMatcher:

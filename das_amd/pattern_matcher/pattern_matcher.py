@@ -14,10 +14,10 @@ forbidden set (:720-724, :741-746), Or with Not terms = And(negated) minus the
 positive union with negation=True (:674-683), top-level Not flips the flag
 (:627-631), `_typed_variable_matched` last-writer-wins (:491-500).
 
-Ordered assignments are evaluated entirely on the GPU.  Joins or negations
-that mix in unordered (Similarity/Set) assignments — the reference's
-CompositeAssignment algebra (:264-368) — raise NotImplementedError in this
-build rather than silently running on the host.
+All assignment kinds are evaluated on the GPU: ordered natural joins, and
+for unordered (Similarity/Set) operands the reference's Unordered /
+CompositeAssignment algebra (:158-368: containment / coverage /
+compatibility checks, XOR set identity), das_amd/csrc/composite.hip.
 """
 from abc import ABC, abstractmethod
 from collections import Counter
@@ -405,18 +405,41 @@ def _materialize(db, rel):
         cols = t.fetch()
         names = [_var_name(v) for v in t.vars]
         hexcols = [db.hex_of(c) for c in cols]
+        if t.kind == _lib.TABLE_COMPOSITE:
+            o_cols = [k for k, m in enumerate(t.members) if m < 0]
+            m_cols = {}
+            for k, m in enumerate(t.members):
+                if m >= 0:
+                    m_cols.setdefault(m, []).append(k)
         for i in range(t.nrows):
             if t.kind == _lib.TABLE_ORDERED:
-                a = OrderedAssignment()
-                for k, name in enumerate(names):
-                    a.assign(name, hexcols[k][i])
+                a = _ordered(names, hexcols, range(len(names)), i)
+            elif t.kind == _lib.TABLE_UNORDERED:
+                a = _unordered(names, hexcols, range(len(names)), i)
             else:
-                a = UnorderedAssignment()
-                for k, name in enumerate(names):
-                    a.assign(name, hexcols[k][i])
-            a.freeze()
+                us = [_unordered(names, hexcols, m_cols[m], i) for m in sorted(m_cols)]
+                a = CompositeAssignment(us[0])
+                a.unordered_mappings = us
+                a.ordered_mapping = _ordered(names, hexcols, o_cols, i) if o_cols else None
+                a._recompute_hash()
             out.add(a)
     return out
+
+
+def _ordered(names, hexcols, cols, i):
+    a = OrderedAssignment()
+    for k in cols:
+        a.assign(names[k], hexcols[k][i])
+    a.freeze()
+    return a
+
+
+def _unordered(names, hexcols, cols, i):
+    a = UnorderedAssignment()
+    for k in cols:
+        a.assign(names[k], hexcols[k][i])
+    a.freeze()
+    return a
 
 
 # ---------------------------------------------------------------------------

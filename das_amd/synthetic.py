@@ -141,3 +141,20 @@ def powerlaw_kb(n_nodes=1 << 16, n_links=1 << 20, frac_arity2=0.7, link_types=4,
         blocks.append((nm, a3[t3 == i]))
     arrays, off = build_arrays(names, [("Concept", "n", n_nodes)], blocks)
     return arrays
+
+
+def similarity_kb(n_nodes=300, n_inh=1200, n_sim=600, n_set=200, seed=SEED):
+    """Mixed ordered / unordered KB for the Composite-assignment algebra:
+    Inheritance(a, b) ordered; Similarity(a, b) and Set(a, b, c) unordered
+    (stored in both directions for Similarity, as data/samples/animals.metta
+    does), Zipf(1.1) endpoints so joins meet on hubs."""
+    rng = np.random.default_rng(seed)
+    inh = zipf_indices(rng, n_nodes, (n_inh, 2))
+    sim = zipf_indices(rng, n_nodes, (n_sim, 2))
+    sim = np.concatenate([sim, sim[:, ::-1]])
+    st = zipf_indices(rng, n_nodes, (n_set, 3))
+    arrays, off = build_arrays(
+        ["Inheritance", "Similarity", "Set"],
+        [("Concept", "c", n_nodes)],
+        [("Inheritance", inh), ("Similarity", sim), ("Set", st)])
+    return arrays

@@ -37,16 +37,20 @@ typedef struct das_table das_table_t;
 #define DAS_ERR_NOT_BUILT (-3)
 #define DAS_ERR_UNSUPPORTED (-4)
 #define DAS_ERR_INTERNAL (-5)
+#define DAS_ERR_ATTRIBUTE (-6)  /* where the reference raises AttributeError (:359-360) */
 
 #define DAS_NONE 0xFFFFFFFFu   /* "no atom / wildcard" id */
 
 #define DAS_TABLE_ORDERED 0    /* column c binds vars[c] (OrderedAssignment.mapping) */
 #define DAS_TABLE_UNORDERED 1  /* vars = variable set, columns = sorted value set
                                   (UnorderedAssignment.symbols / .values)           */
+#define DAS_TABLE_COMPOSITE 2  /* CompositeAssignment: ordered columns first (member -1,
+                                  sorted vars), then each unordered member in join
+                                  order (member m: sorted vars, sorted values)      */
 
 /* ---- context ------------------------------------------------------------ */
 /* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or NULL
- * for a private stream. */
+ * for a private blocking stream (ordered against the legacy null stream). */
 int das_ctx_create(int device, void* stream, das_ctx_t** out);
 int das_ctx_destroy(das_ctx_t* ctx);
 const char* das_last_error(const das_ctx_t* ctx);
@@ -154,16 +158,27 @@ int das_scan_template(das_ctx_t* ctx, const das_template_scan_t* q, das_table_t*
  * (link id) tables per arity: out[a] for a in 0..8 (NULL where empty). */
 int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9);
 
-/* Ordered natural join (OrderedAssignment.join/_join_ordered :105-139). */
+/* And's join step: ordered natural join (OrderedAssignment.join/_join_ordered
+ * :105-139); with an unordered/composite operand the CompositeAssignment
+ * algebra (:203-209, :316-351) -> DAS_TABLE_COMPOSITE. */
 int das_join(das_ctx_t* ctx, const das_table_t* a, const das_table_t* b, uint32_t no_overload,
              das_table_t** out);
-/* Rows of `a` that no row of `t` is covered by (check_negation :112-117 over the
- * forbidden set, And.matched :741-746); also set difference when vars equal. */
+/* Rows of `a` that pass check_negation against every row of `t` (:112-117,
+ * :211-217, :353-362; And.matched :741-746). */
 int das_antijoin(das_ctx_t* ctx, const das_table_t* a, const das_table_t* t, das_table_t** out);
 /* Set semantics (Python set of assignments): unique rows. */
 int das_dedup(das_ctx_t* ctx, const das_table_t* a, das_table_t** out);
 /* Concatenate same-schema tables. */
 int das_concat(das_ctx_t* ctx, const das_table_t* const* ts, uint32_t n, das_table_t** out);
+/* Python-set identity across tables of any kinds and schemas (Assignment.__eq__
+ * is hash equality, pattern_matcher.py:41-47; Composite hash = ordered.hash (or
+ * 1) XOR member hashes, :279-286): keeps the first occurrence of every identity
+ * in input order (table order, then row order); out[i] = rows kept of ts[i]. */
+int das_set_dedup(das_ctx_t* ctx, const das_table_t* const* ts, uint32_t n, das_table_t** out);
+/* out[i] = rows of a[i] whose identity occurs in no table of b (Or's
+ * `term_answer.assignments - or_answer.assignments`, pattern_matcher.py:679). */
+int das_set_minus(das_ctx_t* ctx, const das_table_t* const* a, uint32_t na, const das_table_t* const* b,
+                  uint32_t nb, das_table_t** out);
 
 int das_table_info(const das_table_t* t, int32_t* kind, int32_t* ncols, int32_t* vars,
                    uint64_t* nrows);
@@ -172,9 +187,13 @@ int das_table_fetch(das_ctx_t* ctx, const das_table_t* t, uint64_t row0, uint64_
                     uint32_t* out);
 /* Device pointer of column c (valid until das_table_free). */
 int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
-/* New ordered table from device/host columns (multi-GPU exchange import). */
+/* Member id per column: -1 ordered, m = unordered member m (DAS_TABLE_COMPOSITE;
+ * an UNORDERED table is member 0 throughout). */
+int das_table_members(const das_table_t* t, int32_t* member);
+/* New table from host columns (column-major ncols x nrows); member may be NULL
+ * unless kind == DAS_TABLE_COMPOSITE. */
 int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,
-                        const uint32_t* cols, uint64_t nrows, das_table_t** out);
+                        const int32_t* member, const uint32_t* cols, uint64_t nrows, das_table_t** out);
 int das_table_free(das_table_t* t);
 
 /* ---- multi-GPU exchange (RCCL all-to-all of binding rows) ----- */
@@ -186,7 +205,8 @@ int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars,
 /* Row-major (n x ncols u32) device copies for the collective buffers. */
 int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst);
 int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,
-                          const uint32_t* d_src, uint64_t nrows, das_table_t** out);
+                          const int32_t* member, const uint32_t* d_src, uint64_t nrows,
+                          das_table_t** out);
 
 /* ---- measurement ---------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the context stream (bench.py roofline):

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import das_oracle as O
-from tests.util import build, canon, record, same, uses_composite
+from tests.util import build, canon, record, same
 
 pytestmark = pytest.mark.gpu
 
@@ -123,17 +123,12 @@ def test_gpu_index_probes(golden):
 def test_gpu_queries_match_reference(golden, fixture):
     """Reference DB path semantics (tuple targets): every answer bit-exact."""
     d, db = _fixture_db(golden, fixture, tuple_targets=True)
-    unsupported, bad = [], []
+    bad = []
     for q in d["queries"]:
-        try:
-            got = record(q["query"], db)
-        except NotImplementedError:
-            unsupported.append(q["query"])
-            continue
+        got = record(q["query"], db)
         if not same(got, q):
             bad.append((q["query"], got, {k: q.get(k) for k in ("error", "matched", "negation", "n")}))
     assert not bad, bad
-    assert all(uses_composite(u) for u in unsupported), unsupported
 
 
 @pytest.mark.parametrize("fixture", KB_FIXTURES)
@@ -141,8 +136,6 @@ def test_gpu_queries_list_targets_match_oracle(golden, fixture):
     d, db = _fixture_db(golden, fixture, tuple_targets=False)
     odb = O.RedisMongoSemantics(O.KB.from_tables(d["nodes"], d["links"]), tuple_targets=False)
     for q in d["queries"]:
-        if uses_composite(q["query"]):
-            continue
         want = O.evaluate(q["query"], odb)
         got = record(q["query"], db)
         assert same(got, want), (q["query"], got, want)
@@ -285,3 +278,59 @@ def test_gpu_sharded_two_ranks_one_gpu():
             got = per_rank[r][qi]
             assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
             assert got["rows"] == want_rows, q
+
+
+def _composite_queries(rng, arrays, n):
+    """Similarity / Set (unordered) terms mixed with Inheritance: every
+    Assignment.join / check_negation kind pair of pattern_matcher.py:105-362."""
+    node_leaves = [i for i in range(arrays.n_leaf) if arrays.leaf_kind[i] == 1]
+    V = lambda x: ["Var", x]  # noqa: E731
+
+    def node():
+        t, nm = arrays.leaf_string(node_leaves[rng.integers(len(node_leaves))]).split(" ", 1)
+        return ["Node", t, nm]
+
+    inh = lambda a, b: ["Link", "Inheritance", True, [a, b]]  # noqa: E731
+    sim = lambda a, b: ["Link", "Similarity", False, [a, b]]  # noqa: E731
+    st = lambda a, b, c: ["Link", "Set", False, [a, b, c]]  # noqa: E731
+    shapes = [
+        lambda: sim(V("A"), V("B")),
+        lambda: sim(node(), V("A")),
+        lambda: ["And", [sim(V("A"), V("B")), inh(V("A"), V("C"))]],
+        lambda: ["And", [inh(V("A"), V("B")), sim(V("A"), V("B"))]],
+        lambda: ["And", [inh(V("A"), V("B")), inh(V("B"), V("C")), sim(V("A"), V("C"))]],
+        lambda: ["And", [sim(V("A"), V("B")), sim(V("B"), V("C"))]],
+        lambda: ["And", [sim(V("A"), V("B")), sim(V("A"), V("B"))]],
+        lambda: ["And", [sim(V("A"), V("B")), sim(V("B"), V("C")), inh(V("A"), V("C"))]],
+        lambda: ["And", [st(V("A"), V("B"), V("C")), sim(V("A"), V("B"))]],
+        lambda: ["And", [st(V("A"), V("B"), V("C")), inh(V("A"), V("B"))]],
+        lambda: ["And", [sim(V("A"), V("B")), ["Not", inh(V("A"), V("B"))]]],
+        lambda: ["And", [inh(V("A"), V("B")), ["Not", sim(V("A"), V("B"))]]],
+        lambda: ["And", [sim(V("A"), V("B")), ["Not", sim(V("A"), node())]]],
+        lambda: ["And", [sim(V("A"), V("B")), inh(V("B"), V("C")), ["Not", inh(V("A"), node())]]],
+        lambda: ["And", [st(V("A"), V("B"), V("C")), ["Not", sim(V("A"), V("B"))]]],
+        lambda: ["Or", [inh(V("A"), node()), sim(V("A"), V("B"))]],
+        lambda: ["Or", [["And", [sim(V("A"), V("B")), sim(V("A"), V("B"))]], sim(V("A"), V("B"))]],
+        lambda: ["Or", [["And", [sim(V("A"), V("B")), inh(V("A"), V("B"))]], ["Not", inh(V("A"), node())]]],
+        lambda: ["And", [["Or", [inh(V("A"), node()), sim(V("A"), V("B"))]], inh(V("A"), V("B"))]],
+        lambda: ["And", [sim(V("A"), V("B")), ["Template", "Similarity", False,
+                                                [["TVar", "A", "Concept"], ["TVar", "C", "Concept"]]]]],
+    ]
+    qs = [s() for s in shapes]
+    qs += [shapes[rng.integers(len(shapes))]() for _ in range(n)]
+    return qs
+
+
+@pytest.mark.parametrize("tuple_targets", [False, True])
+def test_gpu_composite_algebra_matches_oracle(tuple_targets):
+    """Unordered / Composite assignments (pattern_matcher.py:158-368) on the
+    GPU against the oracle, on a mixed ordered/unordered KB."""
+    from das_amd import synthetic
+    arrays = synthetic.similarity_kb(n_nodes=40, n_inh=300, n_sim=150, n_set=60, seed=5)
+    db = _hipdb(arrays, tuple_targets=tuple_targets)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays), tuple_targets=tuple_targets)
+    rng = np.random.default_rng(23)
+    for q in _composite_queries(rng, arrays, 20):
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert same(got, want), (q, got, {k: want.get(k) for k in ("error", "matched", "negation", "n")})

@@ -18,13 +18,14 @@ import torch.multiprocessing as mp
 
 from oracle import das_oracle as O
 
-ORDERED, UNORDERED = 0, 1
+ORDERED, UNORDERED, COMPOSITE = 0, 1, 2
 
 
 class NTable:
-    def __init__(self, kind, vars_, rows):
+    def __init__(self, kind, vars_, rows, members=None):
         self.kind = kind
         self.vars = tuple(vars_)
+        self.members = tuple(members) if kind == COMPOSITE else None
         self.rows = np.asarray(rows, dtype=np.uint32).reshape(-1, len(vars_))
 
     @property
@@ -33,10 +34,69 @@ class NTable:
 
     @property
     def schema(self):
-        return (self.kind, self.vars)
+        return (self.kind, self.vars, self.members)
 
     def fetch(self):
         return self.rows.T.copy()
+
+
+# ---- composite rows <-> the oracle's row model (ints as variables and values)
+def _parts(t):
+    """(ordered var list or None, [member var lists]) of a table schema."""
+    if t.kind == ORDERED:
+        return list(t.vars), []
+    if t.kind == UNORDERED:
+        return None, [list(t.vars)]
+    o = [v for v, m in zip(t.vars, t.members) if m < 0]
+    mem = {}
+    for v, m in zip(t.vars, t.members):
+        if m >= 0:
+            mem.setdefault(m, []).append(v)
+    return (o or None), [mem[m] for m in sorted(mem)]
+
+
+def _to_oracle(t, r):
+    r = [int(x) for x in r]
+    if t.kind == ORDERED:
+        return O.o_row(dict(zip(t.vars, r)))
+    if t.kind == UNORDERED:
+        return O.u_row(t.vars, r)
+    o, mems = _parts(t)
+    k = len(o) if o else 0
+    orow = O.o_row(dict(zip(o, r[:k]))) if o else None
+    us = []
+    for mv in mems:
+        us.append(O.u_row(mv, r[k:k + len(mv)]))
+        k += len(mv)
+    return ("C", orow, us)
+
+
+def _join_schema(a, b):
+    """Output schema of the CompositeAssignment join (composite.hip)."""
+    if a.kind == ORDERED or (a.kind == UNORDERED and b.kind == COMPOSITE):
+        x, y = b, a
+    else:
+        x, y = a, b
+    xo, xm = _parts(x)
+    yo, ym = _parts(y)
+    o = set(xo or [])
+    if y.kind != UNORDERED and not (xo and not yo):
+        o |= set(yo or [])
+    mems = xm + (ym if y.kind != ORDERED else [])
+    vars_ = sorted(o) + [v for m in mems for v in m]
+    members = [-1] * len(o) + [i for i, m in enumerate(mems) for _ in m]
+    return vars_, members
+
+
+def _from_oracle(vars_, members, rows):
+    out = []
+    for r in rows:
+        vals = dict(r[1][1]) if r[1] is not None else {}
+        line = [vals[v] for v, m in zip(vars_, members) if m < 0]
+        for u in r[2]:
+            line += list(u[2])
+        out.append(line)
+    return NTable(COMPOSITE, vars_, np.array(out, np.uint32).reshape(-1, len(vars_)), members)
 
 
 class NRel:
@@ -133,8 +193,8 @@ class NumpyLocal:
         return NRel([NTable(ORDERED if ordered else UNORDERED, vars_, sorted(rows))])
 
     # table ops
-    def empty_table(self, kind, vars_):
-        return NTable(kind, vars_, np.zeros((0, len(vars_)), np.uint32))
+    def empty_table(self, kind, vars_, members=None):
+        return NTable(kind, vars_, np.zeros((0, len(vars_)), np.uint32), members)
 
     def partition(self, t, key_vars, nparts):
         cols = [t.vars.index(v) for v in key_vars] if key_vars else list(range(len(t.vars)))
@@ -144,7 +204,7 @@ class NumpyLocal:
         dest = (h % np.uint64(nparts)).astype(np.int64)
         order = np.argsort(dest, kind="stable")
         counts = np.bincount(dest, minlength=nparts).astype(np.uint64)
-        return NTable(t.kind, t.vars, t.rows[order]), counts
+        return NTable(t.kind, t.vars, t.rows[order], t.members), counts
 
     def dedup(self, t):
         if t.nrows == 0:
@@ -152,9 +212,34 @@ class NumpyLocal:
         return NTable(t.kind, t.vars, np.unique(t.rows, axis=0))
 
     def concat(self, ts):
-        return NTable(ts[0].kind, ts[0].vars, np.concatenate([t.rows for t in ts]))
+        return NTable(ts[0].kind, ts[0].vars, np.concatenate([t.rows for t in ts]), ts[0].members)
+
+    def set_dedup(self, ts):
+        seen, out = set(), []
+        for t in ts:
+            keep = []
+            for r in t.rows:
+                k = O.ident(_to_oracle(t, r))
+                if k not in seen:
+                    seen.add(k)
+                    keep.append(r)
+            out.append(NTable(t.kind, t.vars, np.array(keep, np.uint32).reshape(-1, len(t.vars)), t.members))
+        return out
+
+    def set_minus(self, a, b):
+        gone = {O.ident(_to_oracle(t, r)) for t in b for r in t.rows}
+        return [NTable(t.kind, t.vars, np.array([r for r in t.rows if O.ident(_to_oracle(t, r)) not in gone],
+                                                np.uint32).reshape(-1, len(t.vars)), t.members) for t in a]
+
+    def slice(self, t, lo, hi):
+        return NTable(t.kind, t.vars, t.rows[lo:hi], t.members)
 
     def join(self, a, b, no_overload=False):
+        if a.kind != ORDERED or b.kind != ORDERED:
+            vars_, members = _join_schema(a, b)
+            rb = [_to_oracle(b, r) for r in b.rows]
+            out = [j for r in a.rows for y in rb for j in [O.join(_to_oracle(a, r), y)] if j is not None]
+            return _from_oracle(vars_, members, out)
         shared = sorted(set(a.vars) & set(b.vars))
         uni = sorted(set(a.vars) | set(b.vars))
         idx = {}
@@ -169,6 +254,10 @@ class NumpyLocal:
         return NTable(ORDERED, uni, np.array(out, np.uint32).reshape(-1, len(uni)))
 
     def antijoin(self, a, t):
+        if a.kind != ORDERED or t.kind != ORDERED:
+            rt = [_to_oracle(t, r) for r in t.rows]
+            keep = [r for r in a.rows if all(O.check_negation(_to_oracle(a, r), x) for x in rt)]
+            return NTable(a.kind, a.vars, np.array(keep, np.uint32).reshape(-1, len(a.vars)), a.members)
         if not set(t.vars) <= set(a.vars):
             return a
         bad = {tuple(r) for r in t.rows}
@@ -193,12 +282,12 @@ class NumpyLocal:
         out[:buf.shape[0]] = buf
         return out
 
-    def rows_in(self, kind, vars_, buf, n):
-        return NTable(kind, vars_, buf[:n].numpy().astype(np.uint32).reshape(-1, len(vars_)))
+    def rows_in(self, kind, vars_, buf, n, members=None):
+        return NTable(kind, vars_, buf[:n].numpy().astype(np.uint32).reshape(-1, len(vars_)), members)
 
-    def rows_in_many(self, kind, vars_, bufs, counts):
+    def rows_in_many(self, kind, vars_, bufs, counts, members=None):
         parts = [b[:c].numpy() for b, c in zip(bufs, counts)]
-        return NTable(kind, vars_, np.concatenate(parts).astype(np.uint32).reshape(-1, len(vars_)))
+        return NTable(kind, vars_, np.concatenate(parts).astype(np.uint32).reshape(-1, len(vars_)), members)
 
 
 def _queries():
@@ -223,20 +312,54 @@ def _queries():
     ]
 
 
-def _worker(rank, world, port, out_path):
+def _composite_queries():
+    """Similarity / Set terms: the CompositeAssignment exchange paths."""
+    V = lambda n: ["Var", n]  # noqa: E731
+    c = lambda k: ["Node", "Concept", f"c{k}"]  # noqa: E731
+    inh = lambda a, b: ["Link", "Inheritance", True, [a, b]]  # noqa: E731
+    sim = lambda a, b: ["Link", "Similarity", False, [a, b]]  # noqa: E731
+    st = lambda a, b, d: ["Link", "Set", False, [a, b, d]]  # noqa: E731
+    return [
+        sim(V("A"), V("B")),
+        sim(c(0), V("A")),
+        ["And", [inh(V("A"), V("B")), sim(V("A"), V("B"))]],
+        ["And", [sim(V("A"), V("B")), sim(V("B"), V("C"))]],
+        ["And", [sim(V("A"), V("B")), sim(V("A"), V("B"))]],
+        ["And", [inh(V("A"), V("B")), inh(V("B"), V("C")), sim(V("A"), V("C"))]],
+        ["And", [st(V("A"), V("B"), V("C")), sim(V("A"), V("B"))]],
+        ["And", [sim(V("A"), V("B")), ["Not", inh(V("A"), V("B"))]]],
+        ["And", [inh(V("A"), V("B")), ["Not", sim(V("A"), V("B"))]]],
+        ["Or", [inh(V("A"), c(1)), sim(V("A"), V("B"))]],
+        ["Or", [["And", [sim(V("A"), V("B")), inh(V("A"), V("B"))]], ["Not", inh(V("A"), c(0))]]],
+        ["And", [sim(V("A"), V("B")), sim(V("A"), V("C")), ["Not", st(V("A"), V("B"), V("C"))]]],
+    ]
+
+
+def _kb(kind):
+    from das_amd import synthetic
+    if kind == "bio":
+        return O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)), _queries()
+    return O.KB.from_arrays(synthetic.similarity_kb(n_nodes=20, n_inh=90, n_sim=45, n_set=20, seed=9)), \
+        _composite_queries()
+
+
+def _worker(rank, world, port, out_path, kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from das_amd import synthetic
     from das_amd.parallel import ShardedDB
     from tests.util import build, canon
     from das_amd.pattern_matcher import pattern_matcher as pm
-    kb = O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3))
+    kb, queries = _kb(kind)
     sdb = ShardedDB(NumpyLocal(kb, rank, world), dist)
     res = []
-    for q in _queries():
+    for q in queries:
         ans = pm.PatternMatchingAnswer()
-        m = build(q).matched(sdb, ans)
+        try:
+            m = build(q).matched(sdb, ans)
+        except AttributeError as e:
+            res.append({"error": type(e).__name__})
+            continue
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
         res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
                     "local": sdb.rel_local_count(ans._relation())})
@@ -254,16 +377,19 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world", [2])
-def test_sharded_matcher_equals_single_process_oracle(world):
-    from das_amd import synthetic
-    kb = O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3))
+@pytest.mark.parametrize("kind", ["bio", "composite"])
+def test_sharded_matcher_equals_single_process_oracle(world, kind):
+    kb, queries = _kb(kind)
     odb = O.RedisMongoSemantics(kb)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), out, kind), nprocs=world, join=True)
         per_rank = [json.load(open(f"{out}.{r}")) for r in range(world)]
-    for qi, q in enumerate(_queries()):
+    for qi, q in enumerate(queries):
         want = O.evaluate(q, odb)
+        if "error" in want:
+            assert all(per_rank[r][qi] == {"error": want["error"]} for r in range(world)), q
+            continue
         want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])
         locals_ = 0
         for r in range(world):

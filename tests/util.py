@@ -28,11 +28,23 @@ def build(spec):
 
 
 def canon(a):
+    """Canonical identity in the golden-fixture layout (oracle.canon_json)."""
     if isinstance(a, pm.OrderedAssignment):
         return ["O", [list(x) for x in sorted(a.mapping.items())]]
     if isinstance(a, pm.UnorderedAssignment):
         vals = [k for k, c in a.values.items() for _ in range(c)]
         return ["U", sorted(a.symbols.keys()), sorted(vals)]
+    if isinstance(a, pm.CompositeAssignment):
+        parity = {}
+        for u in a.unordered_mappings:
+            k = json.dumps(canon(u))
+            parity[k] = parity.get(k, 0) + 1
+        odd = sorted(k for k, c in parity.items() if c % 2)
+        o = a.ordered_mapping
+        if o is not None and not odd:
+            return canon(o)
+        return ["C", None if o is None else [list(x) for x in sorted(o.mapping.items())],
+                [json.loads(k) for k in odd]]
     raise TypeError(type(a))
 
 
