@@ -86,6 +86,8 @@ das_table_t* wrap(std::unique_ptr<Table> t) {
   w->t.ncols = t->ncols;
   std::memcpy(w->t.vars, t->vars, sizeof(t->vars));
   std::memcpy(w->t.member, t->member, sizeof(t->member));
+  std::memcpy(w->t.lo, t->lo, sizeof(t->lo));
+  std::memcpy(w->t.hi, t->hi, sizeof(t->hi));
   w->t.nrows = t->nrows;
   w->t.cap = t->cap;
   w->t.data = t->data;
@@ -157,6 +159,9 @@ int das_ctx_destroy(das_ctx_t* ctx) {
   if (!ctx) return DAS_OK;
   int rc = guarded(ctx, [&] {
     DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    das::prof_collect(ctx->c);
+    for (hipEvent_t e : ctx->c.ev_pool) (void)hipEventDestroy(e);
+    ctx->c.ev_pool.clear();
     das::free_index(ctx->c.idx);
     if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
   });
@@ -487,8 +492,8 @@ void prof_collect(Ctx& c) {
     k.ms += ms;
     k.bytes += p.bytes;
     k.launches += 1;
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
+    c.ev_pool.push_back(p.a);
+    c.ev_pool.push_back(p.b);
   }
   c.pending.clear();
 }

@@ -464,6 +464,11 @@ std::unique_ptr<Table> theta_join(Ctx& c, const Table& A, const Table& Bt, int n
   const uint64_t total = read_u64(off.p + A.nrows, c.s);
   auto out = new_table(c, DAS_TABLE_COMPOSITE, nout, vars, total, member);
   out->nrows = total;
+  for (int k = 0; k < nout; ++k) {
+    const int u = p.th.out[k];
+    out->lo[k] = u < A.ncols ? A.lo[u] : Bt.lo[u - A.ncols];
+    out->hi[k] = u < A.ncols ? A.hi[u] : Bt.hi[u - A.ncols];
+  }
   if (total) {
     ProfScope ps(c, "k_theta_write", 4.0 * total * nout);
     hipLaunchKernelGGL(k_theta_write, dim3(grid), dim3(B), 0, c.s, p.th, A.nrows, R->nrows, (const uint32_t*)lo.p,

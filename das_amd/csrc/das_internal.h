@@ -66,6 +66,12 @@ struct Index {
   std::array<RowTable, kMaxArity + 1> ctab{};
   std::array<std::array<PosIndex, kMaxPosArity>, kMaxPosArity + 1> pidx{};
   std::array<std::vector<uint64_t>, kMaxArity + 1> type_off;   // host: n_types + 1 per arity
+  // host: id bounds of T_a column c over links of named type t, at
+  // [(t * (a + 1) + c) * 2 + {0: min, 1: max}]; gbound: same over all types.
+  // Ids are clustered by named type, so a variable bound at a position of a
+  // typed link has a tight id range (direct-address joins size their
+  // offsets array from it without a device round trip).
+  std::array<std::vector<uint32_t>, kMaxArity + 1> tbound, gbound;
   std::vector<Digest> ctype_digest;                            // host: sorted ctype digests
   std::vector<CtypeRange> ctype_range;                         // host
   std::vector<void*> owned;                                    // device allocations
@@ -78,6 +84,10 @@ struct Table {
   int ncols = 0;
   int32_t vars[kMaxCols] = {0};
   int32_t member[kMaxCols] = {0};   // DAS_TABLE_COMPOSITE: -1 ordered column, else member index
+  // host-known value bounds per column (inclusive); [0, kNone] = unknown
+  uint32_t lo[kMaxCols] = {0};
+  uint32_t hi[kMaxCols] = {kNone, kNone, kNone, kNone, kNone, kNone, kNone, kNone,
+                           kNone, kNone, kNone, kNone, kNone, kNone, kNone, kNone};
   uint64_t nrows = 0, cap = 0;
   uint32_t* data = nullptr;   // ncols columns of `cap` u32 each
   hipStream_t s = nullptr;
@@ -102,6 +112,17 @@ struct PendingEv {
 struct Ctx {
   bool prof = false;
   std::vector<PendingEv> pending;
+  std::vector<hipEvent_t> ev_pool;   // recycled timing events (creation is not cheap on ROCm)
+  hipEvent_t take_event() {
+    if (ev_pool.empty()) {
+      hipEvent_t e;
+      DAS_HIP(hipEventCreate(&e));
+      return e;
+    }
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
   std::map<std::string, KStat> kstats;
   int device = 0;
   hipStream_t s = nullptr;
@@ -122,8 +143,8 @@ struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, const char* n, double algorithmic_bytes) : c(ctx), name(n), bytes(algorithmic_bytes) {
     if (!c.prof) return;
-    DAS_HIP(hipEventCreate(&a));
-    DAS_HIP(hipEventCreate(&b));
+    a = c.take_event();
+    b = c.take_event();
     DAS_HIP(hipEventRecord(a, c.s));
   }
   ~ProfScope() {
@@ -169,8 +190,14 @@ std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);
 std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* vars, uint64_t cap,
                                  const int32_t* member = nullptr);
+// Same schema and column bounds as `a` (a subset of its rows will be stored).
 inline std::unique_ptr<Table> new_table_like(Ctx& c, const Table& a, uint64_t cap) {
-  return new_table(c, a.kind, a.ncols, a.vars, cap, a.member);
+  auto t = new_table(c, a.kind, a.ncols, a.vars, cap, a.member);
+  for (int k = 0; k < a.ncols; ++k) {
+    t->lo[k] = a.lo[k];
+    t->hi[k] = a.hi[k];
+  }
+  return t;
 }
 std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
                                  uint64_t* counts);

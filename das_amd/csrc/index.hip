@@ -345,6 +345,70 @@ uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hi
   return m;
 }
 
+// Per (named type, column) id bounds of a T_a table: wave-aggregated atomics
+// (rows are sorted by type, so a wave almost always holds one type).
+__global__ void __launch_bounds__(256) k_col_bounds(const uint32_t* data, uint64_t rows, uint32_t ncol,
+                                                    const uint32_t* type, uint32_t* bnd) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < rows; i0 += stride) {
+    const uint64_t r = i0 + threadIdx.x;
+    const bool act = r < rows;
+    const uint32_t ty = act ? type[data[r]] : 0u;
+    const uint64_t am = __ballot(act);
+    const int leader = __ffsll((unsigned long long)am) - 1;
+    const uint32_t lt = __shfl(ty, leader, 64);
+    const bool uniform = __ballot(act && ty != lt) == 0;
+    for (uint32_t c = 0; c < ncol; ++c) {
+      const uint32_t v = act ? data[c * rows + r] : 0u;
+      uint32_t* b = bnd + ((uint64_t)ty * ncol + c) * 2;
+      if (uniform) {
+        uint32_t mn = act ? v : 0xFFFFFFFFu, mx = act ? v : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
+          mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+        }
+        if ((int)__lane_id() == leader) {
+          atomicMin(b, mn);
+          atomicMax(b + 1, mx);
+        }
+      } else if (act) {
+        atomicMin(b, v);
+        atomicMax(b + 1, v);
+      }
+    }
+  }
+}
+
+void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) {
+  const uint32_t ncol = (uint32_t)t.arity + 1;
+  const uint64_t nb = n_types * ncol * 2;
+  std::vector<uint32_t> h(nb);
+  for (uint64_t k = 0; k < nb; k += 2) {
+    h[k] = 0xFFFFFFFFu;
+    h[k + 1] = 0u;
+  }
+  DBuf<uint32_t> d(nb ? nb : 1, s);
+  if (nb) DAS_HIP(hipMemcpyAsync(d.p, h.data(), 4 * nb, hipMemcpyHostToDevice, s));
+  if (t.rows && nb)
+    hipLaunchKernelGGL(k_col_bounds, dim3(grid_for(t.rows, 256, 4096)), dim3(256), 0, s, (const uint32_t*)t.data,
+                       t.rows, ncol, (const uint32_t*)idx.type, d.p);
+  DAS_HIP(hipGetLastError());
+  if (nb) DAS_HIP(hipMemcpyAsync(h.data(), d.p, 4 * nb, hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  std::vector<uint32_t> g(ncol * 2);
+  for (uint32_t c = 0; c < ncol; ++c) {
+    g[2 * c] = 0xFFFFFFFFu;
+    g[2 * c + 1] = 0u;
+    for (uint64_t ty = 0; ty < n_types; ++ty) {
+      g[2 * c] = std::min(g[2 * c], h[(ty * ncol + c) * 2]);
+      g[2 * c + 1] = std::max(g[2 * c + 1], h[(ty * ncol + c) * 2 + 1]);
+    }
+  }
+  idx.tbound[t.arity] = std::move(h);
+  idx.gbound[t.arity] = std::move(g);
+}
+
 // Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact fallback).
 void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s) {
   if (n <= 1) return;
@@ -603,6 +667,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       DAS_HIP(hipMemcpyAsync(hk.data(), ukey, 4 * m, hipMemcpyDeviceToHost, s));
       DAS_HIP(hipMemcpyAsync(ho.data(), uoff, 8 * (m + 1), hipMemcpyDeviceToHost, s));
       DAS_HIP(hipStreamSynchronize(s));
+      col_bounds(idx, t, a.n_types, s);
       auto& to = idx.type_off[ar];
       to.assign(a.n_types + 1, 0);
       // to[t] = first row with type >= t

@@ -312,22 +312,27 @@ __global__ void __launch_bounds__(B) k_key_minmax(const uint32_t* key, uint64_t 
   }
 }
 
-__global__ void __launch_bounds__(B) k_key_hist(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t* cnt) {
+// Keys outside [kmin, kmin + range) cannot occur (range = the key column's
+// bound); they are skipped rather than written out of bounds.
+__global__ void __launch_bounds__(B) k_key_hist(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t range,
+                                                uint32_t* cnt) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {   // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
-    const bool act = i < n;
-    wave_agg_atomic_inc(cnt, act ? key[i] - kmin : 0u, act);
+    const uint32_t d = i < n ? key[i] - kmin : range;
+    const bool act = d < range;
+    wave_agg_atomic_inc(cnt, act ? d : 0u, act);
   }
 }
 
 __global__ void __launch_bounds__(B) k_key_scatter(ColSet src, const uint32_t* key, uint64_t n, uint32_t kmin,
-                                                   uint32_t* cursor, uint32_t* out, uint64_t cap) {
+                                                   uint32_t range, uint32_t* cursor, uint32_t* out, uint64_t cap) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {
     const uint64_t i = i0 + threadIdx.x;
-    const bool act = i < n;
-    const uint32_t pos = wave_agg_atomic_inc(cursor, act ? key[i] - kmin : 0u, act);
+    const uint32_t d = i < n ? key[i] - kmin : range;
+    const bool act = d < range;
+    const uint32_t pos = wave_agg_atomic_inc(cursor, act ? d : 0u, act);
     if (act)
       for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
   }
@@ -572,6 +577,10 @@ std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* var
   t->ncols = ncols;
   for (int i = 0; i < ncols; ++i) t->vars[i] = vars ? vars[i] : 0;
   for (int i = 0; i < ncols; ++i) t->member[i] = member ? member[i] : -1;
+  for (int i = 0; i < ncols; ++i) {
+    t->lo[i] = 0;
+    t->hi[i] = kNone;
+  }
   t->s = c.s;
   t->cap = cap ? cap : 1;
   if (ncols) DAS_HIP(hipMallocAsync((void**)&t->data, 4ull * ncols * t->cap, c.s));
@@ -583,8 +592,57 @@ std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* var
 // ---------------------------------------------------------------------------
 namespace {
 
+std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t end, int kind, int ncols,
+                                     const int32_t* vars);
+
+// Bounds of a scan's output columns from the index's per-type column bounds
+// (ordered: the source position; unordered: the union over wildcard positions).
+void scan_bounds(const Index& idx, const ScanSpec& sp, uint32_t type_id, Table& t) {
+  const uint32_t ar = sp.arity, ncol = ar + 1;
+  auto src = [&](int col, uint32_t& lo, uint32_t& hi) {
+    const auto& tb = idx.tbound[ar];
+    const auto& gb = idx.gbound[ar];
+    if (type_id != kNone && (uint64_t)(type_id + 1) * ncol * 2 <= tb.size()) {
+      lo = tb[((uint64_t)type_id * ncol + col) * 2];
+      hi = tb[((uint64_t)type_id * ncol + col) * 2 + 1];
+    } else if ((uint64_t)col * 2 + 1 < gb.size()) {
+      lo = gb[col * 2];
+      hi = gb[col * 2 + 1];
+    } else {
+      lo = 0;
+      hi = kNone;
+    }
+  };
+  for (int k = 0; k < t.ncols; ++k) {
+    if (!sp.unordered) {
+      src(1 + sp.outpos[k], t.lo[k], t.hi[k]);
+      continue;
+    }
+    if (sp.emit_link && k == 0) {
+      src(0, t.lo[k], t.hi[k]);
+      continue;
+    }
+    uint32_t lo = kNone, hi = 0;
+    for (uint32_t i = 0; i < sp.nupos; ++i) {
+      uint32_t l, h;
+      src(1 + (int)sp.upos[i], l, h);
+      lo = std::min(lo, l);
+      hi = std::max(hi, h);
+    }
+    t.lo[k] = lo;
+    t.hi[k] = hi;
+  }
+}
+
 std::unique_ptr<Table> run_scan(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t end, int kind, int ncols,
-                                const int32_t* vars) {
+                                const int32_t* vars, uint32_t type_id) {
+  auto t = run_scan_rows(c, sp, begin, end, kind, ncols, vars);
+  scan_bounds(c.idx, sp, type_id, *t);
+  return t;
+}
+
+std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t end, int kind, int ncols,
+                                     const int32_t* vars) {
   const uint64_t n = end > begin ? end - begin : 0;
   if (!n) return new_table(c, kind, ncols, vars, 0);
   const uint64_t chunks = (n + kChunk - 1) / kChunk;
@@ -744,7 +802,7 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
   bool filt = false;
   for (uint32_t p = 0; p < ar; ++p) filt |= sp.fixed[p] != kNone;
   sp.all_keep = !filt && sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
-  return run_scan(c, sp, begin, end, kind, ncols, vars);
+  return run_scan(c, sp, begin, end, kind, ncols, vars, q.type_id);
 }
 
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
@@ -788,7 +846,7 @@ std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
   DAS_CHECK(cr.begin <= cr.end && cr.end <= idx.ctab[cr.arity].rows, DAS_E_INTERNAL, "template range outside its table");
   set_cols(sp, idx.ctab[cr.arity]);
   sp.all_keep = sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
-  return run_scan(c, sp, cr.begin, cr.end, kind, ncols, vars);
+  return run_scan(c, sp, cr.begin, cr.end, kind, ncols, vars, kNone);
 }
 
 // ---------------------------------------------------------------------------
@@ -806,7 +864,12 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   const uint32_t* qkey = Q.col(colof(Q, var));
   const uint32_t* pkey = P.col(colof(P, var));
   uint32_t h[2] = {0u, (uint32_t)(c.idx.n_atoms ? c.idx.n_atoms - 1 : 0)};
-  if (c.idx.n_atoms > std::max<uint64_t>(8 * Q.nrows, 1ull << 22)) {
+  const int qk = colof(Q, var);
+  if (Q.hi[qk] != kNone && Q.lo[qk] <= Q.hi[qk]) {
+    // host-known bound of the key column (index column bounds): no round trip
+    h[0] = Q.lo[qk];
+    h[1] = Q.hi[qk];
+  } else if (c.idx.n_atoms > std::max<uint64_t>(8 * Q.nrows, 1ull << 22)) {
     // large id space: bound the offsets array by the build keys' actual range
     DBuf<uint32_t> mm(2, c.s);
     const uint32_t init[2] = {0xFFFFFFFFu, 0u};
@@ -825,12 +888,13 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   {
     ProfScope ps(c, "join_build", 4.0 * Q.nrows * (Q.ncols + 1) + 8.0 * range);
     DAS_HIP(hipMemsetAsync(cnt.p, 0, 4 * (range + 1), c.s));
-    hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, cnt.p);
+    hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, cnt.p);
     exclusive_scan<uint32_t>(cnt.p, range + 1, off.p, c.s);
     DAS_HIP(hipMemcpyAsync(cnt.p, off.p, 4 * (range + 1), hipMemcpyDeviceToDevice, c.s));
     Qs = new_table_like(c, Q, Q.nrows);
     Qs->nrows = Q.nrows;
-    hipLaunchKernelGGL(k_key_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin, cnt.p, Qs->data,
+    hipLaunchKernelGGL(k_key_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin, (uint32_t)range,
+                       cnt.p, Qs->data,
                        Qs->cap);
     DAS_HIP(hipGetLastError());
   }
@@ -947,6 +1011,15 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
                          (const uint32_t*)lo.p, om, total, out->data, out->cap);
       DAS_HIP(hipGetLastError());
     }
+  }
+  // output column bounds: the source column's (both sides' intersection for a shared variable)
+  for (int k = 0; k < out->ncols; ++k) {
+    uint32_t lo = 0, hi = kNone;
+    const int ia = colof(A, out->vars[k]), ib = colof(Bt, out->vars[k]);
+    if (ia >= 0) { lo = std::max(lo, A.lo[ia]); hi = std::min(hi, A.hi[ia]); }
+    if (ib >= 0) { lo = std::max(lo, Bt.lo[ib]); hi = std::min(hi, Bt.hi[ib]); }
+    out->lo[k] = lo;
+    out->hi[k] = hi;
   }
   if (no_overload && out->nrows) {
     // _join_ordered NO_COVERING path re-assigns every value (pattern_matcher.py:128-137);
@@ -1101,6 +1174,11 @@ std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {
   }
   auto t = new_table_like(c, f, total);
   t->nrows = total;
+  for (int i = 1; i < n; ++i)
+    for (int k = 0; k < f.ncols; ++k) {
+      t->lo[k] = std::min(t->lo[k], ts[i]->lo[k]);
+      t->hi[k] = std::max(t->hi[k], ts[i]->hi[k]);
+    }
   uint64_t o = 0;
   for (int i = 0; i < n; ++i) {
     for (int k = 0; k < f.ncols; ++k)
