@@ -98,6 +98,7 @@ _SIGS = {
     "das_set_dedup": (C.c_int, [P, P, C.c_uint32, P]),
     "das_set_minus": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P]),
     "das_table_members": (C.c_int, [P, P]),
+    "das_table_set_bounds": (C.c_int, [P, P, P]),
     "das_table_info": (C.c_int, [P, P, P, P, P]),
     "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
@@ -217,6 +218,12 @@ class Table:
     @property
     def schema(self):
         return (self.kind, self.vars, self.members)
+
+    def set_bounds(self, lo, hi):
+        k = len(self.vars)
+        a = (C.c_uint32 * max(k, 1))(*[int(x) for x in lo])
+        b = (C.c_uint32 * max(k, 1))(*[int(x) for x in hi])
+        check(lib().das_table_set_bounds(self.h, a, b))
 
     def fetch(self):
         n, k = self.nrows, len(self.vars)

@@ -416,6 +416,15 @@ int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int
   });
 }
 
+int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi) {
+  if (!t) return fail(nullptr, DAS_ERR_INVALID, "null table");
+  for (int c = 0; c < t->t.ncols; ++c) {
+    t->t.lo[c] = lo ? lo[c] : 0u;
+    t->t.hi[c] = hi ? hi[c] : 0xFFFFFFFFu;
+  }
+  return DAS_OK;
+}
+
 int das_table_members(const das_table_t* t, int32_t* member) {
   if (!t) return fail(nullptr, DAS_ERR_INVALID, "null table");
   for (int c = 0; c < t->t.ncols; ++c) member[c] = t->t.kind == DAS_TABLE_COMPOSITE ? t->t.member[c]

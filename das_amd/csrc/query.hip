@@ -15,6 +15,7 @@
 // per-block two-pass (count -> scan -> write) so output order is the input
 // order (deterministic) and no global atomics sit on the hot path.
 #include <algorithm>
+#include <cstdlib>
 
 #include "das_internal.h"
 
@@ -267,21 +268,12 @@ __global__ void k_gather_cols(ColSet src, const uint32_t* idx, uint64_t n, uint3
 }
 
 // ---------------------------------------------------------------------------
-// Direct-address join on one shared variable (atom ids are dense):
-//   build  k_key_minmax -> k_key_hist -> scan -> k_key_scatter   (counting sort)
-//   probe  k_dj_count (per-tile output totals) -> scan -> k_dj_write
-// Probe tiles are kDjTile rows.  k_dj_write first resolves the whole tile
-// (all key and bucket loads issued together), compacts the matching rows
-// into LDS with their output prefix, then each wave expands a contiguous
-// quarter of the tile's outputs 64 at a time: the rows starting inside a
-// 64-output window are scattered into a per-wave owner array and a wave
-// max-scan gives every lane its row, so stores are coalesced and no
-// per-output search is needed.
+// Direct-address join on one shared variable (atom ids are dense and the key
+// column's id bounds are known on the host):
+//   build  k_key_hist -> scan -> k_key_scatter (counting sort) -> k_pack_lc
+//   probe  k_dj_count (per wave-unit output totals) -> scan -> k_dj_write
 // ---------------------------------------------------------------------------
-constexpr int kDjItems = 8;
-constexpr uint64_t kDjTile = (uint64_t)B * kDjItems;
 constexpr int kDjWaves = B / 64;
-constexpr int kDjSpan = 256;          // outputs a wave expands per step (4 per lane)
 
 __global__ void __launch_bounds__(B) k_key_minmax(const uint32_t* key, uint64_t n, uint32_t* mm) {
   __shared__ uint32_t s_lo[kDjWaves], s_hi[kDjWaves];
@@ -338,171 +330,162 @@ __global__ void __launch_bounds__(B) k_key_scatter(ColSet src, const uint32_t* k
   }
 }
 
+// (lo, cnt) of a key's bucket packed in one 8-byte entry: one gather per probe
+// row instead of two (random 4-byte gathers are address-unit bound).
+// Bucket descriptor of a key: (lo, cnt) in one 8-byte entry, one gather per
+// probe row.
+__global__ void k_pack_lc(const uint32_t* off, uint32_t range, uint2* lc) {
+  for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < range; d += (uint64_t)gridDim.x * blockDim.x)
+    lc[d] = make_uint2(off[d], off[d + 1] - off[d]);
+}
+
+// Probe = wave units of kXRows consecutive probe rows (kXGroups groups of 64,
+// one row per lane).  No LDS arrays and no block barriers: a unit's counts,
+// prefix and expansion live in registers; each output chunk of 64 finds its
+// owning row by a 6-step binary search over the lanes' prefixes
+// (ds_bpermute), takes the probe values from the owner lane and gathers the
+// build payload at (bucket lo + rank inside the bucket).  Stores are one
+// coalesced 256-byte column segment per chunk.
+constexpr int kXGroups = 4;
+constexpr uint64_t kXRows = 64ull * kXGroups;
+
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
 __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
-                                                const uint32_t* off, uint64_t* tile_tot) {
-  __shared__ uint64_t s_w[kDjWaves];
-  const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
-  uint32_t d[kDjItems];
+                                                const uint2* lc, uint64_t units, uint64_t* unit_tot) {
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  for (uint64_t u = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); u < units; u += waves) {
+    const uint64_t r0 = u * kXRows;
+    uint32_t d[kXGroups];
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it) {
-    const uint64_t r = t0 + (uint64_t)it * B + threadIdx.x;
-    d[it] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;          // wraps for keys below kmin
-  }
-  uint64_t acc = 0;
+    for (int g = 0; g < kXGroups; ++g) {
+      const uint64_t r = r0 + g * 64 + lane;
+      d[g] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;       // wraps for keys below kmin
+    }
+    uint64_t acc = 0;
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it)
-    if (d[it] < range) acc += off[d[it] + 1] - off[d[it]];
-  acc = wave_reduce_sum(acc);
-  if (__lane_id() == 0) s_w[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int w = 0; w < kDjWaves; ++w) t += s_w[w];
-    tile_tot[blockIdx.x] = t;
+    for (int g = 0; g < kXGroups; ++g)
+      if (d[g] < range) acc += lc[d[g]].y;
+    acc = wave_reduce_sum(acc);
+    if (lane == 0) unit_tot[u] = acc;
   }
 }
 
-// om.side[c]: 0 = probe column (row of the probe tile), 1 = build column
-// (bucket row).  T holds tile-local output offsets (uint32_t unless a tile
-// emits >= 2^32 rows).
-template <typename T>
-__global__ void __launch_bounds__(B) k_dj_write(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
-                                                const uint32_t* off, const uint64_t* tile_off, OutMap om,
-                                                uint32_t* out, uint64_t cap) {
-  constexpr int E = kDjItems * kDjWaves;
-  static_assert(E <= 64, "one wave scans the per-(item, wave) totals");
-  __shared__ uint16_t s_row[kDjTile];
-  __shared__ uint32_t s_lo[kDjTile];
-  __shared__ T s_pre[kDjTile + 1];
-  __shared__ uint32_t s_nz[E];
-  __shared__ T s_sum[E];
-  __shared__ uint32_t s_own[kDjWaves][kDjSpan];
-  __shared__ uint32_t s_m;
-  __shared__ T s_tot;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
-  const uint64_t t0 = (uint64_t)blockIdx.x * kDjTile;
-  const uint64_t lt = (1ull << lane) - 1;
-  // 1. resolve the tile: keys, then buckets (independent loads in flight)
-  uint32_t d[kDjItems], lo[kDjItems], cnt[kDjItems];
-  T inc[kDjItems];
-  uint64_t nzm[kDjItems];
+// Output columns of a direct join, split by side so the kernel is
+// specialised on their counts (pointers stay in scalar registers).
+struct JoinCols {
+  const uint32_t* p[kMaxCols];   // probe-side source columns
+  const uint32_t* b[kMaxCols];   // build-side source columns (rows of the sorted build table)
+  int po[kMaxCols], bo[kMaxCols];  // their output column indices
+  int np, nb;
+};
+
+template <int NP, int NB, typename T>
+__global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                                const uint64_t* __restrict__ unit_off, JoinCols jc,
+                                                uint32_t* __restrict__ out, uint64_t cap) {
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  const uint32_t* pp[NP > 0 ? NP : 1];
+  const uint32_t* bb[NB > 0 ? NB : 1];
+  uint32_t* po[NP > 0 ? NP : 1];
+  uint32_t* bo[NB > 0 ? NB : 1];
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it) {
-    const uint64_t r = t0 + (uint64_t)it * B + tid;
-    d[it] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
-  }
+  for (int i = 0; i < NP; ++i) { pp[i] = jc.p[i]; po[i] = out + (uint64_t)jc.po[i] * cap; }
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it) {
-    lo[it] = 0;
-    cnt[it] = 0;
-    if (d[it] < range) {
-      lo[it] = off[d[it]];
-      cnt[it] = off[d[it] + 1] - lo[it];
+  for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
+  for (uint64_t u = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); u < units; u += waves) {
+    const uint64_t r0 = u * kXRows;
+    uint32_t d[kXGroups];
+#pragma unroll
+    for (int g = 0; g < kXGroups; ++g) {
+      const uint64_t r = r0 + g * 64 + lane;
+      d[g] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
     }
-  }
+    uint2 e[kXGroups];
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it) {
-    nzm[it] = __ballot(cnt[it] != 0);
-    inc[it] = wave_inclusive_scan((T)cnt[it]);
-    if (lane == 63) {
-      s_nz[it * kDjWaves + wave] = (uint32_t)__popcll(nzm[it]);
-      s_sum[it * kDjWaves + wave] = inc[it];
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t a = lane < E ? s_nz[lane] : 0u;
-    const T b = lane < E ? s_sum[lane] : (T)0;
-    const uint32_t ai = wave_inclusive_scan(a);
-    const T bi = wave_inclusive_scan(b);
-    if (lane < E) {
-      s_nz[lane] = ai - a;
-      s_sum[lane] = bi - b;
-    }
-    if (lane == E - 1) {
-      s_m = ai;
-      s_tot = bi;
-    }
-  }
-  __syncthreads();
-  // 2. compact matching rows (tile order) with their output prefix
+    for (int g = 0; g < kXGroups; ++g) e[g] = d[g] < range ? lc[d[g]] : make_uint2(0u, 0u);
+    uint32_t pv[kXGroups][NP > 0 ? NP : 1];                 // probe values of this lane's rows
 #pragma unroll
-  for (int it = 0; it < kDjItems; ++it) {
-    if (cnt[it]) {
-      const uint32_t k = s_nz[it * kDjWaves + wave] + (uint32_t)__popcll(nzm[it] & lt);
-      s_row[k] = (uint16_t)(it * B + tid);
-      s_lo[k] = lo[it];
-      s_pre[k] = s_sum[it * kDjWaves + wave] + inc[it] - (T)cnt[it];
+    for (int g = 0; g < kXGroups; ++g) {
+      const uint64_t r = r0 + g * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) pv[g][i] = r < np ? pp[i][r] : 0u;
     }
-  }
-  const uint32_t m = s_m;
-  const T tot = s_tot;
-  if (tid == 0) s_pre[m] = tot;
-  __syncthreads();
-  if (tot == 0) return;
-  // 3. each wave expands a contiguous quarter of the tile's outputs
-  const uint64_t base = tile_off[blockIdx.x];
-  const T q = (tot + kDjWaves - 1) / kDjWaves;
-  T o0 = (T)wave * q < tot ? (T)wave * q : tot;
-  const T w1 = o0 + q < tot ? o0 + q : tot;
-  if (o0 >= w1) return;                                  // no block barrier below
-  uint32_t ka = 0, kb = m;                                // s_pre[ka] <= o0 < s_pre[kb]
-  while (kb - ka > 1) {
-    const uint32_t mid = (ka + kb) >> 1;
-    if (s_pre[mid] <= o0) ka = mid; else kb = mid;
-  }
-  uint32_t k0 = ka;
-  uint32_t* own = s_own[wave];
-  for (; o0 < w1; o0 += kDjSpan) {
-    // owner slots of the window [o0, o0 + 256): rows starting inside it
+    uint64_t base = unit_off[u];
 #pragma unroll
-    for (int j = 0; j < kDjSpan / 64; ++j) own[j * 64 + lane] = 0;
+    for (int g = 0; g < kXGroups; ++g) {
+      const T c = (T)e[g].y;
+      const T inc = wave_inclusive_scan(c);
+      const T tot = (T)__shfl(inc, 63, 64);
+      const T pre = inc - c;                                 // this lane's first output
+      for (T o0 = 0; o0 < tot; o0 += 64) {
+        const T o = o0 + (T)lane;
+        int l = 0;                                           // owner: max lane with pre <= o
 #pragma unroll
-    for (int j = 0; j < kDjSpan / 64; ++j) {
-      const uint32_t c = (uint32_t)(j * 64 + lane);
-      const uint32_t k = k0 + c;
-      if (c && k < m) {
-        const T p = s_pre[k];                              // > o0 for c >= 1
-        if (p < o0 + kDjSpan) own[(uint32_t)(p - o0)] = c;
+        for (int step = 32; step >= 1; step >>= 1) {
+          const T pl = (T)__shfl(pre, l + step, 64);
+          if (l + step < 64 && pl <= o) l += step;
+        }
+        const bool act = o < tot;
+        const uint32_t j = (uint32_t)(o - (T)__shfl(pre, l, 64));
+        const uint32_t br = lane_get(e[g].x, l) + j;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const uint32_t v = lane_get(pv[g][i], l);
+          if (act) po[i][base + o] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (act) bo[i][base + o] = bb[i][br];
       }
+      base += tot;
     }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t ow[kDjSpan / 64];
-#pragma unroll
-    for (int j = 0; j < kDjSpan / 64; ++j) ow[j] = wave_incl_max_u32(own[j * 64 + lane]);
-#pragma unroll
-    for (int j = 1; j < kDjSpan / 64; ++j) {
-      const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)ow[j - 1], 63);
-      ow[j] = ow[j] > carry ? ow[j] : carry;
-    }
-    uint64_t pr[kDjSpan / 64];
-    uint32_t br[kDjSpan / 64];
-#pragma unroll
-    for (int j = 0; j < kDjSpan / 64; ++j) {
-      const uint32_t kk = k0 + ow[j];
-      const T o = o0 + (T)(j * 64 + lane);
-      const T st = s_pre[kk];
-      pr[j] = t0 + s_row[kk];
-      br[j] = s_lo[kk] + (uint32_t)(o - st);
-    }
-    for (int c = 0; c < om.n; ++c) {
-      const uint32_t* col = om.col[c];
-      const bool bside = om.side[c];
-      uint32_t v[kDjSpan / 64];
-#pragma unroll
-      for (int j = 0; j < kDjSpan / 64; ++j)
-        if (o0 + (T)(j * 64 + lane) < w1) v[j] = col[bside ? (uint64_t)br[j] : pr[j]];
-#pragma unroll
-      for (int j = 0; j < kDjSpan / 64; ++j) {
-        const T o = o0 + (T)(j * 64 + lane);
-        if (o < w1) out[(uint64_t)c * cap + base + o] = v[j];
-      }
-    }
-    // row owning output o0 + 255, then the row owning o0 + 256
-    const uint32_t kl = k0 + (uint32_t)__builtin_amdgcn_readlane((int)ow[kDjSpan / 64 - 1], 63);
-    k0 = (kl + 1 < m && s_pre[kl + 1] <= o0 + kDjSpan) ? kl + 1 : kl;
-    __builtin_amdgcn_wave_barrier();
   }
+}
+
+template <int NP, int NB>
+void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
+                     const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out,
+                     uint64_t cap, uint64_t total) {
+  if (total < (1ull << 32) - (1ull << 16))
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+                       toff, jc, out, cap);
+  else
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint64_t>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+                       toff, jc, out, cap);
+}
+
+// dispatch on (probe cols, build cols); wide schemas use the 4 x 4 kernel in
+// column slices
+void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
+              const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out, uint64_t cap,
+              uint64_t total) {
+  int pi = 0, bi = 0;
+  do {
+    JoinCols part{};
+    part.np = std::min(jc.np - pi, 4);
+    part.nb = std::min(jc.nb - bi, 4);
+    for (int i = 0; i < part.np; ++i) { part.p[i] = jc.p[pi + i]; part.po[i] = jc.po[pi + i]; }
+    for (int i = 0; i < part.nb; ++i) { part.b[i] = jc.b[bi + i]; part.bo[i] = jc.bo[bi + i]; }
+    pi += part.np;
+    bi += part.nb;
+#define DJ(NPV, NBV)                                                                                  \
+  if (part.np == NPV && part.nb == NBV) {                                                             \
+    launch_dj_write<NPV, NBV>(grid, s, pkey, np, kmin, range, lc, units, toff, part, out, cap, total); \
+    continue;                                                                                         \
+  }
+    DJ(0, 1) DJ(0, 2) DJ(0, 3) DJ(0, 4)
+    DJ(1, 0) DJ(1, 1) DJ(1, 2) DJ(1, 3) DJ(1, 4)
+    DJ(2, 0) DJ(2, 1) DJ(2, 2) DJ(2, 3) DJ(2, 4)
+    DJ(3, 0) DJ(3, 1) DJ(3, 2) DJ(3, 3) DJ(3, 4)
+    DJ(4, 0) DJ(4, 1) DJ(4, 2) DJ(4, 3) DJ(4, 4)
+#undef DJ
+  } while (pi < jc.np || bi < jc.nb);
 }
 
 }  // namespace
@@ -869,7 +852,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     // host-known bound of the key column (index column bounds): no round trip
     h[0] = Q.lo[qk];
     h[1] = Q.hi[qk];
-  } else if (c.idx.n_atoms > std::max<uint64_t>(8 * Q.nrows, 1ull << 22)) {
+  } else if (!c.idx.n_atoms || c.idx.n_atoms > std::max<uint64_t>(8 * Q.nrows, 1ull << 22)) {
     // large id space: bound the offsets array by the build keys' actual range
     DBuf<uint32_t> mm(2, c.s);
     const uint32_t init[2] = {0xFFFFFFFFu, 0u};
@@ -898,37 +881,36 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
                        Qs->cap);
     DAS_HIP(hipGetLastError());
   }
-  // probe: per-tile totals -> scan -> fused write
-  const uint64_t tiles = (P.nrows + kDjTile - 1) / kDjTile;
-  DBuf<uint64_t> tot(tiles + 1, c.s), toff(tiles + 1, c.s);
+  const int nu = (int)uni.size();
+  JoinCols jc{};
+  for (int k = 0; k < nu; ++k) {
+    const int ip = colof(P, uni[k]);
+    if (ip >= 0) { jc.p[jc.np] = P.col(ip); jc.po[jc.np++] = k; }
+    else { jc.b[jc.nb] = Qs->col(colof(*Qs, uni[k])); jc.bo[jc.nb++] = k; }
+  }
+  DBuf<uint2> lc(range, c.s);
+  hipLaunchKernelGGL(k_pack_lc, dim3(grid_for(range, B, 2048)), dim3(B), 0, c.s, (const uint32_t*)off.p,
+                     (uint32_t)range, lc.p);
+  DAS_HIP(hipGetLastError());
+  const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
+  const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
+  DBuf<uint64_t> tot(units + 1, c.s), toff(units + 1, c.s);
   {
     ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
-    hipLaunchKernelGGL(k_dj_count, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
-                       (const uint32_t*)off.p, tot.p);
+    hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
+                       (const uint2*)lc.p, units, tot.p);
     DAS_HIP(hipGetLastError());
   }
-  DAS_HIP(hipMemsetAsync(tot.p + tiles, 0, 8, c.s));
-  exclusive_scan<uint64_t>(tot.p, tiles + 1, toff.p, c.s);
-  const uint64_t total = read_u64(toff.p + tiles, c.s);
-  const int nu = (int)uni.size();
+  DAS_HIP(hipMemsetAsync(tot.p + units, 0, 8, c.s));
+  exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
+  const uint64_t total = read_u64(toff.p + units, c.s);
   auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
   out->nrows = total;
   if (total) {
-    OutMap om{};
-    om.n = nu;
-    for (int k = 0; k < nu; ++k) {
-      int ip = colof(P, uni[k]);
-      if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
-      else { om.col[k] = Qs->col(colof(*Qs, uni[k])); om.side[k] = 1; }
-    }
     // algorithmic bytes: probe payload + build payload + output
     ProfScope ps(c, "k_dj_write", 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
-    if (total < (1ull << 32) - (1ull << 16))
-      hipLaunchKernelGGL(k_dj_write<uint32_t>, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin,
-                         (uint32_t)range, (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
-    else
-      hipLaunchKernelGGL(k_dj_write<uint64_t>, dim3((unsigned)tiles), dim3(B), 0, c.s, pkey, P.nrows, kmin,
-                         (uint32_t)range, (const uint32_t*)off.p, (const uint64_t*)toff.p, om, out->data, out->cap);
+    dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, (const uint2*)lc.p, units, (const uint64_t*)toff.p, jc,
+             out->data, out->cap, total);
     DAS_HIP(hipGetLastError());
   }
   return out;

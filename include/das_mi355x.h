@@ -187,6 +187,11 @@ int das_table_fetch(das_ctx_t* ctx, const das_table_t* t, uint64_t row0, uint64_
                     uint32_t* out);
 /* Device pointer of column c (valid until das_table_free). */
 int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
+/* Declares inclusive value bounds per column (NULL = unknown).  Joins size their
+ * direct-address buckets from the build key's bound; every value must lie inside
+ * it (values outside are dropped by the build).  Scan and join results carry
+ * bounds derived from the index, so callers only set them on imported tables. */
+int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi);
 /* Member id per column: -1 ordered, m = unordered member m (DAS_TABLE_COMPOSITE;
  * an UNORDERED table is member 0 throughout). */
 int das_table_members(const das_table_t* t, int32_t* member);
