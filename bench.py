@@ -182,7 +182,10 @@ def main():
     value = bindings / elapsed
 
     # dominant kernel of the timed region -> roofline
-    dom = max(stats.items(), key=lambda kv: kv[1]["ms"]) if stats else None
+    # single-kernel scopes only ("k_*"); multi-launch phases such as join_build
+    # are reported under "kernels" but are not a kernel's roofline
+    single = {k: v for k, v in stats.items() if k.startswith("k_")}
+    dom = max(single.items(), key=lambda kv: kv[1]["ms"]) if single else None
     roofline = None
     if dom:
         name, st = dom

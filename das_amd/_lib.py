@@ -57,7 +57,7 @@ class das_link_scan_t(C.Structure):
     _fields_ = [
         ("arity", C.c_uint32), ("type_id", C.c_uint32), ("target", C.c_uint32 * 8),
         ("var", C.c_int32 * 8), ("n_vars", C.c_uint32), ("ordered", C.c_uint32),
-        ("no_overload", C.c_uint32), ("emit_link", C.c_uint32),
+        ("no_overload", C.c_uint32), ("emit_link", C.c_uint32), ("order_pos", C.c_int32),
     ]
 
 
@@ -322,8 +322,10 @@ class Context:
         check(lib().das_ctype_lookup(self.h, ptr(d), C.byref(out)), self.h)
         return out.value
 
-    def scan_link(self, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False):
+    def scan_link(self, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False,
+                  order_pos=-1):
         q = das_link_scan_t()
+        q.order_pos = order_pos
         q.arity = arity
         q.type_id = DAS_NONE if type_id is None else type_id
         for i in range(8):

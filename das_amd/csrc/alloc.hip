@@ -1,0 +1,128 @@
+// Caching device allocator for query-time buffers.
+//
+// Every table and scratch buffer of a query lives on its context's stream, so
+// a freed block can be handed to the next allocation on the same stream with
+// no fence: stream order already puts the new work after the old.  Blocks are
+// kept per (stream, size class) and only returned to the driver when the
+// context's stream is destroyed or the cache exceeds its budget, so a query
+// step performs no runtime allocation calls once warm (the runtime's own
+// stream-ordered allocator costs microseconds per call and, under a step's
+// mix of sizes, occasionally hundreds of microseconds).
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace das {
+
+namespace {
+
+struct Cache {
+  std::mutex mu;
+  std::map<std::pair<hipStream_t, size_t>, std::vector<void*>> free_blocks;
+  std::unordered_map<void*, std::pair<hipStream_t, size_t>> live;
+  size_t cached_bytes = 0;
+};
+
+Cache& cache() {
+  static Cache* c = new Cache();   // never destroyed: frees may arrive during exit
+  return *c;
+}
+
+constexpr size_t kCacheBudget = 64ull << 30;   // cached (idle) bytes kept at most
+
+size_t size_class(size_t bytes) {
+  if (bytes <= 256) return 256;
+  if (bytes <= (1u << 20)) {                     // powers of two up to 1 MiB
+    size_t c = 512;
+    while (c < bytes) c <<= 1;
+    return c;
+  }
+  const size_t g = bytes <= (64ull << 20) ? (1ull << 20) : (16ull << 20);
+  return (bytes + g - 1) / g * g;                // 1 MiB / 16 MiB granules above
+}
+
+}  // namespace
+
+void* cache_alloc(size_t bytes, hipStream_t s) {
+  if (!bytes) return nullptr;
+  const size_t cls = size_class(bytes);
+  Cache& c = cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.free_blocks.find({s, cls});
+    if (it != c.free_blocks.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      c.cached_bytes -= cls;
+      c.live[p] = {s, cls};
+      return p;
+    }
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, cls);
+  if (e != hipSuccess) {
+    // out of memory with idle blocks cached: give them back and retry once
+    (void)hipGetLastError();
+    std::vector<void*> idle;
+    {
+      std::lock_guard<std::mutex> lk(c.mu);
+      for (auto& kv : c.free_blocks) idle.insert(idle.end(), kv.second.begin(), kv.second.end());
+      c.free_blocks.clear();
+      c.cached_bytes = 0;
+    }
+    DAS_HIP(hipDeviceSynchronize());
+    for (void* q : idle) (void)hipFree(q);
+    DAS_HIP(hipMalloc(&p, cls));
+  }
+  std::lock_guard<std::mutex> lk(c.mu);
+  c.live[p] = {s, cls};
+  return p;
+}
+
+void cache_free(void* p) {
+  if (!p) return;
+  Cache& c = cache();
+  void* drop = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return;
+    const auto key = it->second;
+    c.live.erase(it);
+    if (c.cached_bytes + key.second > kCacheBudget) {
+      drop = p;
+    } else {
+      c.free_blocks[key].push_back(p);
+      c.cached_bytes += key.second;
+    }
+  }
+  if (drop) {
+    (void)hipDeviceSynchronize();   // the block may still be in use by queued work
+    (void)hipFree(drop);
+  }
+}
+
+void cache_release_stream(hipStream_t s) {
+  Cache& c = cache();
+  std::vector<void*> idle;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto it = c.free_blocks.begin(); it != c.free_blocks.end();) {
+      if (it->first.first == s) {
+        for (void* p : it->second) {
+          idle.push_back(p);
+          c.cached_bytes -= it->first.second;
+        }
+        it = c.free_blocks.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (void* p : idle) (void)hipFree(p);
+}
+
+}  // namespace das

@@ -1,6 +1,8 @@
 // extern "C" boundary (include/das_mi355x.h).  Every entry point catches
 // das::Error / std::exception and returns a status; the message is kept per
 // context for das_last_error.
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -39,12 +41,39 @@ bool sync_check() {
   return on;
 }
 
+// DAS_HOST_TRACE=1: one stderr line per entry point with its host time (us),
+// to attribute host-side gaps between kernels.
+bool host_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("DAS_HOST_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+struct HostTrace {
+  const char* fn;
+  std::chrono::steady_clock::time_point t0;
+  explicit HostTrace(const char* f) : fn(f) {
+    if (host_trace()) t0 = std::chrono::steady_clock::now();
+  }
+  ~HostTrace() {
+    if (!host_trace()) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[das] %-26s %12.1f %8.1f\n", fn,
+                 std::chrono::duration<double, std::micro>(t0.time_since_epoch()).count(),
+                 std::chrono::duration<double, std::micro>(t1 - t0).count());
+  }
+};
+
 template <typename F>
-int guarded(das_ctx_t* ctx, F&& f) {
+int guarded(das_ctx_t* ctx, F&& f, const char* fn = __builtin_FUNCTION()) {
+  HostTrace tr(fn);
   try {
     if (ctx) {
       std::lock_guard<std::mutex> lk(ctx->c.mu);
-      DAS_HIP(hipSetDevice(ctx->c.device));
+      int cur = -1;
+      if (hipGetDevice(&cur) != hipSuccess || cur != ctx->c.device) DAS_HIP(hipSetDevice(ctx->c.device));
       f();
       if (sync_check()) {
         DAS_HIP(hipStreamSynchronize(ctx->c.s));
@@ -80,18 +109,9 @@ void check_schema(int32_t kind, int32_t ncols, const int32_t* vars, const int32_
 }
 
 das_table_t* wrap(std::unique_ptr<Table> t) {
-  // das_table is layout-identical to Table; move the object into a wrapper.
+  // das_table holds a Table; take over every field and the device buffer
   auto* w = new das_table;
-  w->t.kind = t->kind;
-  w->t.ncols = t->ncols;
-  std::memcpy(w->t.vars, t->vars, sizeof(t->vars));
-  std::memcpy(w->t.member, t->member, sizeof(t->member));
-  std::memcpy(w->t.lo, t->lo, sizeof(t->lo));
-  std::memcpy(w->t.hi, t->hi, sizeof(t->hi));
-  w->t.nrows = t->nrows;
-  w->t.cap = t->cap;
-  w->t.data = t->data;
-  w->t.s = t->s;
+  w->t = *t;
   t->data = nullptr;
   return w;
 }
@@ -163,6 +183,7 @@ int das_ctx_destroy(das_ctx_t* ctx) {
     for (hipEvent_t e : ctx->c.ev_pool) (void)hipEventDestroy(e);
     ctx->c.ev_pool.clear();
     das::free_index(ctx->c.idx);
+    das::cache_release_stream(ctx->c.s);
     if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
   });
   delete ctx;
@@ -329,7 +350,7 @@ int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9) {
       auto t = das::new_table(ctx->c, DAS_TABLE_ORDERED, a + 1, vars, e - b);
       t->nrows = e - b;
       for (int k = 0; k <= a; ++k)
-        DAS_HIP(hipMemcpyAsync(t->col(k), rt.col(k) + b, 4 * (e - b), hipMemcpyDeviceToDevice, ctx->c.s));
+        das::copy_dev(t->col(k), rt.col(k) + b, 4 * (e - b), ctx->c.s);
       out9[a] = wrap(std::move(t));
     }
   });

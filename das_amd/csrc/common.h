@@ -48,7 +48,12 @@ inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 8u)
   return (unsigned)g;
 }
 
-// Stream-ordered device buffer (hipMallocAsync / hipFreeAsync on the ctx stream).
+// Caching allocator (alloc.hip): blocks reused per (stream, size class).
+void* cache_alloc(size_t bytes, hipStream_t s);
+void cache_free(void* p);
+void cache_release_stream(hipStream_t s);
+
+// Stream-ordered device buffer from the caching allocator (ctx stream).
 template <typename T>
 struct DBuf {
   T* p = nullptr;
@@ -60,10 +65,10 @@ struct DBuf {
     release();
     s = st;
     n = count;
-    if (count) DAS_HIP(hipMallocAsync((void**)&p, sizeof(T) * count, st));
+    if (count) p = (T*)cache_alloc(sizeof(T) * count, st);
   }
   void release() {
-    if (p) (void)hipFreeAsync(p, s);
+    if (p) cache_free(p);
     p = nullptr;
     n = 0;
   }

@@ -17,7 +17,7 @@ namespace das {
 constexpr int kMaxArity = 8;      // index tables exist for arity 1..kMaxArity
 constexpr int kMaxPosArity = 3;   // per-position (pattern) index: arity 1..3, as the reference
 constexpr int kMaxCols = 16;      // columns in a binding table
-constexpr int kTypeBits = 24;     // P-index key = target << 24 | named-type id
+constexpr int kTypeBits = 24;     // named types < 2^24 (P-index key = type << 32 | target)
 
 // External category codes (das_lookup): a remote link is an atom of the global
 // id space whose index rows live on another shard (multi-GPU).
@@ -40,7 +40,7 @@ struct RowTable {
 struct PosIndex {
   RowTable t;
   uint64_t nkeys = 0;
-  uint64_t* ukey = nullptr;   // sorted unique (t_p << 24 | type)
+  uint64_t* ukey = nullptr;   // sorted unique (type << 32 | t_p)
   uint64_t* uoff = nullptr;   // nkeys + 1 row offsets
 };
 
@@ -82,6 +82,7 @@ struct Index {
 struct Table {
   int kind = DAS_TABLE_ORDERED;
   int ncols = 0;
+  int sorted_col = -1;              // rows ascending by this column (-1: no known order)
   int32_t vars[kMaxCols] = {0};
   int32_t member[kMaxCols] = {0};   // DAS_TABLE_COMPOSITE: -1 ordered column, else member index
   // host-known value bounds per column (inclusive); [0, kNone] = unknown
@@ -93,7 +94,7 @@ struct Table {
   hipStream_t s = nullptr;
   uint32_t* col(int c) const { return data + (uint64_t)c * cap; }
   ~Table() {
-    if (data) (void)hipFreeAsync(data, s);
+    if (data) cache_free(data);
   }
 };
 
@@ -193,6 +194,7 @@ std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* var
 // Same schema and column bounds as `a` (a subset of its rows will be stored).
 inline std::unique_ptr<Table> new_table_like(Ctx& c, const Table& a, uint64_t cap) {
   auto t = new_table(c, a.kind, a.ncols, a.vars, cap, a.member);
+  t->sorted_col = a.sorted_col;
   for (int k = 0; k < a.ncols; ++k) {
     t->lo[k] = a.lo[k];
     t->hi[k] = a.hi[k];

@@ -8,12 +8,13 @@
 //   atoms        sorted by digest (== sorted hex handle): id order == handle order
 //   T_a          links of arity a, rows (link, t0..t_{a-1}) sorted by (type, id)
 //   C_a          same rows sorted by (composite type, id)       -> templates:*
-//   P_{a,p}      same rows sorted by (t_p, type, id), a <= 3     -> patterns:* with a
-//                grounded target at p; unique (t_p<<24|type) keys + row offsets
+//   P_{a,p}      same rows sorted by (type, t_p, id), a <= 3     -> patterns:* with a
+//                grounded target at p (unique (type<<32|t_p) keys + row offsets), and
+//                typed all-wildcard scans whose output must come sorted by t_p
 //   tgt_off/tgt  outgoing sets (stored target order)
 // Pattern keys with only wildcard targets are served by T_a (typed) or all of
-// T_a ('*' type); a '*' type with grounded targets by the untyped key range of
-// P_{a,p}.  This covers exactly the families the reference writes for arity
+// T_a ('*' type); a '*' type with grounded targets by one key range of P_{a,p}
+// per named type.  This covers exactly the families the reference writes for arity
 // 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
 #include "das_internal.h"
 
@@ -28,17 +29,43 @@ __global__ void k_gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t*
     dst[i] = src[idx[i]];
 }
 
+__global__ void k_copy_u32(uint32_t* dst, const uint32_t* src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+__global__ void k_fill_u32(uint32_t* dst, uint32_t v, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = v;
+}
+__global__ void k_copy_u128(uint4* dst, const uint4* src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+namespace {
+// Pinned landing slot for scalar read-backs (a pageable destination costs a
+// staging copy: about twice the round trip).  One per host thread.
+uint64_t* pinned_slot() {
+  thread_local struct Slot {
+    uint64_t* p = nullptr;
+    Slot() { DAS_HIP(hipHostMalloc((void**)&p, 64, hipHostMallocDefault)); }
+    ~Slot() { if (p) (void)hipHostFree(p); }
+  } slot;
+  return slot.p;
+}
+}  // namespace
+
 uint64_t read_u64(const uint64_t* d, hipStream_t s) {
-  uint64_t v = 0;
-  DAS_HIP(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, s));
+  uint64_t* h = pinned_slot();
+  DAS_HIP(hipMemcpyAsync(h, d, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   DAS_HIP(hipStreamSynchronize(s));
-  return v;
+  return *h;
 }
 uint32_t read_u32(const uint32_t* d, hipStream_t s) {
-  uint32_t v = 0;
-  DAS_HIP(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, s));
+  uint64_t* h = pinned_slot();
+  DAS_HIP(hipMemcpyAsync(h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   DAS_HIP(hipStreamSynchronize(s));
-  return v;
+  return (uint32_t)*h;
 }
 
 namespace {
@@ -268,7 +295,7 @@ __global__ void k_pos_key(const uint32_t* type, const uint64_t* tgt_off, const u
                           uint64_t n, uint32_t p, uint64_t* key) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t id = ids[i];
-    key[i] = ((uint64_t)tgt[tgt_off[id] + p] << kTypeBits) | (uint64_t)type[id];
+    key[i] = ((uint64_t)type[id] << 32) | (uint64_t)tgt[tgt_off[id] + p];
   }
 }
 
@@ -416,7 +443,7 @@ void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s)
   hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
   radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
   DBuf<uint32_t> bad(1, s);
-  DAS_HIP(hipMemsetAsync(bad.p, 0, 4, s));
+  fill_dev(bad.p, 0, 4, s);
   hipLaunchKernelGGL(k_hi_ties, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, bad.p);
   if (read_u32(bad.p, s) == 0) return;
   // exact: LSD over (lo, hi)
@@ -513,9 +540,9 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
   }
   DBuf<uint32_t> local2id(nu, s), catmax(n_atoms ? n_atoms : 1, s), rep(n_atoms ? n_atoms : 1, s);
-  DAS_HIP(hipMemsetAsync(local2id.p, 0xFF, 4 * nu, s));
-  DAS_HIP(hipMemsetAsync(catmax.p, 0, 4 * catmax.n, s));
-  DAS_HIP(hipMemsetAsync(rep.p, 0xFF, 4 * rep.n, s));
+  fill_dev(local2id.p, 0xFF, 4 * nu, s);
+  fill_dev(catmax.p, 0, 4 * catmax.n, s);
+  fill_dev(rep.p, 0xFF, 4 * rep.n, s);
   if (nc) {
     hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
                        (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p);
@@ -567,7 +594,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
                        (const uint32_t*)d_child.p, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf);
     DAS_HIP(hipGetLastError());
   }
-  DAS_HIP(hipMemsetAsync(idx.ctype, 0xFF, 4 * (n_atoms ? n_atoms : 1), s));
+  fill_dev(idx.ctype, 0xFF, 4 * (n_atoms ? n_atoms : 1), s);
   // outgoing CSR
   {
     // widen arity to u64 for the scan (sum of arities may exceed 2^32 at 1B links)
@@ -586,7 +613,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   // 5. counts per arity, node count
   {
     DBuf<unsigned long long> h(64, s);
-    DAS_HIP(hipMemsetAsync(h.p, 0, 64 * 8, s));
+    fill_dev(h.p, 0, 64 * 8, s);
     if (n_atoms) hipLaunchKernelGGL(k_arity_hist, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
                                     (const uint32_t*)idx.arity, n_atoms, h.p);
     unsigned long long hh[64];
@@ -612,7 +639,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
       radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
       DBuf<uint32_t> bad(1, s);
-      DAS_HIP(hipMemsetAsync(bad.p, 0, 4, s));
+      fill_dev(bad.p, 0, 4, s);
       hipLaunchKernelGGL(k_hi_ties, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, bad.p);
       if (read_u32(bad.p, s)) {
         hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, false);
@@ -650,7 +677,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     // T_a by (type, id)
     {
       DBuf<uint32_t> key(R, s), perm(R, s);
-      DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+      copy_dev(perm.p, ids.p, 4 * R, s);
       hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint32_t*)perm.p, R, key.p);
       radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, tbits > 0 ? tbits : 1, s);
       RowTable& t = idx.ttab[ar];
@@ -680,7 +707,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     // C_a by (ctype, id)
     {
       DBuf<uint32_t> key(R, s), perm(R, s);
-      DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+      copy_dev(perm.p, ids.p, 4 * R, s);
       hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.ctype, (const uint32_t*)perm.p, R, key.p);
       const int cbits = bits_for(n_ctypes ? n_ctypes - 1 : 0);
       radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, cbits > 0 ? cbits : 1, s);
@@ -704,11 +731,12 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       for (uint32_t p = 0; p < ar; ++p) {
         DBuf<uint64_t> key(R, s);
         DBuf<uint32_t> perm(R, s);
-        DAS_HIP(hipMemcpyAsync(perm.p, ids.p, 4 * R, hipMemcpyDeviceToDevice, s));
+        copy_dev(perm.p, ids.p, 4 * R, s);
         hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,
                            (const uint32_t*)idx.tgt, (const uint32_t*)perm.p, R, p, key.p);
-        const int kb = kTypeBits + bits_for(n_atoms ? n_atoms - 1 : 0);
-        radix_sort_pairs<uint64_t>(key.p, perm.p, R, 0, kb, s);
+        // (type, t_p, id): sort by t_p, then (stable) by type; ids arrive in order
+        radix_sort_pairs<uint64_t>(key.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
+        radix_sort_pairs<uint64_t>(key.p, perm.p, R, 32, 32 + std::max(1, tbits), s);
         PosIndex& P = idx.pidx[ar][p];
         P.t.arity = (int)ar;
         P.t.rows = R;

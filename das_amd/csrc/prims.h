@@ -160,6 +160,23 @@ void exclusive_scan(const T* in, uint64_t n, T* out, hipStream_t s) {
   exclusive_scan_fn<T>(PtrIn<T>{in}, n, out, s);
 }
 
+// Device-to-device copy of `bytes` (a multiple of 4) as a kernel: the
+// runtime's copy path costs far more host time per call than a launch.
+__global__ void k_copy_u32(uint32_t* dst, const uint32_t* src, uint64_t n);
+__global__ void k_copy_u128(uint4* dst, const uint4* src, uint64_t n);
+inline void copy_dev(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  if (((((uintptr_t)dst) | ((uintptr_t)src) | bytes) & 15) == 0) {
+    const uint64_t n = bytes / 16;
+    hipLaunchKernelGGL(k_copy_u128, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, (uint4*)dst, (const uint4*)src, n);
+  } else {
+    const uint64_t n = bytes / 4;
+    hipLaunchKernelGGL(k_copy_u32, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, (uint32_t*)dst,
+                       (const uint32_t*)src, n);
+  }
+  DAS_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------
 // Stable LSD radix sort of (key, u32 value) pairs, 8-bit digits.
 // Upsweep: per-tile LDS histogram -> digit-major table -> exclusive scan.
@@ -263,8 +280,8 @@ void radix_sort_pairs(K* keys, uint32_t* vals, uint64_t n, int begin_bit, int en
     std::swap(va, vb);
   }
   if (passes & 1) {
-    DAS_HIP(hipMemcpyAsync(keys, ka, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
-    if (vals) DAS_HIP(hipMemcpyAsync(vals, va, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+    copy_dev(keys, ka, sizeof(K) * n, s);
+    if (vals) copy_dev(vals, va, sizeof(uint32_t) * n, s);
   }
 }
 
@@ -291,7 +308,20 @@ inline void gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t* dst, 
   DAS_HIP(hipGetLastError());
 }
 
-// Reads one device u64 (or u32) back to the host; synchronises the stream.
+// hipMemsetAsync replacement (a multiple of 4 bytes, every byte = `byte`): the
+// runtime's fill path also costs far more host time than a launch.
+__global__ void k_fill_u32(uint32_t* dst, uint32_t v, uint64_t n);
+inline void fill_dev(void* dst, int byte, uint64_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  const uint32_t b = (uint32_t)(byte & 0xFF);
+  const uint64_t n = bytes / 4;
+  hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, (uint32_t*)dst,
+                     b | (b << 8) | (b << 16) | (b << 24), n);
+  DAS_HIP(hipGetLastError());
+}
+
+// Reads one device u64 (or u32) back to the host through pinned memory;
+// synchronises the stream.
 uint64_t read_u64(const uint64_t* d, hipStream_t s);
 uint32_t read_u32(const uint32_t* d, hipStream_t s);
 

@@ -28,6 +28,12 @@ __global__ void k_compact_index_q(const uint32_t* flag, const uint32_t* scan, ui
 
 namespace {
 
+struct FlagIn {
+  const uint32_t* a;
+  uint64_t n;
+  __device__ uint32_t operator()(uint64_t i) const { return i < n ? a[i] : 0u; }
+};
+
 struct WidenCnt {
   const uint32_t* a;
   uint64_t n;
@@ -155,7 +161,7 @@ __global__ void __launch_bounds__(B) k_project(ScanSpec sp, uint64_t begin, uint
 // Range lookup in a P_{a,p} key array: [lower_bound(lo), lower_bound(hi)) -> rows.
 __global__ void k_key_ranges(const uint64_t* ukey, const uint64_t* uoff, uint64_t nkeys, const uint64_t* qlo,
                              const uint64_t* qhi, uint32_t nq, uint64_t* out) {
-  const uint32_t i = threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * nq) return;
   const uint64_t q = (i & 1) ? qhi[i >> 1] : qlo[i >> 1];
   uint64_t lo = 0, hi = nkeys;
@@ -314,6 +320,16 @@ __global__ void __launch_bounds__(B) k_key_hist(const uint32_t* key, uint64_t n,
     const uint32_t d = i < n ? key[i] - kmin : range;
     const bool act = d < range;
     wave_agg_atomic_inc(cnt, act ? d : 0u, act);
+  }
+}
+
+// Sorted build keys: off[d] = first row whose key >= kmin + d, d in [0, range].
+// Row i fills the offsets of the key gap (key[i-1], key[i]].
+__global__ void k_bucket_bounds(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t range, uint32_t* off) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lo = i == 0 ? 0u : key[i - 1] - kmin + 1;
+    const uint32_t hi = i == n ? range : key[i] - kmin;
+    for (uint32_t d = lo; d <= hi && d <= range; ++d) off[d] = (uint32_t)i;
   }
 }
 
@@ -525,18 +541,14 @@ std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx,
 std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
-  DBuf<uint32_t> scan(n, c.s);
-  exclusive_scan<uint32_t>(keep, n, scan.p, c.s);
-  uint32_t h[2];
-  DAS_HIP(hipMemcpyAsync(&h[0], scan.p + n - 1, 4, hipMemcpyDeviceToHost, c.s));
-  DAS_HIP(hipMemcpyAsync(&h[1], keep + n - 1, 4, hipMemcpyDeviceToHost, c.s));
-  DAS_HIP(hipStreamSynchronize(c.s));
-  const uint64_t m = (uint64_t)h[0] + h[1];
+  DBuf<uint32_t> scan(n + 1, c.s);
+  exclusive_scan_fn<uint32_t>(FlagIn{keep, n}, n + 1, scan.p, c.s);   // scan[n] = kept rows
+  const uint64_t m = read_u32(scan.p + n, c.s);
   if (m == n) {   // nothing dropped: copy
     auto t = new_table_like(c, a, n);
     t->nrows = n;
     for (int k = 0; k < a.ncols; ++k)
-      DAS_HIP(hipMemcpyAsync(t->col(k), a.col(k), 4 * n, hipMemcpyDeviceToDevice, c.s));
+      copy_dev(t->col(k), a.col(k), 4 * n, c.s);
     return t;
   }
   DBuf<uint32_t> idx(m ? m : 1, c.s);
@@ -566,7 +578,7 @@ std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* var
   }
   t->s = c.s;
   t->cap = cap ? cap : 1;
-  if (ncols) DAS_HIP(hipMallocAsync((void**)&t->data, 4ull * ncols * t->cap, c.s));
+  if (ncols) t->data = (uint32_t*)cache_alloc(4ull * ncols * t->cap, c.s);
   return t;
 }
 
@@ -732,46 +744,77 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
   if (ar > (uint32_t)kMaxPosArity) {
     if (q.type_id != kNone || any_wild) return empty();   // only [*, e0..en]
   }
-  uint64_t begin = 0, end = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;     // row ranges of rt to scan
   const RowTable* rt = nullptr;
   std::vector<uint32_t> grounded;
   for (uint32_t p = 0; p < ar; ++p)
     if (q.target[p] != kNone) grounded.push_back(p);
+  int sorted_pos = -1;                                    // output comes sorted by this position
   if (grounded.empty() || ar > (uint32_t)kMaxPosArity) {
-    rt = &idx.ttab[ar];
-    if (q.type_id == kNone) { begin = 0; end = rt->rows; }
-    else { begin = idx.type_off[ar][q.type_id]; end = idx.type_off[ar][q.type_id + 1]; }
+    const bool typed = q.type_id != kNone;
+    if (typed && ar <= (uint32_t)kMaxPosArity && q.order_pos >= 0 && (uint32_t)q.order_pos < ar &&
+        idx.pidx[ar][q.order_pos].t.rows == idx.ttab[ar].rows) {
+      // P_{a,p} holds the type's rows sorted by t_p: same range, sorted output
+      rt = &idx.pidx[ar][q.order_pos].t;
+      sorted_pos = q.order_pos;
+    } else {
+      rt = &idx.ttab[ar];
+    }
+    if (!typed) ranges.push_back({0, rt->rows});
+    else ranges.push_back({idx.type_off[ar][q.type_id], idx.type_off[ar][q.type_id + 1]});
   } else {
-    // smallest P_{a,p} range among the grounded positions
+    // the cheapest P_{a,p} among the grounded positions: its key range(s)
+    // (one per named type for a '*' type)
+    std::vector<uint32_t> types;
+    if (q.type_id != kNone) types.push_back(q.type_id);
+    else
+      for (uint32_t ty = 0; ty < idx.n_types; ++ty)
+        if (idx.type_off[ar][ty + 1] > idx.type_off[ar][ty]) types.push_back(ty);
     uint64_t best = ~0ull;
     for (uint32_t p : grounded) {
       const PosIndex& P = idx.pidx[ar][p];
-      if (!P.nkeys) return empty();
-      const uint64_t t = q.target[p];
-      uint64_t qlo = (t << kTypeBits) | (q.type_id == kNone ? 0 : q.type_id);
-      uint64_t qhi = q.type_id == kNone ? ((t + 1) << kTypeBits) : qlo + 1;
-      uint64_t hr[2];
-      const std::array<uint64_t, 4> ck{ar, p, qlo, qhi};
-      auto hit = idx.range_cache.find(ck);
-      if (hit != idx.range_cache.end()) {
-        hr[0] = hit->second.first;
-        hr[1] = hit->second.second;
-      } else {
-        DBuf<uint64_t> dq(2, c.s), dr(2, c.s);
-        uint64_t hq[2] = {qlo, qhi};
-        DAS_HIP(hipMemcpyAsync(dq.p, hq, 16, hipMemcpyHostToDevice, c.s));
-        hipLaunchKernelGGL(k_key_ranges, dim3(1), dim3(64), 0, c.s, (const uint64_t*)P.ukey, (const uint64_t*)P.uoff,
-                           P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + 1, 1u, dr.p);
+      if (!P.nkeys || types.empty()) return empty();
+      std::vector<std::pair<uint64_t, uint64_t>> rr;
+      std::vector<uint64_t> qlo, qhi;
+      uint64_t total = 0;
+      for (uint32_t ty : types) {
+        const uint64_t k = ((uint64_t)ty << 32) | q.target[p];
+        const std::array<uint64_t, 4> ck{ar, p, k, 0};
+        auto hit = idx.range_cache.find(ck);
+        if (hit != idx.range_cache.end()) {
+          rr.push_back(hit->second);
+        } else {
+          qlo.push_back(k);
+          qhi.push_back(k + 1);
+          rr.push_back({~0ull, ~0ull});
+        }
+      }
+      if (!qlo.empty()) {
+        const uint32_t nq = (uint32_t)qlo.size();
+        DBuf<uint64_t> dq(2 * nq, c.s), dr(2 * nq, c.s);
+        DAS_HIP(hipMemcpyAsync(dq.p, qlo.data(), 8 * nq, hipMemcpyHostToDevice, c.s));
+        DAS_HIP(hipMemcpyAsync(dq.p + nq, qhi.data(), 8 * nq, hipMemcpyHostToDevice, c.s));
+        hipLaunchKernelGGL(k_key_ranges, dim3((2 * nq + 63) / 64), dim3(64), 0, c.s, (const uint64_t*)P.ukey,
+                           (const uint64_t*)P.uoff, P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + nq, nq, dr.p);
         DAS_HIP(hipGetLastError());
-        DAS_HIP(hipMemcpyAsync(hr, dr.p, 16, hipMemcpyDeviceToHost, c.s));
+        std::vector<uint64_t> hr(2 * nq);
+        DAS_HIP(hipMemcpyAsync(hr.data(), dr.p, 16 * nq, hipMemcpyDeviceToHost, c.s));
         DAS_HIP(hipStreamSynchronize(c.s));
         if (idx.range_cache.size() > (1u << 20)) idx.range_cache.clear();
-        idx.range_cache[ck] = {hr[0], hr[1]};
+        uint32_t j = 0;
+        for (size_t i = 0; i < rr.size(); ++i)
+          if (rr[i].first == ~0ull) {
+            rr[i] = {hr[2 * j], hr[2 * j + 1]};
+            idx.range_cache[std::array<uint64_t, 4>{ar, p, qlo[j], 0}] = rr[i];
+            ++j;
+          }
       }
-      if (hr[1] - hr[0] < best) {
-        best = hr[1] - hr[0];
-        begin = hr[0];
-        end = hr[1];
+      for (auto& r : rr) total += r.second - r.first;
+      if (total < best) {
+        best = total;
+        ranges.clear();
+        for (auto& r : rr)
+          if (r.second > r.first) ranges.push_back(r);
         rt = &P.t;
         // this position's filter is implied by the range
         for (uint32_t pp = 0; pp < ar; ++pp) sp.fixed[pp] = q.target[pp];
@@ -780,12 +823,29 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
       if (best == 0) return empty();
     }
   }
-  DAS_CHECK(rt && begin <= end && end <= rt->rows, DAS_E_INTERNAL, "scan range outside its table");
+  DAS_CHECK(rt != nullptr, DAS_E_INTERNAL, "scan without a table");
+  for (auto& r : ranges) DAS_CHECK(r.first <= r.second && r.second <= rt->rows, DAS_E_INTERNAL, "scan range outside its table");
   set_cols(sp, *rt);
   bool filt = false;
   for (uint32_t p = 0; p < ar; ++p) filt |= sp.fixed[p] != kNone;
   sp.all_keep = !filt && sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
-  return run_scan(c, sp, begin, end, kind, ncols, vars, q.type_id);
+  if (ranges.empty()) return empty();
+  std::unique_ptr<Table> t;
+  if (ranges.size() == 1) {
+    t = run_scan(c, sp, ranges[0].first, ranges[0].second, kind, ncols, vars, q.type_id);
+  } else {
+    std::vector<std::unique_ptr<Table>> parts;
+    std::vector<const Table*> pp;
+    for (auto& r : ranges) {
+      parts.push_back(run_scan(c, sp, r.first, r.second, kind, ncols, vars, q.type_id));
+      pp.push_back(parts.back().get());
+    }
+    t = concat(c, pp.data(), (int)pp.size());
+  }
+  if (sorted_pos >= 0 && q.ordered)
+    for (int k = 0; k < t->ncols; ++k)
+      if (sp.outpos[k] == sorted_pos) t->sorted_col = k;
+  return t;
 }
 
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
@@ -865,28 +925,35 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   if (range > std::max<uint64_t>(8 * Q.nrows, 1ull << 26) || range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
   const uint32_t kmin = h[0];
-  // counting sort of the build side by key
-  DBuf<uint32_t> cnt(range + 1, c.s), off(range + 1, c.s);
+  // bucket offsets of the build side: already grouped by key when it comes
+  // sorted (an order-aware scan), else a counting sort
+  DBuf<uint32_t> off(range + 1, c.s);
   std::unique_ptr<Table> Qs;
-  {
+  const Table* Qb = &Q;
+  if (Q.sorted_col == qk) {
+    ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * range);
+    hipLaunchKernelGGL(k_bucket_bounds, G(Q.nrows + 1), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, off.p);
+    DAS_HIP(hipGetLastError());
+  } else {
+    DBuf<uint32_t> cnt(range + 1, c.s);
     ProfScope ps(c, "join_build", 4.0 * Q.nrows * (Q.ncols + 1) + 8.0 * range);
-    DAS_HIP(hipMemsetAsync(cnt.p, 0, 4 * (range + 1), c.s));
+    fill_dev(cnt.p, 0, 4 * (range + 1), c.s);
     hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, cnt.p);
     exclusive_scan<uint32_t>(cnt.p, range + 1, off.p, c.s);
-    DAS_HIP(hipMemcpyAsync(cnt.p, off.p, 4 * (range + 1), hipMemcpyDeviceToDevice, c.s));
+    copy_dev(cnt.p, off.p, 4 * (range + 1), c.s);
     Qs = new_table_like(c, Q, Q.nrows);
     Qs->nrows = Q.nrows;
     hipLaunchKernelGGL(k_key_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin, (uint32_t)range,
-                       cnt.p, Qs->data,
-                       Qs->cap);
+                       cnt.p, Qs->data, Qs->cap);
     DAS_HIP(hipGetLastError());
+    Qb = Qs.get();
   }
   const int nu = (int)uni.size();
   JoinCols jc{};
   for (int k = 0; k < nu; ++k) {
     const int ip = colof(P, uni[k]);
     if (ip >= 0) { jc.p[jc.np] = P.col(ip); jc.po[jc.np++] = k; }
-    else { jc.b[jc.nb] = Qs->col(colof(*Qs, uni[k])); jc.bo[jc.nb++] = k; }
+    else { jc.b[jc.nb] = Qb->col(colof(*Qb, uni[k])); jc.bo[jc.nb++] = k; }
   }
   DBuf<uint2> lc(range, c.s);
   hipLaunchKernelGGL(k_pack_lc, dim3(grid_for(range, B, 2048)), dim3(B), 0, c.s, (const uint32_t*)off.p,
@@ -901,7 +968,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
                        (const uint2*)lc.p, units, tot.p);
     DAS_HIP(hipGetLastError());
   }
-  DAS_HIP(hipMemsetAsync(tot.p + units, 0, 8, c.s));
+  fill_dev(tot.p + units, 0, 8, c.s);
   exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
   const uint64_t total = read_u64(toff.p + units, c.s);
   auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
@@ -994,6 +1061,12 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       DAS_HIP(hipGetLastError());
     }
   }
+  // the output keeps the probe side's row order (direct, sort-merge and
+  // cartesian joins all emit in probe order)
+  {
+    const Table& Pt = A.nrows >= Bt.nrows ? A : Bt;
+    out->sorted_col = Pt.sorted_col >= 0 ? colof(*out, Pt.vars[Pt.sorted_col]) : -1;
+  }
   // output column bounds: the source column's (both sides' intersection for a shared variable)
   for (int k = 0; k < out->ncols; ++k) {
     uint32_t lo = 0, hi = kNone;
@@ -1060,6 +1133,7 @@ std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
   DBuf<uint32_t> perm(A.nrows, c.s);
   sort_perm(cols_of(A), A.nrows, perm.p, id_bits(c), c.s);
   auto S = gather_table(c, A, perm.p, A.nrows);
+  S->sorted_col = A.ncols ? 0 : -1;
   DBuf<uint32_t> keep(A.nrows, c.s);
   hipLaunchKernelGGL(k_distinct_flags, G(A.nrows), dim3(B), 0, c.s, cols_of(*S), A.nrows, keep.p);
   DAS_HIP(hipGetLastError());
@@ -1114,7 +1188,7 @@ std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars
   if (t.nrows == 0) return gather_table(c, t, nullptr, 0);
   DBuf<uint32_t> dest(t.nrows, c.s), perm(t.nrows, c.s);
   DBuf<unsigned long long> h(nparts, c.s);
-  DAS_HIP(hipMemsetAsync(h.p, 0, 8 * nparts, c.s));
+  fill_dev(h.p, 0, 8 * nparts, c.s);
   hipLaunchKernelGGL(k_dest, G(t.nrows), dim3(B), 0, c.s, key, t.nrows, nparts, dest.p);
   hipLaunchKernelGGL(k_dest_hist, G(t.nrows), dim3(B), 0, c.s, (const uint32_t*)dest.p, t.nrows, h.p);
   DAS_HIP(hipGetLastError());
@@ -1124,7 +1198,9 @@ std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars
   DAS_HIP(hipMemcpyAsync(hh.data(), h.p, 8 * nparts, hipMemcpyDeviceToHost, c.s));
   DAS_HIP(hipStreamSynchronize(c.s));
   for (uint32_t d = 0; d < nparts; ++d) counts[d] = hh[d];
-  return gather_table(c, t, perm.p, t.nrows);
+  auto out = gather_table(c, t, perm.p, t.nrows);
+  out->sorted_col = -1;
+  return out;
 }
 
 void export_rows(Ctx& c, const Table& t, uint32_t* dst) {
@@ -1156,6 +1232,7 @@ std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {
   }
   auto t = new_table_like(c, f, total);
   t->nrows = total;
+  if (n > 1) t->sorted_col = -1;
   for (int i = 1; i < n; ++i)
     for (int k = 0; k < f.ncols; ++k) {
       t->lo[k] = std::min(t->lo[k], ts[i]->lo[k]);
@@ -1165,7 +1242,7 @@ std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n) {
   for (int i = 0; i < n; ++i) {
     for (int k = 0; k < f.ncols; ++k)
       if (ts[i]->nrows)
-        DAS_HIP(hipMemcpyAsync(t->col(k) + o, ts[i]->col(k), 4 * ts[i]->nrows, hipMemcpyDeviceToDevice, c.s));
+        copy_dev(t->col(k) + o, ts[i]->col(k), 4 * ts[i]->nrows, c.s);
     o += ts[i]->nrows;
   }
   return t;

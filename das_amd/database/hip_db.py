@@ -388,11 +388,13 @@ class HipDB(RelationalDB):
         it = iter(ids.tolist())
         return [_lib.DAS_NONE if h == WILDCARD else next(it) for h in handles]
 
-    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         """Link.matched's wildcard branch fused with _assign_variables
         (pattern_matcher.py:515-535 over redis_mongo_db.py:235-252).
         handles: reference-order target handles ('*' for variables);
-        var_ids: variable id per position in the Link's own target order."""
+        var_ids: variable id per position in the Link's own target order;
+        order_var: the variable the caller will join on -- a typed scan then
+        returns its rows sorted by it (same answer, join-friendly order)."""
         if link_type in UNORDERED_LINK_TYPES:
             order = sorted(range(len(handles)), key=lambda i: handles[i])
             key_handles = [handles[i] for i in order]
@@ -407,7 +409,10 @@ class HipDB(RelationalDB):
         repeated = len(set(names)) != len(names)
         if ordered:
             var = [v if v is not None else -1 for v in var_ids]
-            t = self.ctx.scan_link(arity, ttype, tids, var, 0, True, no_overload)
+            order_pos = -1
+            if order_var is not None and order_var in var and link_type not in UNORDERED_LINK_TYPES:
+                order_pos = var.index(order_var)
+            t = self.ctx.scan_link(arity, ttype, tids, var, 0, True, no_overload, order_pos=order_pos)
         else:
             if repeated:
                 return Relation()       # UnorderedAssignment.assign rejects a repeat (:196-197)

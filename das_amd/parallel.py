@@ -187,12 +187,13 @@ class ShardedDB(RelationalDB):
             return tables[0]
         return self.local.empty_table(kind, list(vars_))
 
-    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         kind, vars_ = self._schema(var_ids, ordered)
         names = [v for v in var_ids if v is not None]
         if not ordered and len(set(names)) != len(names):
             return DRel([])
-        t = self._ensure(self.local.match_link(link_type, handles, var_ids, ordered, no_overload), kind, vars_)
+        t = self._ensure(self.local.match_link(link_type, handles, var_ids, ordered, no_overload, order_var=order_var),
+                         kind, vars_)
         dup = link_type == WILDCARD or len(set(names)) != len(names) or not ordered or \
             link_type in UNORDERED_LINK_TYPES
         if dup:

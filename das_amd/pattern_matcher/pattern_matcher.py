@@ -528,7 +528,12 @@ class Link(Atom):
         if WILDCARD not in handles:
             return db.link_exists(self.atom_type, handles)
         var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in self.targets]
-        rel = db.match_link(self.atom_type, handles, var_ids, self.ordered, CONFIG['no_overload'])
+        hint = getattr(self, '_order_var', None)
+        if hint is not None:
+            rel = db.match_link(self.atom_type, handles, var_ids, self.ordered, CONFIG['no_overload'],
+                                order_var=_vid(hint))
+        else:
+            rel = db.match_link(self.atom_type, handles, var_ids, self.ordered, CONFIG['no_overload'])
         found = db.rel_nonempty(rel)
         if db.tuple_targets and not self.ordered and found and any(v is None for v in var_ids):
             # reference DB path: list.remove on a tuple (pattern_matcher.py:484)
@@ -644,10 +649,26 @@ class And(LogicalExpression):
     def post_process(self, assignment) -> Assignment:
         return assignment
 
+    def _plan_orders(self):
+        """Scan-order hints: each positive Link term is asked for its rows
+        sorted by its first variable that another term also binds (the join
+        key), so joins probe sorted keys.  Answers are unchanged."""
+        def names(t):
+            return [x.name for x in t.targets if isinstance(x, Variable)] if isinstance(t, Link) else []
+        vs = [set(names(t)) for t in self.terms]
+        for i, t in enumerate(self.terms):
+            if not isinstance(t, Link):
+                continue
+            others = set().union(*(v for j, v in enumerate(vs) if j != i)) if len(vs) > 1 else set()
+            t._order_var = next((n for n in names(t) if n in others), None)
+
     def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
         db = _hip(db)
         if not self.terms:
             return False
+        if not getattr(self, '_planned', False):
+            self._plan_orders()
+            self._planned = True
         acc = None
         forbidden = []
         for term in self.terms:

@@ -139,6 +139,8 @@ typedef struct {
   uint32_t ordered;
   uint32_t no_overload;
   uint32_t emit_link;
+  int32_t order_pos;   /* >= 0: a typed all-wildcard scan returns its rows sorted by the
+                          target at this position (the planner's join variable); -1 none */
 } das_link_scan_t;
 
 /* LinkTemplate (get_matched_type_template :269-275 + LinkTemplate._assign_variables

@@ -145,7 +145,7 @@ class NumpyLocal:
         return rel.tables
 
     # scans (oracle semantics, local links only)
-    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False):
+    def match_link(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         from das_amd.pattern_matcher.pattern_matcher import _var_name
         pairs = self.odb.get_matched_links(link_type, handles)
         names = [v for v in var_ids if v is not None]
