@@ -372,41 +372,43 @@ uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hi
   return m;
 }
 
-// Per (named type, column) id bounds of a T_a table: wave-aggregated atomics
-// (rows are sorted by type, so a wave almost always holds one type).
-__global__ void __launch_bounds__(256) k_col_bounds(const uint32_t* data, uint64_t rows, uint32_t ncol,
-                                                    const uint32_t* type, uint32_t* bnd) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < rows; i0 += stride) {
-    const uint64_t r = i0 + threadIdx.x;
-    const bool act = r < rows;
-    const uint32_t ty = act ? type[data[r]] : 0u;
-    const uint64_t am = __ballot(act);
-    const int leader = __ffsll((unsigned long long)am) - 1;
-    const uint32_t lt = __shfl(ty, leader, 64);
-    const bool uniform = __ballot(act && ty != lt) == 0;
-    for (uint32_t c = 0; c < ncol; ++c) {
-      const uint32_t v = act ? data[c * rows + r] : 0u;
-      uint32_t* b = bnd + ((uint64_t)ty * ncol + c) * 2;
-      if (uniform) {
-        uint32_t mn = act ? v : 0xFFFFFFFFu, mx = act ? v : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-          mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
-          mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-        }
-        if ((int)__lane_id() == leader) {
-          atomicMin(b, mn);
-          atomicMax(b + 1, mx);
-        }
-      } else if (act) {
-        atomicMin(b, v);
-        atomicMax(b + 1, v);
-      }
+// Column id bounds of rows [b, e) of a T_a table (one named type's segment):
+// per-thread running min/max, wave + block reduction, one atomic per block
+// and column (per-row or per-wave atomics on one address serialise).
+__global__ void __launch_bounds__(256) k_seg_minmax(const uint32_t* data, uint64_t rows, uint32_t ncol, uint64_t b,
+                                                    uint64_t e, uint32_t* bnd) {
+  __shared__ uint32_t s_mn[4], s_mx[4];
+  for (uint32_t c = 0; c < ncol; ++c) {
+    const uint32_t* col = data + (uint64_t)c * rows;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (uint64_t r = b + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < e; r += (uint64_t)gridDim.x * blockDim.x) {
+      const uint32_t v = col[r];
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
     }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
+      mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+    }
+    if (__lane_id() == 0) {
+      s_mn[threadIdx.x >> 6] = mn;
+      s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 4; ++w) {
+        mn = min(mn, s_mn[w]);
+        mx = max(mx, s_mx[w]);
+      }
+      atomicMin(&bnd[2 * c], mn);
+      atomicMax(&bnd[2 * c + 1], mx);
+    }
+    __syncthreads();
   }
 }
 
+// tbound/gbound of T_a (type_off must already hold its per-type row offsets).
 void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) {
   const uint32_t ncol = (uint32_t)t.arity + 1;
   const uint64_t nb = n_types * ncol * 2;
@@ -417,9 +419,13 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
   }
   DBuf<uint32_t> d(nb ? nb : 1, s);
   if (nb) DAS_HIP(hipMemcpyAsync(d.p, h.data(), 4 * nb, hipMemcpyHostToDevice, s));
-  if (t.rows && nb)
-    hipLaunchKernelGGL(k_col_bounds, dim3(grid_for(t.rows, 256, 4096)), dim3(256), 0, s, (const uint32_t*)t.data,
-                       t.rows, ncol, (const uint32_t*)idx.type, d.p);
+  const auto& to = idx.type_off[t.arity];
+  for (uint64_t ty = 0; ty < n_types && ty + 1 < to.size(); ++ty) {
+    const uint64_t b = to[ty], e = to[ty + 1];
+    if (e <= b) continue;
+    hipLaunchKernelGGL(k_seg_minmax, dim3(grid_for(e - b, 256, 1024)), dim3(256), 0, s, (const uint32_t*)t.data,
+                       t.rows, ncol, b, e, d.p + ty * ncol * 2);
+  }
   DAS_HIP(hipGetLastError());
   if (nb) DAS_HIP(hipMemcpyAsync(h.data(), d.p, 4 * nb, hipMemcpyDeviceToHost, s));
   DAS_HIP(hipStreamSynchronize(s));
@@ -694,7 +700,6 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       DAS_HIP(hipMemcpyAsync(hk.data(), ukey, 4 * m, hipMemcpyDeviceToHost, s));
       DAS_HIP(hipMemcpyAsync(ho.data(), uoff, 8 * (m + 1), hipMemcpyDeviceToHost, s));
       DAS_HIP(hipStreamSynchronize(s));
-      col_bounds(idx, t, a.n_types, s);
       auto& to = idx.type_off[ar];
       to.assign(a.n_types + 1, 0);
       // to[t] = first row with type >= t
@@ -703,6 +708,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
         while (r < m && hk[r] < ty) ++r;
         to[ty] = r < m ? ho[r] : R;
       }
+      col_bounds(idx, t, a.n_types, s);
     }
     // C_a by (ctype, id)
     {

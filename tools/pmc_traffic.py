@@ -1,0 +1,57 @@
+"""Per-kernel HBM traffic per launch from two rocprofv3 --pmc rocpd databases
+(FETCH_SIZE pass, WRITE_SIZE pass), keyed by the short kernel names bench.py's
+HIP-event scopes use.
+
+    python tools/pmc_traffic.py <fetch-dir> <write-dir> [steps]
+
+FETCH_SIZE and WRITE_SIZE are reported in KiB.  On gfx950 FETCH_SIZE counts half
+the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM), so
+fetched bytes are taken as 2 x FETCH_SIZE; WRITE_SIZE is used as is.
+"""
+import glob
+import json
+import os
+import re
+import sqlite3
+import sys
+
+
+def short(name):
+    n = name.replace("das::(anonymous namespace)::", "").replace("das::", "").replace("void ", "")
+    return re.sub(r"[<(].*", "", n)
+
+
+def per_kernel(db_dir, counter):
+    dbs = glob.glob(os.path.join(db_dir, "**", "*.db"), recursive=True)
+    out = {}
+    for db in dbs:
+        c = sqlite3.connect(db)
+        for name, v in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                                 (counter,)):
+            s = short(name)
+            tot, n = out.get(s, (0.0, 0))
+            out[s] = (tot + float(v) * 1024.0, n + 1)
+    return out
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        if not k.startswith("k_"):
+            continue
+        fb, fn = fetch.get(k, (0.0, 0))
+        wb, wn = write.get(k, (0.0, 0))
+        if not fn or not wn:
+            continue
+        rd = 2.0 * fb / fn
+        wr = wb / wn
+        res[k] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                  "launches_fetch_pass": fn, "launches_write_pass": wn,
+                  "note": "read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; mean over all launches"}
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()
