@@ -61,6 +61,13 @@ uint64_t read_u64(const uint64_t* d, hipStream_t s) {
   DAS_HIP(hipStreamSynchronize(s));
   return *h;
 }
+void read_u64x2(const uint64_t* d, hipStream_t s, uint64_t out[2]) {
+  uint64_t* h = pinned_slot();
+  DAS_HIP(hipMemcpyAsync(h, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  out[0] = h[0];
+  out[1] = h[1];
+}
 uint32_t read_u32(const uint32_t* d, hipStream_t s) {
   uint64_t* h = pinned_slot();
   DAS_HIP(hipMemcpyAsync(h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s));

@@ -364,6 +364,7 @@ __global__ void k_pack_lc(const uint32_t* off, uint32_t range, uint2* lc) {
 // coalesced 256-byte column segment per chunk.
 constexpr int kXGroups = 4;
 constexpr uint64_t kXRows = 64ull * kXGroups;
+constexpr uint64_t kHeavyUnit = 1ull << 16;   // outputs above which a unit is expanded output-balanced
 
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
@@ -386,7 +387,12 @@ __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t n
     for (int g = 0; g < kXGroups; ++g)
       if (d[g] < range) acc += lc[d[g]].y;
     acc = wave_reduce_sum(acc);
-    if (lane == 0) unit_tot[u] = acc;
+    if (lane == 0) {
+      unit_tot[u] = acc;
+      // only "is any unit heavy" is needed: skip the (same-address) atomic
+      // for ordinary units
+      if (acc > kHeavyUnit) atomicMax((unsigned long long*)&unit_tot[units + 1], (unsigned long long)acc);
+    }
   }
 }
 
@@ -464,10 +470,106 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
   }
 }
 
+// Skew-balanced variant (hub keys: one probe unit can own millions of
+// outputs): waves own fixed OUTPUT chunks instead of probe units.  A wave
+// finds the unit holding its first output by a 64-ary search over the unit
+// offsets, then expands only the slice of each group that falls in its chunk.
+constexpr uint64_t kBalChunk = 1024;
+
+template <int NP, int NB, typename T>
+__global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                                    uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                                    const uint64_t* __restrict__ unit_off, JoinCols jc,
+                                                    uint32_t* __restrict__ out, uint64_t cap, uint64_t total) {
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  const uint32_t* pp[NP > 0 ? NP : 1];
+  const uint32_t* bb[NB > 0 ? NB : 1];
+  uint32_t* po[NP > 0 ? NP : 1];
+  uint32_t* bo[NB > 0 ? NB : 1];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) { pp[i] = jc.p[i]; po[i] = out + (uint64_t)jc.po[i] * cap; }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
+  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
+    const uint64_t ob = w * kBalChunk;
+    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+    // last unit with unit_off[u] <= ob   (unit_off[units] == total > ob)
+    uint64_t lo = 0, hi = units;
+    while (hi - lo > 1) {
+      const uint64_t step = (hi - lo + 63) / 64;
+      const uint64_t idx = lo + (uint64_t)lane * step;
+      const bool ok = idx < hi && unit_off[idx] <= ob;
+      const uint64_t m = __ballot(ok);
+      const uint64_t nlo = lo + (uint64_t)(63 - __clzll((long long)m)) * step;
+      hi = nlo + step < hi ? nlo + step : hi;
+      lo = nlo;
+    }
+    for (uint64_t u = lo; u < units; ++u) {
+      uint64_t base = unit_off[u];
+      if (base >= oe) break;
+      const uint64_t r0 = u * kXRows;
+      uint2 e[kXGroups];
+#pragma unroll
+      for (int g = 0; g < kXGroups; ++g) {
+        const uint64_t r = r0 + g * 64 + lane;
+        const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+        e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int g = 0; g < kXGroups; ++g) {
+        const T c = (T)e[g].y;
+        const T inc = wave_inclusive_scan(c);
+        const T tot = (T)__shfl(inc, 63, 64);
+        const T pre = inc - c;
+        const uint64_t gb = base, ge = base + tot;
+        base = ge;
+        if (ge <= ob || gb >= oe) continue;
+        const T rs = (T)((ob > gb ? ob : gb) - gb), re = (T)((oe < ge ? oe : ge) - gb);
+        const uint64_t r = r0 + g * 64 + lane;
+        uint32_t pv[NP > 0 ? NP : 1];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) pv[i] = r < np ? pp[i][r] : 0u;
+        for (T o0 = rs; o0 < re; o0 += 64) {
+          const T o = o0 + (T)lane;
+          int l = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1) {
+            const T pl = (T)__shfl(pre, l + step, 64);
+            if (l + step < 64 && pl <= o) l += step;
+          }
+          const bool act = o < re;
+          const uint32_t j = (uint32_t)(o - (T)__shfl(pre, l, 64));
+          const uint32_t br = lane_get(e[g].x, l) + j;
+#pragma unroll
+          for (int i = 0; i < NP; ++i) {
+            const uint32_t v = lane_get(pv[i], l);
+            if (act) po[i][gb + o] = v;
+          }
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+            if (act) bo[i][gb + o] = bb[i][br];
+        }
+      }
+    }
+  }
+}
+
 template <int NP, int NB>
 void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
                      const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out,
-                     uint64_t cap, uint64_t total) {
+                     uint64_t cap, uint64_t total, bool balanced) {
+  if (balanced) {
+    const unsigned g = grid_for((total + kBalChunk - 1) / kBalChunk, B / 64, 65535u * 4u);
+    if (total < (1ull << 32) - (1ull << 16))
+      hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint32_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+                         toff, jc, out, cap, total);
+    else
+      hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint64_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+                         toff, jc, out, cap, total);
+    return;
+  }
   if (total < (1ull << 32) - (1ull << 16))
     hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
                        toff, jc, out, cap);
@@ -480,7 +582,7 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
 // column slices
 void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
               const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out, uint64_t cap,
-              uint64_t total) {
+              uint64_t total, bool balanced) {
   int pi = 0, bi = 0;
   do {
     JoinCols part{};
@@ -492,7 +594,7 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
     bi += part.nb;
 #define DJ(NPV, NBV)                                                                                  \
   if (part.np == NPV && part.nb == NBV) {                                                             \
-    launch_dj_write<NPV, NBV>(grid, s, pkey, np, kmin, range, lc, units, toff, part, out, cap, total); \
+    launch_dj_write<NPV, NBV>(grid, s, pkey, np, kmin, range, lc, units, toff, part, out, cap, total, balanced); \
     continue;                                                                                         \
   }
     DJ(0, 1) DJ(0, 2) DJ(0, 3) DJ(0, 4)
@@ -961,23 +1063,31 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   DAS_HIP(hipGetLastError());
   const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
   const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
-  DBuf<uint64_t> tot(units + 1, c.s), toff(units + 1, c.s);
+  // tot[units] = 0 (scan sentinel), tot[units + 1] = the largest unit total
+  DBuf<uint64_t> tot(units + 2, c.s), toff(units + 2, c.s);
+  fill_dev(tot.p + units, 0, 16, c.s);
   {
     ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
     hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
                        (const uint2*)lc.p, units, tot.p);
     DAS_HIP(hipGetLastError());
   }
-  fill_dev(tot.p + units, 0, 8, c.s);
   exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
-  const uint64_t total = read_u64(toff.p + units, c.s);
+  copy_dev(toff.p + units + 1, tot.p + units + 1, 8, c.s);
+  uint64_t tm[2];
+  read_u64x2(toff.p + units, c.s, tm);
+  const uint64_t total = tm[0];
+  // a unit owning far more outputs than a wave should expand alone (hub
+  // keys) -> output-balanced expansion
+  const char* fb = std::getenv("DAS_DJ_BALANCED");        // tests: force either expansion
+  const bool balanced = fb ? fb[0] == '1' : tm[1] > kHeavyUnit;
   auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
   out->nrows = total;
   if (total) {
     // algorithmic bytes: probe payload + build payload + output
     ProfScope ps(c, "k_dj_write", 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
     dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, (const uint2*)lc.p, units, (const uint64_t*)toff.p, jc,
-             out->data, out->cap, total);
+             out->data, out->cap, total, balanced);
     DAS_HIP(hipGetLastError());
   }
   return out;

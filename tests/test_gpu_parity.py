@@ -334,3 +334,33 @@ def test_gpu_composite_algebra_matches_oracle(tuple_targets):
         want = O.evaluate(q, odb)
         got = record(q, db)
         assert same(got, want), (q, got, {k: want.get(k) for k in ("error", "matched", "negation", "n")})
+
+
+@pytest.mark.parametrize("force", ["0", "1", ""])
+def test_gpu_hub_join_expansion(force, monkeypatch):
+    """A hub key whose probe unit owns > 64K outputs (config 5 skew): the
+    output-balanced expansion, the per-unit expansion (forced) and the
+    automatic choice all equal the oracle."""
+    from das_amd import synthetic
+    if force:
+        monkeypatch.setenv("DAS_DJ_BALANCED", force)
+    else:
+        monkeypatch.delenv("DAS_DJ_BALANCED", raising=False)
+    n = 1200
+    rng = np.random.default_rng(4)
+    hub = 0
+    src = np.concatenate([np.arange(1, 301), rng.integers(1, n, 500)])           # 300 rows -> hub
+    dst = np.concatenate([np.full(300, hub), rng.integers(1, n, 500)])
+    src2 = np.concatenate([np.full(300, hub), rng.integers(1, n, 400)])          # hub -> 300 rows
+    dst2 = np.concatenate([np.arange(301, 601), rng.integers(1, n, 400)])
+    arrays, _ = synthetic.build_arrays(["T"], [("Concept", "n", n)],
+                                       [("T", np.stack([src, dst], 1)), ("T", np.stack([src2, dst2], 1))])
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    V = lambda x: ["Var", x]  # noqa: E731
+    t = lambda a, b: ["Link", "T", True, [a, b]]  # noqa: E731
+    for q in [["And", [t(V("A"), V("B")), t(V("B"), V("C"))]],
+              ["And", [t(V("A"), ["Node", "Concept", "n0"]), t(V("X"), V("A")), t(["Node", "Concept", "n0"], V("Y"))]]]:
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
