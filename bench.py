@@ -1,7 +1,7 @@
 """bench.py — DAS query hot path on MI355X: bindings/s + HBM roofline.
 
-Workload (BASELINE.json configs[1], the config the metric is quoted on that
-fits one GPU): a seeded synthetic gene-level KB in scripts/benchmark.py's
+Default workload (BASELINE.json configs[1], the config the metric is quoted on
+that fits one GPU): a seeded synthetic gene-level KB in scripts/benchmark.py's
 shape (Member(Gene, BiologicalProcess) with Zipf(1.1) process popularity,
 Inheritance(BP, BP)); the real bio_atomspace dump is not available offline.
 One step = one pass of the query batch below through the reference API
@@ -17,6 +17,15 @@ on the device, no Python object materialisation).  Multi-GPU: links are
 partitioned across ranks (Member by gene range, Inheritance by content hash)
 and And joins repartition both binding tables by the join key with an RCCL
 all-to-all (das_amd/parallel.py); per-rank KB size is fixed (weak scaling).
+
+Other workloads (`--workload`, one JSON line each; not the driver's default):
+  flybase  config 3: FlyBase-shaped Execution(Schema, key, value) KB, the
+           QueryFlyBase.ipynb And / And+Not / Or query shapes (fixed KB,
+           links content-hash sharded: strong scaling)
+  hub      config 5: power-law KB, 4-clause And on the top-degree hub nodes
+  build    config 4: bulk ExpressionHasher + interning + pattern / template /
+           incoming CSR index build; value = links indexed per second of
+           device time (host parse and PCIe upload excluded, reported apart)
 """
 import argparse
 import json
@@ -35,31 +44,127 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="bio", choices=["bio", "flybase", "hub", "build"])
+    # bio (config 2)
     ap.add_argument("--genes", type=int, default=200_000)
     ap.add_argument("--bps", type=int, default=50_000)
     ap.add_argument("--members", type=int, default=20_000_000)
     ap.add_argument("--inheritance", type=int, default=100_000)
+    # flybase (config 3): ~27.9M links like the notebook KB (SimplePatternMiner.ipynb:19)
+    ap.add_argument("--fb-genes", type=int, default=300_000)
+    ap.add_argument("--fb-schema", type=int, default=60)
+    ap.add_argument("--fb-rows", type=int, default=450_000)
+    # hub (config 5): H4's output grows ~ links^1.6 (Zipf hubs): 3M links -> ~4.3e8 bindings
+    ap.add_argument("--hub-links", type=int, default=3_000_000)
+    ap.add_argument("--hub-nodes", type=int, default=1 << 21)
+    # build (config 4)
+    ap.add_argument("--links", type=int, default=100_000_000)
+    ap.add_argument("--nodes", type=int, default=1 << 24)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
     return ap.parse_args()
 
 
-def queries(pm, rank_genes, n_bps, seed):
+# ---------------------------------------------------------------------------
+# workloads: KB + queries (the same spec drives the oracle's CPU baseline)
+# ---------------------------------------------------------------------------
+def _V(n):
+    return ["Var", n]
+
+
+def _L(t, *targets):
+    return ["Link", t, True, list(targets)]
+
+
+def bio_specs(rank_genes, seed=17):
     import numpy as np
     rng = np.random.default_rng(seed)
-    V = pm.Variable
-    g = lambda i: pm.Node("Gene", f"g{i}")  # noqa: E731
-    bp = lambda i: pm.Node("BiologicalProcess", f"bp{i}")  # noqa: E731
-    member = lambda a, b: pm.Link("Member", [a, b], True)  # noqa: E731
-    inh = lambda a, b: pm.Link("Inheritance", [a, b], True)  # noqa: E731
     ga, gb = (int(x) for x in rng.choice(rank_genes, 2, replace=False))
+    g = lambda i: ["Node", "Gene", f"g{i}"]  # noqa: E731
+    bp = lambda i: ["Node", "BiologicalProcess", f"bp{i}"]  # noqa: E731
     return [
-        ("Q1 Member(Vg,Vbp)", member(V("V_g"), V("V_bp"))),
-        ("Q2 Member*Inheritance", pm.And([member(V("V_g"), V("V_bp")), inh(V("V_bp"), V("V_p"))])),
-        ("Q3 same_biological_process", pm.And([member(g(ga), V("V_bp")), member(g(gb), V("V_bp"))])),
-        ("Q4 hub join", pm.And([member(V("V_g"), bp(0)), member(V("V_g"), V("V_bp"))])),
+        ("Q1 Member(Vg,Vbp)", _L("Member", _V("V_g"), _V("V_bp"))),
+        ("Q2 Member*Inheritance", ["And", [_L("Member", _V("V_g"), _V("V_bp")),
+                                           _L("Inheritance", _V("V_bp"), _V("V_p"))]]),
+        ("Q3 same_biological_process", ["And", [_L("Member", g(ga), _V("V_bp")), _L("Member", g(gb), _V("V_bp"))]]),
+        ("Q4 hub join", ["And", [_L("Member", _V("V_g"), bp(0)), _L("Member", _V("V_g"), _V("V_bp"))]]),
     ]
+
+
+def flybase_specs(gene=7, do_terms=()):
+    """QueryFlyBase.ipynb cells 5, 6, 7 and 9 (and the full uniquename x
+    recombination_loc join the notebook's loops walk), on one gene's FB id."""
+    s = lambda n: ["Node", "Schema", "Schema:" + n]  # noqa: E731
+    fb = ["Node", "Verbatim", f"FBgn{gene:07d}"]
+    E = lambda *t: _L("Execution", *t)  # noqa: E731
+    rec, cyto, uniq, do = (s("gene_map_table_recombination_loc"), s("gene_map_table_cytogenetic_loc"),
+                           s("gene_uniquename"), s("disease_model_annotations_DO_term"))
+    v = _V
+    specs = [
+        ("F5 same recombination_loc", ["And", [E(rec, fb, v("v1")), E(rec, v("v2"), v("v1")), E(uniq, v("v3"), v("v2"))]]),
+        ("F6 same cytogenetic_loc", ["And", [E(cyto, fb, v("v1")), E(cyto, v("v2"), v("v1")), E(uniq, v("v3"), v("v2"))]]),
+        ("F7 same recomb, different cyto", ["And", [E(rec, fb, v("v1")), E(rec, v("v2"), v("v1")), E(cyto, fb, v("v3")),
+                                                   ["Not", E(cyto, v("v2"), v("v3"))], E(uniq, v("v4"), v("v2"))]]),
+        ("F9 DO-term Or", ["Or", [E(do, v("v1"), ["Node", "Verbatim", d]) for d in do_terms] or
+                           [E(do, v("v1"), ["Node", "Verbatim", "DOID:0"])]]),
+        ("FJ uniquename x recombination_loc", ["And", [E(uniq, v("v3"), v("v2")), E(rec, v("v2"), v("v1"))]]),
+    ]
+    return specs
+
+
+def hub_specs():
+    """Config 5: 4-clause And anchored on the two highest-degree nodes (Zipf
+    ranks 0 and 1) of link type T0."""
+    n = lambda i: ["Node", "Concept", f"n{i}"]  # noqa: E731
+    return [
+        ("H4 T(V1,h0) T(V1,V2) T(V2,h1) T(V2,V3)",
+         ["And", [_L("T0", _V("V1"), n(0)), _L("T0", _V("V1"), _V("V2")), _L("T0", _V("V2"), n(1)),
+                  _L("T0", _V("V2"), _V("V3"))]]),
+        ("H2 T(V1,h0) T(V1,V2)", ["And", [_L("T0", _V("V1"), n(0)), _L("T0", _V("V1"), _V("V2"))]]),
+    ]
+
+
+def build_expr(pm, spec):
+    k = spec[0]
+    if k == "Node":
+        return pm.Node(spec[1], spec[2])
+    if k == "Var":
+        return pm.Variable(spec[1])
+    if k == "Link":
+        return pm.Link(spec[1], [build_expr(pm, t) for t in spec[3]], spec[2])
+    if k == "Not":
+        return pm.Not(build_expr(pm, spec[1]))
+    return (pm.And if k == "And" else pm.Or)([build_expr(pm, t) for t in spec[1]])
+
+
+def make_kb(args, rank, world):
+    """(AtomArrays for this rank, query specs, config dict, scaling)."""
+    import numpy as np
+    from das_amd import parallel, synthetic
+    if args.workload == "bio":
+        if world == 1:
+            arrays = synthetic.bio_kb(args.genes, args.bps, args.members, args.inheritance)
+            rank_genes = np.arange(args.genes)
+        else:
+            arrays, rank_genes = parallel.bio_shard(args.genes, args.bps, args.members, args.inheritance, rank, world)
+        cfg = {"workload": "config2 bio gene-level KB: single-Link + 2-clause And (Q1-Q4)",
+               "genes_per_rank": int(len(rank_genes)), "bps": args.bps, "member_links_per_rank": args.members,
+               "inheritance_links": args.inheritance}
+        return arrays, bio_specs(rank_genes), cfg, "weak"
+    if args.workload == "flybase":
+        arrays = synthetic.flybase_kb(args.fb_genes, args.fb_schema, args.fb_rows)
+        # the gene's DO terms (cell 9 builds its Or from them), read off the arrays
+        do_terms = synthetic.flybase_do_terms(arrays, gene=7)
+        arrays = parallel.shard_arrays(arrays, rank, world)
+        cfg = {"workload": "config3 FlyBase-shaped Execution KB: QueryFlyBase.ipynb And/And+Not/Or shapes",
+               "links": int(arrays.n_expr), "genes": args.fb_genes, "schemas": args.fb_schema}
+        return arrays, flybase_specs(7, do_terms), cfg, "strong"
+    arrays = synthetic.powerlaw_kb(args.hub_nodes, args.hub_links, link_types=4)
+    arrays = parallel.shard_arrays(arrays, rank, world)
+    cfg = {"workload": "config5 power-law hypergraph: 4-clause And on hub nodes",
+           "links": args.hub_links, "nodes": args.hub_nodes, "link_types": 4, "arity": "70% 2 / 30% 3"}
+    return arrays, hub_specs(), cfg, "strong"
 
 
 def cpu_baseline(args, budget_s):
@@ -67,18 +172,26 @@ def cpu_baseline(args, budget_s):
     complexity) on a bounded sample of the same workload, one core."""
     from das_amd import synthetic
     from oracle import das_oracle as O
-    scale = 1000
-    genes, bps = max(args.genes // scale, 50), max(args.bps // scale, 20)
-    members, inh = max(args.members // scale, 500), max(args.inheritance // scale, 40)
-    arrays = synthetic.bio_kb(genes, bps, members, inh)
+    if args.workload == "bio":
+        scale = 1000
+        genes, bps = max(args.genes // scale, 50), max(args.bps // scale, 20)
+        members, inh = max(args.members // scale, 500), max(args.inheritance // scale, 40)
+        arrays = synthetic.bio_kb(genes, bps, members, inh)
+        specs = [s for _, s in bio_specs(range(1, genes))]
+        what = f"bio_kb(genes={genes}, bps={bps}, members={members}, inheritance={inh}) = 1/{scale} of the GPU workload"
+    elif args.workload == "flybase":
+        scale = 1000
+        arrays = synthetic.flybase_kb(max(args.fb_genes // scale, 100), max(args.fb_schema // 10, 4),
+                                      max(args.fb_rows // scale, 200), n_loc=50, n_do=40)
+        specs = [s for _, s in flybase_specs(7, synthetic.flybase_do_terms(arrays, gene=7))]
+        what = f"flybase_kb at 1/{scale} of the GPU workload"
+    else:
+        scale = 100
+        arrays = synthetic.powerlaw_kb(max(args.hub_nodes // scale, 200), max(args.hub_links // scale, 2000),
+                                       link_types=4)
+        specs = [s for _, s in hub_specs()]
+        what = f"powerlaw_kb at 1/{scale} of the GPU workload"
     db = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
-    V = lambda n: ["Var", n]  # noqa: E731
-    member = lambda a, b: ["Link", "Member", True, [a, b]]  # noqa: E731
-    inh_l = lambda a, b: ["Link", "Inheritance", True, [a, b]]  # noqa: E731
-    specs = [member(V("V_g"), V("V_bp")),
-             ["And", [member(V("V_g"), V("V_bp")), inh_l(V("V_bp"), V("V_p"))]],
-             ["And", [member(["Node", "Gene", "g1"], V("V_bp")), member(["Node", "Gene", "g2"], V("V_bp"))]],
-             ["And", [member(V("V_g"), ["Node", "BiologicalProcess", "bp0"]), member(V("V_g"), V("V_bp"))]]]
     total, t0, passes = 0, time.perf_counter(), 0
     while True:
         for s in specs:
@@ -88,9 +201,92 @@ def cpu_baseline(args, budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": total / dt, "unit": "bindings/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (nested-loop And, reference complexity) on bio_kb(genes={genes}, bps={bps}, "
-                      f"members={members}, inheritance={inh}) = 1/{scale} of the GPU workload, Q1-Q4, "
+            "sample": f"oracle (nested-loop And, reference complexity) on {what}, {len(specs)} queries, "
                       f"{passes} passes in {dt:.1f} s"}
+
+
+def roofline_of(stats):
+    """Dominant single-kernel scope ("k_*") of the timed region -> roofline;
+    multi-launch phases (join_build, incoming_csr, ...) are reported under
+    "kernels" but are not a kernel's roofline."""
+    single = {k: v for k, v in stats.items() if k.startswith("k_")}
+    if not single:
+        return None
+    name, st = max(single.items(), key=lambda kv: kv[1]["ms"])
+    achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9 if st["ms"] > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get(name, {}).get("bytes_per_launch")
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
+            "avg_launch_us": round(st["ms"] * 1e3 / max(st["launches"], 1), 2),
+            "algorithmic_bytes_per_launch": st["bytes"] / max(st["launches"], 1)}
+
+
+def kernels_of(stats):
+    return {k: {"ms": round(v["ms"], 3), "launches": v["launches"],
+                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in stats.items()}
+
+
+# ---------------------------------------------------------------------------
+# config 4: bulk index build
+# ---------------------------------------------------------------------------
+def run_build(args, rank, world, dist, local_rank):
+    import torch
+    from das_amd import parallel, synthetic
+    from das_amd.database.hip_db import HipDB
+    t0 = time.perf_counter()
+    log(f"generating {args.links} links")
+    arrays = synthetic.powerlaw_kb(args.nodes, args.links, link_types=4)
+    arrays = parallel.shard_arrays(arrays, rank, world)
+    t_gen = time.perf_counter() - t0
+    db = HipDB(device=local_rank)
+    db.load_arrays(synthetic.powerlaw_kb(1000, 10000, link_types=4))    # warm-up build (code objects, pools)
+    torch.cuda.synchronize()
+    db.ctx.prof_reset()
+    db.ctx.prof_enable(True)
+    if dist:
+        dist.barrier()
+    log("building")
+    t1 = time.perf_counter()
+    db.load_arrays(arrays)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t1
+    db.ctx.prof_enable(False)
+    stats = db.ctx.prof_stats()
+    dev_ms = stats.get("build_device", {}).get("ms", wall * 1e3)
+    st = db.stats()
+    local_links = int(sum(arrays.expr_kind == 1))
+    links = local_links
+    if dist:
+        t = torch.tensor([dev_ms, wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dev_ms, wall = float(t[0]), float(t[1])
+        n = torch.tensor([local_links], dtype=torch.float64, device="cuda")
+        dist.all_reduce(n)
+        links = int(n.item())
+    if rank == 0:
+        hs = stats.get("k_hash_group", {"ms": 0, "bytes": 0, "launches": 0})
+        out = {"metric": "links indexed/s (bulk ExpressionHasher + intern + pattern/template/incoming CSR build)",
+               "value": links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
+               "ms_per_step": dev_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "u32",
+               "data": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets), generated on the host",
+               "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
+                          "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
+                          "parallelism": f"links sharded x{world} (every rank hashes the whole directory)"},
+               "roofline": roofline_of(stats), "cpu_baseline": None,
+               "hash": {"ms": round(hs["ms"], 3), "GBps": round(hs["bytes"] / max(hs["ms"], 1e-9) / 1e6, 1),
+                        "md5_blocks_per_s": None},
+               "kernels": kernels_of(stats), "wall_incl_upload_s": round(wall, 3), "host_generate_s": round(t_gen, 2),
+               "atoms": int(st.n_atoms), "device_bytes": int(st.device_bytes)}
+        print(json.dumps(out))
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -98,7 +294,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
     import torch
     # DAS_BENCH_SAME_DEVICE=1 + DAS_DIST_BACKEND=gloo rehearse N ranks on one GPU
     if os.environ.get("DAS_BENCH_SAME_DEVICE") == "1":
@@ -112,23 +307,24 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
-    from das_amd import synthetic
+    if args.workload == "build":
+        run_build(args, rank, world, dist, local_rank)
+        if dist:
+            dist.destroy_process_group()
+        return
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
 
     # ---- knowledge base (per-rank partition for N > 1) ----
     t_build = time.perf_counter()
-    if world == 1:
-        arrays = synthetic.bio_kb(args.genes, args.bps, args.members, args.inheritance)
-        rank_genes = np.arange(args.genes)
-    else:
-        from das_amd import parallel
-        arrays, rank_genes = parallel.bio_shard(args.genes, args.bps, args.members, args.inheritance, rank, world)
+    log(f"generating {args.workload} KB")
+    arrays, specs, cfg, scaling = make_kb(args, rank, world)
+    log(f"building the device index ({arrays.n_expr} expressions)")
     db = HipDB(device=local_rank)
     db.load_arrays(arrays)
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
-    qs = queries(pm, rank_genes, args.bps, seed=17)
+    qs = [(name, build_expr(pm, s)) for name, s in specs]
     if world > 1:
         from das_amd import parallel
         engine = parallel.ShardedMatcher(db, dist, cpu_staging=(backend != "nccl"))
@@ -144,6 +340,7 @@ def main():
     def step():
         return sum(run(q) for _, q in qs)
 
+    log("warmup")
     for _ in range(args.warmup):
         step()
     per_query = {name: run(q) for name, q in qs}
@@ -153,6 +350,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    log("timed steps")
     bindings = 0
     for _ in range(args.steps):
         bindings += step()
@@ -180,43 +378,24 @@ def main():
         dist.all_reduce(b)
         bindings = float(b.item())
     value = bindings / elapsed
-
-    # dominant kernel of the timed region -> roofline
-    # single-kernel scopes only ("k_*"); multi-launch phases such as join_build
-    # are reported under "kernels" but are not a kernel's roofline
-    single = {k: v for k, v in stats.items() if k.startswith("k_")}
-    dom = max(single.items(), key=lambda kv: kv[1]["ms"]) if single else None
-    roofline = None
-    if dom:
-        name, st = dom
-        achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9 if st["ms"] > 0 else 0.0
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get(name, {}).get("bytes_per_launch")
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
-                    "avg_launch_us": round(st["ms"] * 1e3 / max(st["launches"], 1), 2),
-                    "algorithmic_bytes_per_launch": st["bytes"] / max(st["launches"], 1)}
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline")
             cpu = cpu_baseline(args, args.cpu_baseline_seconds)
+        data = {"bio": "synthetic (seeded bio_kb in scripts/benchmark.py shape; bio_atomspace dump unavailable offline)",
+                "flybase": "synthetic FlyBase-shaped KB (flybase2metta Execution layout; the FlyBase dump needs a "
+                           "network fetch)",
+                "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[args.workload]
+        cfg = dict(cfg, bindings_per_step_rank0=per_query, parallelism=f"links sharded x{world}")
         out = {
             "metric": "pattern matches/sec (bindings/s) + % HBM roofline",
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (seeded bio_kb in scripts/benchmark.py shape; bio_atomspace dump unavailable offline)",
-            "config": {"workload": "config2 bio gene-level KB: single-Link + 2-clause And (Q1-Q4)",
-                       "genes_per_rank": int(len(rank_genes)), "bps": args.bps,
-                       "member_links_per_rank": args.members, "inheritance_links": args.inheritance,
-                       "bindings_per_step_rank0": per_query, "parallelism": f"links sharded x{world}"},
-            "roofline": roofline,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "u32", "data": data, "config": cfg,
+            "roofline": roofline_of(stats),
             "cpu_baseline": cpu,
-            "kernels": {k: {"ms": round(v["ms"], 3), "launches": v["launches"],
-                            "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in stats.items()},
+            "kernels": kernels_of(stats),
             "build_s": round(t_build, 2),
         }
         print(json.dumps(out))

@@ -88,6 +88,7 @@ _SIGS = {
     "das_atoms_info": (C.c_int, [P, P, C.c_uint64, P, P, P, P, P]),
     "das_link_targets": (C.c_int, [P, C.c_uint32, P, C.c_uint32, P]),
     "das_ctype_lookup": (C.c_int, [P, P, P]),
+    "das_incoming": (C.c_int, [P, C.c_uint32, P, C.c_uint64, P]),
     "das_scan_link": (C.c_int, [P, C.POINTER(das_link_scan_t), C.POINTER(P)]),
     "das_scan_template": (C.c_int, [P, C.POINTER(das_template_scan_t), C.POINTER(P)]),
     "das_scan_type": (C.c_int, [P, C.c_uint32, P]),
@@ -315,6 +316,14 @@ class Context:
         n = C.c_uint32()
         check(lib().das_link_targets(self.h, int(atom_id), ptr(buf), 64, C.byref(n)), self.h)
         return buf[:n.value].copy()
+
+    def incoming(self, atom_id):
+        n = C.c_uint64()
+        check(lib().das_incoming(self.h, int(atom_id), None, 0, C.byref(n)), self.h)
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        if n.value:
+            check(lib().das_incoming(self.h, int(atom_id), ptr(out), n.value, C.byref(n)), self.h)
+        return out[:n.value]
 
     def ctype_lookup(self, digest):
         d = np.ascontiguousarray(np.asarray(digest, dtype=np.uint32))

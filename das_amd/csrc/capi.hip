@@ -315,6 +315,23 @@ int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, u
   });
 }
 
+int das_incoming(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint64_t cap, uint64_t* n) {
+  return guarded(ctx, [&] {
+    const das::Index& idx = ctx->c.idx;
+    DAS_CHECK(idx.built, das::DAS_E_NOT_BUILT, "index not built");
+    DAS_CHECK(id < idx.n_atoms, das::DAS_E_INVALID, "atom id out of range");
+    uint32_t be[2];
+    DAS_HIP(hipMemcpyAsync(be, idx.in_off + id, 8, hipMemcpyDeviceToHost, ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    *n = be[1] - be[0];
+    const uint64_t m = std::min<uint64_t>(*n, cap);
+    if (m) {
+      DAS_HIP(hipMemcpyAsync(out, idx.in_link + be[0], 4 * m, hipMemcpyDeviceToHost, ctx->c.s));
+      DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    }
+  });
+}
+
 int das_ctype_lookup(das_ctx_t* ctx, const uint32_t digest[4], int64_t* ctype_id) {
   return guarded(ctx, [&] {
     const auto& v = ctx->c.idx.ctype_digest;

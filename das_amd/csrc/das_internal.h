@@ -58,6 +58,9 @@ struct Index {
   uint32_t* type = nullptr;    // [n_atoms] named type id (kNone for CAT_OTHER)
   uint32_t* arity = nullptr;   // [n_atoms]
   uint64_t* tgt_off = nullptr; // [n_atoms + 1]
+  uint32_t* in_off = nullptr;  // [n_atoms + 1] incoming CSR offsets
+  uint32_t* in_link = nullptr; // [in_total] links containing each atom, by (target, link id)
+  uint64_t in_total = 0;
   uint32_t* tgt = nullptr;     // [sum arity]
   uint32_t* ctype = nullptr;   // [n_atoms] composite-type id of links, kNone otherwise
   uint32_t* name_leaf = nullptr; // [n_atoms] loader leaf index of nodes (kNone otherwise)

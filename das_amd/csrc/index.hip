@@ -16,6 +16,7 @@
 // T_a ('*' type); a '*' type with grounded targets by one key range of P_{a,p}
 // per named type.  This covers exactly the families the reference writes for arity
 // 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
+#include <optional>
 #include "das_internal.h"
 
 namespace das {
@@ -379,6 +380,25 @@ uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hi
   return m;
 }
 
+// link id of every outgoing-set entry: out[tgt_off[a] + k] = a
+__global__ void k_owner_fill(const uint64_t* tgt_off, uint64_t n_atoms, uint32_t* out) {
+  for (uint64_t a = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; a < n_atoms; a += (uint64_t)gridDim.x * blockDim.x)
+    for (uint64_t i = tgt_off[a]; i < tgt_off[a + 1]; ++i) out[i] = (uint32_t)a;
+}
+
+// sorted keys in [0, n_keys) -> off[k] = first index with key >= k, k in [0, n_keys]
+// (one binary search per k: runs of absent keys can be long)
+__global__ void k_bounds_u32(const uint32_t* key, uint64_t n, uint32_t n_keys, uint32_t* off) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (key[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    off[k] = (uint32_t)lo;
+  }
+}
+
 // Column id bounds of rows [b, e) of a T_a table (one named type's segment):
 // per-thread running min/max, wave + block reduction, one atomic per block
 // and column (per-row or per-wave atomics on one address serialise).
@@ -510,6 +530,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   c.leaf_bytes.assign(a.leaf_bytes, a.leaf_bytes + n_bytes);
   c.leaf_off.assign(a.leaf_off, a.leaf_off + nl + 1);
 
+  std::optional<ProfScope> up(std::in_place, c, "upload", (double)n_bytes + 8.0 * (nl + ne) + 4.0 * n_child + 13.0 * nl + 5.0 * ne);
   auto d_bytes = upload(a.leaf_bytes, n_bytes, s);
   auto d_loff = upload(a.leaf_off, nl + 1, s);
   auto d_lkind = upload(a.leaf_kind, nl, s);
@@ -519,15 +540,23 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   auto d_child = upload(a.expr_child, n_child, s);
   auto d_ekind = upload(a.expr_kind, ne, s);
   auto d_ectl = upload(a.expr_ctype_leaf, ne, s);
+  up.reset();
+  // device-side build (hash, intern, CSRs, index tables): config 4's timed region
+  ProfScope whole(c, "build_device", 0.0);
 
   // 1. digests + composite types of every unified index
   DBuf<Digest> dig(nu, s), ct(nu, s);
-  hash_strings(d_bytes.p, d_loff.p, nl, dig.p, s);
+  {
+    ProfScope ps(c, "k_hash_strings", (double)n_bytes + 8.0 * nl + 16.0 * nl);
+    hash_strings(d_bytes.p, d_loff.p, nl, dig.p, s);
+  }
   if (nl) hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)d_lct.p, ct.p, nl);
   for (uint32_t g = 0; g < a.n_levels; ++g) {
     const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
     if (e <= b) continue;
     const uint32_t K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
+    // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
+    ProfScope ps(c, "k_hash_group", (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
     hash_group(dig.p, ct.p, d_child.p, d_eoff.p, d_ectl.p, nl, b, e - b, K, s);
   }
 
@@ -622,6 +651,29 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   }
   dig.release(); ct.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
   d_child.release(); d_bytes.release();
+
+  // incoming CSR (the reference's `incomming_set:<target>` family,
+  // canonical_parser.py:141-143): every (target, link) pair of the outgoing
+  // sets, sorted by target then link id; in_off by bucket bounds.
+  {
+    ProfScope ps(c, "incoming_csr", 0.0);
+    const uint64_t total = read_u64(idx.tgt_off + n_atoms, s);
+    DAS_CHECK(total < (1ull << 32), DAS_E_UNSUPPORTED, "incoming CSR: more than 2^32 link targets");
+    idx.in_off = dalloc<uint32_t>(idx, n_atoms + 1);
+    idx.in_link = dalloc<uint32_t>(idx, total);
+    if (total) {
+      DBuf<uint32_t> key(total, s);
+      hipLaunchKernelGGL(k_owner_fill, G(n_atoms), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, n_atoms, idx.in_link);
+      copy_dev(key.p, idx.tgt, 4 * total, s);
+      radix_sort_pairs<uint32_t>(key.p, idx.in_link, total, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
+      hipLaunchKernelGGL(k_bounds_u32, G(n_atoms + 1), dim3(B), 0, s, (const uint32_t*)key.p, total,
+                         (uint32_t)n_atoms, idx.in_off);
+    } else {
+      fill_dev(idx.in_off, 0, 4 * (n_atoms + 1), s);
+    }
+    DAS_HIP(hipGetLastError());
+    idx.in_total = total;
+  }
 
   // 5. counts per arity, node count
   {

@@ -323,13 +323,17 @@ __global__ void __launch_bounds__(B) k_key_hist(const uint32_t* key, uint64_t n,
   }
 }
 
-// Sorted build keys: off[d] = first row whose key >= kmin + d, d in [0, range].
-// Row i fills the offsets of the key gap (key[i-1], key[i]].
+// Sorted build keys: off[d] = first row whose key >= kmin + d, d in [0, range]
+// (a binary search per d: gaps between present keys can be long).
 __global__ void k_bucket_bounds(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t range, uint32_t* off) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t lo = i == 0 ? 0u : key[i - 1] - kmin + 1;
-    const uint32_t hi = i == n ? range : key[i] - kmin;
-    for (uint32_t d = lo; d <= hi && d <= range; ++d) off[d] = (uint32_t)i;
+  for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d <= range; d += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = kmin + d;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((uint64_t)key[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    off[d] = (uint32_t)lo;
   }
 }
 
@@ -1034,7 +1038,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   const Table* Qb = &Q;
   if (Q.sorted_col == qk) {
     ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * range);
-    hipLaunchKernelGGL(k_bucket_bounds, G(Q.nrows + 1), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, off.p);
+    hipLaunchKernelGGL(k_bucket_bounds, G(range + 1), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, off.p);
     DAS_HIP(hipGetLastError());
   } else {
     DBuf<uint32_t> cnt(range + 1, c.s);

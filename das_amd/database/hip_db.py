@@ -220,6 +220,16 @@ class HipDB(RelationalDB):
             raise ValueError(f"Invalid handle: {link_handle}")
         return self.hex_of(self.ctx.link_targets(aid))
 
+    def get_incoming_links(self, atom_handle: str) -> List[str]:
+        """The `incomming_set:<handle>` index family (canonical_parser.py:141-143,
+        parser_threads.py:155-159; no reference DBInterface method reads it):
+        every link whose targets contain the atom.  Redis returns a set; here
+        the handles come sorted by link id."""
+        aid, cat, _ = self._lookup(atom_handle)
+        if aid < 0:
+            raise ValueError(f"Invalid handle: {atom_handle}")
+        return list(dict.fromkeys(self.hex_of(self.ctx.incoming(aid))))   # a set, as SADD builds it
+
     def is_ordered(self, link_handle: str) -> bool:
         """redis_mongo_db.py:229-233"""
         aid, cat, _ = self._lookup(link_handle)

@@ -468,3 +468,26 @@ def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
     arrays, _ = synthetic.build_arrays(["Member", "Inheritance"],
                                        [("Gene", "g", total_genes), ("BiologicalProcess", "bp", n_bps)], blocks)
     return arrays, np.arange(rank * n_genes, (rank + 1) * n_genes)
+
+
+def shard_arrays(arrays, rank, world):
+    """Generic link sharding for a fixed KB (strong scaling): every rank keeps
+    the whole atom directory; a link's pattern-index rows stay on the rank its
+    content hash (type + targets) selects, elsewhere it becomes a remote link
+    (expr kind 3).  Typedef expressions are never sharded."""
+    if world == 1:
+        return arrays
+    kinds = arrays.expr_kind.copy()
+    off = arrays.expr_off
+    for g in range(len(arrays.level_off) - 1):
+        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
+        if e <= b:
+            continue
+        k = int(off[b + 1] - off[b])
+        ch = arrays.expr_child[int(off[b]):int(off[e])].reshape(e - b, k).astype(np.int64)
+        own = owner_of(ch, world)
+        seg = kinds[b:e]
+        seg[(seg == 1) & (own != rank)] = 3
+        kinds[b:e] = seg
+    arrays.expr_kind = kinds
+    return arrays

@@ -48,13 +48,18 @@ def build_arrays(type_names, node_blocks, link_blocks):
     # leaves: the type names, then the nodes
     strings = [t.encode() for t in types]
     node_off = []
-    node_ctype = []
+    node_ctype, name_start = [], []
     n_nodes = 0
     for t, prefix, count in node_blocks:
         node_off.append(n_types + n_nodes)
         strings.extend(f"{t} {prefix}{i}".encode() for i in range(count))
         node_ctype.append(np.full(count, tid[t], dtype=np.uint32))
+        name_start.append(np.full(count, len(t.encode()) + 1, np.uint32))
         n_nodes += count
+    return _finish_arrays(types, tid, strings, n_types, n_nodes, node_ctype, name_start, link_blocks), node_off
+
+
+def _finish_arrays(types, tid, strings, n_types, n_nodes, node_ctype, name_start, link_blocks):
     n_leaf = n_types + n_nodes
     lens = np.fromiter((len(s) for s in strings), dtype=np.uint64, count=n_leaf)
     leaf_off = np.zeros(n_leaf + 1, dtype=np.uint64)
@@ -64,8 +69,7 @@ def build_arrays(type_names, node_blocks, link_blocks):
     leaf_ctype = np.concatenate([np.arange(n_types, dtype=np.uint32)] + node_ctype) if n_nodes else \
         np.arange(n_types, dtype=np.uint32)
     leaf_type_id = np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, NONE, np.uint32)])
-    name_start = np.concatenate([np.zeros(n_types, np.uint32)] +
-                                [np.full(c, len(t.encode()) + 1 + 0, np.uint32) for t, _, c in node_blocks])
+    name_start = np.concatenate([np.zeros(n_types, np.uint32)] + list(name_start))
     # expressions: one group per arity (all at level 1)
     by_k, kinds_k = {}, {}
     for blk in link_blocks:
@@ -90,10 +94,33 @@ def build_arrays(type_names, node_blocks, link_blocks):
     np.cumsum(nch, out=expr_off[1:])
     expr_child = np.concatenate(childs) if childs else np.zeros(0, np.uint32)
     expr_kind = np.concatenate(ekinds) if ekinds else np.zeros(0, np.uint8)
-    arrays = AtomArrays(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start, expr_off,
-                        expr_child, expr_kind, np.full(n_expr, -1, np.int32),
-                        np.array(groups, np.uint64), types)
-    return arrays, node_off
+    return AtomArrays(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start, expr_off,
+                      expr_child, expr_kind, np.full(n_expr, -1, np.int32),
+                      np.array(groups, np.uint64), types)
+
+
+def build_arrays_named(type_names, node_lists, link_blocks):
+    """build_arrays with explicit node names: node_lists = [(type, [names])]."""
+    types = list(type_names)
+    tid = {t: i for i, t in enumerate(types)}
+    for t, _ in node_lists:
+        if t not in tid:
+            tid[t] = len(types)
+            types.append(t)
+    for blk in link_blocks:
+        if blk[0] not in tid:
+            tid[blk[0]] = len(types)
+            types.append(blk[0])
+    n_types = len(types)
+    strings = [t.encode() for t in types]
+    node_ctype, name_start = [], []
+    n_nodes = 0
+    for t, names in node_lists:
+        strings.extend(f"{t} {n}".encode() for n in names)
+        node_ctype.append(np.full(len(names), tid[t], dtype=np.uint32))
+        name_start.append(np.full(len(names), len(t.encode()) + 1, np.uint32))
+        n_nodes += len(names)
+    return _finish_arrays(types, tid, strings, n_types, n_nodes, node_ctype, name_start, link_blocks)
 
 
 def bio_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, seed=SEED):
@@ -112,17 +139,87 @@ def bio_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, seed=SEED
     return arrays
 
 
-def flybase_kb(n_rows=100_000, n_schema=60, n_pk=200_000, n_values=50_000, seed=SEED):
-    """Config 3 shape: Execution(Schema s, Concept pk, Verbatim value), Zipf values."""
+def flybase_kb(n_genes=200_000, n_schema=60, rows_per_schema=400_000, n_loc=5_000, n_do=2_000,
+               seed=SEED):
+    """Config 3: FlyBase-shaped canonical KB in flybase2metta's
+    Execution(Schema s, key, value) layout (sql_reader.py:297-302), arity 3.
+    Genes have a pk node and an FB id (Verbatim); the tables QueryFlyBase.ipynb
+    queries are present with their semantics, the rest are filler tables
+    keyed by FB id with Zipf(1.1) values:
+      Schema:gene_uniquename                     (gene pk, FB id)
+      Schema:gene_map_table_recombination_loc    (FB id, location)
+      Schema:gene_map_table_cytogenetic_loc      (FB id, cyto location)
+      Schema:disease_model_annotations_DO_term   (FB id, DO term), ~2 per gene
+    Node names: "FBgn%07d" (Verbatim), "g%d" (gene), "loc%d"/"cyto%d"/"DOID:%d"."""
     rng = np.random.default_rng(seed)
-    s = rng.integers(0, n_schema, n_rows)
-    pk = rng.integers(0, n_pk, n_rows)
-    v = zipf_indices(rng, n_values, n_rows)
-    arrays, off = build_arrays(
-        ["Execution"],
-        [("Schema", "s", n_schema), ("Concept", "pk", n_pk), ("Verbatim", "v", n_values)],
-        [("Execution", np.stack([s, n_schema + pk, n_schema + n_pk + v], 1))])
+    named = ["Schema:gene_uniquename", "Schema:gene_map_table_recombination_loc",
+             "Schema:gene_map_table_cytogenetic_loc", "Schema:disease_model_annotations_DO_term"]
+    n_fill = max(n_schema - len(named), 0)
+    n_val = max(rows_per_schema // 4, 1000)
+    # node blocks (global index = block offset + i)
+    blocks = [("Schema", "Schema:fill", 0), ("gene", "g", n_genes), ("Verbatim", "FBgn", n_genes),
+              ("Verbatim", "loc", n_loc), ("Verbatim", "cyto", n_loc), ("Verbatim", "DOID:", n_do),
+              ("Verbatim", "val", n_val)]
+    off = {}
+    o = 0
+    for t, p, c in blocks:
+        off[p] = o
+        o += c
+    schema_names = named + [f"Schema:table{i}_col" for i in range(n_fill)]
+    genes = np.arange(n_genes)
+    fb = off["FBgn"] + genes
+    links = []
+
+    def ex(si, a, b):
+        links.append(np.stack([np.full(len(a), si, np.int64), a, b], 1))
+    ex(0, off["g"] + genes, fb)
+    ex(1, fb, off["loc"] + zipf_indices(rng, n_loc, n_genes))
+    ex(2, fb, off["cyto"] + zipf_indices(rng, n_loc, n_genes))
+    k = 2 * n_genes
+    ex(3, fb[rng.integers(0, n_genes, k)], off["DOID:"] + zipf_indices(rng, n_do, k))
+    for i in range(n_fill):
+        ex(len(named) + i, fb[rng.integers(0, n_genes, rows_per_schema)],
+           off["val"] + zipf_indices(rng, n_val, rows_per_schema))
+    ch = np.concatenate(links)
+    # schema nodes go first as their own block: shift every other index
+    n_s = len(schema_names)
+    ch[:, 1:] += n_s
+    arrays = build_arrays_named(["Execution"], [("Schema", schema_names)] +
+                                [(t, [f"{p}{i}" if p != "FBgn" else f"FBgn{i:07d}" for i in range(c)])
+                                 for t, p, c in blocks[1:]],
+                                [("Execution", ch)])
     return arrays
+
+
+def _leaf_name(arrays, i):
+    a, b = int(arrays.leaf_off[i]), int(arrays.leaf_off[i + 1])
+    return bytes(arrays.leaf_bytes[a + int(arrays.name_start[i]):b]).decode()
+
+
+def flybase_do_terms(arrays, gene=7):
+    """DO terms of one gene in a flybase_kb (QueryFlyBase.ipynb cell 9 builds
+    its Or over them), read back from the arrays."""
+    want_s, want_g = "Schema:disease_model_annotations_DO_term", f"FBgn{gene:07d}"
+    off = arrays.expr_off
+    out = []
+    for g in range(len(arrays.level_off) - 1):
+        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
+        if e <= b or int(off[b + 1] - off[b]) != 4:
+            continue
+        ch = arrays.expr_child[int(off[b]):int(off[e])].reshape(e - b, 4)
+        s_leaf = g_leaf = None
+        for i in np.unique(ch[:, 1]):
+            if _leaf_name(arrays, i) == want_s:
+                s_leaf = i
+        if s_leaf is None:
+            continue
+        rows = ch[ch[:, 1] == s_leaf]
+        for i in np.unique(rows[:, 2]):
+            if _leaf_name(arrays, i) == want_g:
+                g_leaf = i
+        if g_leaf is not None:
+            out = sorted({_leaf_name(arrays, i) for i in rows[rows[:, 2] == g_leaf][:, 3]})
+    return out
 
 
 def powerlaw_kb(n_nodes=1 << 16, n_links=1 << 20, frac_arity2=0.7, link_types=4, seed=SEED):

@@ -117,6 +117,10 @@ int das_atoms_info(das_ctx_t* ctx, const uint32_t* ids, uint64_t n, uint32_t* di
                    uint8_t* cat, uint32_t* arity, uint32_t* type, uint32_t* name_leaf);
 /* outgoing set of a link: targets in stored order (get_link_targets) */
 int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, uint32_t* n);
+/* incoming set of an atom: the links whose outgoing set contains it, ascending
+ * link id (`incomming_set:<handle>`, canonical_parser.py:141-143).  *n = the set
+ * size; min(*n, cap) ids are copied to `out`. */
+int das_incoming(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint64_t cap, uint64_t* n);
 /* composite-type digest -> ctype id, or -1 (templates:<composite_type_hash>) */
 int das_ctype_lookup(das_ctx_t* ctx, const uint32_t digest[4], int64_t* ctype_id);
 
