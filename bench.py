@@ -26,6 +26,10 @@ Other workloads (`--workload`, one JSON line each; not the driver's default):
   build    config 4: bulk ExpressionHasher + interning + pattern / template /
            incoming CSR index build; value = links indexed per second of
            device time (host parse and PCIe upload excluded, reported apart)
+  load     canonical MeTTa text (FlyBase-shaped) -> native multi-threaded
+           reader (canonical.cpp) -> device index; value = links per second
+           of the whole load (parse + upload + build), the reference's
+           CanonicalParser path (canonical_parser.py:315-365)
 """
 import argparse
 import json
@@ -44,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="bio", choices=["bio", "flybase", "hub", "build"])
+    ap.add_argument("--workload", default="bio", choices=["bio", "flybase", "hub", "build", "load"])
     # bio (config 2)
     ap.add_argument("--genes", type=int, default=200_000)
     ap.add_argument("--bps", type=int, default=50_000)
@@ -60,6 +64,9 @@ def parse():
     # build (config 4)
     ap.add_argument("--links", type=int, default=100_000_000)
     ap.add_argument("--nodes", type=int, default=1 << 24)
+    # load (canonical text): ~100 B a line
+    ap.add_argument("--load-genes", type=int, default=200_000)
+    ap.add_argument("--load-rows", type=int, default=200_000)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
@@ -205,7 +212,7 @@ def cpu_baseline(args, budget_s):
                       f"{passes} passes in {dt:.1f} s"}
 
 
-def roofline_of(stats):
+def roofline_of(stats, workload="bio"):
     """Dominant single-kernel scope ("k_*") of the timed region -> roofline;
     multi-launch phases (join_build, incoming_csr, ...) are reported under
     "kernels" but are not a kernel's roofline."""
@@ -215,7 +222,8 @@ def roofline_of(stats):
     name, st = max(single.items(), key=lambda kv: kv[1]["ms"])
     achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9 if st["ms"] > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    # per-kernel HBM bytes from this workload's rocprofv3 PMC passes (tools/profile_bench.sh)
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "bio" else f"pmc_traffic_{workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get(name, {}).get("bytes_per_launch")
@@ -267,8 +275,17 @@ def run_build(args, rank, world, dist, local_rank):
         n = torch.tensor([local_links], dtype=torch.float64, device="cuda")
         dist.all_reduce(n)
         links = int(n.item())
+    # MD5 blocks hashed: a message of L bytes takes
+    # ceil((L + 9) / 64) blocks; a composite message is K 32-hex handles joined
+    # by spaces (33 K - 1 bytes), a terminal one its "Type name" string
+    import numpy as np
+    leaf_len = np.diff(arrays.leaf_off.astype(np.int64))
+    blocks_leaf = int(((leaf_len + 9 + 63) // 64).sum())
+    nch = np.diff(arrays.expr_off.astype(np.int64))
+    blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum())
     if rank == 0:
         hs = stats.get("k_hash_group", {"ms": 0, "bytes": 0, "launches": 0})
+        hl = stats.get("k_hash_strings", {"ms": 0, "bytes": 0, "launches": 0})
         out = {"metric": "links indexed/s (bulk ExpressionHasher + intern + pattern/template/incoming CSR build)",
                "value": links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
                "ms_per_step": dev_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -277,9 +294,11 @@ def run_build(args, rank, world, dist, local_rank):
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
                           "parallelism": f"links sharded x{world} (every rank hashes the whole directory)"},
-               "roofline": roofline_of(stats), "cpu_baseline": None,
+               "roofline": roofline_of(stats, "build"), "cpu_baseline": None,
                "hash": {"ms": round(hs["ms"], 3), "GBps": round(hs["bytes"] / max(hs["ms"], 1e-9) / 1e6, 1),
-                        "md5_blocks_per_s": None},
+                        "md5_blocks_per_s": (blocks_leaf + blocks_expr) / max((hs["ms"] + hl["ms"]) * 1e-3, 1e-12),
+                        "md5_blocks": blocks_leaf + blocks_expr,
+                        "terminal_ms": round(hl["ms"], 3)},
                "kernels": kernels_of(stats), "wall_incl_upload_s": round(wall, 3), "host_generate_s": round(t_gen, 2),
                "atoms": int(st.n_atoms), "device_bytes": int(st.device_bytes)}
         print(json.dumps(out))
@@ -287,6 +306,63 @@ def run_build(args, rank, world, dist, local_rank):
 
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def run_load(args, rank, world, local_rank):
+    import numpy as np
+    import torch
+    from das_amd import _lib, synthetic
+    from das_amd.database.hip_db import HipDB
+    if world > 1 and rank != 0:
+        return                      # host parse: one replica is the measurement
+    log("generating the canonical text")
+    arrays = synthetic.flybase_kb(args.load_genes, 20, args.load_rows)
+    text = synthetic.to_canonical(arrays).encode()
+    n_lines = text.count(b"\n")
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    db = HipDB(device=local_rank)
+    db.load_arrays(_lib.parse_canonical(text[:200000].rsplit(b"\n", 1)[0] + b"\n", threads))   # warm-up
+    torch.cuda.synchronize()
+    db.ctx.prof_reset()
+    db.ctx.prof_enable(True)
+    log(f"parsing {len(text) / 1e6:.0f} MB ({n_lines} lines) on {threads} threads")
+    t0 = time.perf_counter()
+    parsed = _lib.parse_canonical(text, threads)
+    t1 = time.perf_counter()
+    db.load_arrays(parsed)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    db.ctx.prof_enable(False)
+    stats = db.ctx.prof_stats()
+    links = int(db.stats().n_links)
+    out = {"metric": "links loaded/s (canonical MeTTa text -> native reader -> device index)",
+           "value": links / (t2 - t0), "unit": "links/s", "n_gpus": 1, "steps": 1, "warmup": 1,
+           "ms_per_step": (t2 - t0) * 1e3, "higher_is_better": True, "scaling": "replicas only",
+           "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic FlyBase-shaped canonical text (flybase_kb -> to_canonical)",
+           "config": {"workload": "canonical load: CanonicalParser.parse + index build", "bytes": len(text),
+                      "lines": n_lines, "host_threads": threads},
+           "parse_s": round(t1 - t0, 3), "parse_MBps": round(len(text) / (t1 - t0) / 1e6, 1),
+           "index_s": round(t2 - t1, 3), "kernels": kernels_of(stats), "roofline": roofline_of(stats, "load"),
+           "cpu_baseline": None, "atoms": int(db.stats().n_atoms)}
+    if not args.no_cpu_baseline:
+        # the oracle's CanonicalParser restatement (parse + md5 of every atom), one core
+        from das_amd import loader
+        from oracle import das_oracle as O
+        small = synthetic.to_canonical(synthetic.flybase_kb(4000, 20, 4000))
+        t = time.perf_counter()
+        reps = 0
+        while True:
+            kb = O.KB.from_arrays(loader.parse_canonical(small).finish())
+            reps += 1
+            if time.perf_counter() - t > args.cpu_baseline_seconds:
+                break
+        dt = time.perf_counter() - t
+        n = len(kb.links)
+        out["cpu_baseline"] = {"value": n * reps / dt, "unit": "links/s", "cores": 1, "kind": "port",
+                               "sample": f"loader.parse_canonical + oracle md5 hashing of a {len(small)} B "
+                                         f"FlyBase-shaped text ({n} links), {reps} passes in {dt:.1f} s"}
+    print(json.dumps(out))
 
 
 def main():
@@ -307,6 +383,11 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+    if args.workload == "load":
+        run_load(args, rank, world, local_rank)
+        if dist:
+            dist.destroy_process_group()
+        return
     if args.workload == "build":
         run_build(args, rank, world, dist, local_rank)
         if dist:
@@ -393,7 +474,7 @@ def main():
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "u32", "data": data, "config": cfg,
-            "roofline": roofline_of(stats),
+            "roofline": roofline_of(stats, args.workload),
             "cpu_baseline": cpu,
             "kernels": kernels_of(stats),
             "build_s": round(t_build, 2),

@@ -18,6 +18,7 @@ TABLE_UNORDERED = 1
 TABLE_COMPOSITE = 2
 
 ERR_INVALID, ERR_HIP, ERR_NOT_BUILT, ERR_UNSUPPORTED, ERR_INTERNAL, ERR_ATTRIBUTE = -1, -2, -3, -4, -5, -6
+ERR_SYNTAX = -7
 
 
 class DasNativeError(RuntimeError):
@@ -108,6 +109,10 @@ _SIGS = {
     "das_partition": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P), P]),
     "das_table_export_rows": (C.c_int, [P, P, P]),
     "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
+    "das_parse_canonical": (C.c_int, [P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "das_parsed_atoms": (C.c_int, [P, C.POINTER(das_atoms_t), C.POINTER(P)]),
+    "das_parsed_type_name": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]),
+    "das_parsed_free": (C.c_int, [P]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
@@ -147,11 +152,59 @@ def check(rc, ctx=None):
             raise NotImplementedError(msg)
         if rc == ERR_ATTRIBUTE:
             raise AttributeError(msg)
+        if rc == ERR_SYNTAX:
+            raise AssertionError(msg)
         raise DasNativeError(rc, msg)
 
 
 def ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ---------------------------------------------------------------------------
+# canonical MeTTa reader (host C++, canonical.cpp)
+# ---------------------------------------------------------------------------
+
+def parse_canonical(texts, threads=0):
+    """Canonical MeTTa text(s) -> loader.AtomArrays through das_parse_canonical
+    (CanonicalParser.parse, canonical_parser.py:242-365).  Each text is one
+    file with its own typedef / terminal / expression sections."""
+    from .loader import AtomArrays
+    if isinstance(texts, (str, bytes)):
+        texts = [texts]
+    bufs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+    n = len(bufs)
+    arr = (C.c_char_p * max(n, 1))(*bufs)
+    lens = np.array([len(b) for b in bufs] or [0], dtype=np.uint64)
+    h = P()
+    check(lib().das_parse_canonical(C.cast(arr, P), ptr(lens), n, int(threads), C.byref(h)))
+    try:
+        a = das_atoms_t()
+        ns = P()
+        check(lib().das_parsed_atoms(h, C.byref(a), C.byref(ns)))
+
+        def take(p, count, dt):
+            if not count:
+                return np.zeros(0, dtype=dt)
+            addr = p.value if isinstance(p, P) else p
+            buf = (C.c_char * (count * np.dtype(dt).itemsize)).from_address(addr)
+            return np.frombuffer(buf, dtype=dt).copy()
+
+        nl, ne, ng = int(a.n_leaf), int(a.n_expr), int(a.n_levels)
+        leaf_off = take(a.leaf_off, nl + 1, np.uint64)
+        expr_off = take(a.expr_off, ne + 1, np.uint64)
+        names = []
+        for i in range(int(a.n_types)):
+            sp, ln = C.c_char_p(), C.c_uint64()
+            check(lib().das_parsed_type_name(h, i, C.byref(sp), C.byref(ln)))
+            names.append(C.string_at(sp, ln.value).decode("utf-8"))
+        return AtomArrays(take(a.leaf_bytes, int(leaf_off[-1]), np.uint8), leaf_off,
+                          take(a.leaf_kind, nl, np.uint8), take(a.leaf_ctype, nl, np.uint32),
+                          take(a.leaf_type_id, nl, np.uint32), take(ns, nl, np.uint32), expr_off,
+                          take(a.expr_child, int(expr_off[-1]), np.uint32), take(a.expr_kind, ne, np.uint8),
+                          take(a.expr_ctype_leaf, ne, np.int32), take(a.level_off, ng + 1, np.uint64), names)
+    finally:
+        lib().das_parsed_free(h)
 
 
 # ---------------------------------------------------------------------------

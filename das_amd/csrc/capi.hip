@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "canonical.h"
 #include "das_internal.h"
 #include "md5.h"
 
@@ -19,6 +20,9 @@ struct das_ctx {
 };
 struct das_table {
   Table t;
+};
+struct das_parsed {
+  std::unique_ptr<das::Parsed> p;
 };
 
 namespace {
@@ -225,6 +229,51 @@ int das_hash_strings_dev(das_ctx_t* ctx, const uint8_t* d_bytes, const uint64_t*
 
 int das_hash_fixed_dev(das_ctx_t* ctx, const uint32_t* d_elems, uint32_t k, uint64_t n, uint32_t* d_out) {
   return guarded(ctx, [&] { das::hash_fixed((const Digest*)d_elems, k, n, (Digest*)d_out, ctx->c.s); });
+}
+
+int das_parse_canonical(const char* const* texts, const uint64_t* lens, uint32_t n_texts, uint32_t n_threads,
+                        das_parsed_t** out) {
+  return guarded(nullptr, [&] {
+    DAS_CHECK(out && (n_texts == 0 || (texts && lens)), das::DAS_E_INVALID, "null argument");
+    auto p = das::parse_canonical(texts, lens, n_texts, n_threads);
+    *out = new das_parsed{std::move(p)};
+  });
+}
+
+int das_parsed_atoms(const das_parsed_t* p, das_atoms_t* a, const uint32_t** name_start) {
+  return guarded(nullptr, [&] {
+    DAS_CHECK(p && a, das::DAS_E_INVALID, "null argument");
+    const das::Parsed& x = *p->p;
+    a->n_leaf = x.leaf_kind.size();
+    a->leaf_bytes = x.leaf_bytes.data();
+    a->leaf_off = x.leaf_off.data();
+    a->leaf_kind = x.leaf_kind.data();
+    a->leaf_ctype = x.leaf_ctype.data();
+    a->leaf_type_id = x.leaf_type_id.data();
+    a->n_expr = x.expr_kind.size();
+    a->expr_off = x.expr_off.data();
+    a->expr_child = x.expr_child.data();
+    a->expr_kind = x.expr_kind.data();
+    a->expr_ctype_leaf = x.expr_ctype_leaf.data();
+    a->n_levels = (uint32_t)(x.level_off.size() - 1);
+    a->level_off = x.level_off.data();
+    a->n_types = (uint32_t)x.type_names.size();
+    if (name_start) *name_start = x.name_start.data();
+  });
+}
+
+int das_parsed_type_name(const das_parsed_t* p, uint32_t type_id, const char** name, uint64_t* len) {
+  return guarded(nullptr, [&] {
+    DAS_CHECK(p && name && len, das::DAS_E_INVALID, "null argument");
+    DAS_CHECK(type_id < p->p->type_names.size(), das::DAS_E_INVALID, "type id out of range");
+    *name = p->p->type_names[type_id].data();
+    *len = p->p->type_names[type_id].size();
+  });
+}
+
+int das_parsed_free(das_parsed_t* p) {
+  delete p;
+  return DAS_OK;
 }
 
 int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms) {

@@ -25,6 +25,7 @@ enum Status : int {
   DAS_E_UNSUPPORTED = -4, // shape outside this build       -> NotImplementedError
   DAS_E_INTERNAL = -5,
   DAS_E_ATTRIBUTE = -6,   // the reference raises AttributeError here -> AttributeError
+  DAS_E_SYNTAX = -7,      // malformed input where the reference asserts -> AssertionError
 };
 
 #define DAS_HIP(expr)                                                              \

@@ -116,7 +116,8 @@ class HipDB(RelationalDB):
         self.load_arrays(_loader.parse_metta(texts).finish())
 
     def load_canonical(self, texts):
-        self.load_arrays(_loader.parse_canonical(texts).finish())
+        """Canonical MeTTa through the native reader (das_parse_canonical)."""
+        self.load_arrays(_lib.parse_canonical(texts))
 
     def clear(self):
         b = _loader.AtomBuilder()

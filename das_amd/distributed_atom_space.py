@@ -11,6 +11,7 @@ import os
 from enum import Enum, auto
 from typing import Dict, List, Tuple, Union
 
+from . import _lib
 from . import loader as _loader
 from .database.db_interface import WILDCARD
 from .database.hip_db import HipDB
@@ -53,12 +54,14 @@ class DistributedAtomSpace:
         return answer
 
     def _rebuild(self):
-        b = _loader.AtomBuilder()
+        # canonical files through the native reader (canonical.cpp), general
+        # MeTTa through the Python MettaYacc restatement, one device index
+        parts = []
         if self._canonical_sources:
-            _loader.parse_canonical(self._canonical_sources, b)
-        if self._metta_sources:
-            _loader.parse_metta(self._metta_sources, b)
-        self.db.load_arrays(b.finish())
+            parts.append(_lib.parse_canonical(self._canonical_sources))
+        if self._metta_sources or not parts:
+            parts.append(_loader.parse_metta(self._metta_sources).finish())
+        self.db.load_arrays(_loader.concat_arrays(parts))
 
     def load_knowledge_base(self, source):
         """distributed_atom_space.py:336-363 (general MeTTa)."""

@@ -305,7 +305,12 @@ def _canonical_expression(line, b):
     while i < n:
         c = line[i]
         if c == '"':
-            j = line.index('"', i + 1)
+            # closing quote: the first '"' not preceded by a backslash (canonical_parser.py:287)
+            j = i + 1
+            while j < n and not (line[j] == '"' and line[j - 1] != "\\"):
+                j += 1
+            if j >= n:
+                raise SyntaxError(f"unterminated string: {line[:80]}")
             parts = line[i + 1:j].split()
             stype, name = parts[0], " ".join(parts[1:])
             stack.append(b.terminal(stype, name, node=False))
@@ -341,6 +346,9 @@ def _canonical_expression(line, b):
         raise SyntaxError(f"unbalanced canonical line: {line[:80]}")
 
 
+_LINE_BREAK = re.compile(r"\r\n|\r|\n")
+
+
 def parse_canonical(texts, builder=None):
     """Canonical MeTTa -> AtomBuilder (canonical_parser.py:315-365)."""
     if isinstance(texts, str):
@@ -348,7 +356,7 @@ def parse_canonical(texts, builder=None):
     b = builder or AtomBuilder()
     for text in texts:
         state = 0
-        for raw in text.splitlines():
+        for raw in _LINE_BREAK.split(text):      # universal newlines, as `for line in file`
             line = raw.strip()
             if not line:
                 continue
@@ -372,6 +380,87 @@ def parse_canonical(texts, builder=None):
                     raise SyntaxError(f"bad canonical expression line: {line[:80]}")
                 _canonical_expression(line, b)
     return b
+
+
+def _nesting_levels(p):
+    """1 + the deepest expression child, per expression (groups are children-first)."""
+    lev = np.zeros(p.n_expr, dtype=np.int64)
+    for g in range(len(p.level_off) - 1):
+        b, e = int(p.level_off[g]), int(p.level_off[g + 1])
+        if e <= b:
+            continue
+        k = int(p.expr_off[b + 1] - p.expr_off[b])
+        ch = p.expr_child[int(p.expr_off[b]):int(p.expr_off[e])].reshape(e - b, k).astype(np.int64)
+        sub = np.where(ch >= p.n_leaf, lev[np.maximum(ch - p.n_leaf, 0)], 0)
+        lev[b:e] = 1 + sub.max(axis=1)
+    return lev
+
+
+def concat_arrays(parts):
+    """One AtomArrays from several (e.g. the native canonical reader's output
+    and a MeTTa builder's): leaves are appended (the device interns repeats by
+    digest), named types are merged by name, expression groups are re-formed
+    by (level, number of children) keeping each part's order."""
+    parts = [p for p in parts if p is not None]
+    if len(parts) == 1:
+        return parts[0]
+    names, tid = [], {}
+    leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start = [], [], [], [], [], []
+    e_child, e_nch, e_level, e_kind, e_ctl, e_part_pos = [], [], [], [], [], []
+    leaf_base, byte_base = 0, 0
+    total_leaf = sum(p.n_leaf for p in parts)
+    expr_base = 0
+    for p in parts:
+        remap = np.array([tid.setdefault(n, len(tid)) for n in p.type_names], dtype=np.uint32)
+        names = sorted(tid, key=tid.get)
+        ltid = p.leaf_type_id.copy()
+        m = ltid != NONE
+        ltid[m] = remap[ltid[m]]
+        leaf_bytes.append(p.leaf_bytes)
+        leaf_off.append(p.leaf_off[:-1] + np.uint64(byte_base))
+        leaf_kind.append(p.leaf_kind)
+        leaf_ctype.append(p.leaf_ctype + np.uint32(leaf_base))
+        leaf_type_id.append(ltid)
+        name_start.append(p.name_start)
+        nch = np.diff(p.expr_off.astype(np.int64))
+        lev = _nesting_levels(p)
+        ch = p.expr_child.astype(np.int64)
+        is_expr = ch >= p.n_leaf
+        ch = np.where(is_expr, ch - p.n_leaf + total_leaf + expr_base, ch + leaf_base)
+        e_child.append(ch)
+        e_nch.append(nch)
+        e_level.append(lev)
+        e_kind.append(p.expr_kind)
+        ctl = p.expr_ctype_leaf.astype(np.int64)
+        e_ctl.append(np.where(ctl >= 0, ctl + leaf_base, -1))
+        leaf_base += p.n_leaf
+        byte_base += int(p.leaf_off[-1])
+        expr_base += p.n_expr
+    nch = np.concatenate(e_nch)
+    lev = np.concatenate(e_level)
+    n_expr = len(nch)
+    order = np.lexsort((np.arange(n_expr), nch, lev))
+    newpos = np.empty(n_expr, dtype=np.int64)
+    newpos[order] = np.arange(n_expr)
+    old_off = np.zeros(n_expr + 1, dtype=np.int64)
+    np.cumsum(nch, out=old_off[1:])
+    ch = np.concatenate(e_child)
+    ch = np.where(ch >= total_leaf, newpos[np.maximum(ch - total_leaf, 0)] + total_leaf, ch)
+    expr_off = np.zeros(n_expr + 1, dtype=np.uint64)
+    np.cumsum(nch[order], out=expr_off[1:])
+    idx = np.concatenate([np.arange(old_off[j], old_off[j + 1]) for j in order]) if n_expr else np.zeros(0, np.int64)
+    groups = [0]
+    for k in range(1, n_expr):
+        a, b = order[k - 1], order[k]
+        if lev[a] != lev[b] or nch[a] != nch[b]:
+            groups.append(k)
+    if n_expr:
+        groups.append(n_expr)
+    off = np.concatenate(leaf_off + [np.array([byte_base], dtype=np.uint64)])
+    return AtomArrays(np.concatenate(leaf_bytes), off, np.concatenate(leaf_kind), np.concatenate(leaf_ctype),
+                      np.concatenate(leaf_type_id), np.concatenate(name_start), expr_off,
+                      ch[idx].astype(np.uint32), np.concatenate(e_kind)[order],
+                      np.concatenate(e_ctl)[order].astype(np.int32), np.array(groups, dtype=np.uint64), names)
 
 
 # ---------------------------------------------------------------------------

@@ -191,6 +191,39 @@ def flybase_kb(n_genes=200_000, n_schema=60, rows_per_schema=400_000, n_loc=5_00
     return arrays
 
 
+def to_canonical(arrays):
+    """Canonical MeTTa text of an AtomArrays KB (the format CanonicalParser
+    reads, canonical_parser.py:315-365): typedefs, declared terminals (the
+    node leaves), then one line per top-level expression."""
+    nl, ne = arrays.n_leaf, arrays.n_expr
+    off, ch = arrays.expr_off, arrays.expr_child
+    leaf = [bytes(arrays.leaf_bytes[int(arrays.leaf_off[i]):int(arrays.leaf_off[i + 1])]).decode()
+            for i in range(nl)]
+    out = [f"(: {t} Type)" for t in arrays.type_names]
+    for i in range(nl):
+        if arrays.leaf_kind[i] == LEAF_NODE:
+            ns = int(arrays.name_start[i])
+            out.append(f'(: "{leaf[i][ns:]}" {leaf[i][:ns - 1]})')
+    nested = np.zeros(ne, dtype=bool)
+    kids = ch[ch >= nl].astype(np.int64) - nl
+    nested[kids[:]] = True
+    # every expression's first child is its type leaf, except those whose
+    # parent marks them as nested (they print inline)
+
+    def render(j):
+        c = ch[int(off[j]):int(off[j + 1])]
+        parts = [leaf[int(c[0])]]
+        for x in c[1:]:
+            x = int(x)
+            parts.append(render(x - nl) if x >= nl else f'"{leaf[x]}"')
+        return "(" + " ".join(parts) + ")"
+
+    for j in range(ne):
+        if not nested[j] and arrays.expr_kind[j] != 2:
+            out.append(render(j))
+    return "\n".join(out) + "\n"
+
+
 def _leaf_name(arrays, i):
     a, b = int(arrays.leaf_off[i]), int(arrays.leaf_off[i + 1])
     return bytes(arrays.leaf_bytes[a + int(arrays.name_start[i]):b]).decode()

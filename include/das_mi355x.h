@@ -38,6 +38,7 @@ typedef struct das_table das_table_t;
 #define DAS_ERR_UNSUPPORTED (-4)
 #define DAS_ERR_INTERNAL (-5)
 #define DAS_ERR_ATTRIBUTE (-6)  /* where the reference raises AttributeError (:359-360) */
+#define DAS_ERR_SYNTAX (-7)     /* malformed input where the reference asserts (canonical_parser.py:307-310) */
 
 #define DAS_NONE 0xFFFFFFFFu   /* "no atom / wildcard" id */
 
@@ -96,6 +97,21 @@ typedef struct {
   const uint64_t* level_off;       /* n_levels + 1, expression ranges per nesting level */
   uint32_t n_types;
 } das_atoms_t;
+
+/* ---- canonical MeTTa reader (host, multi-threaded) ----------------------- */
+/* Parses n_texts canonical files -- `(: Name Type)` typedefs, `(: "name" Type)`
+ * terminals, then one `(Type "T name" (Type ...) ...)` expression per line --
+ * into the das_atoms_t layout (CanonicalParser.parse / _parse_expression,
+ * canonical_parser.py:242-365).  n_threads 0 = up to 16.  Syntax errors return
+ * DAS_ERR_SYNTAX with "line N: ..." in das_last_error(NULL). */
+typedef struct das_parsed das_parsed_t;
+int das_parse_canonical(const char* const* texts, const uint64_t* lens, uint32_t n_texts, uint32_t n_threads,
+                        das_parsed_t** out);
+/* Views into the parsed arrays (valid until das_parsed_free); name_start[i] is
+ * the byte offset of a terminal's name inside its "Type name" leaf string. */
+int das_parsed_atoms(const das_parsed_t* p, das_atoms_t* atoms, const uint32_t** name_start);
+int das_parsed_type_name(const das_parsed_t* p, uint32_t type_id, const char** name, uint64_t* len);
+int das_parsed_free(das_parsed_t* p);
 
 typedef struct {
   uint64_t n_atoms, n_nodes, n_links, n_types, n_ctypes;
