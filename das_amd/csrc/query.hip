@@ -1089,7 +1089,8 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   out->nrows = total;
   if (total) {
     // algorithmic bytes: probe payload + build payload + output
-    ProfScope ps(c, "k_dj_write", 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
+    ProfScope ps(c, balanced ? "k_dj_write_bal" : "k_dj_write",
+                 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
     dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, (const uint2*)lc.p, units, (const uint64_t*)toff.p, jc,
              out->data, out->cap, total, balanced);
     DAS_HIP(hipGetLastError());
