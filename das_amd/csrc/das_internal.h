@@ -32,9 +32,11 @@ __host__ __device__ inline uint8_t cat_of_prio(uint32_t p) {
 struct RowTable {
   int arity = 0;
   uint64_t rows = 0;
+  uint64_t ld = 0;                 // column stride: rows rounded up to 64 (16-byte aligned columns)
   uint32_t* data = nullptr;
-  uint32_t* col(int c) const { return data + (uint64_t)c * rows; }
+  uint32_t* col(int c) const { return data + (uint64_t)c * ld; }
 };
+inline uint64_t col_stride(uint64_t rows) { return (rows + 63) & ~63ull; }
 
 // P_{a,p}: RowTable sorted by (t_p, type, link id) + unique keys -> row offsets.
 struct PosIndex {

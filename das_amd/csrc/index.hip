@@ -308,13 +308,13 @@ __global__ void k_pos_key(const uint32_t* type, const uint64_t* tgt_off, const u
 }
 
 // rows: col 0 = link id, col 1+k = target k
-__global__ void k_gather_rows(const uint32_t* ids, uint64_t R, uint32_t arity, const uint64_t* tgt_off,
+__global__ void k_gather_rows(const uint32_t* ids, uint64_t R, uint64_t ld, uint32_t arity, const uint64_t* tgt_off,
                               const uint32_t* tgt, uint32_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t id = ids[i];
     out[i] = id;
     const uint64_t o = tgt_off[id];
-    for (uint32_t k = 0; k < arity; ++k) out[(uint64_t)(k + 1) * R + i] = tgt[o + k];
+    for (uint32_t k = 0; k < arity; ++k) out[(uint64_t)(k + 1) * ld + i] = tgt[o + k];
   }
 }
 
@@ -451,7 +451,7 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
     const uint64_t b = to[ty], e = to[ty + 1];
     if (e <= b) continue;
     hipLaunchKernelGGL(k_seg_minmax, dim3(grid_for(e - b, 256, 1024)), dim3(256), 0, s, (const uint32_t*)t.data,
-                       t.rows, ncol, b, e, d.p + ty * ncol * 2);
+                       t.ld, ncol, b, e, d.p + ty * ncol * 2);
   }
   DAS_HIP(hipGetLastError());
   if (nb) DAS_HIP(hipMemcpyAsync(h.data(), d.p, 4 * nb, hipMemcpyDeviceToHost, s));
@@ -748,8 +748,9 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       RowTable& t = idx.ttab[ar];
       t.arity = (int)ar;
       t.rows = R;
-      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
-      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+      t.ld = col_stride(R);
+      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * t.ld);
+      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
                          (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
       // host type offsets
       uint32_t* ukey; uint64_t* uoff;
@@ -779,8 +780,9 @@ void build_index(Ctx& c, const das_atoms_t& a) {
       RowTable& t = idx.ctab[ar];
       t.arity = (int)ar;
       t.rows = R;
-      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
-      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+      t.ld = col_stride(R);
+      t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * t.ld);
+      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
                          (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
       uint32_t* ukey; uint64_t* uoff;
       const uint64_t m = rle<uint32_t>(key.p, R, &ukey, &uoff, idx, s);
@@ -805,8 +807,9 @@ void build_index(Ctx& c, const das_atoms_t& a) {
         PosIndex& P = idx.pidx[ar][p];
         P.t.arity = (int)ar;
         P.t.rows = R;
-        P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * R);
-        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, ar,
+        P.t.ld = col_stride(R);
+        P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * P.t.ld);
+        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, P.t.ld, ar,
                            (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, P.t.data);
         P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
       }

@@ -138,22 +138,39 @@ __global__ void __launch_bounds__(B) k_scan_write(ScanSpec sp, uint64_t begin, u
 }
 
 // Pure projection (a scan with no predicate): out column c = source column
-// outpos[c] over [begin, end).  16-byte loads/stores where alignment allows.
+// outpos[c] over [begin, end).  Output columns are 16-byte aligned (table
+// column strides are multiples of 64 rows); a source column is too when
+// `begin` is a multiple of 4, then 16-byte lanes, two in flight per thread;
+// otherwise 4-byte lanes, four in flight (each load instruction still covers
+// 256 contiguous bytes per wave).
 __global__ void __launch_bounds__(B) k_project(ScanSpec sp, uint64_t begin, uint64_t n, uint32_t* out, uint64_t cap) {
   const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint32_t c = 0; c < sp.nout; ++c) {
-    const uint32_t* src = sp.col[1 + sp.outpos[c]] + begin;
-    uint32_t* dst = out + c * cap;
-    const bool vec = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
-    if (vec) {
+    const uint32_t* __restrict__ src = sp.col[1 + sp.outpos[c]] + begin;
+    uint32_t* __restrict__ dst = out + c * cap;
+    if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0) {
       const uint64_t n4 = n >> 2;
       const uint4* s4 = reinterpret_cast<const uint4*>(src);
       uint4* d4 = reinterpret_cast<uint4*>(dst);
-      for (uint64_t i = tid; i < n4; i += stride) d4[i] = s4[i];
-      for (uint64_t i = (n4 << 2) + tid; i < n; i += stride) dst[i] = src[i];
+      uint64_t i = tid;
+      for (; i + stride < n4; i += 2 * stride) {
+        const uint4 a = s4[i], b = s4[i + stride];
+        d4[i] = a;
+        d4[i + stride] = b;
+      }
+      if (i < n4) d4[i] = s4[i];
+      for (uint64_t j = (n4 << 2) + tid; j < n; j += stride) dst[j] = src[j];
     } else {
-      for (uint64_t i = tid; i < n; i += stride) dst[i] = src[i];
+      uint64_t i = tid;
+      for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint32_t a = src[i], b = src[i + stride], x = src[i + 2 * stride], y = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = x;
+        dst[i + 3 * stride] = y;
+      }
+      for (; i < n; i += stride) dst[i] = src[i];
     }
   }
 }
@@ -683,7 +700,7 @@ std::unique_ptr<Table> new_table(Ctx& c, int kind, int ncols, const int32_t* var
     t->hi[i] = kNone;
   }
   t->s = c.s;
-  t->cap = cap ? cap : 1;
+  t->cap = col_stride(cap ? cap : 1);      // 16-byte aligned columns
   if (ncols) t->data = (uint32_t*)cache_alloc(4ull * ncols * t->cap, c.s);
   return t;
 }
@@ -753,7 +770,7 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
     t->nrows = n;
     if (!sp.unordered) {   // pure projection
       ProfScope ps(c, "k_project", 8.0 * sp.nout * n);
-      hipLaunchKernelGGL(k_project, dim3(grid_for(n / 4 + 1, B, 2048)), dim3(B), 0, c.s, sp, begin, n, t->data, t->cap);
+      hipLaunchKernelGGL(k_project, dim3(grid_for(n / 8 + 1, B, 8192)), dim3(B), 0, c.s, sp, begin, n, t->data, t->cap);
       DAS_HIP(hipGetLastError());
       return t;
     }

@@ -211,6 +211,14 @@ def test_gpu_facade_readme_examples():
                  Not(inh(Variable("$1"), Node("Concept", "mammal")))]),
             inh(Node("Concept", "human"), Variable("$2"))])
     assert q.matched(das.db, ans) and len(ans.assignments) == 4
+    # the service's query string (scripts/service_regression_test.sh:52-59) through _parse_query
+    from das_amd.service import _parse_query
+    assert das.query(_parse_query("Node n1 Concept human, Link Inheritance n1 $2")) == \
+        "{{'$2': 'bdfe4e7a431f73386f37c6448afe5840'}}"
+    q = _parse_query("Node m Concept mammal, Link Inheritance $1 $2, Link Inheritance $2 $3, AND, "
+                     "Link Inheritance $1 m, NOT, AND")
+    ans = PatternMatchingAnswer()
+    assert q.matched(das.db, ans) and len(ans.assignments) == 3        # service/README.md:316-337
     assert sorted(das.get_links("Inheritance", None, ["*", "bdfe4e7a431f73386f37c6448afe5840"])) == sorted(
         das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"]) and
         [h for h, _ in das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"])])
