@@ -110,6 +110,7 @@ _SIGS = {
     "das_table_export_rows": (C.c_int, [P, P, P]),
     "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_parse_canonical": (C.c_int, [P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "das_export_keyspace": (C.c_int, [P, C.c_char_p, P]),
     "das_parsed_atoms": (C.c_int, [P, C.POINTER(das_atoms_t), C.POINTER(P)]),
     "das_parsed_type_name": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]),
     "das_parsed_free": (C.c_int, [P]),
@@ -335,6 +336,13 @@ class Context:
             n_types=len(a.type_names))
         check(lib().das_build_index(self.h, C.byref(s)), self.h)
         del keep
+
+    def export_keyspace(self, directory):
+        """Redis key-space files of the index (das_export_keyspace) -> line counts."""
+        counts = np.zeros(5, dtype=np.uint64)
+        check(lib().das_export_keyspace(self.h, str(directory).encode(), ptr(counts)), self.h)
+        return dict(zip(("outgoing_set", "incomming_set", "patterns", "templates", "names"),
+                        (int(x) for x in counts)))
 
     def stats(self):
         st = das_index_stats_t()

@@ -276,6 +276,20 @@ int das_parsed_free(das_parsed_t* p) {
   return DAS_OK;
 }
 
+int das_export_keyspace(das_ctx_t* ctx, const char* dir, uint64_t counts[5]) {
+  return guarded(ctx, [&] {
+    DAS_CHECK(dir, das::DAS_E_INVALID, "null directory");
+    const das::ExportCounts n = das::export_keyspace(ctx->c, dir);
+    if (counts) {
+      counts[0] = n.outgoing;
+      counts[1] = n.incoming;
+      counts[2] = n.patterns;
+      counts[3] = n.templates;
+      counts[4] = n.names;
+    }
+  });
+}
+
 int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms) {
   if (!ctx || !atoms) return fail(ctx, DAS_ERR_INVALID, "null argument");
   return guarded(ctx, [&] { das::build_index(ctx->c, *atoms); });

@@ -78,6 +78,8 @@ struct Index {
   // offsets array from it without a device round trip).
   std::array<std::vector<uint32_t>, kMaxArity + 1> tbound, gbound;
   std::vector<Digest> ctype_digest;                            // host: sorted ctype digests
+  std::vector<Digest> type_digest;                             // host: md5(type name) per named type
+  std::vector<uint32_t> type_name_len;                         // host: bytes of each type name
   std::vector<CtypeRange> ctype_range;                         // host
   std::vector<void*> owned;                                    // device allocations
   std::map<std::array<uint64_t, 4>, std::pair<uint64_t, uint64_t>> range_cache;   // P lookups
@@ -211,6 +213,12 @@ std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars
 void export_rows(Ctx& c, const Table& t, uint32_t* dst);
 std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
                                    const uint32_t* src, uint64_t n);
+
+// export.hip: Redis key-space files (canonical_parser.py:119-183)
+struct ExportCounts {
+  uint64_t outgoing = 0, incoming = 0, patterns = 0, templates = 0, names = 0;
+};
+ExportCounts export_keyspace(Ctx& c, const std::string& dir);
 
 // composite.hip: Unordered / Composite assignment algebra (pattern_matcher.py:158-368)
 std::unique_ptr<Table> theta_join(Ctx& c, const Table& a, const Table& b, int no_overload);

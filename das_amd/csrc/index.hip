@@ -18,6 +18,7 @@
 // 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
 #include <optional>
 #include "das_internal.h"
+#include "md5.h"
 
 namespace das {
 
@@ -529,6 +530,16 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   // host copies for metadata (node names)
   c.leaf_bytes.assign(a.leaf_bytes, a.leaf_bytes + n_bytes);
   c.leaf_off.assign(a.leaf_off, a.leaf_off + nl + 1);
+  // named types: md5(name) (named_type_hash, expression_hasher.py:13-14) and name length
+  idx.type_digest.assign(a.n_types, Digest{});
+  idx.type_name_len.assign(a.n_types, 0);
+  for (uint64_t i = 0; i < nl; ++i) {
+    const uint32_t t = a.leaf_type_id[i];
+    if (t == kNone || t >= a.n_types) continue;
+    const uint64_t b = a.leaf_off[i], e = a.leaf_off[i + 1];
+    md5::digest_bytes(a.leaf_bytes + b, e - b, idx.type_digest[t].w);
+    idx.type_name_len[t] = (uint32_t)(e - b);
+  }
 
   std::optional<ProfScope> up(std::in_place, c, "upload", (double)n_bytes + 8.0 * (nl + ne) + 4.0 * n_child + 13.0 * nl + 5.0 * ne);
   auto d_bytes = upload(a.leaf_bytes, n_bytes, s);

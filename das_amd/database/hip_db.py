@@ -11,6 +11,7 @@ Two extra, non-reference entry points feed the pattern matcher without
 materialising Python tuples: `match_link` and `match_template` return device
 binding tables (`Relation`).
 """
+import os
 import re
 from typing import Any, List, Tuple
 
@@ -125,6 +126,13 @@ class HipDB(RelationalDB):
 
     def stats(self):
         return self.ctx.stats()
+
+    def export_keyspace(self, directory):
+        """Writes the Redis key-value files of the reference's loader
+        (outgoing_set / incomming_set / patterns / templates / names,
+        canonical_parser.py:119-183) for the loaded KB into `directory`."""
+        os.makedirs(directory, exist_ok=True)
+        return self.ctx.export_keyspace(directory)
 
     # --------------------------------------------------------------- helpers
     def _resolve(self, handles):

@@ -98,6 +98,13 @@ typedef struct {
   uint32_t n_types;
 } das_atoms_t;
 
+/* ---- Redis key-space export ---------------------------------------------- */
+/* Writes outgoing_set.txt, incomming_set.txt, patterns.txt, templates.txt and
+ * names.txt into `dir`: the key-value files CanonicalParser builds before it
+ * populates Redis (canonical_parser.py:119-183, key_value_file.py:8-16), lines
+ * sorted bytewise.  counts (optional) = lines per file in that order. */
+int das_export_keyspace(das_ctx_t* ctx, const char* dir, uint64_t counts[5]);
+
 /* ---- canonical MeTTa reader (host, multi-threaded) ----------------------- */
 /* Parses n_texts canonical files -- `(: Name Type)` typedefs, `(: "name" Type)`
  * terminals, then one `(Type "T name" (Type ...) ...)` expression per line --

@@ -134,6 +134,34 @@ def _pattern_keys(type_hash, elements):
     return keys
 
 
+def keyspace_lines(kb):
+    """The key-value files CanonicalParser writes before populating Redis
+    (canonical_parser.py:119-183 via key_value_file.py:8-16), as sorted line
+    lists: outgoing / incoming sets, patterns (the reference's key list per
+    arity, including the [*, e...] key it appends twice for arities 1-3),
+    templates (composite type hash and named type hash) and names."""
+    out = {"outgoing_set": [], "incomming_set": [], "patterns": [], "templates": [], "names": []}
+    for h, (t, targets, ct) in kb.links.items():
+        for x in targets:                                     # :139-143
+            out["outgoing_set"].append(f"{h}\t{x}")
+            out["incomming_set"].append(f"{x}\t{h}")
+        th = named_type_hash(t)
+        arity = len(targets)
+        keys = [[WILDCARD, *targets]]                         # :145
+        if 1 <= arity <= 3:                                   # :146-175, every mask with >= 1 wildcard
+            for mask in range(1, 1 << (arity + 1)):
+                keys.append([WILDCARD if mask & 1 else th] +
+                            [WILDCARD if mask >> (i + 1) & 1 else e for i, e in enumerate(targets)])
+        value = "\t".join([h, *targets])
+        for k in keys:                                        # :176-177
+            out["patterns"].append(f"{composite_hash(k)}\t{value}")
+        out["templates"].append(f"{ct}\t{value}")            # :179-180
+        out["templates"].append(f"{th}\t{value}")
+    for h, (_, name) in kb.nodes.items():                     # :119-121
+        out["names"].append(f"{h}\t{name}")
+    return {k: sorted(v) for k, v in out.items()}
+
+
 class RedisMongoSemantics:
     """Restatement of RedisMongoDB over an in-memory KB."""
 

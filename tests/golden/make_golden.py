@@ -599,6 +599,18 @@ def main():
         das = load_canonical(os.path.join(REF, "data/samples/canonical_toy-example-mining.metta"))
         write("kb_toy_mining.json", kb_fixture("toy_mining", das, toy_mining_queries(), None,
                                                "data/samples/canonical_toy-example-mining.metta"))
+    if "kv_toy_mining" in which:
+        # the key-value files CanonicalParser writes before populating Redis
+        # (canonical_parser.py:132-183, key_value_file.py:8-16), sorted by the
+        # reference's own `sort` call: the byte-level target of das_export_keyspace
+        load_canonical(os.path.join(REF, "data/samples/canonical_toy-example-mining.metta"))
+        out_dir = os.path.join(HERE, "kv_toy_mining")
+        os.makedirs(out_dir, exist_ok=True)
+        for name in ("outgoing_set", "incomming_set", "patterns", "templates", "names"):
+            with open(os.path.join(SCRATCH, f"parser_{name}.txt")) as f:
+                lines = sorted(l.rstrip("\n") for l in f if l.strip())
+            with open(os.path.join(out_dir, f"{name}.txt"), "w") as f:
+                f.write("".join(l + "\n" for l in lines))
     if "stub_like" in which:
         p = os.path.join(SCRATCH, "stub_like.metta")
         with open(p, "w") as f:

@@ -461,3 +461,50 @@ def test_gpu_facade_canonical_file(golden):
                                                    "canonical_toy-example-mining.metta"))
     d = golden("kb_toy_mining.json")
     assert das.count_atoms() == (len(d["nodes"]), len(d["links"]))
+
+
+def _read_lines(path):
+    with open(path) as f:
+        return [l.rstrip("\n") for l in f if l.strip()]
+
+
+def test_gpu_keyspace_export_matches_reference_files(tmp_path):
+    """das_export_keyspace on the canonical toy KB reproduces, byte for byte
+    (after the reference's own sort), the key-value files the reference's
+    CanonicalParser wrote (tests/golden/kv_toy_mining, make_golden.py)."""
+    from das_amd.database.hip_db import HipDB
+    db = HipDB(device=0)
+    with open(os.path.join(DATA, "canonical_toy-example-mining.metta")) as f:
+        db.load_canonical(f.read())
+    counts = db.export_keyspace(str(tmp_path))
+    base = os.path.join(os.path.dirname(__file__), "golden", "kv_toy_mining")
+    for name, n in counts.items():
+        got = _read_lines(tmp_path / f"{name}.txt")
+        assert got == sorted(got), name                      # written in bytewise order
+        assert got == sorted(_read_lines(os.path.join(base, f"{name}.txt"))), name
+        assert n == len(got)
+
+
+@pytest.mark.parametrize("gen", ["powerlaw", "nested"])
+def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
+    """Arity 1-4 links, nested links, repeated targets: the export equals the
+    oracle's restatement of the reference's key-value files."""
+    from das_amd import loader, synthetic
+    from das_amd.database.hip_db import HipDB
+    if gen == "powerlaw":
+        arrays = synthetic.powerlaw_kb(120, 900, link_types=3, seed=4)
+    else:
+        b = loader.AtomBuilder()
+        n = [b.terminal("Concept", f"c{i}", True) for i in range(6)]
+        l1 = b.expr("List", [n[0], n[1]])
+        b.expr("Evaluation", [n[2], l1])
+        b.expr("Set", [n[3]])
+        b.expr("List", [n[0], n[1], n[2], n[3]])
+        b.expr("Inheritance", [n[4], n[4]])
+        b.expr("Member", [b.expr("List", [n[5], l1, n[5]]), n[1], n[2]])
+        arrays = b.finish()
+    db = _hipdb(arrays)
+    db.export_keyspace(str(tmp_path))
+    want = O.keyspace_lines(O.KB.from_arrays(arrays))
+    for name, lines in want.items():
+        assert _read_lines(tmp_path / f"{name}.txt") == lines, name

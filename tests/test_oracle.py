@@ -106,3 +106,17 @@ def test_readme_examples(golden):
     assert O.evaluate(q2, db)["n"] == 3
     assert O.evaluate(q3, db)["n"] == 4
     assert O.evaluate(["Link", "Similarity", False, [V("$1"), V("$2")]], db)["n"] == 7
+
+
+def test_oracle_keyspace_matches_reference_files(golden):
+    """keyspace_lines restates the key-value files the reference's
+    CanonicalParser wrote for the toy-mining KB (tests/golden/kv_toy_mining)."""
+    import os
+    d = golden("kb_toy_mining.json")
+    kb = O.KB.from_tables(d["nodes"], d["links"])
+    got = O.keyspace_lines(kb)
+    base = os.path.join(os.path.dirname(__file__), "golden", "kv_toy_mining")
+    for name, lines in got.items():
+        with open(os.path.join(base, f"{name}.txt")) as f:
+            want = sorted(l.rstrip("\n") for l in f if l.strip())
+        assert lines == want, name
