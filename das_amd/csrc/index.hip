@@ -308,6 +308,13 @@ __global__ void k_pos_key(const uint32_t* type, const uint64_t* tgt_off, const u
   }
 }
 
+// target q of each link in ids (the secondary key of P_{a,p})
+__global__ void k_tgt_key(const uint64_t* tgt_off, const uint32_t* tgt, const uint32_t* ids, uint64_t n, uint32_t q,
+                          uint32_t* key) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    key[i] = tgt[tgt_off[ids[i]] + q];
+}
+
 // rows: col 0 = link id, col 1+k = target k
 __global__ void k_gather_rows(const uint32_t* ids, uint64_t R, uint64_t ld, uint32_t arity, const uint64_t* tgt_off,
                               const uint32_t* tgt, uint32_t* out) {
@@ -810,9 +817,18 @@ void build_index(Ctx& c, const das_atoms_t& a) {
         DBuf<uint64_t> key(R, s);
         DBuf<uint32_t> perm(R, s);
         copy_dev(perm.p, ids.p, 4 * R, s);
+        if (ar >= 2) {
+          // secondary order by the first other target (LSD: least significant key
+          // first), so an anchored range of P_{a,p} comes out sorted by that
+          // target and can be a join's build side without a sort
+          DBuf<uint32_t> k2(R, s);
+          hipLaunchKernelGGL(k_tgt_key, G(R), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt,
+                             (const uint32_t*)perm.p, R, p == 0 ? 1u : 0u, k2.p);
+          radix_sort_pairs<uint32_t>(k2.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
+        }
         hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,
                            (const uint32_t*)idx.tgt, (const uint32_t*)perm.p, R, p, key.p);
-        // (type, t_p, id): sort by t_p, then (stable) by type; ids arrive in order
+        // (type, t_p, t_q, id): sort by t_p, then (stable) by type
         radix_sort_pairs<uint64_t>(key.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
         radix_sort_pairs<uint64_t>(key.p, perm.p, R, 32, 32 + std::max(1, tbits), s);
         PosIndex& P = idx.pidx[ar][p];
