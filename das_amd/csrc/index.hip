@@ -16,6 +16,7 @@
 // T_a ('*' type); a '*' type with grounded targets by one key range of P_{a,p}
 // per named type.  This covers exactly the families the reference writes for arity
 // 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
+#include <cstring>
 #include <optional>
 #include "das_internal.h"
 #include "md5.h"
@@ -45,36 +46,94 @@ __global__ void k_copy_u128(uint4* dst, const uint4* src, uint64_t n) {
 }
 
 namespace {
-// Pinned landing slot for scalar read-backs (a pageable destination costs a
-// staging copy: about twice the round trip).  One per host thread.
-uint64_t* pinned_slot() {
-  thread_local struct Slot {
-    uint64_t* p = nullptr;
-    Slot() { DAS_HIP(hipHostMalloc((void**)&p, 64, hipHostMallocDefault)); }
-    ~Slot() { if (p) (void)hipHostFree(p); }
-  } slot;
-  return slot.p;
+// Scalar read-backs (output sizes) without the runtime's blocking wait: a
+// one-wave kernel copies up to 8 words into fine-grained pinned host memory
+// with system-scope stores, then releases a sequence number; the host spins
+// on it.  hipStreamSynchronize's wake-up after a short kernel costs tens of
+// microseconds, which is most of a small join.  The spin polls the stream
+// every 256 rounds so a faulting kernel is reported instead of waited on.
+struct PubArgs {
+  const uint32_t* p[8];
+  uint32_t n;
+};
+
+__global__ void k_publish(PubArgs a, uint32_t* slot, uint32_t seq) {
+  const uint32_t i = threadIdx.x;
+  if (i < a.n) __hip_atomic_store(&slot[i], *a.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __syncthreads();
+  if (i == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct Slot {
+  uint32_t* p = nullptr;
+  uint32_t seq = 0;
+  Slot() {
+    DAS_HIP(hipHostMalloc((void**)&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(p, 0, 64);
+  }
+  ~Slot() { if (p) (void)hipHostFree(p); }
+};
+Slot& slot() {
+  thread_local Slot s;
+  return s;
+}
+
+void read_words(const PubArgs& a, hipStream_t s, uint32_t* out) {
+  Slot& sl = slot();
+  const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;      // never 0 (the initial value)
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, a, sl.p, seq);
+  DAS_HIP(hipGetLastError());
+  for (uint64_t it = 1;; ++it) {
+    if (__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq) break;
+    if ((it & 255) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq) break;
+        DAS_HIP(hipStreamSynchronize(s));
+        DAS_CHECK(__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq, DAS_E_INTERNAL, "read-back slot not written");
+        break;
+      }
+      if (e != hipErrorNotReady) DAS_HIP(e);
+    }
+    __builtin_ia32_pause();
+  }
+  for (uint32_t i = 0; i < a.n; ++i) out[i] = __atomic_load_n(&sl.p[i], __ATOMIC_RELAXED);
 }
 }  // namespace
 
 uint64_t read_u64(const uint64_t* d, hipStream_t s) {
-  uint64_t* h = pinned_slot();
-  DAS_HIP(hipMemcpyAsync(h, d, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  DAS_HIP(hipStreamSynchronize(s));
-  return *h;
+  PubArgs a{};
+  a.p[0] = reinterpret_cast<const uint32_t*>(d);
+  a.p[1] = a.p[0] + 1;
+  a.n = 2;
+  uint32_t w[2];
+  read_words(a, s, w);
+  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
 }
 void read_u64x2(const uint64_t* d, hipStream_t s, uint64_t out[2]) {
-  uint64_t* h = pinned_slot();
-  DAS_HIP(hipMemcpyAsync(h, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  DAS_HIP(hipStreamSynchronize(s));
-  out[0] = h[0];
-  out[1] = h[1];
+  PubArgs a{};
+  for (int i = 0; i < 4; ++i) a.p[i] = reinterpret_cast<const uint32_t*>(d) + i;
+  a.n = 4;
+  uint32_t w[4];
+  read_words(a, s, w);
+  out[0] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  out[1] = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
 }
 uint32_t read_u32(const uint32_t* d, hipStream_t s) {
-  uint64_t* h = pinned_slot();
-  DAS_HIP(hipMemcpyAsync(h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  DAS_HIP(hipStreamSynchronize(s));
-  return (uint32_t)*h;
+  PubArgs a{};
+  a.p[0] = d;
+  a.n = 1;
+  uint32_t w;
+  read_words(a, s, &w);
+  return w;
+}
+void read_u32x2(const uint32_t* d0, const uint32_t* d1, hipStream_t s, uint32_t out[2]) {
+  PubArgs a{};
+  a.p[0] = d0;
+  a.p[1] = d1;
+  a.n = 2;
+  read_words(a, s, out);
 }
 
 namespace {
@@ -377,11 +436,9 @@ uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hi
   if (!n) { out.alloc(1, s); return 0; }
   DBuf<uint32_t> scan(n, s);
   exclusive_scan<uint32_t>(flag, n, scan.p, s);
-  uint32_t last_scan = 0, last_flag = 0;
-  DAS_HIP(hipMemcpyAsync(&last_scan, scan.p + n - 1, 4, hipMemcpyDeviceToHost, s));
-  DAS_HIP(hipMemcpyAsync(&last_flag, flag + n - 1, 4, hipMemcpyDeviceToHost, s));
-  DAS_HIP(hipStreamSynchronize(s));
-  const uint64_t m = (uint64_t)last_scan + last_flag;
+  uint32_t last[2];
+  read_u32x2(scan.p + n - 1, flag + n - 1, s, last);
+  const uint64_t m = (uint64_t)last[0] + last[1];
   out.alloc(m ? m : 1, s);
   hipLaunchKernelGGL(k_compact_index, G(n), dim3(B), 0, s, flag, (const uint32_t*)scan.p, n, out.p);
   DAS_HIP(hipGetLastError());

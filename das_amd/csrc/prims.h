@@ -325,5 +325,6 @@ inline void fill_dev(void* dst, int byte, uint64_t bytes, hipStream_t s) {
 uint64_t read_u64(const uint64_t* d, hipStream_t s);
 uint32_t read_u32(const uint32_t* d, hipStream_t s);
 void read_u64x2(const uint64_t* d, hipStream_t s, uint64_t out[2]);   // d[0], d[1] in one round trip
+void read_u32x2(const uint32_t* d0, const uint32_t* d1, hipStream_t s, uint32_t out[2]);
 
 }  // namespace das

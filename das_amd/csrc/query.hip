@@ -788,9 +788,7 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
   }
   exclusive_scan<uint32_t>(cnt.p, chunks, off.p, c.s);
   uint32_t h[2];
-  DAS_HIP(hipMemcpyAsync(&h[0], off.p + chunks - 1, 4, hipMemcpyDeviceToHost, c.s));
-  DAS_HIP(hipMemcpyAsync(&h[1], cnt.p + chunks - 1, 4, hipMemcpyDeviceToHost, c.s));
-  DAS_HIP(hipStreamSynchronize(c.s));
+  read_u32x2(off.p + chunks - 1, cnt.p + chunks - 1, c.s, h);
   const uint64_t m = (uint64_t)h[0] + h[1];
   auto t = new_table(c, kind, ncols, vars, m);
   t->nrows = m;
