@@ -38,8 +38,8 @@ struct RowTable {
 };
 inline uint64_t col_stride(uint64_t rows) { return (rows + 63) & ~63ull; }
 
-// P_{a,p}: RowTable sorted by (type, t_p, t_q, link id), q = the first other
-// position (a >= 2), + unique (type, t_p) keys -> row offsets.
+// P_{a,p}: RowTable sorted by (type, t_p, the other targets in position
+// order, link id) + unique (type, t_p) keys -> row offsets.
 struct PosIndex {
   RowTable t;
   uint64_t nkeys = 0;

@@ -874,13 +874,15 @@ void build_index(Ctx& c, const das_atoms_t& a) {
         DBuf<uint64_t> key(R, s);
         DBuf<uint32_t> perm(R, s);
         copy_dev(perm.p, ids.p, 4 * R, s);
-        if (ar >= 2) {
-          // secondary order by the first other target (LSD: least significant key
-          // first), so an anchored range of P_{a,p} comes out sorted by that
-          // target and can be a join's build side without a sort
+        // secondary order by the other targets in position order (LSD: least
+        // significant key first), so an anchored range of P_{a,p} comes out
+        // sorted by its first non-grounded other target and can be a join's
+        // build side without a sort
+        for (int q = (int)ar - 1; q >= 0; --q) {
+          if ((uint32_t)q == p) continue;
           DBuf<uint32_t> k2(R, s);
           hipLaunchKernelGGL(k_tgt_key, G(R), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt,
-                             (const uint32_t*)perm.p, R, p == 0 ? 1u : 0u, k2.p);
+                             (const uint32_t*)perm.p, R, (uint32_t)q, k2.p);
           radix_sort_pairs<uint32_t>(k2.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
         }
         hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,

@@ -940,10 +940,16 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
         // this position's filter is implied by the range
         for (uint32_t pp = 0; pp < ar; ++pp) sp.fixed[pp] = q.target[pp];
         sp.fixed[p] = kNone;
-        // P_{a,p} rows are (type, t_p, t_q, id) with q the first other position:
-        // one key range comes out sorted by t_q
-        const uint32_t q2 = p == 0 ? 1u : 0u;
-        sorted_pos = (ar >= 2 && ranges.size() == 1 && q.target[q2] == kNone) ? (int)q2 : -1;
+        // P_{a,p} rows are (type, t_p, other targets in position order, id):
+        // one key range comes out sorted by the first other target that is
+        // not grounded (the grounded ones before it are filtered to one value)
+        sorted_pos = -1;
+        if (ranges.size() == 1)
+          for (uint32_t q2 = 0; q2 < ar; ++q2) {
+            if (q2 == p || q.target[q2] != kNone) continue;
+            sorted_pos = (int)q2;
+            break;
+          }
       }
       if (best == 0) return empty();
     }
