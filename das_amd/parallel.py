@@ -491,3 +491,54 @@ def shard_arrays(arrays, rank, world):
         kinds[b:e] = seg
     arrays.expr_kind = kinds
     return arrays
+
+
+def partition_arrays(arrays, rank, world):
+    """Independent shards for the bulk build (config 4 at N GPUs): rank r keeps
+    only the links its content hash selects, plus the nested expressions they
+    contain and every leaf; it hashes and indexes nothing else.  Atom ids are
+    then local to the shard (the reference's sharded Redis keys, not the
+    replicated directory ShardedDB queries need)."""
+    from .loader import AtomArrays
+    if world == 1:
+        return arrays
+    nl, ne = arrays.n_leaf, arrays.n_expr
+    off = arrays.expr_off.astype(np.int64)
+    child = arrays.expr_child.astype(np.int64)
+    nested = np.zeros(ne, dtype=bool)
+    nested[child[child >= nl] - nl] = True
+    keep = np.zeros(ne, dtype=bool)
+    groups = [(int(arrays.level_off[g]), int(arrays.level_off[g + 1])) for g in range(len(arrays.level_off) - 1)]
+    for b, e in groups:
+        if e <= b:
+            continue
+        k = int(off[b + 1] - off[b])
+        ch = child[off[b]:off[e]].reshape(e - b, k)
+        top = ~nested[b:e]
+        own = owner_of(ch, world) == rank
+        keep[b:e] = (top & own) | (arrays.expr_kind[b:e] == 2)
+    for b, e in reversed(groups):          # parents before children: close over nesting
+        if e <= b:
+            continue
+        k = int(off[b + 1] - off[b])
+        ch = child[off[b]:off[e]].reshape(e - b, k)[keep[b:e]]
+        sub = ch[ch >= nl] - nl
+        keep[sub] = True
+    newpos = np.cumsum(keep) - 1
+    nch = np.diff(off)[keep]
+    expr_off = np.zeros(int(keep.sum()) + 1, dtype=np.uint64)
+    np.cumsum(nch, out=expr_off[1:])
+    parts = []
+    for b, e in groups:
+        if e <= b:
+            continue
+        k = int(off[b + 1] - off[b])
+        parts.append(child[off[b]:off[e]].reshape(e - b, k)[keep[b:e]].reshape(-1))
+    ch = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+    ch = np.where(ch >= nl, nl + newpos[np.maximum(ch - nl, 0)], ch)
+    level_off = [0]
+    for b, e in groups:
+        level_off.append(level_off[-1] + int(keep[b:e].sum()))
+    return AtomArrays(arrays.leaf_bytes, arrays.leaf_off, arrays.leaf_kind, arrays.leaf_ctype, arrays.leaf_type_id,
+                      arrays.name_start, expr_off, ch.astype(np.uint32), arrays.expr_kind[keep],
+                      arrays.expr_ctype_leaf[keep], np.array(level_off, dtype=np.uint64), arrays.type_names)
