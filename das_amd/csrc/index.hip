@@ -222,23 +222,35 @@ __global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n
   }
 }
 
-// id = inclusive run index; catmax = max category over the run.
+// id = inclusive run index; catmax = max category over the run; rep = the
+// smallest unified index of that category.  Runs are digest-sorted, so ids
+// are sequential in i; a run of one (the common case) is settled here with
+// plain stores, longer runs (duplicate atoms) with atomics plus k_pick_rep.
 __global__ void k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan, uint64_t n,
-                             const uint8_t* catl, uint32_t* local2id, uint32_t* catmax) {
+                             const uint8_t* catl, uint32_t* local2id, uint32_t* catmax, uint32_t* rep,
+                             uint8_t* cat_sorted) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t id = scan[i] + first[i] - 1;
     const uint32_t u = idx[i];
+    const uint8_t c = catl[u];
     local2id[u] = id;
-    atomicMax(&catmax[id], (uint32_t)catl[u]);
+    cat_sorted[i] = c;
+    const bool single = first[i] && (i + 1 == n || first[i + 1]);
+    if (single) {
+      catmax[id] = c;
+      rep[id] = u;
+    } else {
+      atomicMax(&catmax[id], (uint32_t)c);
+    }
   }
 }
 
-__global__ void k_pick_rep(const uint32_t* idx, uint64_t n, const uint32_t* local2id, const uint8_t* catl,
-                           const uint32_t* catmax, uint32_t* rep) {
+__global__ void k_pick_rep(const uint32_t* idx, const uint32_t* first, const uint32_t* scan, uint64_t n,
+                           const uint8_t* cat_sorted, const uint32_t* catmax, uint32_t* rep) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t u = idx[i];
-    const uint32_t id = local2id[u];
-    if ((uint32_t)catl[u] == catmax[id]) atomicMin(&rep[id], u);
+    if (first[i] && (i + 1 == n || first[i + 1])) continue;        // singleton: done
+    const uint32_t id = scan[i] + first[i] - 1;
+    if ((uint32_t)cat_sorted[i] == catmax[id]) atomicMin(&rep[id], idx[i]);
   }
 }
 
@@ -322,15 +334,32 @@ __global__ void k_link_flags(const uint8_t* cat, const uint32_t* arity, uint64_t
 }
 
 __global__ void k_arity_hist(const uint8_t* cat, const uint32_t* arity, uint64_t n, unsigned long long* h) {
+  // per-thread counters for nodes and arities 0..kMaxArity (registers), one LDS
+  // add per counter per thread, one global add per counter per block: the
+  // same-address LDS atomics of a per-element histogram serialise a wave
+  constexpr int NC = kMaxArity + 2;               // [0..kMaxArity] arities, [NC-1] nodes
   __shared__ unsigned int sh[64];
   if (threadIdx.x < 64) sh[threadIdx.x] = 0;
   __syncthreads();
+  uint32_t cnt[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) cnt[k] = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (cat[i] == CAT_NODE) atomicAdd(&sh[63], 1u);
-    if (cat[i] != CAT_LINK) continue;
-    uint32_t a = arity[i] > 62 ? 62 : arity[i];
-    atomicAdd(&sh[a], 1u);
+    const uint8_t c = cat[i];
+    if (c == CAT_NODE) { ++cnt[NC - 1]; continue; }
+    if (c != CAT_LINK) continue;
+    const uint32_t a = arity[i];
+    if (a <= (uint32_t)kMaxArity) {
+#pragma unroll
+      for (int k = 0; k <= kMaxArity; ++k) cnt[k] += (a == (uint32_t)k);
+    } else {
+      atomicAdd(&sh[a > 62 ? 62 : a], 1u);        // rare: reported as unsupported by the caller
+    }
   }
+#pragma unroll
+  for (int k = 0; k < NC - 1; ++k)
+    if (cnt[k]) atomicAdd(&sh[k], cnt[k]);
+  if (cnt[NC - 1]) atomicAdd(&sh[63], cnt[NC - 1]);
   __syncthreads();
   if (threadIdx.x < 64 && sh[threadIdx.x]) atomicAdd(&h[threadIdx.x], (unsigned long long)sh[threadIdx.x]);
 }
@@ -661,10 +690,11 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   fill_dev(catmax.p, 0, 4 * catmax.n, s);
   fill_dev(rep.p, 0xFF, 4 * rep.n, s);
   if (nc) {
+    DBuf<uint8_t> cs(nc, s);
     hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
-                       (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p);
-    hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, nc, (const uint32_t*)local2id.p,
-                       (const uint8_t*)catl.p, (const uint32_t*)catmax.p, rep.p);
+                       (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p, rep.p, cs.p);
+    hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
+                       (const uint32_t*)scan.p, nc, (const uint8_t*)cs.p, (const uint32_t*)catmax.p, rep.p);
     DAS_HIP(hipGetLastError());
   }
   first.release(); scan.release(); list.release();
@@ -754,7 +784,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   {
     DBuf<unsigned long long> h(64, s);
     fill_dev(h.p, 0, 64 * 8, s);
-    if (n_atoms) hipLaunchKernelGGL(k_arity_hist, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+    if (n_atoms) hipLaunchKernelGGL(k_arity_hist, dim3(grid_for(n_atoms, B, 2048)), dim3(B), 0, s, (const uint8_t*)idx.cat,
                                     (const uint32_t*)idx.arity, n_atoms, h.p);
     unsigned long long hh[64];
     DAS_HIP(hipMemcpyAsync(hh, h.p, sizeof(hh), hipMemcpyDeviceToHost, s));
