@@ -408,7 +408,9 @@ def main():
     qs = [(name, build_expr(pm, s)) for name, s in specs]
     if world > 1:
         from das_amd import parallel
-        engine = parallel.ShardedMatcher(db, dist, cpu_staging=(backend != "nccl"))
+        # bio_shard places a gene's Member links on the gene's rank
+        spec = {"Member": 0} if args.workload == "bio" else None
+        engine = parallel.ShardedMatcher(db, dist, cpu_staging=(backend != "nccl"), partition_spec=spec)
 
         def run(q):
             return engine.count(q)

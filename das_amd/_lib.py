@@ -250,11 +250,12 @@ def hex_to_digest(h):
 class Table:
     """Owning wrapper of a das_table_t* (a device binding table)."""
 
-    __slots__ = ("ctx", "h", "kind", "vars", "members", "nrows")
+    __slots__ = ("ctx", "h", "kind", "vars", "members", "nrows", "part")
 
     def __init__(self, ctx, handle):
         self.ctx = ctx
         self.h = handle
+        self.part = None          # multi-GPU: how the rows are spread over ranks (das_amd.parallel)
         kind = C.c_int32()
         ncols = C.c_int32()
         vars_ = (C.c_int32 * 16)()

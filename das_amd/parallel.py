@@ -27,12 +27,29 @@ double with the same surface).
 """
 import zlib
 
+import os
+
 import numpy as np
 
 from .database.db_interface import UNORDERED_LINK_TYPES, WILDCARD
 from .database.hip_db import RelationalDB
 
 ORDERED, UNORDERED, COMPOSITE = 0, 1, 2
+
+
+def _part(t):
+    """How a local table's rows are spread over ranks: ("atom", var) = by the
+    owner of that variable's atom (partition_spec), ("hash", vars) = by
+    hash(vars) after an exchange, None = unknown."""
+    return getattr(t, "part", None)
+
+
+def _with_part(t, part):
+    try:
+        t.part = part
+    except AttributeError:
+        pass
+    return t
 
 
 def _members(t):
@@ -74,13 +91,22 @@ class DRel:
 
 class ShardedDB(RelationalDB):
 
-    def __init__(self, local, dist, group=None):
+    def __init__(self, local, dist, group=None, partition_spec=None):
+        """partition_spec: {link type: target position} for link types whose
+        links are placed on the rank that owns the atom at that position (one
+        owner function for every listed type, e.g. bio_shard's gene ranges).
+        Scans of those types are then known to be partitioned by the variable
+        at that position, and joins on it need no exchange."""
         self.local = local
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.tuple_targets = local.tuple_targets
+        self.spec = dict(partition_spec or {})
+        self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0}   # join placements taken
+        # DAS_JOIN_PLACEMENT=exchange|broadcast forces one placement (tests)
+        self.force = os.environ.get("DAS_JOIN_PLACEMENT", "")
 
     # ------------------------------------------------------------ collectives
     def _allreduce_sum(self, values):
@@ -92,6 +118,12 @@ class ShardedDB(RelationalDB):
         """Repartition `table` by hash(key_vars) (every column if empty)."""
         if self.world == 1:
             return table
+        key = tuple(sorted(key_vars)) if key_vars else ("*",)        # "*": every column
+        if _part(table) == ("hash", key):
+            return table                                   # already placed by this key
+        return _with_part(self._exchange_rows(table, list(key) if key_vars else []), ("hash", key))
+
+    def _exchange_rows(self, table, key_vars):
         part, counts = self.local.partition(table, list(key_vars), self.world)
         send_counts = self.local.xfer_tensor(counts.astype(np.int64))
         recv_counts = self.local.xfer_tensor(np.zeros(self.world, dtype=np.int64))
@@ -197,7 +229,10 @@ class ShardedDB(RelationalDB):
         dup = link_type == WILDCARD or len(set(names)) != len(names) or not ordered or \
             link_type in UNORDERED_LINK_TYPES
         if dup:
-            t = self.local.dedup(self._exchange(t, []))
+            t = _with_part(self.local.dedup(self._exchange(t, [])), ("hash", ("*",)))
+        elif link_type in self.spec and self.spec[link_type] < len(var_ids) and \
+                var_ids[self.spec[link_type]] is not None:
+            t = _with_part(t, ("atom", var_ids[self.spec[link_type]]))
         return DRel([t])
 
     def match_template(self, link_type, target_types, var_ids, ordered, no_overload=False):
@@ -274,8 +309,7 @@ class ShardedDB(RelationalDB):
                     continue
                 shared = sorted(set(ta.vars) & set(tb.vars))
                 if shared:
-                    out.append(self.local.join(self._exchange(ta, shared), self._exchange(tb, shared),
-                                               CONFIG['no_overload']))
+                    out.append(self._join_shared(ta, tb, shared, CONFIG['no_overload']))
                 else:
                     na = self._allreduce_sum([ta.nrows])[0]
                     nb = self._allreduce_sum([tb.nrows])[0]
@@ -284,6 +318,31 @@ class ShardedDB(RelationalDB):
                     else:
                         out.append(self.local.join(ta, self._gather_all(tb), CONFIG['no_overload']))
         return DRel(out)
+
+    def _join_shared(self, ta, tb, shared, no_overload):
+        """Ordered equi-join on `shared`, placed by cost:
+        * both sides partitioned by the same atom variable in `shared`
+          (partition_spec) or by the same hash key: join where the rows are;
+        * one side small (its rows x world < both sides' rows): replicate it
+          to every rank, leave the large side in place (SURVEY §8e's
+          broadcast of heavy / small relations);
+        * otherwise repartition both by hash(shared) (all-to-all)."""
+        pa, pb = _part(ta), _part(tb)
+        if not self.force and pa is not None and pa == pb and ((pa[0] == "atom" and pa[1] in shared) or
+                                            (pa[0] == "hash" and set(pa[1]) <= set(shared))):
+            self.plan_stats["colocated"] += 1
+            return _with_part(self.local.join(ta, tb, no_overload), pa)
+        wa, wb = (int(x) for x in self._allreduce_sum([ta.nrows * max(len(ta.vars), 1),
+                                                       tb.nrows * max(len(tb.vars), 1)]))
+        if self.force == "broadcast" or (not self.force and min(wa, wb) * self.world < wa + wb):
+            self.plan_stats["broadcast"] += 1
+            if wa <= wb:
+                return _with_part(self.local.join(self._gather_all(ta), tb, no_overload), pb)
+            return _with_part(self.local.join(ta, self._gather_all(tb), no_overload), pa)
+        key = tuple(shared)
+        self.plan_stats["exchange"] += 1
+        return _with_part(self.local.join(self._exchange(ta, shared), self._exchange(tb, shared), no_overload),
+                          ("hash", key))
 
     def rel_antijoin(self, rel, forbidden):
         tables = rel.tables
@@ -300,7 +359,13 @@ class ShardedDB(RelationalDB):
                     continue
                 if set(f.vars) <= set(t.vars):
                     key = sorted(f.vars)
-                    nxt.append(self.local.antijoin(self._exchange(t, key), self._exchange(f, key)))
+                    wt, wf = (int(x) for x in self._allreduce_sum([t.nrows * max(len(t.vars), 1),
+                                                                   f.nrows * max(len(f.vars), 1)]))
+                    if self.force != "exchange" and wf * self.world < wt + wf:   # small forbidden set: replicate it
+                        nxt.append(_with_part(self.local.antijoin(t, self._gather_all(f)), _part(t)))
+                    else:
+                        nxt.append(_with_part(self.local.antijoin(self._exchange(t, key), self._exchange(f, key)),
+                                              ("hash", tuple(key))))
                 else:
                     nxt.append(t)
             tables = nxt
@@ -421,8 +486,8 @@ class ShardedMatcher:
     the number of distinct bindings held by this rank (sum over ranks = the
     answer's size)."""
 
-    def __init__(self, db, dist, cpu_staging=False):
-        self.sdb = ShardedDB(HipLocal(db, cpu_staging), dist)
+    def __init__(self, db, dist, cpu_staging=False, partition_spec=None):
+        self.sdb = ShardedDB(HipLocal(db, cpu_staging), dist, partition_spec=partition_spec)
 
     def count(self, expr):
         from .pattern_matcher.pattern_matcher import PatternMatchingAnswer

@@ -110,7 +110,10 @@ class NumpyLocal:
 
     tuple_targets = False
 
-    def __init__(self, kb_full, rank, world):
+    def __init__(self, kb_full, rank, world, by_target=None):
+        """by_target {link type: position}: those links live on the rank that
+        owns the atom at that position (hash of its handle), the rest by the
+        link's own handle -- the layout ShardedDB's partition_spec describes."""
         handles = set(kb_full.nodes) | set(kb_full.links)
         for _, (_, tg, _) in kb_full.links.items():
             handles.update(tg)
@@ -118,7 +121,12 @@ class NumpyLocal:
         self.id_of = {h: i for i, h in enumerate(self.hexes)}
         local = O.KB()
         local.nodes = dict(kb_full.nodes)
-        local.links = {h: v for h, v in kb_full.links.items() if int(h[:8], 16) % world == rank}
+        by_target = by_target or {}
+
+        def owner(h, v):
+            key = v[1][by_target[v[0]]] if v[0] in by_target else h
+            return int(key[:8], 16) % world
+        local.links = {h: v for h, v in kb_full.links.items() if owner(h, v) == rank}
         self.odb = O.RedisMongoSemantics(local)
         self.full = O.RedisMongoSemantics(kb_full)
 
@@ -337,13 +345,14 @@ def _composite_queries():
 
 def _kb(kind):
     from das_amd import synthetic
-    if kind == "bio":
+    if kind in ("bio", "bio_part", "bio_exchange", "bio_broadcast"):
         return O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)), _queries()
     return O.KB.from_arrays(synthetic.similarity_kb(n_nodes=20, n_inh=90, n_sim=45, n_set=20, seed=9)), \
         _composite_queries()
 
 
 def _worker(rank, world, port, out_path, kind):
+    os.environ["DAS_JOIN_PLACEMENT"] = {"bio_exchange": "exchange", "bio_broadcast": "broadcast"}.get(kind, "")
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -351,7 +360,8 @@ def _worker(rank, world, port, out_path, kind):
     from tests.util import build, canon
     from das_amd.pattern_matcher import pattern_matcher as pm
     kb, queries = _kb(kind)
-    sdb = ShardedDB(NumpyLocal(kb, rank, world), dist)
+    spec = {"Member": 0} if kind == "bio_part" else None
+    sdb = ShardedDB(NumpyLocal(kb, rank, world, by_target=spec), dist, partition_spec=spec)
     res = []
     for q in queries:
         ans = pm.PatternMatchingAnswer()
@@ -363,6 +373,7 @@ def _worker(rank, world, port, out_path, kind):
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
         res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
                     "local": sdb.rel_local_count(ans._relation())})
+    res.append(sdb.plan_stats)
     with open(f"{out_path}.{rank}", "w") as f:
         json.dump(res, f)
     dist.destroy_process_group()
@@ -377,7 +388,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world", [2])
-@pytest.mark.parametrize("kind", ["bio", "composite"])
+@pytest.mark.parametrize("kind", ["bio", "bio_part", "bio_exchange", "bio_broadcast", "composite"])
 def test_sharded_matcher_equals_single_process_oracle(world, kind):
     kb, queries = _kb(kind)
     odb = O.RedisMongoSemantics(kb)
@@ -385,6 +396,11 @@ def test_sharded_matcher_equals_single_process_oracle(world, kind):
         out = os.path.join(d, "res")
         mp.spawn(_worker, args=(world, _free_port(), out, kind), nprocs=world, join=True)
         per_rank = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    stats = per_rank[0][-1]
+    if kind == "bio_part":
+        assert stats["colocated"] > 0 and stats["broadcast"] > 0, stats    # both placements exercised
+    if kind in ("bio_exchange", "bio_broadcast"):
+        assert stats[kind[4:]] > 0 and stats["colocated"] == 0, stats
     for qi, q in enumerate(queries):
         want = O.evaluate(q, odb)
         if "error" in want:
