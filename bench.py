@@ -59,11 +59,13 @@ def parse():
     ap.add_argument("--fb-schema", type=int, default=60)
     ap.add_argument("--fb-rows", type=int, default=450_000)
     # hub (config 5): H4's output grows ~ links^1.6 (Zipf hubs): 3M links -> ~4.3e8 bindings
-    ap.add_argument("--hub-links", type=int, default=3_000_000)
-    ap.add_argument("--hub-nodes", type=int, default=1 << 21)
+    ap.add_argument("--hub-links", type=int, default=1_000_000_000)
+    ap.add_argument("--hub-nodes", type=int, default=1 << 27)
     # build (config 4)
-    ap.add_argument("--links", type=int, default=100_000_000)
-    ap.add_argument("--nodes", type=int, default=1 << 24)
+    ap.add_argument("--links", type=int, default=1_000_000_000)
+    ap.add_argument("--nodes", type=int, default=1 << 27)
+    ap.add_argument("--gen", default="device", choices=["device", "host"],
+                    help="build/hub input: generated in HBM (default) or by numpy on the host")
     # load (canonical text): ~100 B a line
     ap.add_argument("--load-genes", type=int, default=200_000)
     ap.add_argument("--load-rows", type=int, default=200_000)
@@ -122,13 +124,16 @@ def flybase_specs(gene=7, do_terms=()):
 
 def hub_specs():
     """Config 5: 4-clause And anchored on the two highest-degree nodes (Zipf
-    ranks 0 and 1) of link type T0."""
+    ranks 0 and 1), one link type per clause, and its 2-clause prefix (the
+    skewed hub join itself: every T1 link out of a T0-neighbour of h0).  At
+    10^9 links an unanchored last clause (T(V2, V3)) would expand through hub
+    out-degrees to ~10^14 rows, so the 4-clause And closes on the hubs."""
     n = lambda i: ["Node", "Concept", f"n{i}"]  # noqa: E731
     return [
-        ("H4 T(V1,h0) T(V1,V2) T(V2,h1) T(V2,V3)",
-         ["And", [_L("T0", _V("V1"), n(0)), _L("T0", _V("V1"), _V("V2")), _L("T0", _V("V2"), n(1)),
-                  _L("T0", _V("V2"), _V("V3"))]]),
-        ("H2 T(V1,h0) T(V1,V2)", ["And", [_L("T0", _V("V1"), n(0)), _L("T0", _V("V1"), _V("V2"))]]),
+        ("H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)",
+         ["And", [_L("T0", _V("V1"), n(0)), _L("T1", _V("V1"), _V("V2")), _L("T2", _V("V2"), n(1)),
+                  _L("T3", _V("V2"), n(0))]]),
+        ("H2 T0(V1,h0) T1(V1,V2)", ["And", [_L("T0", _V("V1"), n(0)), _L("T1", _V("V1"), _V("V2"))]]),
     ]
 
 
@@ -145,7 +150,7 @@ def build_expr(pm, spec):
     return (pm.And if k == "And" else pm.Or)([build_expr(pm, t) for t in spec[1]])
 
 
-def make_kb(args, rank, world):
+def make_kb(args, rank, world, db):
     """(AtomArrays for this rank, query specs, config dict, scaling)."""
     import numpy as np
     from das_amd import parallel, synthetic
@@ -167,10 +172,18 @@ def make_kb(args, rank, world):
         cfg = {"workload": "config3 FlyBase-shaped Execution KB: QueryFlyBase.ipynb And/And+Not/Or shapes",
                "links": int(arrays.n_expr), "genes": args.fb_genes, "schemas": args.fb_schema}
         return arrays, flybase_specs(7, do_terms), cfg, "strong"
-    arrays = synthetic.powerlaw_kb(args.hub_nodes, args.hub_links, link_types=4)
-    arrays = parallel.shard_arrays(arrays, rank, world)
+    if args.gen == "device":
+        # every rank holds the whole atom directory; rank r owns (indexes) the
+        # global link range [r L / N, (r+1) L / N)
+        lo, hi = args.hub_links * rank // world, args.hub_links * (rank + 1) // world
+        arrays = synthetic.powerlaw_kb_device(db.ctx, args.hub_nodes, args.hub_links, link_types=4,
+                                              own=(lo, hi) if world > 1 else None, device=db.ctx.device)
+    else:
+        arrays = synthetic.powerlaw_kb(args.hub_nodes, args.hub_links, link_types=4)
+        arrays = parallel.shard_arrays(arrays, rank, world)
     cfg = {"workload": "config5 power-law hypergraph: 4-clause And on hub nodes",
-           "links": args.hub_links, "nodes": args.hub_nodes, "link_types": 4, "arity": "70% 2 / 30% 3"}
+           "links": args.hub_links, "nodes": args.hub_nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
+           "generated": args.gen}
     return arrays, hub_specs(), cfg, "strong"
 
 
@@ -193,7 +206,7 @@ def cpu_baseline(args, budget_s):
         specs = [s for _, s in flybase_specs(7, synthetic.flybase_do_terms(arrays, gene=7))]
         what = f"flybase_kb at 1/{scale} of the GPU workload"
     else:
-        scale = 100
+        scale = max(args.hub_links // 30_000, 1)      # ~30 k links: a few oracle passes in the budget
         arrays = synthetic.powerlaw_kb(max(args.hub_nodes // scale, 200), max(args.hub_links // scale, 2000),
                                        link_types=4)
         specs = [s for _, s in hub_specs()]
@@ -246,11 +259,20 @@ def run_build(args, rank, world, dist, local_rank):
     from das_amd import parallel, synthetic
     from das_amd.database.hip_db import HipDB
     t0 = time.perf_counter()
-    log(f"generating {args.links} links")
-    arrays = synthetic.powerlaw_kb(args.nodes, args.links, link_types=4)
-    arrays = parallel.partition_arrays(arrays, rank, world)      # independent shards: strong scaling
-    t_gen = time.perf_counter() - t0
     db = HipDB(device=local_rank)
+    log(f"generating {args.links} links ({args.gen})")
+    if args.gen == "device":
+        # generated on the device; rank r materialises
+        # the global link range [r L / N, (r+1) L / N) of the one KB
+        # (independent shards, nodes replicated: strong scaling)
+        lo, hi = args.links * rank // world, args.links * (rank + 1) // world
+        arrays = synthetic.powerlaw_kb_device(db.ctx, args.nodes, args.links, link_types=4, first=lo,
+                                              count=hi - lo, device=local_rank)
+    else:
+        arrays = synthetic.powerlaw_kb(args.nodes, args.links, link_types=4)
+        arrays = parallel.partition_arrays(arrays, rank, world)      # independent shards: strong scaling
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
     db.load_arrays(synthetic.powerlaw_kb(1000, 10000, link_types=4))    # warm-up build (code objects, pools)
     torch.cuda.synchronize()
     db.ctx.prof_reset()
@@ -266,7 +288,7 @@ def run_build(args, rank, world, dist, local_rank):
     stats = db.ctx.prof_stats()
     dev_ms = stats.get("build_device", {}).get("ms", wall * 1e3)
     st = db.stats()
-    local_links = int(sum(arrays.expr_kind == 1))
+    local_links = int((arrays.expr_kind == 1).sum())
     links = local_links
     if dist:
         t = torch.tensor([dev_ms, wall], dtype=torch.float64, device="cuda")
@@ -281,8 +303,13 @@ def run_build(args, rank, world, dist, local_rank):
     import numpy as np
     leaf_len = np.diff(arrays.leaf_off.astype(np.int64))
     blocks_leaf = int(((leaf_len + 9 + 63) // 64).sum())
-    nch = np.diff(arrays.expr_off.astype(np.int64))
-    blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum())
+    if getattr(arrays, "expr_on_device", False):
+        nch = arrays.expr_off[1:] - arrays.expr_off[:-1]
+        blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum().item())
+        del nch
+    else:
+        nch = np.diff(arrays.expr_off.astype(np.int64))
+        blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum())
     if rank == 0:
         hs = stats.get("k_hash_group", {"ms": 0, "bytes": 0, "launches": 0})
         hl = stats.get("k_hash_strings", {"ms": 0, "bytes": 0, "launches": 0})
@@ -290,10 +317,11 @@ def run_build(args, rank, world, dist, local_rank):
                "value": links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
                "ms_per_step": dev_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                "dtype": "u32",
-               "data": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets), generated on the host",
+               "data": "synthetic power-law hypergraph, Zipf(1.1) targets, " + (
+                   "generated in HBM (das_synth_powerlaw_links)" if args.gen == "device" else "generated on the host"),
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
-                          "parallelism": f"links content-hash partitioned x{world} (independent shards, nodes replicated)"},
+                          "parallelism": f"links partitioned x{world} (independent shards, nodes replicated)"},
                "roofline": roofline_of(stats, "build"), "cpu_baseline": None,
                "hash": {"ms": round(hs["ms"], 3), "GBps": round(hs["bytes"] / max(hs["ms"], 1e-9) / 1e6, 1),
                         "md5_blocks_per_s": (blocks_leaf + blocks_expr) / max((hs["ms"] + hl["ms"]) * 1e-3, 1e-12),
@@ -399,10 +427,13 @@ def main():
     # ---- knowledge base (per-rank partition for N > 1) ----
     t_build = time.perf_counter()
     log(f"generating {args.workload} KB")
-    arrays, specs, cfg, scaling = make_kb(args, rank, world)
-    log(f"building the device index ({arrays.n_expr} expressions)")
     db = HipDB(device=local_rank)
+    arrays, specs, cfg, scaling = make_kb(args, rank, world, db)
+    log(f"building the device index ({arrays.n_expr} expressions)")
     db.load_arrays(arrays)
+    if getattr(arrays, "expr_on_device", False):
+        arrays.drop_expr()          # device-generated input: free it once indexed
+    del arrays
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
     qs = [(name, build_expr(pm, s)) for name, s in specs]

@@ -70,6 +70,7 @@ class das_template_scan_t(C.Structure):
 
 
 P = C.c_void_p
+DAS_BUILD_EXPR_ON_DEVICE = 1
 U32P = C.POINTER(C.c_uint32)
 
 # name -> (restype, argtypes); every function returns int status unless noted.
@@ -84,6 +85,9 @@ _SIGS = {
     "das_hash_strings_dev": (C.c_int, [P, P, P, C.c_uint64, P]),
     "das_hash_fixed_dev": (C.c_int, [P, P, C.c_uint32, C.c_uint64, P]),
     "das_build_index": (C.c_int, [P, C.POINTER(das_atoms_t)]),
+    "das_build_index_ex": (C.c_int, [P, C.POINTER(das_atoms_t), C.c_uint32]),
+    "das_synth_powerlaw_links": (C.c_int, [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, C.c_uint64, C.c_double, C.c_uint64]),
     "das_index_stats": (C.c_int, [P, C.POINTER(das_index_stats_t)]),
     "das_lookup": (C.c_int, [P, P, C.c_uint64, P, P, P, P]),
     "das_atoms_info": (C.c_int, [P, P, C.c_uint64, P, P, P, P, P]),
@@ -95,6 +99,7 @@ _SIGS = {
     "das_scan_type": (C.c_int, [P, C.c_uint32, P]),
     "das_join": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
     "das_antijoin": (C.c_int, [P, P, P, C.POINTER(P)]),
+    "das_index_join": (C.c_int, [P, P, C.POINTER(das_link_scan_t), C.POINTER(P)]),
     "das_dedup": (C.c_int, [P, P, C.POINTER(P)]),
     "das_concat": (C.c_int, [P, P, C.c_uint32, C.POINTER(P)]),
     "das_set_dedup": (C.c_int, [P, P, C.c_uint32, P]),
@@ -326,17 +331,31 @@ class Context:
         return Table(self, out)
 
     def build_index(self, arrays):
+        """Host arrays (das_build_index), or a KB whose expression arrays are
+        device tensors (`arrays.expr_on_device`, das_build_index_ex)."""
         a = arrays
+        dev = bool(getattr(a, "expr_on_device", False))
+        eptr = (lambda t: C.c_void_p(t.data_ptr())) if dev else ptr
         keep = [a.leaf_bytes, a.leaf_off, a.leaf_kind, a.leaf_ctype, a.leaf_type_id, a.expr_off,
                 a.expr_child, a.expr_kind, a.expr_ctype_leaf, a.level_off]
         s = das_atoms_t(
             n_leaf=a.n_leaf, leaf_bytes=ptr(a.leaf_bytes), leaf_off=ptr(a.leaf_off), leaf_kind=ptr(a.leaf_kind),
             leaf_ctype=ptr(a.leaf_ctype), leaf_type_id=ptr(a.leaf_type_id), n_expr=a.n_expr,
-            expr_off=ptr(a.expr_off), expr_child=ptr(a.expr_child), expr_kind=ptr(a.expr_kind),
-            expr_ctype_leaf=ptr(a.expr_ctype_leaf), n_levels=len(a.level_off) - 1, level_off=ptr(a.level_off),
+            expr_off=eptr(a.expr_off), expr_child=eptr(a.expr_child), expr_kind=eptr(a.expr_kind),
+            expr_ctype_leaf=eptr(a.expr_ctype_leaf), n_levels=len(a.level_off) - 1, level_off=ptr(a.level_off),
             n_types=len(a.type_names))
-        check(lib().das_build_index(self.h, C.byref(s)), self.h)
+        if dev:
+            check(lib().das_build_index_ex(self.h, C.byref(s), DAS_BUILD_EXPR_ON_DEVICE), self.h)
+        else:
+            check(lib().das_build_index(self.h, C.byref(s)), self.h)
         del keep
+
+    def synth_powerlaw_links(self, d_child, first, n, k, n_link_types, type_leaf0, node_leaf0, n_nodes,
+                             s=1.1, seed=0):
+        """Fills device buffer `d_child` (a u32/i32 tensor of n*k) with links
+        [first, first+n) of the counter-hashed Zipf hypergraph."""
+        check(lib().das_synth_powerlaw_links(self.h, C.c_void_p(d_child.data_ptr()), first, n, k, n_link_types,
+                                             type_leaf0, node_leaf0, n_nodes, s, seed), self.h)
 
     def export_keyspace(self, directory):
         """Redis key-space files of the index (das_export_keyspace) -> line counts."""
@@ -407,6 +426,21 @@ class Context:
         q.no_overload = 1 if no_overload else 0
         q.emit_link = 1 if emit_link else 0
         return self._table(lib().das_scan_link, C.byref(q))
+
+    def index_join(self, a, arity, type_id, targets, var):
+        """das_index_join: join(a, scan_link(ordered q)) through P_{a,p};
+        None when it does not apply (the caller scans and joins)."""
+        q = das_link_scan_t()
+        q.order_pos = -1
+        q.arity = arity
+        q.type_id = DAS_NONE if type_id is None else type_id
+        for i in range(8):
+            q.target[i] = targets[i] if i < len(targets) else DAS_NONE
+            q.var[i] = var[i] if i < len(var) else -1
+        q.ordered = 1
+        out = P()
+        check(lib().das_index_join(self.h, a.h, C.byref(q), C.byref(out)), self.h)
+        return Table(self, out) if out.value else None
 
     def scan_template(self, ctype_id, arity, var, ordered, no_overload=False, emit_link=False):
         q = das_template_scan_t()

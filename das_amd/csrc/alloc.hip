@@ -8,6 +8,9 @@
 // step performs no runtime allocation calls once warm (the runtime's own
 // stream-ordered allocator costs microseconds per call and, under a step's
 // mix of sizes, occasionally hundreds of microseconds).
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -32,6 +35,30 @@ Cache& cache() {
 }
 
 constexpr size_t kCacheBudget = 64ull << 30;   // cached (idle) bytes kept at most
+constexpr size_t kBestFitMin = 64ull << 20;     // best-fit reuse from this block size up
+std::atomic<int> g_hold{0};                     // > 0: keep every freed block (cache_hold)
+
+// DAS_ALLOC_TRACE=1: one stderr line per driver allocation (size, host ms)
+// and per out-of-memory fallback, to attribute host gaps in large builds.
+bool alloc_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("DAS_ALLOC_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+hipError_t traced_malloc(void** p, size_t bytes, const char* what) {
+  if (!alloc_trace()) return hipMalloc(p, bytes);
+  const auto t0 = std::chrono::steady_clock::now();
+  const hipError_t e = hipMalloc(p, bytes);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  std::fprintf(stderr, "[das alloc] %s %.3f GB %.3f ms%s (free %.1f GB, cached %.1f GB)\n", what, bytes / 1e9, ms,
+               e == hipSuccess ? "" : " FAILED", fr / 1e9, cache().cached_bytes / 1e9);
+  return e;
+}
 
 size_t size_class(size_t bytes) {
   if (bytes <= 256) return 256;
@@ -52,17 +79,23 @@ void* cache_alloc(size_t bytes, hipStream_t s) {
   Cache& c = cache();
   {
     std::lock_guard<std::mutex> lk(c.mu);
-    auto it = c.free_blocks.find({s, cls});
-    if (it != c.free_blocks.end() && !it->second.empty()) {
+    // exact class; large requests also take the smallest idle block below
+    // twice their size (a 10^9-link build frees and re-requests tens of GB
+    // in shifting sizes: every block handed back to the driver is cleared
+    // before it can be mapped again, a multi-second stall per allocation)
+    const size_t top = cls >= kBestFitMin ? 2 * cls : cls + 1;
+    for (auto it = c.free_blocks.lower_bound({s, cls});
+         it != c.free_blocks.end() && it->first.first == s && it->first.second < top; ++it) {
+      if (it->second.empty()) continue;
       void* p = it->second.back();
       it->second.pop_back();
-      c.cached_bytes -= cls;
-      c.live[p] = {s, cls};
+      c.cached_bytes -= it->first.second;
+      c.live[p] = it->first;
       return p;
     }
   }
   void* p = nullptr;
-  hipError_t e = hipMalloc(&p, cls);
+  hipError_t e = traced_malloc(&p, cls, "cache");
   if (e != hipSuccess) {
     // out of memory with idle blocks cached: give them back and retry once
     (void)hipGetLastError();
@@ -74,8 +107,9 @@ void* cache_alloc(size_t bytes, hipStream_t s) {
       c.cached_bytes = 0;
     }
     DAS_HIP(hipDeviceSynchronize());
+    if (alloc_trace()) std::fprintf(stderr, "[das alloc] OOM fallback: freeing %zu idle blocks\n", idle.size());
     for (void* q : idle) (void)hipFree(q);
-    DAS_HIP(hipMalloc(&p, cls));
+    DAS_HIP(traced_malloc(&p, cls, "cache-retry"));
   }
   std::lock_guard<std::mutex> lk(c.mu);
   c.live[p] = {s, cls};
@@ -92,7 +126,7 @@ void cache_free(void* p) {
     if (it == c.live.end()) return;
     const auto key = it->second;
     c.live.erase(it);
-    if (c.cached_bytes + key.second > kCacheBudget) {
+    if (c.cached_bytes + key.second > kCacheBudget && g_hold.load() == 0) {
       drop = p;
     } else {
       c.free_blocks[key].push_back(p);
@@ -100,9 +134,29 @@ void cache_free(void* p) {
     }
   }
   if (drop) {
+    const auto t0 = std::chrono::steady_clock::now();
     (void)hipDeviceSynchronize();   // the block may still be in use by queued work
     (void)hipFree(drop);
+    if (alloc_trace())
+      std::fprintf(stderr, "[das alloc] drop (over budget) %.3f ms\n",
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   }
+}
+
+void cache_hold(bool on) { g_hold += on ? 1 : -1; }
+
+void cache_trim() {
+  Cache& c = cache();
+  std::vector<void*> idle;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto& kv : c.free_blocks) idle.insert(idle.end(), kv.second.begin(), kv.second.end());
+    c.free_blocks.clear();
+    c.cached_bytes = 0;
+  }
+  if (idle.empty()) return;
+  (void)hipDeviceSynchronize();   // idle blocks may still be read by queued work
+  for (void* q : idle) (void)hipFree(q);
 }
 
 void cache_release_stream(hipStream_t s) {

@@ -290,9 +290,42 @@ int das_export_keyspace(das_ctx_t* ctx, const char* dir, uint64_t counts[5]) {
   });
 }
 
+// A build keeps every freed scratch block in the caching allocator (best-fit
+// reuse, no budget) and returns the idle ones to the driver when it ends: its
+// scratch sizes are never reused by queries.
+struct BuildHold {
+  BuildHold() { das::cache_hold(true); }
+  ~BuildHold() {
+    das::cache_hold(false);
+    das::cache_trim();
+  }
+};
+
 int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms) {
   if (!ctx || !atoms) return fail(ctx, DAS_ERR_INVALID, "null argument");
-  return guarded(ctx, [&] { das::build_index(ctx->c, *atoms); });
+  return guarded(ctx, [&] {
+    BuildHold hold;
+    das::build_index(ctx->c, *atoms, 0);
+  });
+}
+
+int das_build_index_ex(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags) {
+  if (!ctx || !atoms) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  if (flags & ~DAS_BUILD_EXPR_ON_DEVICE) return fail(ctx, DAS_ERR_INVALID, "unknown build flags");
+  return guarded(ctx, [&] {
+    BuildHold hold;
+    das::build_index(ctx->c, *atoms, flags);
+  });
+}
+
+int das_synth_powerlaw_links(das_ctx_t* ctx, uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K,
+                             uint32_t n_link_types, uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes,
+                             double s, uint64_t seed) {
+  if (!ctx || (n && !d_child)) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    das::synth_powerlaw_links(d_child, first, n, K, n_link_types, type_leaf0, node_leaf0, n_nodes, s, seed,
+                              ctx->c.s);
+  });
 }
 
 int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out) {
@@ -438,6 +471,14 @@ int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9) {
 
 int das_join(das_ctx_t* ctx, const das_table_t* a, const das_table_t* b, uint32_t no_overload, das_table_t** out) {
   return guarded(ctx, [&] { *out = wrap(das::join(ctx->c, a->t, b->t, (int)no_overload)); });
+}
+
+int das_index_join(das_ctx_t* ctx, const das_table_t* a, const das_link_scan_t* q, das_table_t** out) {
+  if (!ctx || !a || !q || !out) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    auto t = das::index_join(ctx->c, a->t, *q);
+    *out = t ? wrap(std::move(t)) : nullptr;
+  });
 }
 
 int das_antijoin(das_ctx_t* ctx, const das_table_t* a, const das_table_t* t, das_table_t** out) {

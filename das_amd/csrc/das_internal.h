@@ -54,6 +54,7 @@ struct CtypeRange {
 
 struct Index {
   bool built = false;
+  hipStream_t stream = nullptr;  // stream the index arrays were allocated on (caching allocator)
   uint64_t n_atoms = 0, n_nodes = 0, n_links = 0, n_types = 0;
   Digest* digest = nullptr;    // [n_atoms] by id (ids clustered by named type)
   uint32_t* by_digest = nullptr; // [n_atoms] ids in handle (digest) order
@@ -172,7 +173,10 @@ void hash_group(Digest* table, Digest* ctab, const uint32_t* child, const uint64
 void hash_fixed(const Digest* elems, uint32_t k, uint64_t n, Digest* out, hipStream_t s);
 
 // index.hip
-void build_index(Ctx& c, const das_atoms_t& a);
+void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags);
+void synth_powerlaw_links(uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K, uint32_t n_link_types,
+                          uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes, double s, uint64_t seed,
+                          hipStream_t st);
 void free_index(Index& idx);
 void lookup_digests(Ctx& c, const Digest* h_digests, uint64_t n, int64_t* h_ids);
 
@@ -194,6 +198,7 @@ void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_s
 std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q);
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q);
 std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
+std::unique_ptr<Table> index_join(Ctx& c, const Table& a, const das_link_scan_t& q);   // nullptr: not applicable
 std::unique_ptr<Table> antijoin(Ctx& c, const Table& a, const Table& t);
 std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);

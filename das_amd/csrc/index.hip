@@ -142,7 +142,7 @@ template <typename T>
 T* dalloc(Index& idx, uint64_t count) {
   T* p = nullptr;
   if (!count) count = 1;
-  DAS_HIP(hipMalloc((void**)&p, sizeof(T) * count));
+  p = (T*)cache_alloc(sizeof(T) * count, idx.stream);   // best-fit from the build's freed scratch
   idx.owned.push_back(p);
   idx.device_bytes += sizeof(T) * count;
   return p;
@@ -605,20 +605,24 @@ uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hi
 }  // namespace
 
 void free_index(Index& idx) {
-  for (void* p : idx.owned) (void)hipFree(p);
+  for (void* p : idx.owned) cache_free(p);
   idx.owned.clear();
   idx = Index();
 }
 
-void build_index(Ctx& c, const das_atoms_t& a) {
+void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
+  // DAS_BUILD_EXPR_ON_DEVICE: expr_off / expr_child / expr_kind /
+  // expr_ctype_leaf are device pointers (resident input, nothing uploaded)
+  const bool dev_expr = (flags & DAS_BUILD_EXPR_ON_DEVICE) != 0;
   hipStream_t s = c.s;
   free_index(c.idx);
   Index& idx = c.idx;
+  idx.stream = s;
   const uint64_t nl = a.n_leaf, ne = a.n_expr, nu = nl + ne;
   DAS_CHECK(nu > 0 && nu < 0xFFFFFFF0ull, DAS_E_INVALID, "atom count out of range");
   DAS_CHECK(a.n_types < (1u << kTypeBits), DAS_E_UNSUPPORTED, "too many named types");
   const uint64_t n_bytes = a.leaf_off[nl];
-  const uint64_t n_child = a.expr_off[ne];
+  const uint64_t n_child = dev_expr ? (ne ? read_u64(a.expr_off + ne, s) : 0) : a.expr_off[ne];
 
   // host copies for metadata (node names)
   c.leaf_bytes.assign(a.leaf_bytes, a.leaf_bytes + n_bytes);
@@ -634,16 +638,27 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     idx.type_name_len[t] = (uint32_t)(e - b);
   }
 
-  std::optional<ProfScope> up(std::in_place, c, "upload", (double)n_bytes + 8.0 * (nl + ne) + 4.0 * n_child + 13.0 * nl + 5.0 * ne);
+  std::optional<ProfScope> up(std::in_place, c, "upload",
+                              (double)n_bytes + 8.0 * nl + 13.0 * nl + (dev_expr ? 0.0 : 8.0 * ne + 4.0 * n_child + 5.0 * ne));
   auto d_bytes = upload(a.leaf_bytes, n_bytes, s);
   auto d_loff = upload(a.leaf_off, nl + 1, s);
   auto d_lkind = upload(a.leaf_kind, nl, s);
   auto d_lct = upload(a.leaf_ctype, nl, s);
   auto d_ltype = upload(a.leaf_type_id, nl, s);
-  auto d_eoff = upload(a.expr_off, ne + 1, s);
-  auto d_child = upload(a.expr_child, n_child, s);
-  auto d_ekind = upload(a.expr_kind, ne, s);
-  auto d_ectl = upload(a.expr_ctype_leaf, ne, s);
+  DBuf<uint64_t> d_eoff;
+  DBuf<uint32_t> d_child;
+  DBuf<uint8_t> d_ekind;
+  DBuf<int32_t> d_ectl;
+  if (!dev_expr) {
+    d_eoff = upload(a.expr_off, ne + 1, s);
+    d_child = upload(a.expr_child, n_child, s);
+    d_ekind = upload(a.expr_kind, ne, s);
+    d_ectl = upload(a.expr_ctype_leaf, ne, s);
+  }
+  const uint64_t* p_eoff = dev_expr ? a.expr_off : d_eoff.p;
+  const uint32_t* p_child = dev_expr ? a.expr_child : d_child.p;
+  const uint8_t* p_ekind = dev_expr ? a.expr_kind : d_ekind.p;
+  const int32_t* p_ectl = dev_expr ? a.expr_ctype_leaf : d_ectl.p;
   up.reset();
   // device-side build (hash, intern, CSRs, index tables): config 4's timed region
   ProfScope whole(c, "build_device", 0.0);
@@ -658,19 +673,26 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   for (uint32_t g = 0; g < a.n_levels; ++g) {
     const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
     if (e <= b) continue;
-    const uint32_t K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
+    uint32_t K;
+    if (dev_expr) {
+      uint64_t o[2];
+      read_u64x2(a.expr_off + b, s, o);
+      K = (uint32_t)(o[1] - o[0]);
+    } else {
+      K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
+    }
     // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
     ProfScope ps(c, "k_hash_group", (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
-    hash_group(dig.p, ct.p, d_child.p, d_eoff.p, d_ectl.p, nl, b, e - b, K, s);
+    hash_group(dig.p, ct.p, p_child, p_eoff, p_ectl, nl, b, e - b, K, s);
   }
 
   // 2. which unified indices are atoms (nodes, links, link targets)
   DBuf<uint8_t> catl(nu, s);
   DBuf<uint32_t> flag(nu, s);
-  hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)d_ekind.p, nl, ne,
+  hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind, nl, ne,
                      catl.p, flag.p);
-  if (ne) hipLaunchKernelGGL(k_mark_targets, G(ne), dim3(B), 0, s, (const uint8_t*)d_ekind.p, (const uint64_t*)d_eoff.p,
-                             (const uint32_t*)d_child.p, ne, flag.p);
+  if (ne) hipLaunchKernelGGL(k_mark_targets, G(ne), dim3(B), 0, s, (const uint8_t*)p_ekind, (const uint64_t*)p_eoff,
+                             (const uint32_t*)p_child, ne, flag.p);
   DAS_HIP(hipGetLastError());
   DBuf<uint32_t> list;
   const uint64_t nc = compact_flags(flag.p, nu, list, s);
@@ -707,7 +729,7 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     if (n_atoms) {
       hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                          (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
-                         (const uint64_t*)d_eoff.p, (const uint32_t*)d_child.p, a.n_types, tkey.p);
+                         (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, tkey.p);
       iota(perm.p, n_atoms, s);
       radix_sort_pairs<uint32_t>(tkey.p, perm.p, n_atoms, 0, std::max(1, bits_for(a.n_types)), s);
     }
@@ -737,8 +759,8 @@ void build_index(Ctx& c, const das_atoms_t& a) {
   if (n_atoms) {
     hipLaunchKernelGGL(k_fill_atoms, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                        (const uint32_t*)catmax.p, (const Digest*)dig.p, (const Digest*)ct.p, nl,
-                       (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)d_eoff.p,
-                       (const uint32_t*)d_child.p, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf);
+                       (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)p_eoff,
+                       (const uint32_t*)p_child, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf);
     DAS_HIP(hipGetLastError());
   }
   fill_dev(idx.ctype, 0xFF, 4 * (n_atoms ? n_atoms : 1), s);
@@ -750,8 +772,8 @@ void build_index(Ctx& c, const das_atoms_t& a) {
     idx.tgt = dalloc<uint32_t>(idx, total);
     if (n_atoms)
       hipLaunchKernelGGL(k_fill_targets, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
-                         (const uint8_t*)idx.cat, (const uint64_t*)idx.tgt_off, nl, (const uint64_t*)d_eoff.p,
-                         (const uint32_t*)d_child.p, (const uint32_t*)local2id.p, idx.tgt);
+                         (const uint8_t*)idx.cat, (const uint64_t*)idx.tgt_off, nl, (const uint64_t*)p_eoff,
+                         (const uint32_t*)p_child, (const uint32_t*)local2id.p, idx.tgt);
     DAS_HIP(hipGetLastError());
   }
   dig.release(); ct.release(); catl.release(); local2id.release(); catmax.release(); rep.release();

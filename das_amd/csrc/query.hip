@@ -1029,6 +1029,48 @@ std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q) {
 // Direct-address join on a single shared variable; nullptr if the build key
 // range is too sparse for a dense offsets array (caller falls back to sort +
 // binary search).
+// Probe expansion shared by the direct-address join and the index join:
+// probe row r matches the build rows lc[pkey[r] - kmin] = (first, count).
+std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, uint32_t kmin, uint64_t range,
+                                 const uint2* lc, const JoinCols& jc, int nu, const int32_t* uni,
+                                 double build_bytes) {
+  const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
+  const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
+  // tot[units] = 0 (scan sentinel), tot[units + 1] = the largest unit total
+  DBuf<uint64_t> tot(units + 2, c.s), toff(units + 2, c.s);
+  fill_dev(tot.p + units, 0, 16, c.s);
+  {
+    ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
+    hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
+                       lc, units, tot.p);
+    DAS_HIP(hipGetLastError());
+  }
+  exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
+  copy_dev(toff.p + units + 1, tot.p + units + 1, 8, c.s);
+  uint64_t tm[2];
+  read_u64x2(toff.p + units, c.s, tm);
+  const uint64_t total = tm[0];
+  // a unit owning far more outputs than a wave should expand alone (hub
+  // keys) -> output-balanced expansion
+  const char* fb = std::getenv("DAS_DJ_BALANCED");        // tests: force either expansion
+  // ... and so should a probe with a high fan-out everywhere (an index join
+  // of 10^5 anchors x 10^2 links each): its few hundred waves would each
+  // expand thousands of outputs while most of the chip idles
+  const bool fanout = total >= (1ull << 14) && total / kBalChunk > 2 * units;
+  const bool balanced = fb ? fb[0] == '1' : (tm[1] > kHeavyUnit || fanout);
+  auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni, total);
+  out->nrows = total;
+  if (total) {
+    // algorithmic bytes (SURVEY.md §8d): probe payload + build payload + output
+    ProfScope ps(c, balanced ? "k_dj_write_bal" : "k_dj_write",
+                 4.0 * P.nrows * P.ncols + build_bytes + 4.0 * total * nu);
+    dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, lc, units, (const uint64_t*)toff.p, jc,
+             out->data, out->cap, total, balanced);
+    DAS_HIP(hipGetLastError());
+  }
+  return out;
+}
+
 std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32_t var,
                                    const std::vector<int32_t>& uni) {
   auto colof = [](const Table& t, int32_t v) {
@@ -1053,7 +1095,12 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     DAS_HIP(hipStreamSynchronize(c.s));
   }
   const uint64_t range = (uint64_t)h[1] - h[0] + 1;
-  if (range > std::max<uint64_t>(8 * Q.nrows, 1ull << 26) || range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
+  // the key-slot arrays cost ~20 B per slot of streaming work; the sort-merge
+  // alternative costs a log2(|Q|)-step random search per probe row, so a
+  // slot range up to a few times either side's rows still pays (10^9-link
+  // KBs: node ranges of 10^8 ids against 10^8-row probes)
+  if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << 26) ||
+      range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
   const uint32_t kmin = h[0];
   // bucket offsets of the build side: already grouped by key when it comes
@@ -1061,9 +1108,18 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   DBuf<uint32_t> off(range + 1, c.s);
   std::unique_ptr<Table> Qs;
   const Table* Qb = &Q;
-  if (Q.sorted_col == qk) {
+  if (Q.sorted_col == qk && range <= 4 * Q.nrows) {
     ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * range);
     hipLaunchKernelGGL(k_bucket_bounds, G(range + 1), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, off.p);
+    DAS_HIP(hipGetLastError());
+  } else if (Q.sorted_col == qk) {
+    // sparse keys over a wide range: a histogram + scan beats a binary
+    // search per slot, and sorted rows need no scatter
+    DBuf<uint32_t> cnt(range + 1, c.s);
+    ProfScope ps(c, "join_build", 4.0 * Q.nrows + 8.0 * range);
+    fill_dev(cnt.p, 0, 4 * (range + 1), c.s);
+    hipLaunchKernelGGL(k_key_hist, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, cnt.p);
+    exclusive_scan<uint32_t>(cnt.p, range + 1, off.p, c.s);
     DAS_HIP(hipGetLastError());
   } else {
     DBuf<uint32_t> cnt(range + 1, c.s);
@@ -1090,35 +1146,157 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   hipLaunchKernelGGL(k_pack_lc, dim3(grid_for(range, B, 2048)), dim3(B), 0, c.s, (const uint32_t*)off.p,
                      (uint32_t)range, lc.p);
   DAS_HIP(hipGetLastError());
-  const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
-  const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
-  // tot[units] = 0 (scan sentinel), tot[units + 1] = the largest unit total
-  DBuf<uint64_t> tot(units + 2, c.s), toff(units + 2, c.s);
-  fill_dev(tot.p + units, 0, 16, c.s);
+  auto out = dj_expand(c, P, pkey, kmin, range, lc.p, jc, nu, uni.data(), 4.0 * Q.nrows * Q.ncols);
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Index (nested-loop) join: And's join of a bound table A with a Link whose
+// join variable sits at an indexed position p.  Instead of scanning the
+// Link's whole type segment and joining, every row of A looks its key up in
+// P_{a,p} (one binary search over the unique (type, t_p) keys) and expands
+// that contiguous row range: the same rows as join(A, scan_link(q)) -- each
+// range holds exactly the links of that type with t_p = key -- at a cost
+// proportional to A and the output, not to the Link's type segment.
+// ---------------------------------------------------------------------------
+struct IjGround {
+  const uint32_t* col[kMaxArity];   // P_{a,p} columns of grounded targets, in the table's secondary order
+  uint32_t val[kMaxArity];
+  int n;
+};
+
+__global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, uint64_t n, uint64_t thi,
+                                             const uint64_t* __restrict__ ukey, const uint64_t* __restrict__ uoff,
+                                             uint64_t nkeys, IjGround g, uint2* __restrict__ lc,
+                                             uint32_t* __restrict__ rowid) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = thi | key[i];
+    uint64_t lo = 0, hi = nkeys;                 // lower_bound
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (ukey[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    uint2 e = make_uint2(0u, 0u);
+    if (lo < nkeys && ukey[lo] == k) {
+      uint32_t b = (uint32_t)uoff[lo], end = (uint32_t)uoff[lo + 1];
+      // grounded targets that lead the range's secondary order: the rows
+      // equal to each value form a sub-range, found by two binary searches
+      for (int j = 0; j < g.n && b < end; ++j) {
+        const uint32_t* col = g.col[j];
+        const uint32_t v = g.val[j];
+        uint32_t l = b, h = end;
+        while (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
+        uint32_t l2 = l, h2 = end;
+        while (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if (col[m] <= v) l2 = m + 1; else h2 = m; }
+        b = l;
+        end = l2;
+      }
+      if (end > b) e = make_uint2(b, end - b);
+    }
+    lc[i] = e;
+    rowid[i] = (uint32_t)i;
+  }
+}
+
+std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+  Index& idx = c.idx;
+  DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
+  const uint32_t ar = q.arity;
+  if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
+      ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
+    return nullptr;
+  auto colof = [](const Table& t, int32_t v) {
+    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+    return -1;
+  };
+  // one bound position; every other position a fresh, distinct variable or
+  // a grounded target that leads P_{a,p}'s secondary order
+  int bp = -1;
+  std::vector<std::pair<int32_t, uint32_t>> fresh;   // (var, position)
+  for (uint32_t p = 0; p < ar; ++p) {
+    if (q.target[p] != kNone) {
+      if (q.var[p] >= 0) return nullptr;
+      continue;
+    }
+    if (q.var[p] < 0) return nullptr;
+    if (colof(A, q.var[p]) >= 0) {
+      if (bp >= 0) return nullptr;
+      bp = (int)p;
+    } else {
+      for (auto& f : fresh) if (f.first == q.var[p]) return nullptr;
+      fresh.push_back({q.var[p], p});
+    }
+  }
+  if (bp < 0) return nullptr;
+  const PosIndex& PI = idx.pidx[ar][bp];
+  IjGround g{};
   {
-    ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
-    hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
-                       (const uint2*)lc.p, units, tot.p);
+    bool prefix = true;                          // still inside the grounded prefix
+    for (uint32_t p = 0; p < ar; ++p) {
+      if ((int)p == bp) continue;
+      if (q.target[p] != kNone) {
+        if (!prefix) return nullptr;             // a grounded target after a free one: rows not contiguous
+        g.col[g.n] = PI.t.col(1 + (int)p);
+        g.val[g.n++] = q.target[p];
+      } else {
+        prefix = false;
+      }
+    }
+  }
+  // cost: a search per row of A against a scan of the Link's type segment
+  {
+    const char* f = std::getenv("DAS_INDEX_JOIN");          // tests: 1 always, 0 never
+    if (f && f[0] == '0') return nullptr;
+    const uint64_t seg = idx.type_off[ar].size() > q.type_id + 1
+                             ? idx.type_off[ar][q.type_id + 1] - idx.type_off[ar][q.type_id] : 0;
+    // (with grounded targets the scan reads one key range, of unknown size
+    // here: index-join only small probes)
+    const bool cheap = g.n == 0 ? 4 * A.nrows <= seg : A.nrows <= (1ull << 20);
+    if (!(f && f[0] == '1') && !cheap) return nullptr;
+  }
+  DAS_CHECK(PI.t.rows < 0xFFFFFFFFull, DAS_E_UNSUPPORTED, "index join: P table too large");
+  // output schema: A's variables and the fresh ones, ascending
+  std::vector<int32_t> uni(A.vars, A.vars + A.ncols);
+  for (auto& f : fresh) uni.push_back(f.first);
+  std::sort(uni.begin(), uni.end());
+  DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
+  const int nu = (int)uni.size();
+  if (A.nrows == 0 || PI.nkeys == 0) return new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), 0);
+  JoinCols jc{};
+  for (int k = 0; k < nu; ++k) {
+    const int ia = colof(A, uni[k]);
+    if (ia >= 0) { jc.p[jc.np] = A.col(ia); jc.po[jc.np++] = k; continue; }
+    for (auto& f : fresh)
+      if (f.first == uni[k]) { jc.b[jc.nb] = PI.t.col(1 + (int)f.second); jc.bo[jc.nb++] = k; }
+  }
+  DBuf<uint2> lc(A.nrows, c.s);
+  DBuf<uint32_t> rowid(A.nrows, c.s);
+  {
+    ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
+    hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, (const uint32_t*)A.col(colof(A, q.var[bp])), A.nrows,
+                       (uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys, g,
+                       lc.p, rowid.p);
     DAS_HIP(hipGetLastError());
   }
-  exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
-  copy_dev(toff.p + units + 1, tot.p + units + 1, 8, c.s);
-  uint64_t tm[2];
-  read_u64x2(toff.p + units, c.s, tm);
-  const uint64_t total = tm[0];
-  // a unit owning far more outputs than a wave should expand alone (hub
-  // keys) -> output-balanced expansion
-  const char* fb = std::getenv("DAS_DJ_BALANCED");        // tests: force either expansion
-  const bool balanced = fb ? fb[0] == '1' : tm[1] > kHeavyUnit;
-  auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
-  out->nrows = total;
-  if (total) {
-    // algorithmic bytes (SURVEY.md §8d): probe payload + build payload + output
-    ProfScope ps(c, balanced ? "k_dj_write_bal" : "k_dj_write",
-                 4.0 * P.nrows * P.ncols + 4.0 * Q.nrows * Q.ncols + 4.0 * total * nu);
-    dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, (const uint2*)lc.p, units, (const uint64_t*)toff.p, jc,
-             out->data, out->cap, total, balanced);
-    DAS_HIP(hipGetLastError());
+  // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
+  auto out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, jc, nu, uni.data(), 0.0);
+  out->sorted_col = A.sorted_col >= 0 ? colof(*out, A.vars[A.sorted_col]) : -1;
+  const uint32_t ncol = ar + 1;
+  const auto& tb = idx.tbound[ar];
+  for (int k = 0; k < nu; ++k) {
+    const int ia = colof(A, uni[k]);
+    if (ia >= 0) {
+      out->lo[k] = A.lo[ia];
+      out->hi[k] = A.hi[ia];
+      continue;
+    }
+    out->lo[k] = 0;
+    out->hi[k] = kNone;
+    for (auto& f : fresh)
+      if (f.first == uni[k] && (uint64_t)(q.type_id + 1) * ncol * 2 <= tb.size()) {
+        out->lo[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2];
+        out->hi[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2 + 1];
+      }
   }
   return out;
 }

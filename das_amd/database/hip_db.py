@@ -489,6 +489,30 @@ class HipDB(RelationalDB):
                 out.append(self.ctx.join(ta, tb, CONFIG['no_overload']))
         return Relation(out)
 
+    def rel_index_join(self, acc, link_type, handles, var_ids):
+        """And's join of the running relation with one ordered Link term
+        through the pattern index (das_index_join): the rows of
+        rel_join(acc, match_link(...)) without scanning the term.  None when
+        it does not apply to every table of acc (the caller scans + joins)."""
+        if link_type in UNORDERED_LINK_TYPES or not acc.tables:
+            return None
+        ttype = self._type_or_empty(link_type)
+        if ttype is None or ttype is False:
+            return None
+        tids = self._target_ids(list(handles))
+        if tids is None:
+            return None
+        var = [v if v is not None else -1 for v in var_ids]
+        out = []
+        for t in acc.tables:
+            if t.kind != _lib.TABLE_ORDERED:
+                return None
+            r = self.ctx.index_join(t, len(handles), ttype, tids, var)
+            if r is None:
+                return None
+            out.append(r)
+        return Relation(out)
+
     def rel_antijoin(self, rel, forbidden):
         """check_negation of every row against every forbidden row (:741-746)."""
         tables = rel.tables

@@ -542,6 +542,20 @@ class Link(Atom):
         return found
 
 
+    def _index_join(self, db, acc):
+        """rel_join(acc, this term's relation) through the pattern index, or
+        None when the shape does not allow it (And.matched scans instead)."""
+        if not self.ordered or CONFIG['no_overload'] or not hasattr(db, 'rel_index_join'):
+            return None
+        if not all(isinstance(t, Variable) or type(t) is Node for t in self.targets):
+            return None
+        if any(isinstance(t, TypedVariable) for t in self.targets):
+            return None
+        handles = [t.get_handle(db) for t in self.targets]
+        var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in self.targets]
+        return db.rel_index_join(acc, self.atom_type, handles, var_ids)
+
+
 class Variable(Atom):
 
     def __init__(self, variable_name: str):
@@ -672,6 +686,15 @@ class And(LogicalExpression):
         acc = None
         forbidden = []
         for term in self.terms:
+            if acc is not None and isinstance(term, Link) and db.rel_nonempty(acc):
+                # index join (das_index_join): the term's rows are looked up
+                # from the running result's keys instead of scanned; an empty
+                # result takes the scan path, which tells a failing term
+                # (And -> False) from an empty join (reset-on-empty)
+                rel = term._index_join(db, acc)
+                if rel is not None and db.rel_nonempty(rel):
+                    acc = rel
+                    continue
             sub = PatternMatchingAnswer()
             if not term.matched(db, sub):
                 return False

@@ -288,3 +288,119 @@ def similarity_kb(n_nodes=300, n_inh=1200, n_sim=600, n_set=200, seed=SEED):
         [("Concept", "c", n_nodes)],
         [("Inheritance", inh), ("Similarity", sim), ("Set", st)])
     return arrays
+
+
+def numbered_leaves(prefix, n):
+    """Leaf bytes + offsets of the n strings prefix + str(i), i = 0..n-1.
+    The numbers with d digits are one contiguous run of fixed-length strings,
+    written as the columns of a (count, len) view (no per-string objects)."""
+    pre = np.frombuffer(prefix.encode(), dtype=np.uint8)
+    P = len(pre)
+    nd = np.ones(n, dtype=np.uint64)
+    p = 10
+    while p <= max(n - 1, 0):
+        nd[p:] += 1
+        p *= 10
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(nd + np.uint64(P), out=off[1:])
+    buf = np.empty(int(off[-1]), dtype=np.uint8)
+    lo, d = 0, 1
+    while lo < n:
+        hi = min(n, 10 ** d)
+        L = P + d
+        view = buf[int(off[lo]):int(off[hi])].reshape(hi - lo, L)
+        view[:, :P] = pre
+        q = np.arange(lo, hi, dtype=np.uint32)
+        for k in range(d - 1, -1, -1):
+            view[:, P + k] = q % 10 + 48
+            q //= 10
+        lo, d = hi, d + 1
+    return buf, off
+
+
+class DeviceAtomArrays(AtomArrays):
+    """AtomArrays whose expression arrays (expr_off / expr_child / expr_kind /
+    expr_ctype_leaf) are torch tensors resident on a GPU; the leaves stay on
+    the host (node names are read back from them).  `HipDB.load_arrays`
+    builds it through das_build_index_ex(DAS_BUILD_EXPR_ON_DEVICE)."""
+    expr_on_device = True
+
+    def __init__(self, leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start,
+                 expr_off, expr_child, expr_kind, expr_ctype_leaf, level_off, type_names):
+        super().__init__(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start,
+                         np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint8),
+                         np.zeros(0, np.int32), level_off, type_names)
+        self.expr_off, self.expr_child, self.expr_kind, self.expr_ctype_leaf = \
+            expr_off, expr_child, expr_kind, expr_ctype_leaf
+
+    @property
+    def n_expr(self):
+        return int(self.expr_off.numel()) - 1
+
+    def drop_expr(self):
+        """Frees the device expression arrays once the index is built (the
+        index keeps everything queries need; leaves stay for node names)."""
+        import torch
+        dev = self.expr_off.device
+        self._n_expr = self.n_expr
+        self.expr_off = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.expr_child = torch.zeros(0, dtype=torch.int32, device=dev)
+        self.expr_kind = torch.zeros(0, dtype=torch.uint8, device=dev)
+        self.expr_ctype_leaf = torch.zeros(0, dtype=torch.int32, device=dev)
+
+    def to_host(self):
+        """The same KB as host AtomArrays (tests: host-input build parity)."""
+        return AtomArrays(self.leaf_bytes, self.leaf_off, self.leaf_kind, self.leaf_ctype, self.leaf_type_id,
+                          self.name_start, self.expr_off.cpu().numpy().view(np.uint64),
+                          self.expr_child.cpu().numpy().view(np.uint32), self.expr_kind.cpu().numpy(),
+                          self.expr_ctype_leaf.cpu().numpy(), self.level_off, self.type_names)
+
+
+def powerlaw_kb_device(ctx, n_nodes, n_links, frac_arity2=0.7, link_types=4, seed=SEED, s=1.1,
+                       first=0, count=None, own=None, device=0):
+    """Configs 4-5 shape generated on the GPU (das_synth_powerlaw_links):
+    global links 0 .. n2-1 have arity 2, n2 .. n_links-1 arity 3 (n2 =
+    frac_arity2 * n_links); link i's type and Zipf(s) targets are a hash of
+    (seed, i).  This call materialises links [first, first+count); with
+    `own=(lo, hi)` only links lo..hi-1 get index rows (kind 1), the rest are
+    directory-only (kind 3, the multi-GPU layout of parallel.shard_arrays).
+    Nodes are the terminals "Concept n<i>"; link types T0..T{link_types-1}."""
+    import torch
+    count = n_links - first if count is None else count
+    end = first + count
+    n2 = int(n_links * frac_arity2)
+    r2 = (min(max(first, 0), n2), min(end, n2))
+    r3 = (max(first, n2), max(end, n2))
+    c2, c3 = r2[1] - r2[0], r3[1] - r3[0]
+    names = [f"T{i}" for i in range(link_types)] + ["Concept"]
+    n_types = len(names)
+    nb, noff = numbered_leaves("Concept n", n_nodes)
+    tb = [t.encode() for t in names]
+    tlen = np.array([len(t) for t in tb], dtype=np.uint64)
+    leaf_bytes = np.concatenate([np.frombuffer(b"".join(tb), np.uint8), nb])
+    leaf_off = np.concatenate([np.concatenate([[0], np.cumsum(tlen)]).astype(np.uint64),
+                               noff[1:] + np.uint64(tlen.sum())])
+    leaf_kind = np.concatenate([np.full(n_types, LEAF_TYPE, np.uint8), np.full(n_nodes, LEAF_NODE, np.uint8)])
+    leaf_ctype = np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, n_types - 1, np.uint32)])
+    leaf_type_id = np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, NONE, np.uint32)])
+    name_start = np.concatenate([np.zeros(n_types, np.uint32), np.full(n_nodes, len("Concept") + 1, np.uint32)])
+    dev = torch.device("cuda", device)
+    child = torch.empty(3 * c2 + 4 * c3, dtype=torch.int32, device=dev)
+    if c2:
+        ctx.synth_powerlaw_links(child[:3 * c2], r2[0], c2, 3, link_types, 0, n_types, n_nodes, s, seed)
+    if c3:
+        ctx.synth_powerlaw_links(child[3 * c2:], r3[0], c3, 4, link_types, 0, n_types, n_nodes, s, seed)
+    ne = c2 + c3
+    eoff = torch.empty(ne + 1, dtype=torch.int64, device=dev)
+    eoff[:c2 + 1] = torch.arange(c2 + 1, dtype=torch.int64, device=dev) * 3
+    if c3:
+        eoff[c2 + 1:] = 3 * c2 + torch.arange(1, c3 + 1, dtype=torch.int64, device=dev) * 4
+    kind = torch.ones(ne, dtype=torch.uint8, device=dev)
+    if own is not None:
+        gid = torch.cat([torch.arange(r2[0], r2[1], device=dev), torch.arange(r3[0], r3[1], device=dev)])
+        kind[(gid < own[0]) | (gid >= own[1])] = 3
+        del gid
+    ctl = torch.full((ne,), -1, dtype=torch.int32, device=dev)
+    level_off = np.array([0, c2, ne], dtype=np.uint64)
+    return DeviceAtomArrays(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start,
+                            eoff, child, kind, ctl, level_off, names)

@@ -130,7 +130,23 @@ typedef struct {
  * Mongo insert + key-value files + sort + Redis SADD of canonical_parser.py:
  * 111-240).  Rebuilds from scratch if called again. */
 int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms);
+/* Same build from a KB whose expressions are already resident in HBM: with
+ * DAS_BUILD_EXPR_ON_DEVICE, expr_off / expr_child / expr_kind / expr_ctype_leaf
+ * are device pointers on ctx's device (read, not copied, not freed); the leaf
+ * arrays and level_off stay host arrays.  flags 0 = das_build_index. */
+#define DAS_BUILD_EXPR_ON_DEVICE 1u
+int das_build_index_ex(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags);
 int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out);
+
+/* ---- synthetic input (bench / tests) ---------- */
+/* Writes n links of K-1 targets (K = 3 or 4 u32 per row: type leaf, then node
+ * leaves) into device memory d_child, for global link indices first ..
+ * first+n-1: type leaf = type_leaf0 + h % n_link_types, targets = node_leaf0 +
+ * Zipf(s) rank over n_nodes, every field a counter-based hash of (seed, index),
+ * so any split of the index range reproduces the same KB. */
+int das_synth_powerlaw_links(das_ctx_t* ctx, uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K,
+                             uint32_t n_link_types, uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes,
+                             double s, uint64_t seed);
 
 /* digests -> atom ids (-1 if absent); cat: 0 other, 1 node, 2 link. */
 int das_lookup(das_ctx_t* ctx, const uint32_t* digests, uint64_t n, int64_t* ids,
@@ -192,6 +208,13 @@ int das_scan_type(das_ctx_t* ctx, uint32_t type_id, das_table_t** out9);
  * algebra (:203-209, :316-351) -> DAS_TABLE_COMPOSITE. */
 int das_join(das_ctx_t* ctx, const das_table_t* a, const das_table_t* b, uint32_t no_overload,
              das_table_t** out);
+/* And's join of `a` with one Link term, evaluated through the pattern index
+ * instead of a scan of the term: equal to das_join(a, das_scan_link(q)) when
+ * it applies -- `a` ordered, q ordered and typed, arity <= 3, exactly one
+ * target variable bound by `a`, every other target a fresh distinct variable,
+ * no link column.  Each row of `a` looks its key up in P_{arity,p} and
+ * expands that row range.  *out = NULL (status 0) when it does not apply. */
+int das_index_join(das_ctx_t* ctx, const das_table_t* a, const das_link_scan_t* q, das_table_t** out);
 /* Rows of `a` that pass check_negation against every row of `t` (:112-117,
  * :211-217, :353-362; And.matched :741-746). */
 int das_antijoin(das_ctx_t* ctx, const das_table_t* a, const das_table_t* t, das_table_t** out);

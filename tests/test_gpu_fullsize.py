@@ -1,6 +1,6 @@
 """Parity at BASELINE.json's full sizes through size-independent properties:
 the bench workloads' binding counts (config 2 bio at 20 M Member links,
-config 5 hub at 3 M links) against closed-form counts computed with numpy
+config 5 hub at 10^9 links generated in HBM) against closed-form counts (numpy / torch)
 from the generator's own arrays (distinct-pair joins as degree sums), so a
 wrong row anywhere in a 10^7-10^8-row join changes the count."""
 import numpy as np
@@ -61,28 +61,46 @@ def test_gpu_bio_fullsize_counts():
         assert _count(db, spec) == want[name], name
 
 
+def _dev_pairs(arrays, k):
+    """Distinct (t0, t1) leaf-index pairs (as t0 << 32 | t1, int64 on the GPU)
+    of the arity-2 links of type T<k> in a device-generated KB."""
+    import torch
+    c2 = int(arrays.level_off[1])
+    ch = arrays.expr_child[:3 * c2].view(-1, 3)
+    sel = ch[:, 0] == k
+    key = (ch[sel, 1].to(torch.int64) << 32) | ch[sel, 2].to(torch.int64)
+    return torch.unique(key)
+
+
 def test_gpu_hub_fullsize_counts():
+    """Config 5 at BASELINE size (10^9 links generated in HBM): the bench's
+    hub queries against semi-join closed forms over the generator's arrays."""
     import bench
+    import torch
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
-    n_nodes = 1 << 21
-    arrays = synthetic.powerlaw_kb(n_nodes, 3_000_000, link_types=4)
+    n_nodes, n_links = 1 << 27, 1_000_000_000
     db = HipDB(device=0)
+    arrays = synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links)
     db.load_arrays(arrays)
     base = len(arrays.type_names)
-    t = _pairs(arrays, "T0")
-    src, dst = t >> 32, t & 0xFFFFFFFF
-    outdeg = np.bincount(src, minlength=base + n_nodes)
     h0, h1 = base, base + 1
-    v1 = src[dst == h0]
-    is_v1 = np.zeros(base + n_nodes, bool)
-    is_v1[v1] = True
-    is_v2 = np.zeros(base + n_nodes, bool)
-    is_v2[src[dst == h1]] = True
-    mid = is_v1[src] & is_v2[dst]                    # T(V1,V2) with T(V1,h0) and T(V2,h1)
+    pairs = {k: _dev_pairs(arrays, k) for k in range(4)}
+    arrays.drop_expr()
+    src = {k: (p >> 32) for k, p in pairs.items()}
+    dst = {k: (p & 0xFFFFFFFF) for k, p in pairs.items()}
+
+    def member(k, h):
+        m = torch.zeros(base + n_nodes, dtype=torch.bool, device="cuda")
+        m[src[k][dst[k] == h]] = True
+        return m
+    s1 = member(0, h0)
+    s23 = member(2, h1) & member(3, h0)
+    in1 = s1[src[1]]
     want = {
-        "H4 T(V1,h0) T(V1,V2) T(V2,h1) T(V2,V3)": int(outdeg[dst[mid]].sum()),
-        "H2 T(V1,h0) T(V1,V2)": int(outdeg[v1].sum()),
+        "H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)": int((in1 & s23[dst[1]]).sum()),
+        "H2 T0(V1,h0) T1(V1,V2)": int(in1.sum()),
     }
+    assert want["H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)"] > 10_000_000
     for name, spec in bench.hub_specs():
         assert _count(db, spec) == want[name], name

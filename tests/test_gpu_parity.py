@@ -422,10 +422,16 @@ def test_gpu_hub_four_clause_matches_oracle():
     """Config 5: the 4-clause hub And of bench.py --workload hub."""
     import bench
     from das_amd import synthetic
-    arrays = synthetic.powerlaw_kb(200, 1500, link_types=2, seed=5)
+    arrays = synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
     db = _hipdb(arrays)
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
-    for name, q in bench.hub_specs():
+    n = lambda i: ["Node", "Concept", f"n{i}"]  # noqa: E731
+    V = bench._V
+    # plus the unanchored 4-clause chain (hub out-degree expansion in the last clause)
+    chain = ("T0(V1,h0) T0(V1,V2) T0(V2,h1) T0(V2,V3)",
+             ["And", [bench._L("T0", V("V1"), n(0)), bench._L("T0", V("V1"), V("V2")),
+                      bench._L("T0", V("V2"), n(1)), bench._L("T0", V("V2"), V("V3"))]])
+    for name, q in bench.hub_specs() + [chain]:
         want = O.evaluate(q, odb)
         got = record(q, db)
         assert want.get("n", 0) > 0, name
@@ -508,3 +514,38 @@ def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
     want = O.keyspace_lines(O.KB.from_arrays(arrays))
     for name, lines in want.items():
         assert _read_lines(tmp_path / f"{name}.txt") == lines, name
+
+
+# ------------------------------------------------------------ index join
+
+@pytest.mark.parametrize("mode", ["1", "0"])
+@pytest.mark.parametrize("gen", ["bio", "powerlaw", "flybase"])
+def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
+    """And with das_index_join forced on every eligible term (1) and never
+    (0): the same answers as the oracle, incl. grounded-prefix terms
+    (FlyBase Execution(Schema s, V, V)), hub keys and empty joins that fall
+    back to the scan path (reset-on-empty)."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_INDEX_JOIN", mode)
+    if gen == "bio":
+        arrays = synthetic.bio_kb(300, 120, 3000, seed=8)
+    elif gen == "powerlaw":
+        arrays = synthetic.powerlaw_kb(400, 6000, link_types=4, seed=8)
+    else:
+        arrays = synthetic.flybase_kb(200, 6, 400, n_loc=20, n_do=15, seed=3)
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    rng = np.random.default_rng(23)
+    qs = [] if gen == "flybase" else _random_queries(rng, arrays, 40)
+    if gen == "flybase":
+        for gene in (0, 7, 11):
+            qs += [q for _, q in bench.flybase_specs(gene, synthetic.flybase_do_terms(arrays, gene))]
+    if gen == "powerlaw":
+        qs += [q for _, q in bench.hub_specs()]
+    if gen == "bio":
+        qs += [q for _, q in bench.bio_specs(np.arange(300))]
+    for q in qs:
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
