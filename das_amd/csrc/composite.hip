@@ -459,9 +459,7 @@ std::unique_ptr<Table> theta_join(Ctx& c, const Table& A, const Table& Bt, int n
                        (const uint32_t*)cnt.p, n.p);
     DAS_HIP(hipGetLastError());
   }
-  fill_dev(n.p + A.nrows, 0, 8, c.s);
-  exclusive_scan<uint64_t>(n.p, A.nrows + 1, off.p, c.s);
-  const uint64_t total = read_u64(off.p + A.nrows, c.s);
+  const uint64_t total = scan_total<uint64_t>(SpanIn<uint64_t>{n.p}, A.nrows, off.p, c.s);
   auto out = new_table(c, DAS_TABLE_COMPOSITE, nout, vars, total, member);
   out->nrows = total;
   for (int k = 0; k < nout; ++k) {

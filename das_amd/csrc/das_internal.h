@@ -45,6 +45,11 @@ struct PosIndex {
   uint64_t nkeys = 0;
   uint64_t* ukey = nullptr;   // sorted unique (type << 32 | t_p)
   uint64_t* uoff = nullptr;   // nkeys + 1 row offsets
+  // Dense key directory per type (index joins): dir[ty][t - dir_lo[ty]] =
+  // the index of key (ty, t) in ukey, or kNone; built where the type's t_p
+  // span is at most 2x its key count (else dir[ty] == nullptr: binary search).
+  std::vector<uint32_t*> dir;
+  std::vector<uint32_t> dir_lo, dir_n;
 };
 
 struct CtypeRange {

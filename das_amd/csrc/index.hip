@@ -17,6 +17,8 @@
 // per named type.  This covers exactly the families the reference writes for arity
 // 1..3 (canonical_parser.py:148-176); arity >= 4 only has [*, e0..en].
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <optional>
 #include "das_internal.h"
 #include "md5.h"
@@ -79,26 +81,52 @@ Slot& slot() {
   return s;
 }
 
-void read_words(const PubArgs& a, hipStream_t s, uint32_t* out) {
+}  // namespace
+
+PubSlot pub_reserve() {
   Slot& sl = slot();
   const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;      // never 0 (the initial value)
-  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, a, sl.p, seq);
-  DAS_HIP(hipGetLastError());
+  return PubSlot{sl.p, seq};
+}
+
+void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
   for (uint64_t it = 1;; ++it) {
-    if (__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq) break;
+    if (__atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq) break;
     if ((it & 255) == 0) {
       const hipError_t e = hipStreamQuery(s);
       if (e == hipSuccess) {
-        if (__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq) break;
+        if (__atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq) break;
         DAS_HIP(hipStreamSynchronize(s));
-        DAS_CHECK(__atomic_load_n(&sl.p[15], __ATOMIC_ACQUIRE) == seq, DAS_E_INTERNAL, "read-back slot not written");
+        DAS_CHECK(__atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq, DAS_E_INTERNAL, "read-back slot not written");
         break;
       }
       if (e != hipErrorNotReady) DAS_HIP(e);
     }
     __builtin_ia32_pause();
   }
-  for (uint32_t i = 0; i < a.n; ++i) out[i] = __atomic_load_n(&sl.p[i], __ATOMIC_RELAXED);
+  for (uint32_t i = 0; i < n; ++i) out[i] = __atomic_load_n(&ps.p[i], __ATOMIC_RELAXED);
+}
+
+ScanCtr& scan_ctr(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, ScanCtr> m;
+  int dev = 0;
+  DAS_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = m.find({dev, s});
+  if (it != m.end()) return it->second;
+  ScanCtr c{nullptr, 0};
+  DAS_HIP(hipMalloc((void**)&c.p, 64));
+  DAS_HIP(hipMemsetAsync(c.p, 0, 64, s));
+  return m.emplace(std::make_pair(dev, s), c).first->second;
+}
+
+namespace {
+void read_words(const PubArgs& a, hipStream_t s, uint32_t* out) {
+  const PubSlot ps = pub_reserve();
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, a, ps.p, ps.seq);
+  DAS_HIP(hipGetLastError());
+  pub_wait(ps, s, out, a.n);
 }
 }  // namespace
 
@@ -604,10 +632,66 @@ uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hi
 
 }  // namespace
 
+namespace {
+// Per type ty: first/last key index of (ty, *) in the sorted unique keys and
+// their t_p values -> out[4 ty .. 4 ty + 3] = {klo, khi, tmin, tmax}.
+__global__ void k_type_key_bounds(const uint64_t* ukey, uint64_t nkeys, uint32_t ntypes, uint64_t* out) {
+  const uint32_t ty = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ty >= ntypes) return;
+  uint64_t b[2];
+  for (int e = 0; e < 2; ++e) {
+    const uint64_t q = (uint64_t)(ty + e) << 32;
+    uint64_t lo = 0, hi = nkeys;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (ukey[mid] < q) lo = mid + 1; else hi = mid;
+    }
+    b[e] = lo;
+  }
+  out[4 * ty] = b[0];
+  out[4 * ty + 1] = b[1];
+  out[4 * ty + 2] = b[1] > b[0] ? (uint32_t)ukey[b[0]] : 0;
+  out[4 * ty + 3] = b[1] > b[0] ? (uint32_t)ukey[b[1] - 1] : 0;
+}
+__global__ void k_dir_scatter(const uint64_t* ukey, uint64_t klo, uint64_t n, uint32_t tlo, uint32_t* dir) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dir[(uint32_t)ukey[klo + i] - tlo] = (uint32_t)(klo + i);
+}
+}  // namespace
+
 void free_index(Index& idx) {
   for (void* p : idx.owned) cache_free(p);
   idx.owned.clear();
   idx = Index();
+}
+
+void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
+  const uint32_t nt = (uint32_t)idx.n_types;
+  P.dir.assign(nt, nullptr);
+  P.dir_lo.assign(nt, 0);
+  P.dir_n.assign(nt, 0);
+  if (!P.nkeys || !nt || P.nkeys >= 0xFFFFFFFFull) return;
+  DBuf<uint64_t> kb(4ull * nt, s);
+  hipLaunchKernelGGL(k_type_key_bounds, dim3((nt + 63) / 64), dim3(64), 0, s, (const uint64_t*)P.ukey, P.nkeys, nt,
+                     kb.p);
+  DAS_HIP(hipGetLastError());
+  std::vector<uint64_t> hb(4ull * nt);
+  DAS_HIP(hipMemcpyAsync(hb.data(), kb.p, 32ull * nt, hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  for (uint32_t ty = 0; ty < nt; ++ty) {
+    const uint64_t klo = hb[4 * ty], khi = hb[4 * ty + 1], tmin = hb[4 * ty + 2], tmax = hb[4 * ty + 3];
+    if (khi <= klo) continue;
+    const uint64_t span = tmax - tmin + 1;
+    if (span > 2 * (khi - klo) + 4096) continue;
+    uint32_t* d = dalloc<uint32_t>(idx, span);
+    fill_dev(d, 0xFF, 4 * span, s);
+    hipLaunchKernelGGL(k_dir_scatter, dim3(grid_for(khi - klo, 256, 8192)), dim3(256), 0, s, (const uint64_t*)P.ukey,
+                       klo, khi - klo, (uint32_t)tmin, d);
+    DAS_HIP(hipGetLastError());
+    P.dir[ty] = d;
+    P.dir_lo[ty] = (uint32_t)tmin;
+    P.dir_n[ty] = (uint32_t)span;
+  }
 }
 
 void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
@@ -950,6 +1034,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, P.t.ld, ar,
                            (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, P.t.data);
         P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
+        build_key_dir(P, idx, s);
       }
     }
     DAS_HIP(hipGetLastError());

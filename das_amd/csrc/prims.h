@@ -160,6 +160,162 @@ void exclusive_scan(const T* in, uint64_t n, T* out, hipStream_t s) {
   exclusive_scan_fn<T>(PtrIn<T>{in}, n, out, s);
 }
 
+// ---------------------------------------------------------------------------
+// Exclusive scan whose total reaches the host without extra launches.
+// `scan_total` writes out[0..n] (out[n] = total) and returns {total, max of
+// in()}: the reduce pass's last block to finish (an acq_rel ticket on a
+// per-stream counter) scans the tile sums in place and publishes total and
+// max straight into the pinned read-back slot, then the tile pass runs while
+// the host spins.  Two launches and one round trip per count -> size step,
+// where scan + copy + publish took five.
+// ---------------------------------------------------------------------------
+struct PubSlot {
+  uint32_t* p;      // pinned, coherent host words 0..15 (15 = sequence)
+  uint32_t seq;
+};
+PubSlot pub_reserve();
+void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
+// Per-(device, stream) completion counter of the reduce pass; `base` = its
+// value before the next launch (the host advances it by the launch's tiles).
+struct ScanCtr {
+  unsigned long long* p;
+  uint64_t base;
+};
+ScanCtr& scan_ctr(hipStream_t s);
+
+// Called by every thread of one block: lanes < n store w[lane], then the
+// sequence number is released (system scope) after them.
+__device__ __forceinline__ void pub_store(uint32_t* slot, uint32_t seq, const uint32_t* w, int n) {
+  if ((int)threadIdx.x < n) __hip_atomic_store(&slot[threadIdx.x], w[threadIdx.x], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename T>
+__device__ __forceinline__ void block_sum_max(T& sum, uint64_t& mx, T* s_sum, uint64_t* s_mx) {
+  sum = wave_reduce_sum(sum);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+  if (__lane_id() == 0) { s_sum[threadIdx.x >> 6] = sum; s_mx[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  sum = 0;
+  mx = 0;
+  for (int w = 0; w < kScanBlock / 64; ++w) { sum += s_sum[w]; mx = s_mx[w] > mx ? s_mx[w] : mx; }
+  __syncthreads();
+}
+
+// One block scans rows [0, n) of `in` into out (block loop with carry),
+// accumulating the max; used for n <= one tile and for the tile sums.
+template <typename T, typename In>
+__device__ __forceinline__ void block_scan_loop(In in, uint64_t n, T* out, T& total, uint64_t& mx, T* s_wave,
+                                                uint64_t* s_mx) {
+  const int wave = threadIdx.x >> 6;
+  T carry = 0;
+  uint64_t m = 0;
+  for (uint64_t base = 0; base < n; base += kScanBlock) {
+    const uint64_t i = base + threadIdx.x;
+    const T x = i < n ? (T)in(i) : (T)0;
+    m = (uint64_t)x > m ? (uint64_t)x : m;
+    const T inc = wave_inclusive_scan(x);
+    if (__lane_id() == 63) s_wave[wave] = inc;
+    __syncthreads();
+    T pre = carry;
+    for (int w = 0; w < wave; ++w) pre += s_wave[w];
+    if (i < n) out[i] = pre + inc - x;
+    for (int w = 0; w < kScanBlock / 64; ++w) carry += s_wave[w];
+    __syncthreads();
+  }
+  T dummy = 0;
+  block_sum_max(dummy, m, s_wave, s_mx);
+  total = carry;
+  mx = m;
+}
+
+template <typename T, typename In>
+__global__ void __launch_bounds__(kScanBlock) k_scan_single_pub(In in, uint64_t n, T* out, uint32_t* slot,
+                                                               uint32_t seq) {
+  __shared__ T s_wave[kScanBlock / 64];
+  __shared__ uint64_t s_mx[kScanBlock / 64];
+  T total;
+  uint64_t mx;
+  block_scan_loop<T>(in, n, out, total, mx, s_wave, s_mx);
+  if (threadIdx.x == 0) out[n] = total;
+  const uint64_t t64 = (uint64_t)total;
+  const uint32_t w[4] = {(uint32_t)t64, (uint32_t)(t64 >> 32), (uint32_t)mx, (uint32_t)(mx >> 32)};
+  pub_store(slot, seq, w, 4);
+}
+
+template <typename T>
+struct SpanIn {
+  const T* p;
+  __device__ __forceinline__ T operator()(uint64_t i) const { return p[i]; }
+};
+
+template <typename T, typename In>
+__global__ void __launch_bounds__(kScanBlock) k_scan_reduce_pub(In in, uint64_t n, T* tsum, uint64_t* tmax,
+                                                               uint64_t tiles, unsigned long long* ctr,
+                                                               unsigned long long last, T* out, uint32_t* slot,
+                                                               uint32_t seq) {
+  __shared__ T s_sum[kScanBlock / 64];
+  __shared__ uint64_t s_mx[kScanBlock / 64];
+  __shared__ int s_last;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  T acc = 0;
+  uint64_t m = 0;
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    if (i < n) {
+      const T x = (T)in(i);
+      acc += x;
+      m = (uint64_t)x > m ? (uint64_t)x : m;
+    }
+  }
+  block_sum_max(acc, m, s_sum, s_mx);
+  if (threadIdx.x == 0) {
+    tsum[blockIdx.x] = acc;
+    tmax[blockIdx.x] = m;
+    const unsigned long long t =
+        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the other tiles' sums
+  T total;
+  uint64_t mx;
+  block_scan_loop<T>(SpanIn<T>{tsum}, tiles, tsum, total, mx, s_sum, s_mx);   // in place, element-wise
+  uint64_t mx2 = 0;
+  for (uint64_t i = threadIdx.x; i < tiles; i += kScanBlock) mx2 = tmax[i] > mx2 ? tmax[i] : mx2;
+  T dummy = 0;
+  block_sum_max(dummy, mx2, s_sum, s_mx);
+  if (threadIdx.x == 0) out[n] = total;
+  const uint64_t t64 = (uint64_t)total;
+  const uint32_t w[4] = {(uint32_t)t64, (uint32_t)(t64 >> 32), (uint32_t)mx2, (uint32_t)(mx2 >> 32)};
+  pub_store(slot, seq, w, 4);
+}
+
+template <typename In>
+struct Bounded {
+  In in;
+  uint64_t n;
+  __device__ __forceinline__ auto operator()(uint64_t i) const -> decltype(in(i)) { return i < n ? in(i) : 0; }
+};
+
+template <typename T, typename In>
+__global__ void k_max_of(In in, uint64_t n, unsigned long long* mx) {
+  uint64_t m = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    m = (uint64_t)in(i) > m ? (uint64_t)in(i) : m;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(m, d, 64); m = o > m ? o : m; }
+  if (__lane_id() == 0 && m) atomicMax(mx, (unsigned long long)m);
+}
+
+constexpr uint64_t kPubMaxTiles = 1u << 15;   // tile sums the last block scans alone
+
 // Device-to-device copy of `bytes` (a multiple of 4) as a kernel: the
 // runtime's copy path costs far more host time per call than a launch.
 __global__ void k_copy_u32(uint32_t* dst, const uint32_t* src, uint64_t n);
@@ -326,5 +482,47 @@ uint64_t read_u64(const uint64_t* d, hipStream_t s);
 uint32_t read_u32(const uint32_t* d, hipStream_t s);
 void read_u64x2(const uint64_t* d, hipStream_t s, uint64_t out[2]);   // d[0], d[1] in one round trip
 void read_u32x2(const uint32_t* d0, const uint32_t* d1, hipStream_t s, uint32_t out[2]);
+
+template <typename T, typename In>
+uint64_t scan_total(In in, uint64_t n, T* out, hipStream_t s, uint64_t* max_out = nullptr) {
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  uint32_t w[4];
+  if (tiles <= 1) {
+    const PubSlot ps = pub_reserve();
+    hipLaunchKernelGGL((k_scan_single_pub<T, In>), dim3(1), dim3(kScanBlock), 0, s, in, n, out, ps.p, ps.seq);
+    DAS_HIP(hipGetLastError());
+    pub_wait(ps, s, w, 4);
+  } else if (tiles <= kPubMaxTiles) {
+    DBuf<T> tsum(tiles, s);
+    DBuf<uint64_t> tmax(tiles, s);
+    ScanCtr& ct = scan_ctr(s);
+    const PubSlot ps = pub_reserve();
+    hipLaunchKernelGGL((k_scan_reduce_pub<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n, tsum.p,
+                       tmax.p, tiles, ct.p, (unsigned long long)(ct.base + tiles - 1), out, ps.p, ps.seq);
+    DAS_HIP(hipGetLastError());
+    ct.base += tiles;
+    hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n,
+                       (const T*)tsum.p, out);
+    DAS_HIP(hipGetLastError());
+    pub_wait(ps, s, w, 4);
+  } else {
+    exclusive_scan_fn<T>(Bounded<In>{in, n}, n + 1, out, s);
+    DBuf<uint64_t> m(2, s);
+    uint64_t r[2];
+    if (max_out) {
+      fill_dev(m.p + 1, 0, 8, s);
+      hipLaunchKernelGGL((k_max_of<T, In>), dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, in, n,
+                         (unsigned long long*)(m.p + 1));
+      DAS_HIP(hipGetLastError());
+    }
+    copy_dev(m.p, out + n, sizeof(T), s);
+    if (sizeof(T) == 4) fill_dev(reinterpret_cast<uint32_t*>(m.p) + 1, 0, 4, s);
+    read_u64x2(m.p, s, r);
+    w[0] = (uint32_t)r[0]; w[1] = (uint32_t)(r[0] >> 32);
+    w[2] = max_out ? (uint32_t)r[1] : 0u; w[3] = max_out ? (uint32_t)(r[1] >> 32) : 0u;
+  }
+  if (max_out) *max_out = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+}
 
 }  // namespace das

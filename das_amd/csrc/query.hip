@@ -259,6 +259,75 @@ __global__ void k_cartesian(OutMap om, uint64_t nb, uint64_t total, uint32_t* ou
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row hash sets (Not / Or / dedup without sorting): open addressing, linear
+// probing, slots hold row indices (kEmpty = free), insert-only so a slot
+// never returns to free and every tuple owns exactly one slot.  Row equality
+// compares the full tuples, so the result is exact whatever the hash.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t hs_mix(uint32_t h) {   // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t row_hash(const ColSet& k, uint64_t i) {
+  uint32_t h = 0x2545f491u;
+  for (int c = 0; c < k.n; ++c) h = hs_mix(h ^ (k.c[c][i] + 0x9e3779b9u * (uint32_t)(c + 1)));
+  return h;
+}
+__device__ __forceinline__ bool rows_equal(const ColSet& a, uint64_t i, const ColSet& b, uint64_t j) {
+  for (int c = 0; c < a.n; ++c)
+    if (a.c[c][i] != b.c[c][j]) return false;
+  return true;
+}
+__device__ __forceinline__ uint32_t slot_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Inserts rows [0, n); with `keep_min` the slot ends holding the smallest
+// index of its tuple (the first occurrence).
+__global__ void k_hset_insert(ColSet k, uint64_t n, uint32_t* tab, uint32_t mask, int keep_min) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t h = row_hash(k, i) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+      uint32_t cur = slot_load(&tab[h]);
+      if (cur == kEmpty) {
+        cur = atomicCAS(&tab[h], kEmpty, (uint32_t)i);
+        if (cur == kEmpty) break;
+      }
+      if (rows_equal(k, cur, k, i)) {
+        if (keep_min) atomicMin(&tab[h], (uint32_t)i);
+        break;
+      }
+    }
+  }
+}
+// keep[i] = row i is its tuple's first occurrence
+__global__ void k_hset_first(ColSet k, uint64_t n, const uint32_t* tab, uint32_t mask, uint32_t* keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t h = row_hash(k, i) & mask, f = 0;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+      const uint32_t cur = tab[h];
+      if (cur == kEmpty) break;                     // (unreachable: row i was inserted)
+      if (rows_equal(k, cur, k, i)) { f = cur == (uint32_t)i; break; }
+    }
+    keep[i] = f;
+  }
+}
+// keep[i] = probe row i (columns in the set's order) is NOT in the set of `t`
+__global__ void k_hset_anti(ColSet a, uint64_t n, ColSet t, const uint32_t* tab, uint32_t mask, uint32_t* keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t h = row_hash(a, i) & mask, k = 1;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+      const uint32_t cur = tab[h];
+      if (cur == kEmpty) break;
+      if (rows_equal(t, cur, a, i)) { k = 0; break; }
+    }
+    keep[i] = k;
+  }
+}
+
 // keep[i] = 0 if a matching row exists in `sorted`
 __global__ void k_anti_flags(ColSet probe, uint64_t np, ColSet sorted, uint64_t ns, uint32_t* keep) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -391,6 +460,52 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
+// Expands outputs [rs, re) of one 64-row group (relative to the group's first
+// output, written at obase + o): output o belongs to the max lane l with
+// pre[l] <= o and is build row ex[l] + (o - pre[l]).  kXUnroll rounds of 64
+// outputs are resolved first and their build loads issued together, so a
+// wave keeps several loads in flight instead of one load -> store round trip
+// per 64 outputs.
+constexpr int kXUnroll = 4;
+template <int NP, int NB, typename T>
+__device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, const uint32_t* pv,
+                                             const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
+                                             uint64_t obase, int lane) {
+  for (T o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+    T o[kXUnroll];
+    int l[kXUnroll];
+    uint32_t br[kXUnroll];
+#pragma unroll
+    for (int u = 0; u < kXUnroll; ++u) {
+      o[u] = o0 + (T)(u * 64 + lane);
+      int ll = 0;                                            // owner: max lane with pre <= o
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const T pl = (T)__shfl(pre, ll + step, 64);
+        if (ll + step < 64 && pl <= o[u]) ll += step;
+      }
+      l[u] = ll;
+      br[u] = lane_get(ex, ll) + (uint32_t)(o[u] - (T)__shfl(pre, ll, 64));
+    }
+    uint32_t bv[kXUnroll][NB > 0 ? NB : 1];
+#pragma unroll
+    for (int u = 0; u < kXUnroll; ++u)
+#pragma unroll
+      for (int i = 0; i < NB; ++i) bv[u][i] = o[u] < re ? bb[i][br[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < kXUnroll; ++u) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const uint32_t v = lane_get(pv[i], l[u]);
+        if (o[u] < re) po[i][obase + o[u]] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (o[u] < re) bo[i][obase + o[u]] = bv[u][i];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
                                                 const uint2* lc, uint64_t units, uint64_t* unit_tot) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
@@ -408,12 +523,7 @@ __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t n
     for (int g = 0; g < kXGroups; ++g)
       if (d[g] < range) acc += lc[d[g]].y;
     acc = wave_reduce_sum(acc);
-    if (lane == 0) {
-      unit_tot[u] = acc;
-      // only "is any unit heavy" is needed: skip the (same-address) atomic
-      // for ordinary units
-      if (acc > kHeavyUnit) atomicMax((unsigned long long*)&unit_tot[units + 1], (unsigned long long)acc);
-    }
+    if (lane == 0) unit_tot[u] = acc;      // the scan also yields the largest unit
   }
 }
 
@@ -466,26 +576,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
       const T inc = wave_inclusive_scan(c);
       const T tot = (T)__shfl(inc, 63, 64);
       const T pre = inc - c;                                 // this lane's first output
-      for (T o0 = 0; o0 < tot; o0 += 64) {
-        const T o = o0 + (T)lane;
-        int l = 0;                                           // owner: max lane with pre <= o
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-          const T pl = (T)__shfl(pre, l + step, 64);
-          if (l + step < 64 && pl <= o) l += step;
-        }
-        const bool act = o < tot;
-        const uint32_t j = (uint32_t)(o - (T)__shfl(pre, l, 64));
-        const uint32_t br = lane_get(e[g].x, l) + j;
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const uint32_t v = lane_get(pv[g][i], l);
-          if (act) po[i][base + o] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-          if (act) bo[i][base + o] = bb[i][br];
-      }
+      expand_group<NP, NB, T>((T)0, tot, pre, e[g].x, pv[g], bb, po, bo, base, lane);
       base += tot;
     }
   }
@@ -552,26 +643,7 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
         uint32_t pv[NP > 0 ? NP : 1];
 #pragma unroll
         for (int i = 0; i < NP; ++i) pv[i] = r < np ? pp[i][r] : 0u;
-        for (T o0 = rs; o0 < re; o0 += 64) {
-          const T o = o0 + (T)lane;
-          int l = 0;
-#pragma unroll
-          for (int step = 32; step >= 1; step >>= 1) {
-            const T pl = (T)__shfl(pre, l + step, 64);
-            if (l + step < 64 && pl <= o) l += step;
-          }
-          const bool act = o < re;
-          const uint32_t j = (uint32_t)(o - (T)__shfl(pre, l, 64));
-          const uint32_t br = lane_get(e[g].x, l) + j;
-#pragma unroll
-          for (int i = 0; i < NP; ++i) {
-            const uint32_t v = lane_get(pv[i], l);
-            if (act) po[i][gb + o] = v;
-          }
-#pragma unroll
-          for (int i = 0; i < NB; ++i)
-            if (act) bo[i][gb + o] = bb[i][br];
-        }
+        expand_group<NP, NB, T>(rs, re, pre, e[g].x, pv, bb, po, bo, gb, lane);
       }
     }
   }
@@ -665,8 +737,7 @@ std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* kee
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
   DBuf<uint32_t> scan(n + 1, c.s);
-  exclusive_scan_fn<uint32_t>(FlagIn{keep, n}, n + 1, scan.p, c.s);   // scan[n] = kept rows
-  const uint64_t m = read_u32(scan.p + n, c.s);
+  const uint64_t m = scan_total<uint32_t>(FlagIn{keep, n}, n, scan.p, c.s);   // scan[n] = kept rows
   if (m == n) {   // nothing dropped: copy
     auto t = new_table_like(c, a, n);
     t->nrows = n;
@@ -780,16 +851,13 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
     DAS_HIP(hipGetLastError());
     return t;
   }
-  DBuf<uint32_t> cnt(chunks, c.s), off(chunks, c.s);
+  DBuf<uint32_t> cnt(chunks, c.s), off(chunks + 1, c.s);
   {
     ProfScope ps(c, "k_scan_count", 4.0 * n * sp.arity);
     hipLaunchKernelGGL(k_scan_count, dim3((unsigned)chunks), dim3(B), 0, c.s, sp, begin, end, cnt.p);
     DAS_HIP(hipGetLastError());
   }
-  exclusive_scan<uint32_t>(cnt.p, chunks, off.p, c.s);
-  uint32_t h[2];
-  read_u32x2(off.p + chunks - 1, cnt.p + chunks - 1, c.s, h);
-  const uint64_t m = (uint64_t)h[0] + h[1];
+  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{cnt.p}, chunks, off.p, c.s);
   auto t = new_table(c, kind, ncols, vars, m);
   t->nrows = m;
   if (m) {
@@ -1036,19 +1104,15 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
                                  double build_bytes) {
   const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
   const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
-  // tot[units] = 0 (scan sentinel), tot[units + 1] = the largest unit total
-  DBuf<uint64_t> tot(units + 2, c.s), toff(units + 2, c.s);
-  fill_dev(tot.p + units, 0, 16, c.s);
+  DBuf<uint64_t> tot(units, c.s), toff(units + 1, c.s);
   {
     ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
     hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
                        lc, units, tot.p);
     DAS_HIP(hipGetLastError());
   }
-  exclusive_scan<uint64_t>(tot.p, units + 1, toff.p, c.s);
-  copy_dev(toff.p + units + 1, tot.p + units + 1, 8, c.s);
   uint64_t tm[2];
-  read_u64x2(toff.p + units, c.s, tm);
+  tm[0] = scan_total<uint64_t>(SpanIn<uint64_t>{tot.p}, units, toff.p, c.s, &tm[1]);   // toff[units] = total
   const uint64_t total = tm[0];
   // a unit owning far more outputs than a wave should expand alone (hub
   // keys) -> output-balanced expansion
@@ -1167,17 +1231,30 @@ struct IjGround {
 
 __global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, uint64_t n, uint64_t thi,
                                              const uint64_t* __restrict__ ukey, const uint64_t* __restrict__ uoff,
-                                             uint64_t nkeys, IjGround g, uint2* __restrict__ lc,
+                                             uint64_t nkeys, const uint32_t* __restrict__ dir, uint32_t dlo,
+                                             uint32_t dn, IjGround g, uint2* __restrict__ lc,
                                              uint32_t* __restrict__ rowid) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = thi | key[i];
-    uint64_t lo = 0, hi = nkeys;                 // lower_bound
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (ukey[mid] < k) lo = mid + 1; else hi = mid;
+    const uint32_t t = key[i];
+    const uint64_t k = thi | t;
+    uint64_t lo;
+    bool hit;
+    if (dir) {                                   // dense directory: one load
+      const uint32_t d = t - dlo;
+      const uint32_t j = d < dn ? dir[d] : 0xFFFFFFFFu;
+      lo = j;
+      hit = j != 0xFFFFFFFFu;
+    } else {                                     // lower_bound
+      uint64_t l = 0, h = nkeys;
+      while (l < h) {
+        const uint64_t mid = (l + h) >> 1;
+        if (ukey[mid] < k) l = mid + 1; else h = mid;
+      }
+      lo = l;
+      hit = lo < nkeys && ukey[lo] == k;
     }
     uint2 e = make_uint2(0u, 0u);
-    if (lo < nkeys && ukey[lo] == k) {
+    if (hit) {
       uint32_t b = (uint32_t)uoff[lo], end = (uint32_t)uoff[lo + 1];
       // grounded targets that lead the range's secondary order: the rows
       // equal to each value form a sub-range, found by two binary searches
@@ -1271,11 +1348,14 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
   }
   DBuf<uint2> lc(A.nrows, c.s);
   DBuf<uint32_t> rowid(A.nrows, c.s);
+  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !std::getenv("DAS_NO_KEY_DIR");
+  const uint32_t* dir = use_dir ? PI.dir[q.type_id] : nullptr;
+  const uint32_t dlo = use_dir ? PI.dir_lo[q.type_id] : 0, dn = use_dir ? PI.dir_n[q.type_id] : 0;
   {
     ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
     hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, (const uint32_t*)A.col(colof(A, q.var[bp])), A.nrows,
-                       (uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys, g,
-                       lc.p, rowid.p);
+                       (uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
+                       (const uint32_t*)dir, dlo, dn, g, lc.p, rowid.p);
     DAS_HIP(hipGetLastError());
   }
   // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
@@ -1360,8 +1440,7 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       hipLaunchKernelGGL(k_join_count, G(P.nrows), dim3(B), 0, c.s, pk, P.nrows, qks, Qs->nrows, lo.p, cnt.p);
       DAS_HIP(hipGetLastError());
     }
-    exclusive_scan_fn<uint64_t>(WidenCnt{cnt.p, P.nrows}, P.nrows + 1, offs.p, c.s);
-    const uint64_t total = read_u64(offs.p + P.nrows, c.s);
+    const uint64_t total = scan_total<uint64_t>(WidenCnt{cnt.p, P.nrows}, P.nrows, offs.p, c.s);
     out = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), total);
     out->nrows = total;
     if (total) {
@@ -1409,6 +1488,18 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
   return out;
 }
 
+// Hash sets below 2^26 rows (a table of <= 2^28 slots); DAS_SET_SORT=1 forces
+// the sort-based path (tests cover both).
+bool use_hash_set(uint64_t n) {
+  const char* f = std::getenv("DAS_SET_SORT");
+  return n <= (1ull << 26) && !(f && f[0] == '1');
+}
+uint32_t hset_mask(uint64_t n) {
+  uint64_t m = 1024;
+  while (m < 2 * n) m <<= 1;
+  return (uint32_t)(m - 1);
+}
+
 std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
   if (A.kind != DAS_TABLE_ORDERED || T.kind != DAS_TABLE_ORDERED) return theta_antijoin(c, A, T);
   std::vector<int32_t> va(A.vars, A.vars + A.ncols), vt(T.vars, T.vars + T.ncols);
@@ -1423,6 +1514,23 @@ std::unique_ptr<Table> antijoin(Ctx& c, const Table& A, const Table& T) {
     return -1;
   };
   ColSet tk = cols_of(T);
+  if (use_hash_set(T.nrows)) {
+    ColSet ak{};
+    ak.n = T.ncols;
+    for (int k = 0; k < T.ncols; ++k) ak.c[k] = A.col(colof(A, T.vars[k]));
+    const uint32_t mask = hset_mask(T.nrows);
+    DBuf<uint32_t> tab((uint64_t)mask + 1, c.s), keep(A.nrows, c.s);
+    fill_dev(tab.p, 0xFF, 4ull * (mask + 1), c.s);
+    hipLaunchKernelGGL(k_hset_insert, G(T.nrows), dim3(B), 0, c.s, tk, T.nrows, tab.p, mask, 0);
+    DAS_HIP(hipGetLastError());
+    {
+      ProfScope ps(c, "k_hset_anti", 4.0 * A.nrows * (T.ncols + 1));
+      hipLaunchKernelGGL(k_hset_anti, G(A.nrows), dim3(B), 0, c.s, ak, A.nrows, tk, (const uint32_t*)tab.p, mask,
+                         keep.p);
+      DAS_HIP(hipGetLastError());
+    }
+    return compact_table(c, A, keep.p);
+  }
   DBuf<uint32_t> perm(T.nrows, c.s);
   sort_perm(tk, T.nrows, perm.p, id_bits(c), c.s);
   auto Ts = gather_table(c, T, perm.p, T.nrows);
@@ -1447,6 +1555,21 @@ std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
     DBuf<uint32_t> idx(A.nrows ? A.nrows : 1, c.s);
     iota(idx.p, A.nrows, c.s);
     return gather_table(c, A, idx.p, A.nrows);
+  }
+  if (use_hash_set(A.nrows)) {
+    // first occurrences, in input order (the input's row order is kept)
+    const uint32_t mask = hset_mask(A.nrows);
+    DBuf<uint32_t> tab((uint64_t)mask + 1, c.s), keep(A.nrows, c.s);
+    fill_dev(tab.p, 0xFF, 4ull * (mask + 1), c.s);
+    hipLaunchKernelGGL(k_hset_insert, G(A.nrows), dim3(B), 0, c.s, cols_of(A), A.nrows, tab.p, mask, 1);
+    DAS_HIP(hipGetLastError());
+    {
+      ProfScope ps(c, "k_hset_first", 4.0 * A.nrows * (A.ncols + 1));
+      hipLaunchKernelGGL(k_hset_first, G(A.nrows), dim3(B), 0, c.s, cols_of(A), A.nrows, (const uint32_t*)tab.p, mask,
+                         keep.p);
+      DAS_HIP(hipGetLastError());
+    }
+    return compact_table(c, A, keep.p);
   }
   DBuf<uint32_t> perm(A.nrows, c.s);
   sort_perm(cols_of(A), A.nrows, perm.p, id_bits(c), c.s);

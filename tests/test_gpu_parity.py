@@ -174,9 +174,14 @@ def _random_queries(rng, arrays, n):
     return qs
 
 
+@pytest.mark.parametrize("sets", ["hash", "sort"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw"])
-def test_gpu_synthetic_matches_oracle(gen):
+def test_gpu_synthetic_matches_oracle(gen, sets, monkeypatch):
+    """Random Link / And / Or / Not queries; Or's dedup and Not's anti-join
+    through the row hash sets and through the sort-based path."""
     from das_amd import synthetic
+    if sets == "sort":
+        monkeypatch.setenv("DAS_SET_SORT", "1")
     if gen == "bio":
         arrays = synthetic.bio_kb(300, 120, 3000, seed=7)
     else:
@@ -403,10 +408,14 @@ def test_gpu_incoming_sets_synthetic():
         assert set(db.get_incoming_links(h)) == want.get(h, set()), h
 
 
-def test_gpu_flybase_queries_match_oracle():
+@pytest.mark.parametrize("sets", ["hash", "sort"])
+def test_gpu_flybase_queries_match_oracle(sets, monkeypatch):
     """Config 3: the QueryFlyBase.ipynb And / And+Not / Or shapes (bench.py
-    --workload flybase) on a small FlyBase-shaped KB, every gene anchor."""
+    --workload flybase) on a small FlyBase-shaped KB, every gene anchor;
+    set operations through hash sets and through sorting."""
     import bench
+    if sets == "sort":
+        monkeypatch.setenv("DAS_SET_SORT", "1")
     from das_amd import synthetic
     arrays = synthetic.flybase_kb(200, 6, 400, n_loc=20, n_do=15, seed=3)
     db = _hipdb(arrays)
@@ -518,16 +527,19 @@ def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
 
 # ------------------------------------------------------------ index join
 
-@pytest.mark.parametrize("mode", ["1", "0"])
+@pytest.mark.parametrize("mode", ["1", "1-bsearch", "0"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw", "flybase"])
 def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
-    """And with das_index_join forced on every eligible term (1) and never
-    (0): the same answers as the oracle, incl. grounded-prefix terms
-    (FlyBase Execution(Schema s, V, V)), hub keys and empty joins that fall
-    back to the scan path (reset-on-empty)."""
+    """And with das_index_join forced on every eligible term (1: keys found
+    through the dense per-type key directory; 1-bsearch: by binary search
+    over the unique keys) and never (0): the same answers as the oracle,
+    incl. grounded-prefix terms (FlyBase Execution(Schema s, V, V)), hub
+    keys and empty joins that fall back to the scan path (reset-on-empty)."""
     import bench
     from das_amd import synthetic
-    monkeypatch.setenv("DAS_INDEX_JOIN", mode)
+    monkeypatch.setenv("DAS_INDEX_JOIN", mode[0])
+    if mode == "1-bsearch":
+        monkeypatch.setenv("DAS_NO_KEY_DIR", "1")
     if gen == "bio":
         arrays = synthetic.bio_kb(300, 120, 3000, seed=8)
     elif gen == "powerlaw":
