@@ -314,7 +314,31 @@ __global__ void k_max_of(In in, uint64_t n, unsigned long long* mx) {
   if (__lane_id() == 0 && m) atomicMax(mx, (unsigned long long)m);
 }
 
-constexpr uint64_t kPubMaxTiles = 1u << 15;   // tile sums the last block scans alone
+constexpr uint64_t kPubMaxTiles = 1024;   // tile sums the last block scans alone (4 block rounds)
+
+// Per-tile sum and max (the multi-level path of scan_total).
+template <typename T, typename In>
+__global__ void __launch_bounds__(kScanBlock) k_scan_reduce_mx(In in, uint64_t n, T* tsum, uint64_t* tmax) {
+  __shared__ T s_sum[kScanBlock / 64];
+  __shared__ uint64_t s_mx[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  T acc = 0;
+  uint64_t m = 0;
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    if (i < n) {
+      const T x = (T)in(i);
+      acc += x;
+      m = (uint64_t)x > m ? (uint64_t)x : m;
+    }
+  }
+  block_sum_max(acc, m, s_sum, s_mx);
+  if (threadIdx.x == 0) {
+    tsum[blockIdx.x] = acc;
+    tmax[blockIdx.x] = m;
+  }
+}
 
 // Device-to-device copy of `bytes` (a multiple of 4) as a kernel: the
 // runtime's copy path costs far more host time per call than a launch.
@@ -506,20 +530,25 @@ uint64_t scan_total(In in, uint64_t n, T* out, hipStream_t s, uint64_t* max_out 
     DAS_HIP(hipGetLastError());
     pub_wait(ps, s, w, 4);
   } else {
-    exclusive_scan_fn<T>(Bounded<In>{in, n}, n + 1, out, s);
-    DBuf<uint64_t> m(2, s);
-    uint64_t r[2];
+    // multi-level: tile sums (and maxima), scanned by this function, then
+    // the tile pass; the total reaches the host through the inner scan
+    DBuf<T> tsum(tiles, s), toff(tiles + 1, s);
+    DBuf<uint64_t> tmax(tiles, s);
+    hipLaunchKernelGGL((k_scan_reduce_mx<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n, tsum.p,
+                       tmax.p);
+    DAS_HIP(hipGetLastError());
+    uint64_t mx = 0;
+    const uint64_t total = scan_total<T>(SpanIn<T>{tsum.p}, tiles, toff.p, s, nullptr);
+    hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n,
+                       (const T*)toff.p, out);
+    DAS_HIP(hipGetLastError());
+    copy_dev(out + n, toff.p + tiles, sizeof(T), s);
     if (max_out) {
-      fill_dev(m.p + 1, 0, 8, s);
-      hipLaunchKernelGGL((k_max_of<T, In>), dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, in, n,
-                         (unsigned long long*)(m.p + 1));
-      DAS_HIP(hipGetLastError());
+      DBuf<uint64_t> tm(tiles + 1, s);
+      scan_total<uint64_t>(SpanIn<uint64_t>{tmax.p}, tiles, tm.p, s, &mx);
     }
-    copy_dev(m.p, out + n, sizeof(T), s);
-    if (sizeof(T) == 4) fill_dev(reinterpret_cast<uint32_t*>(m.p) + 1, 0, 4, s);
-    read_u64x2(m.p, s, r);
-    w[0] = (uint32_t)r[0]; w[1] = (uint32_t)(r[0] >> 32);
-    w[2] = max_out ? (uint32_t)r[1] : 0u; w[3] = max_out ? (uint32_t)(r[1] >> 32) : 0u;
+    w[0] = (uint32_t)total; w[1] = (uint32_t)(total >> 32);
+    w[2] = (uint32_t)mx; w[3] = (uint32_t)(mx >> 32);
   }
   if (max_out) *max_out = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
   return (uint64_t)w[0] | ((uint64_t)w[1] << 32);

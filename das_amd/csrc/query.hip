@@ -16,6 +16,7 @@
 // order (deterministic) and no global atomics sit on the hot path.
 #include <algorithm>
 #include <cstdlib>
+#include <optional>
 
 #include "das_internal.h"
 
@@ -732,23 +733,112 @@ std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx,
   return t;
 }
 
-// keep flags -> compacted table
-std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep) {
+// ---------------------------------------------------------------------------
+// Stream compaction by a row predicate, order kept: per-tile counts -> scan
+// of the tile counts (its total sizes the output; one read-back) -> each
+// tile re-evaluates the predicate, ranks its rows with wave scans and writes
+// the kept rows' columns straight to their slots.  No per-row scan or index
+// array goes through HBM.
+// ---------------------------------------------------------------------------
+// The tile's predicates are evaluated for all kScanItems rounds at once, on
+// clamped (always valid) row indices, so their loads are issued together
+// instead of one dependent round trip per round.
+template <typename Pred>
+__device__ __forceinline__ uint32_t tile_flags(const Pred& pred, uint64_t base, uint64_t n) {
+  bool f[kScanItems];
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    f[r] = pred(i < n ? i : n - 1) && i < n;
+  }
+  uint32_t bits = 0;
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) bits |= (f[r] ? 1u : 0u) << r;
+  return bits;
+}
+
+template <typename Pred>
+__global__ void __launch_bounds__(kScanBlock) k_tile_count(Pred pred, uint64_t n, uint32_t* tcnt) {
+  __shared__ uint32_t s[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  uint32_t acc = __popc(tile_flags(pred, base, n));
+  acc = wave_reduce_sum(acc);
+  if (__lane_id() == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+template <typename Pred>
+__global__ void __launch_bounds__(kScanBlock) k_compact_rows(Pred pred, uint64_t n, const uint32_t* __restrict__ toff,
+                                                             ColSet src, uint32_t* __restrict__ out, uint64_t cap) {
+  constexpr int W = kScanBlock / 64;
+  __shared__ uint32_t s_wave[kScanItems][W];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t bits = tile_flags(pred, base, n);
+  uint32_t inc[kScanItems];
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    inc[r] = wave_incl_sum_u32((bits >> r) & 1u);
+    if (__lane_id() == 63) s_wave[r][wave] = inc[r];
+  }
+  __syncthreads();
+  uint32_t carry = toff[blockIdx.x], o[kScanItems];
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    uint32_t pre = carry, all = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      pre += w < wave ? s_wave[r][w] : 0u;
+      all += s_wave[r][w];
+    }
+    o[r] = pre + inc[r] - 1;
+    carry += all;
+  }
+  // column by column, the kept rows' loads of all rounds in flight together
+  for (int k = 0; k < src.n; ++k) {
+    const uint32_t* col = src.c[k];
+    uint32_t v[kScanItems];
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r)
+      v[r] = ((bits >> r) & 1u) ? col[base + (uint64_t)r * kScanBlock + threadIdx.x] : 0u;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r)
+      if ((bits >> r) & 1u) out[(uint64_t)k * cap + o[r]] = v[r];
+  }
+}
+
+struct FlagPred {
+  const uint32_t* keep;
+  __device__ __forceinline__ bool operator()(uint64_t i) const { return keep[i] != 0; }
+};
+
+template <typename Pred>
+std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const char* prof = nullptr,
+                                    double pred_bytes = 4.0) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
-  DBuf<uint32_t> scan(n + 1, c.s);
-  const uint64_t m = scan_total<uint32_t>(FlagIn{keep, n}, n, scan.p, c.s);   // scan[n] = kept rows
-  if (m == n) {   // nothing dropped: copy
-    auto t = new_table_like(c, a, n);
-    t->nrows = n;
-    for (int k = 0; k < a.ncols; ++k)
-      copy_dev(t->col(k), a.col(k), 4 * n, c.s);
-    return t;
-  }
-  DBuf<uint32_t> idx(m ? m : 1, c.s);
-  hipLaunchKernelGGL(k_compact_index_q, G(n), dim3(B), 0, c.s, keep, (const uint32_t*)scan.p, n, idx.p);
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  DAS_CHECK(tiles < (1ull << 31), DAS_E_UNSUPPORTED, "compaction: too many rows");
+  DBuf<uint32_t> tcnt(tiles, c.s), toff(tiles + 1, c.s);
+  hipLaunchKernelGGL((k_tile_count<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n, tcnt.p);
   DAS_HIP(hipGetLastError());
-  return gather_table(c, a, idx.p, m);
+  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{tcnt.p}, tiles, toff.p, c.s);
+  auto t = new_table_like(c, a, m);
+  t->nrows = m;
+  if (m && a.ncols) {
+    std::optional<ProfScope> ps;
+    if (prof) ps.emplace(c, prof, pred_bytes * n + 8.0 * a.ncols * m);
+    hipLaunchKernelGGL((k_compact_rows<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n,
+                       (const uint32_t*)toff.p, cols_of(a), t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return t;
+}
+
+// keep flags -> compacted table
+std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep) {
+  return compact_pred(c, a, FlagPred{keep});
 }
 
 void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_sorted, uint64_t nb, uint32_t* lo,
@@ -1381,6 +1471,66 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
   return out;
 }
 
+// ---------------------------------------------------------------------------
+// Semi-join: the build side Q holds only the join variable.  When its keys
+// are distinct (a typed Link with one variable and grounded other targets:
+// each row is a different link, e.g. T(V2, h1) of the hub And), the join is
+// a filter of P by Q's key set -- one bit per id of the key range (16 MB for
+// 2^27 ids, L2/MALL-resident) instead of offsets and (first, count) pairs per
+// key slot and two random lookups per probe row.  Duplicate keys (a bit
+// already set) are detected while the bits are set; then the caller takes
+// the direct join (multiplicities matter).
+// ---------------------------------------------------------------------------
+__global__ void k_bits_set(const uint32_t* __restrict__ key, uint64_t n, uint32_t kmin, uint32_t range,
+                           uint32_t* bits, uint32_t* dup) {
+  uint32_t d = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = key[i] - kmin;
+    if (k >= range) continue;
+    const uint32_t m = 1u << (k & 31);
+    if (atomicOr(&bits[k >> 5], m) & m) d = 1;
+  }
+  if (__ballot(d) && __lane_id() == 0) atomicOr(dup, 1u);
+}
+struct BitsPred {
+  const uint32_t* key;
+  uint32_t kmin, range;
+  const uint32_t* bits;
+  __device__ __forceinline__ bool operator()(uint64_t i) const {
+    const uint32_t k = key[i] - kmin;
+    return k < range && ((bits[k >> 5] >> (k & 31)) & 1u);
+  }
+};
+
+std::unique_ptr<Table> semi_join(Ctx& c, const Table& P, const Table& Q) {
+  const char* f = std::getenv("DAS_SEMI_JOIN");           // tests: 0 never
+  if (f && f[0] == '0') return nullptr;
+  const int32_t var = Q.vars[0];
+  int pk = -1;
+  for (int i = 0; i < P.ncols; ++i) if (P.vars[i] == var) pk = i;
+  if (pk < 0 || Q.nrows >= 0xFFFFFFFFull) return nullptr;
+  uint32_t lo = Q.lo[0], hi = Q.hi[0];
+  if (hi == kNone || lo > hi) {
+    lo = 0;
+    hi = (uint32_t)(c.idx.n_atoms ? c.idx.n_atoms - 1 : 0);
+  }
+  const uint64_t range = (uint64_t)hi - lo + 1;
+  if (range > (1ull << 31)) return nullptr;
+  const uint64_t words = (range + 31) / 32;
+  DBuf<uint32_t> bits(words + 1, c.s);                     // + the duplicate flag
+  fill_dev(bits.p, 0, 4 * (words + 1), c.s);
+  {
+    ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * words);
+    hipLaunchKernelGGL(k_bits_set, G(Q.nrows), dim3(B), 0, c.s, (const uint32_t*)Q.col(0), Q.nrows, lo, (uint32_t)range,
+                       bits.p, bits.p + words);
+    DAS_HIP(hipGetLastError());
+  }
+  if (read_u32(bits.p + words, c.s)) return nullptr;       // duplicate keys: counts matter
+  // the probe is the compaction's predicate: no flag array
+  return compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), lo, (uint32_t)range, (const uint32_t*)bits.p},
+                      "k_semi_compact", 4.0);
+}
+
 std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {
   if (A.kind != DAS_TABLE_ORDERED || Bt.kind != DAS_TABLE_ORDERED) return theta_join(c, A, Bt, no_overload);
   // schemas
@@ -1413,6 +1563,8 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
     ProfScope ps(c, "k_cartesian", 4.0 * nu * total);
     hipLaunchKernelGGL(k_cartesian, G(total), dim3(B), 0, c.s, om, Q.nrows, total, out->data, out->cap);
     DAS_HIP(hipGetLastError());
+  } else if (shared.size() == 1 && Q.ncols == 1 && (out = semi_join(c, P, Q))) {
+    // key-set filter taken (the build side adds no columns)
   } else if (shared.size() == 1 && (out = direct_join(c, P, Q, shared[0], uni))) {
     // direct-address path taken
   } else {

@@ -178,10 +178,12 @@ def _random_queries(rng, arrays, n):
 @pytest.mark.parametrize("gen", ["bio", "powerlaw"])
 def test_gpu_synthetic_matches_oracle(gen, sets, monkeypatch):
     """Random Link / And / Or / Not queries; Or's dedup and Not's anti-join
-    through the row hash sets and through the sort-based path."""
+    through the row hash sets and through the sort-based path (which also
+    turns the semi-join off, so one-variable And terms take the direct join)."""
     from das_amd import synthetic
     if sets == "sort":
         monkeypatch.setenv("DAS_SET_SORT", "1")
+        monkeypatch.setenv("DAS_SEMI_JOIN", "0")
     if gen == "bio":
         arrays = synthetic.bio_kb(300, 120, 3000, seed=7)
     else:
@@ -427,10 +429,14 @@ def test_gpu_flybase_queries_match_oracle(sets, monkeypatch):
             assert same(got, want), (name, gene, got.get("n"), want.get("n"))
 
 
-def test_gpu_hub_four_clause_matches_oracle():
-    """Config 5: the 4-clause hub And of bench.py --workload hub."""
+@pytest.mark.parametrize("semi", ["1", "0"])
+def test_gpu_hub_four_clause_matches_oracle(semi, monkeypatch):
+    """Config 5: the 4-clause hub And of bench.py --workload hub; the
+    one-variable hub clauses through the key-bitmap semi-join (1) and the
+    direct join (0)."""
     import bench
     from das_amd import synthetic
+    monkeypatch.setenv("DAS_SEMI_JOIN", semi)
     arrays = synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
     db = _hipdb(arrays)
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
