@@ -105,28 +105,36 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_reduce(In in, uint64_t n, T
 // Scan each tile with its (already scanned) tile offset.
 template <typename T, typename In>
 __global__ void __launch_bounds__(kScanBlock) k_scan_tiles(In in, uint64_t n, const T* tile_off, T* out) {
-  __shared__ T s_wave[kScanBlock / 64];
-  __shared__ T s_carry;
+  constexpr int W = kScanBlock / 64;
+  __shared__ T s_wave[kScanItems][W];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
   const int wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_carry = tile_off ? tile_off[blockIdx.x] : (T)0;
-  __syncthreads();
+  // every round's input loaded up front (one round trip, not one per round),
+  // then all wave scans, one barrier, and the stores
+  T x[kScanItems], inc[kScanItems];
+#pragma unroll
   for (int r = 0; r < kScanItems; ++r) {
-    uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
-    T x = (i < n) ? (T)in(i) : (T)0;
-    T inc = wave_inclusive_scan(x);
-    if (__lane_id() == 63) s_wave[wave] = inc;
-    __syncthreads();
-    T pre = s_carry;
-    for (int w = 0; w < wave; ++w) pre += s_wave[w];
-    if (i < n) out[i] = pre + inc - x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      T t = 0;
-      for (int w = 0; w < kScanBlock / 64; ++w) t += s_wave[w];
-      s_carry += t;
+    const uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    x[r] = (i < n) ? (T)in(i) : (T)0;
+  }
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    inc[r] = wave_inclusive_scan(x[r]);
+    if (__lane_id() == 63) s_wave[r][wave] = inc[r];
+  }
+  __syncthreads();
+  T carry = tile_off ? tile_off[blockIdx.x] : (T)0;
+#pragma unroll
+  for (int r = 0; r < kScanItems; ++r) {
+    T pre = carry, all = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      pre += w < wave ? s_wave[r][w] : (T)0;
+      all += s_wave[r][w];
     }
-    __syncthreads();
+    const uint64_t i = base + (uint64_t)r * kScanBlock + threadIdx.x;
+    if (i < n) out[i] = pre + inc[r] - x[r];
+    carry += all;
   }
 }
 
@@ -432,6 +440,89 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter(const K* kin, cons
   }
 }
 
+// LDS-staged scatter: the tile's keys are first placed in LDS in digit order
+// (tile-local offsets from the tile's histogram), then written out by
+// consecutive threads, so each digit's run of the tile (~16 keys at 256
+// digits) leaves as one contiguous store instead of 64 lanes hitting up to
+// 64 buckets per wave store.  Same stable order as k_radix_scatter.
+template <typename K, bool kHasVals>
+__global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, const uint32_t* vin, K* kout,
+                                                                 uint32_t* vout, uint64_t n, int shift,
+                                                                 const uint32_t* hist, const uint32_t* offs,
+                                                                 uint32_t n_tiles) {
+  __shared__ K s_key[kSortTile];
+  __shared__ uint32_t s_val[kHasVals ? kSortTile : 1];
+  __shared__ uint32_t s_gbase[256], s_loff[256], s_run[256];
+  __shared__ uint32_t s_cnt[kSortBlock / 64][256];
+  __shared__ uint32_t s_wsum[kSortBlock / 64];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+  // keys (and values) of all rounds loaded up front
+  K kr[kSortItems];
+  uint32_t vr[kHasVals ? kSortItems : 1];
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
+    kr[r] = i < n ? kin[i] : (K)0;
+    if (kHasVals) vr[r] = i < n ? vin[i] : 0u;
+  }
+  {
+    // tile-local exclusive offset of each digit (thread = digit)
+    const uint32_t c = hist[(uint64_t)tid * n_tiles + blockIdx.x];
+    const uint32_t inc = wave_incl_sum_u32(c);
+    if (__lane_id() == 63) s_wsum[wave] = inc;
+    s_gbase[tid] = offs[(uint64_t)tid * n_tiles + blockIdx.x];
+    s_run[tid] = 0;
+#pragma unroll
+    for (int w = 0; w < kSortBlock / 64; ++w) s_cnt[w][tid] = 0;
+    __syncthreads();
+    uint32_t pre = inc - c;
+    for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+    s_loff[tid] = pre;
+    __syncthreads();
+  }
+  const uint64_t lt = __lanemask_lt();
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
+    const bool valid = i < n;
+    const uint32_t d = (uint32_t)(kr[r] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = __popcll(peers & lt);
+    if (valid && rank == 0) s_cnt[wave][d] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = s_loff[d] + s_run[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += s_cnt[w][d];
+      s_key[pos] = kr[r];
+      if (kHasVals) s_val[pos] = vr[r];
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < kSortBlock / 64; ++w) {
+      add += s_cnt[w][tid];
+      s_cnt[w][tid] = 0;
+    }
+    s_run[tid] += add;
+    __syncthreads();
+  }
+  const uint32_t valid_n = (uint32_t)(n - base < (uint64_t)kSortTile ? n - base : (uint64_t)kSortTile);
+  for (uint32_t j = tid; j < valid_n; j += kSortBlock) {
+    const K k = s_key[j];
+    const uint32_t d = (uint32_t)(k >> shift) & 255u;
+    const uint64_t g = (uint64_t)s_gbase[d] + (j - s_loff[d]);
+    kout[g] = k;
+    if (kHasVals) vout[g] = s_val[j];
+  }
+}
+
 // Sorts keys[0..n) (and vals alongside, if given) by bits [begin_bit, end_bit).
 // Result lands back in keys/vals.
 template <typename K>
@@ -449,7 +540,16 @@ void radix_sort_pairs(K* keys, uint32_t* vals, uint64_t n, int begin_bit, int en
     hipLaunchKernelGGL((k_radix_hist<K>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka, n, shift, hist.p, tiles);
     DAS_HIP(hipGetLastError());
     exclusive_scan<uint32_t>(hist.p, (uint64_t)tiles * 256, offs.p, s);
-    if (vals)
+    static const bool lds = !(std::getenv("DAS_SORT_LDS") && std::getenv("DAS_SORT_LDS")[0] == '0');
+    if (lds && vals)
+      hipLaunchKernelGGL((k_radix_scatter_lds<K, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                         (const uint32_t*)va, kb, vb, n, shift, (const uint32_t*)hist.p, (const uint32_t*)offs.p,
+                         tiles);
+    else if (lds)
+      hipLaunchKernelGGL((k_radix_scatter_lds<K, false>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                         (const uint32_t*)nullptr, kb, (uint32_t*)nullptr, n, shift, (const uint32_t*)hist.p,
+                         (const uint32_t*)offs.p, tiles);
+    else if (vals)
       hipLaunchKernelGGL((k_radix_scatter<K, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
                          (const uint32_t*)va, kb, vb, n, shift, (const uint32_t*)offs.p, tiles);
     else

@@ -757,25 +757,31 @@ __device__ __forceinline__ uint32_t tile_flags(const Pred& pred, uint64_t base, 
   return bits;
 }
 
+// Also stores each thread's kScanItems flags as one byte (n / 8 bytes in all),
+// so the compaction pass reads the flags instead of re-evaluating the
+// predicate (a semi-join's bitmap probe is random and L2-missing).
 template <typename Pred>
-__global__ void __launch_bounds__(kScanBlock) k_tile_count(Pred pred, uint64_t n, uint32_t* tcnt) {
+__global__ void __launch_bounds__(kScanBlock) k_tile_count(Pred pred, uint64_t n, uint32_t* tcnt, uint8_t* fl) {
+  static_assert(kScanItems <= 8, "one flag byte per thread");
   __shared__ uint32_t s[kScanBlock / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  uint32_t acc = __popc(tile_flags(pred, base, n));
+  const uint32_t bits = tile_flags(pred, base, n);
+  fl[(uint64_t)blockIdx.x * kScanBlock + threadIdx.x] = (uint8_t)bits;
+  uint32_t acc = __popc(bits);
   acc = wave_reduce_sum(acc);
   if (__lane_id() == 0) s[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) tcnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
 
-template <typename Pred>
-__global__ void __launch_bounds__(kScanBlock) k_compact_rows(Pred pred, uint64_t n, const uint32_t* __restrict__ toff,
-                                                             ColSet src, uint32_t* __restrict__ out, uint64_t cap) {
+__global__ void __launch_bounds__(kScanBlock) k_compact_rows(const uint8_t* __restrict__ fl,
+                                                             const uint32_t* __restrict__ toff, ColSet src,
+                                                             uint32_t* __restrict__ out, uint64_t cap) {
   constexpr int W = kScanBlock / 64;
   __shared__ uint32_t s_wave[kScanItems][W];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
   const int wave = threadIdx.x >> 6;
-  const uint32_t bits = tile_flags(pred, base, n);
+  const uint32_t bits = fl[(uint64_t)blockIdx.x * kScanBlock + threadIdx.x];
   uint32_t inc[kScanItems];
 #pragma unroll
   for (int r = 0; r < kScanItems; ++r) {
@@ -821,15 +827,20 @@ std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const cha
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
   DAS_CHECK(tiles < (1ull << 31), DAS_E_UNSUPPORTED, "compaction: too many rows");
   DBuf<uint32_t> tcnt(tiles, c.s), toff(tiles + 1, c.s);
-  hipLaunchKernelGGL((k_tile_count<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n, tcnt.p);
-  DAS_HIP(hipGetLastError());
+  DBuf<uint8_t> fl(tiles * kScanBlock, c.s);
+  {
+    std::optional<ProfScope> ps;
+    if (prof) ps.emplace(c, prof, pred_bytes * n);
+    hipLaunchKernelGGL((k_tile_count<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n, tcnt.p, fl.p);
+    DAS_HIP(hipGetLastError());
+  }
   const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{tcnt.p}, tiles, toff.p, c.s);
   auto t = new_table_like(c, a, m);
   t->nrows = m;
   if (m && a.ncols) {
     std::optional<ProfScope> ps;
-    if (prof) ps.emplace(c, prof, pred_bytes * n + 8.0 * a.ncols * m);
-    hipLaunchKernelGGL((k_compact_rows<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n,
+    if (prof) ps.emplace(c, "k_compact_rows", n / 8.0 + 8.0 * a.ncols * m);
+    hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, (const uint8_t*)fl.p,
                        (const uint32_t*)toff.p, cols_of(a), t->data, t->cap);
     DAS_HIP(hipGetLastError());
   }
@@ -1528,7 +1539,7 @@ std::unique_ptr<Table> semi_join(Ctx& c, const Table& P, const Table& Q) {
   if (read_u32(bits.p + words, c.s)) return nullptr;       // duplicate keys: counts matter
   // the probe is the compaction's predicate: no flag array
   return compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), lo, (uint32_t)range, (const uint32_t*)bits.p},
-                      "k_semi_compact", 4.0);
+                      "k_tile_count<BitsPred>", 4.0);
 }
 
 std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {

@@ -18,6 +18,8 @@ import sys
 
 def short(name):
     n = name.replace("das::(anonymous namespace)::", "").replace("das::", "").replace("void ", "")
+    if n.startswith("k_tile_count<"):          # predicate kernels: scope names keep the predicate
+        return re.sub(r">.*", ">", n)
     return re.sub(r"[<(].*", "", n)
 
 
