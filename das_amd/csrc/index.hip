@@ -254,32 +254,78 @@ __global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n
 // smallest unified index of that category.  Runs are digest-sorted, so ids
 // are sequential in i; a run of one (the common case) is settled here with
 // plain stores, longer runs (duplicate atoms) with atomics plus k_pick_rep.
-__global__ void k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan, uint64_t n,
-                             const uint8_t* catl, uint32_t* local2id, uint32_t* catmax, uint32_t* rep,
-                             uint8_t* cat_sorted) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t id = scan[i] + first[i] - 1;
-    const uint32_t u = idx[i];
-    const uint8_t c = catl[u];
-    local2id[u] = id;
-    cat_sorted[i] = c;
-    const bool single = first[i] && (i + 1 == n || first[i + 1]);
-    if (single) {
-      catmax[id] = c;
-      rep[id] = u;
-    } else {
-      atomicMax(&catmax[id], (uint32_t)c);
+// A hub node's run spans hundreds of millions of entries, so same-address
+// atomics would serialise: lanes of one run first reduce inside the wave
+// (a run is contiguous in i), the run's last lane in the wave issues the
+// atomic, and only when a plain load says the stored value would change.
+__device__ __forceinline__ bool wave_run_tail(uint32_t id) {
+  const uint32_t nid = __shfl_down(id, 1, 64);
+  return __lane_id() == 63 || nid != id;
+}
+
+__global__ void __launch_bounds__(256) k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan,
+                                                    uint64_t n, const uint8_t* catl, uint32_t* local2id,
+                                                    uint32_t* catmax, uint32_t* rep, uint8_t* cat_sorted) {
+  const int lane = __lane_id();
+  for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = base + threadIdx.x;           // block-uniform trip count: the whole wave shuffles
+    const bool act = i < n;
+    uint32_t id = kNone, m = 0;
+    bool single = true;
+    if (act) {
+      id = scan[i] + first[i] - 1;
+      const uint32_t u = idx[i];
+      const uint8_t c = catl[u];
+      local2id[u] = id;
+      cat_sorted[i] = c;
+      single = first[i] && (i + 1 == n || first[i + 1]);
+      if (single) {
+        catmax[id] = c;
+        rep[id] = u;
+      }
+      m = c;
     }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {               // segmented max over equal ids
+      const uint32_t om = __shfl_up(m, d, 64), oid = __shfl_up(id, d, 64);
+      if (lane >= d && oid == id) m = om > m ? om : m;
+    }
+    const bool tail = wave_run_tail(id);             // every lane shuffles, outside the branch
+    if (act && !single && tail && catmax[id] < m) atomicMax(&catmax[id], m);
   }
 }
 
-__global__ void k_pick_rep(const uint32_t* idx, const uint32_t* first, const uint32_t* scan, uint64_t n,
-                           const uint8_t* cat_sorted, const uint32_t* catmax, uint32_t* rep) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (first[i] && (i + 1 == n || first[i + 1])) continue;        // singleton: done
-    const uint32_t id = scan[i] + first[i] - 1;
-    if ((uint32_t)cat_sorted[i] == catmax[id]) atomicMin(&rep[id], idx[i]);
+__global__ void __launch_bounds__(256) k_pick_rep(const uint32_t* idx, const uint32_t* first, const uint32_t* scan,
+                                                  uint64_t n, const uint8_t* cat_sorted, const uint32_t* catmax,
+                                                  uint32_t* rep) {
+  const int lane = __lane_id();
+  for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    const bool act = i < n;
+    uint32_t id = kNone, mn = kNone;
+    bool single = true;
+    if (act) {
+      id = scan[i] + first[i] - 1;
+      single = first[i] && (i + 1 == n || first[i + 1]);   // singleton: settled by k_assign_ids
+      if (!single && (uint32_t)cat_sorted[i] == catmax[id]) mn = idx[i];
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {               // segmented min over equal ids
+      const uint32_t om = __shfl_up(mn, d, 64), oid = __shfl_up(id, d, 64);
+      if (lane >= d && oid == id) mn = om < mn ? om : mn;
+    }
+    const bool tail = wave_run_tail(id);
+    if (act && !single && mn != kNone && tail && mn < rep[id]) atomicMin(&rep[id], mn);
   }
+}
+
+// every run must have found its representative (a miss would send later
+// gathers to index kNone): flagged here and reported as an error instead
+__global__ void k_rep_missing(const uint32_t* rep, uint64_t n, uint32_t* bad) {
+  uint32_t miss = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    miss |= rep[i] == kNone;
+  if (__ballot(miss) && __lane_id() == 0) atomicOr(bad, 1u);
 }
 
 // named-type cluster key of a temp (digest-order) id; kNone types last
@@ -801,7 +847,11 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
                        (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p, rep.p, cs.p);
     hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
                        (const uint32_t*)scan.p, nc, (const uint8_t*)cs.p, (const uint32_t*)catmax.p, rep.p);
+    DBuf<uint32_t> bad(1, s);
+    fill_dev(bad.p, 0, 4, s);
+    hipLaunchKernelGGL(k_rep_missing, G(n_atoms), dim3(B), 0, s, (const uint32_t*)rep.p, n_atoms, bad.p);
     DAS_HIP(hipGetLastError());
+    DAS_CHECK(read_u32(bad.p, s) == 0, DAS_E_INTERNAL, "intern: a digest run has no representative");
   }
   first.release(); scan.release(); list.release();
 

@@ -7,6 +7,8 @@ HIP-event scopes use.
 FETCH_SIZE and WRITE_SIZE are reported in KiB.  On gfx950 FETCH_SIZE counts half
 the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM), so
 fetched bytes are taken as 2 x FETCH_SIZE; WRITE_SIZE is used as is.
+TOPK=k (env) averages only each kernel's k largest launches (the timed
+full-size launches of a run whose warm-up step is a small KB, e.g. the build).
 """
 import glob
 import json
@@ -30,10 +32,9 @@ def per_kernel(db_dir, counter):
         c = sqlite3.connect(db)
         for name, v in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
                                  (counter,)):
-            s = short(name)
-            tot, n = out.get(s, (0.0, 0))
-            out[s] = (tot + float(v) * 1024.0, n + 1)
-    return out
+            out.setdefault(short(name), []).append(float(v) * 1024.0)
+    k = int(os.environ.get("TOPK", "0"))
+    return {s: (sum(sorted(v)[-k:] if k else v), min(k, len(v)) if k else len(v)) for s, v in out.items()}
 
 
 def main():
@@ -51,7 +52,8 @@ def main():
         wr = wb / wn
         res[k] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "launches_fetch_pass": fn, "launches_write_pass": wn,
-                  "note": "read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; mean over all launches"}
+                  "note": "read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; mean over "
+                          + (f"the {os.environ['TOPK']} largest launches" if os.environ.get("TOPK") else "all launches")}
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
