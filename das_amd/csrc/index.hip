@@ -239,6 +239,17 @@ __global__ void k_hi_ties(const Digest* dig, const uint32_t* idx, uint64_t n, ui
   }
 }
 
+// Adjacent sorted keys that agree on bits [shift, 64) but differ below: the
+// prefix-only sort did not fully order them.
+__global__ void k_prefix_ties(const uint64_t* key, uint64_t n, int shift, uint32_t* bad) {
+  uint32_t b = 0;
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = key[i - 1], y = key[i];
+    b |= (x >> shift) == (y >> shift) && x != y;
+  }
+  if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+
 __global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* first) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t f = 1;
@@ -963,9 +974,13 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
       // sort link ids by ctype digest (hi, exact fallback)
       DBuf<uint64_t> key(nlk, s);
       hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
-      radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
+      // composite types are few: order by the top 16 bits of hi (2 passes, not
+      // 8); exact unless two different hi values share those bits, or two
+      // different digests share hi -- either sends us to the full sort
+      radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 48, 64, s);
       DBuf<uint32_t> bad(1, s);
       fill_dev(bad.p, 0, 4, s);
+      hipLaunchKernelGGL(k_prefix_ties, G(nlk), dim3(B), 0, s, (const uint64_t*)key.p, nlk, 48, bad.p);
       hipLaunchKernelGGL(k_hi_ties, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, bad.p);
       if (read_u32(bad.p, s)) {
         hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, false);
