@@ -120,6 +120,7 @@ _SIGS = {
     "das_parsed_type_name": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]),
     "das_parsed_free": (C.c_int, [P]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
+    "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
     "das_prof_names": (C.c_int, [P, P, C.c_uint64]),
@@ -513,6 +514,10 @@ class Context:
 
     def prof_reset(self):
         check(lib().das_prof_reset(self.h), self.h)
+
+    def prof_only(self, name=None):
+        """Record events only for scopes named `name` (None: every scope)."""
+        check(lib().das_prof_only(self.h, name.encode() if name else None), self.h)
 
     def prof_stats(self):
         buf = C.create_string_buffer(1 << 16)

@@ -601,6 +601,13 @@ int das_prof_enable(das_ctx_t* ctx, int on) {
   });
 }
 
+int das_prof_only(das_ctx_t* ctx, const char* name) {
+  return guarded(ctx, [&] {
+    das::prof_collect(ctx->c);
+    ctx->c.prof_only = name ? name : "";
+  });
+}
+
 int das_prof_reset(das_ctx_t* ctx) {
   return guarded(ctx, [&] {
     das::prof_collect(ctx->c);

@@ -126,6 +126,7 @@ struct PendingEv {
 
 struct Ctx {
   bool prof = false;
+  std::string prof_only;             // non-empty: only scopes of this name record events
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;   // recycled timing events (creation is not cheap on ROCm)
   hipEvent_t take_event() {
@@ -157,7 +158,7 @@ struct ProfScope {
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, const char* n, double algorithmic_bytes) : c(ctx), name(n), bytes(algorithmic_bytes) {
-    if (!c.prof) return;
+    if (!c.prof || (!c.prof_only.empty() && c.prof_only != n)) return;
     a = c.take_event();
     b = c.take_event();
     DAS_HIP(hipEventRecord(a, c.s));

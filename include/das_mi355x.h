@@ -269,6 +269,10 @@ int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int
 /* Per-kernel HIP-event timing on the context stream (bench.py roofline):
  * totals of elapsed ms, launches and algorithmic bytes since the last reset. */
 int das_prof_enable(das_ctx_t* ctx, int on);
+/* Restrict event recording to the scopes named `name` (NULL or "" = every
+ * scope): the bench times its dominant kernel live without paying two event
+ * records per launch for every other kernel. */
+int das_prof_only(das_ctx_t* ctx, const char* name);
 int das_prof_reset(das_ctx_t* ctx);
 int das_prof_read(das_ctx_t* ctx, const char* name, double* ms, uint64_t* launches, double* bytes);
 int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap);
