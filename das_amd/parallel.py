@@ -381,7 +381,7 @@ class ShardedDB(RelationalDB):
         groups = self._group(b.tables)
         out = []
         for t in a.tables:
-            fs = groups.get((t.kind, tuple(t.vars)), [])
+            fs = groups.get((t.kind, tuple(t.vars), _members(t)), [])
             if fs:
                 t = self._exchange(t, [])
                 for f in fs:

@@ -139,6 +139,130 @@ def bio_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, seed=SEED
     return arrays
 
 
+def expr_ref(block, rows):
+    """Child reference to rows of an earlier link block (build_nested)."""
+    return -(1 + (np.int64(block) << np.int64(32)) + np.asarray(rows, dtype=np.int64))
+
+
+def build_nested(type_names, node_blocks, link_blocks):
+    """build_arrays for nested expressions: link block children are global
+    node indices (>= 0) or expr_ref(b, row) references to rows of an earlier
+    block b; a node block (type, [names], n) names its nodes explicitly.
+    Expressions are grouped by (nesting level, arity) as the
+    AtomArrays layout requires, each block keeping its row order."""
+    types = list(type_names)
+    tid = {t: i for i, t in enumerate(types)}
+    for t, _, _ in node_blocks:
+        tid.setdefault(t, len(tid))
+    for blk in link_blocks:
+        tid.setdefault(blk[0], len(tid))
+    types = sorted(tid, key=tid.get)
+    n_types = len(types)
+    strings = [t.encode() for t in types]
+    node_ctype, name_start, n_nodes = [], [], 0
+    for t, prefix, count in node_blocks:
+        names = prefix if isinstance(prefix, list) else [f"{prefix}{i}" for i in range(count)]
+        strings.extend(f"{t} {n}".encode() for n in names)
+        node_ctype.append(np.full(len(names), tid[t], dtype=np.uint32))
+        name_start.append(np.full(len(names), len(t.encode()) + 1, np.uint32))
+        n_nodes += len(names)
+    n_leaf = n_types + n_nodes
+    # nesting level and arity of every block
+    level, chs = [], []
+    for t, ch in link_blocks:
+        ch = np.asarray(ch, dtype=np.int64)
+        refs = -(ch[ch < 0] + 1) >> np.int64(32)
+        level.append(1 + max([level[int(b)] for b in np.unique(refs)], default=0))
+        chs.append(ch)
+    key = sorted(range(len(link_blocks)), key=lambda b: (level[b], chs[b].shape[1], b))
+    start, total = {}, 0
+    for b in key:
+        start[b] = total
+        total += chs[b].shape[0]
+    childs, nchs, groups, prev = [], [], [0], None
+    run = 0
+    for b in key:
+        ch = chs[b]
+        neg = ch < 0
+        r = -(ch[neg] + 1)
+        src, row = r >> np.int64(32), r & np.int64(0xFFFFFFFF)
+        out = ch + n_types
+        out[neg] = n_leaf + np.array([start[int(s)] for s in src], dtype=np.int64) + row
+        full = np.concatenate([np.full((ch.shape[0], 1), tid[link_blocks[b][0]], np.int64), out], axis=1)
+        g = (level[b], ch.shape[1])
+        if prev is not None and g != prev:
+            groups.append(run)
+        prev = g
+        run += ch.shape[0]
+        childs.append(full.reshape(-1).astype(np.uint32))
+        nchs.append(np.full(ch.shape[0], ch.shape[1] + 1, np.uint64))
+    groups.append(run)
+    lens = np.fromiter((len(s) for s in strings), dtype=np.uint64, count=n_leaf)
+    leaf_off = np.zeros(n_leaf + 1, dtype=np.uint64)
+    np.cumsum(lens, out=leaf_off[1:])
+    nch = np.concatenate(nchs)
+    expr_off = np.zeros(total + 1, dtype=np.uint64)
+    np.cumsum(nch, out=expr_off[1:])
+    return AtomArrays(np.frombuffer(b"".join(strings), dtype=np.uint8), leaf_off,
+                      np.concatenate([np.full(n_types, LEAF_TYPE, np.uint8), np.full(n_nodes, LEAF_NODE, np.uint8)]),
+                      np.concatenate([np.arange(n_types, dtype=np.uint32)] + node_ctype),
+                      np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, NONE, np.uint32)]),
+                      np.concatenate([np.zeros(n_types, np.uint32)] + name_start),
+                      expr_off, np.concatenate(childs), np.ones(total, np.uint8), np.full(total, -1, np.int32),
+                      np.array(groups, np.uint64), types)
+
+
+def bio_full_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, n_uniprot=5000,
+                n_up_member=50_000, n_reactome=1000, n_context=20_000, n_loc=40, seed=SEED):
+    """The gene-level KB scripts/benchmark.py's three query layouts need
+    (benchmark.py:40-128), with the annotation-service file shapes
+    (data/annotation_service/*.metta):
+      Member(Gene, BiologicalProcess)           Zipf(1.1) process popularity
+      Inheritance(BP, BP)                       parents have lower index
+      Member(Uniprot, BiologicalProcess)        Zipf(1.1)
+      Evaluation(has_name, List(Uniprot, Concept name))     one per protein
+      Evaluation(has_name, List(Reactome, Concept name))    one per pathway
+      Context(Member(Uniprot, Reactome),
+              Evaluation(has_location, List(Uniprot, Concept location)))
+    Nodes: g<i>, bp<i>, up<i>, r<i>, upname<i>, rname<i>, loc<i>, and the
+    predicates has_name / has_location."""
+    rng = np.random.default_rng(seed)
+    n_inh = n_inh if n_inh is not None else 2 * n_bps
+    nodes = [("Gene", "g", n_genes), ("BiologicalProcess", "bp", n_bps), ("Uniprot", "up", n_uniprot),
+             ("Reactome", "r", n_reactome), ("Concept", "upname", n_uniprot), ("Concept", "rname", n_reactome),
+             ("Concept", "loc", n_loc), ("Predicate", ["has_name"], 1), ("Predicate", ["has_location"], 1)]
+    off, o = {}, 0
+    for t, p, c in nodes:
+        off[p if isinstance(p, str) else p[0]] = o
+        o += c
+    genes = rng.integers(0, n_genes, n_member)
+    bps = zipf_indices(rng, n_bps, n_member)
+    child = rng.integers(1, n_bps, n_inh)
+    parent = (rng.random(n_inh) * child).astype(np.int64)
+    up_m = rng.integers(0, n_uniprot, n_up_member)
+    up_bp = zipf_indices(rng, n_bps, n_up_member)
+    ctx_up = rng.integers(0, n_uniprot, n_context)
+    ctx_r = zipf_indices(rng, n_reactome, n_context)
+    ctx_loc = zipf_indices(rng, n_loc, n_context)
+    ups, rs = np.arange(n_uniprot), np.arange(n_reactome)
+    name_pred = lambda n: np.full(n, off["has_name"], np.int64)  # noqa: E731
+    blocks = [
+        ("Member", np.stack([off["g"] + genes, off["bp"] + bps], 1)),                    # 0
+        ("Inheritance", np.stack([off["bp"] + child, off["bp"] + parent], 1)),           # 1
+        ("Member", np.stack([off["up"] + up_m, off["bp"] + up_bp], 1)),                  # 2
+        ("List", np.stack([off["up"] + ups, off["upname"] + ups], 1)),                   # 3
+        ("List", np.stack([off["r"] + rs, off["rname"] + rs], 1)),                       # 4
+        ("Member", np.stack([off["up"] + ctx_up, off["r"] + ctx_r], 1)),                 # 5
+        ("List", np.stack([off["up"] + ctx_up, off["loc"] + ctx_loc], 1)),               # 6
+        ("Evaluation", np.stack([name_pred(n_uniprot), expr_ref(3, ups)], 1)),           # 7
+        ("Evaluation", np.stack([name_pred(n_reactome), expr_ref(4, rs)], 1)),           # 8
+        ("Evaluation", np.stack([np.full(n_context, off["has_location"], np.int64),
+                                 expr_ref(6, np.arange(n_context))], 1)),                # 9
+        ("Context", np.stack([expr_ref(5, np.arange(n_context)), expr_ref(9, np.arange(n_context))], 1)),
+    ]
+    return build_nested(["Member", "Inheritance", "List", "Evaluation", "Context"], nodes, blocks)
+
+
 def flybase_kb(n_genes=200_000, n_schema=60, rows_per_schema=400_000, n_loc=5_000, n_do=2_000,
                seed=SEED):
     """Config 3: FlyBase-shaped canonical KB in flybase2metta's

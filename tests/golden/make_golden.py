@@ -232,15 +232,24 @@ def canon(a):
     raise TypeError(type(a))
 
 
-def answer_record(db, spec, inline_limit=400):
+def answer_record(db, spec, inline_limit=400, no_overload=False):
+    import time
     expr = build(spec)
     answer = pm.PatternMatchingAnswer()
     rec = {"query": spec}
+    if no_overload:
+        rec["no_overload"] = True
+    pm.CONFIG["no_overload"] = no_overload          # pattern_matcher.py:16-19
+    t0 = time.perf_counter()
     try:
         matched = expr.matched(db, answer)
     except Exception as e:  # reference raises (A7 tuple targets, composite negation ...)
         rec["error"] = type(e).__name__
         return rec
+    finally:
+        pm.CONFIG["no_overload"] = False
+    # reference matched() wall time in this container (CPU-baseline calibration)
+    rec["ref_seconds"] = round(time.perf_counter() - t0, 6)
     rows = sorted(json.dumps(canon(a), sort_keys=True) for a in answer.assignments)
     rec["matched"] = bool(matched)
     rec["negation"] = bool(answer.negation)
@@ -497,18 +506,20 @@ def write(name, obj):
     print("wrote", path)
 
 
-def kb_fixture(name, das, queries, probes=None, source=None):
+def kb_fixture(name, das, queries, probes=None, source=None, table_limit=(2000, 4000)):
+    """queries: specs, or {"query": spec, "no_overload": bool} entries."""
     nodes, links = atom_table(das)
     db = das.db
+    entries = [q if isinstance(q, dict) else {"query": q} for q in queries]
     out = {
         "kb": name,
         "source": source,
         "count_atoms": list(das.count_atoms()),
-        "nodes": nodes if len(nodes) <= 2000 else None,
-        "links": links if len(links) <= 4000 else None,
+        "nodes": nodes if len(nodes) <= table_limit[0] else None,
+        "links": links if len(links) <= table_limit[1] else None,
         "nodes_sha256": hashlib.sha256("\n".join(json.dumps(n) for n in nodes).encode()).hexdigest(),
         "links_sha256": hashlib.sha256("\n".join(json.dumps(l) for l in links).encode()).hexdigest(),
-        "queries": [answer_record(db, q) for q in queries],
+        "queries": [answer_record(db, e["query"], no_overload=e.get("no_overload", False)) for e in entries],
     }
     if probes is not None:
         out["index"] = index_counts(das, probes)
@@ -624,7 +635,9 @@ def main():
                 specs = json.load(f)
             for s in specs:
                 das = load_canonical(s["path"])
-                write(f"kb_{s['name']}.json", kb_fixture(s["name"], das, s["queries"], None, s["generator"]))
+                fx = kb_fixture(s["name"], das, s["queries"], None, s["generator"], table_limit=(0, 0))
+                fx["text_sha256"] = s["text_sha256"]
+                write(f"kb_{s['name']}.json", fx)
 
 
 if __name__ == "__main__":

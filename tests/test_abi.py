@@ -53,5 +53,9 @@ def test_expression_hasher_api(golden):
     for parts, h in hv["composite"]:
         assert EH.composite_hash(parts) == h
     assert EH.composite_hash("x") == "x"
+    # upper-case hex elements are joined as written (expression_hasher.py:33)
+    import hashlib
+    up = ["AF12F10F9AE2002A1607BA0B47BA8407", "bdfe4e7a431f73386f37c6448afe5840"]
+    assert EH.composite_hash(up) == hashlib.md5(" ".join(up).encode()).hexdigest()
     with pytest.raises(ValueError):
         EH.composite_hash(3)

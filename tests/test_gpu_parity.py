@@ -567,3 +567,27 @@ def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
         want = O.evaluate(q, odb)
         got = record(q, db)
         assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+@pytest.mark.parametrize("gen", ["bio", "powerlaw"])
+def test_gpu_no_overload_matches_oracle(gen):
+    """CONFIG['no_overload'] = True (pattern_matcher.py:16-19, :98): distinct
+    variables of an ordered assignment take distinct values, in scans and
+    in joins; random shapes against the oracle under the same flag."""
+    from das_amd import synthetic
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    if gen == "bio":
+        arrays = synthetic.bio_kb(200, 60, 2500, seed=12)
+    else:
+        arrays = synthetic.powerlaw_kb(150, 3000, link_types=2, seed=12)
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    rng = np.random.default_rng(5)
+    pm.CONFIG["no_overload"] = O.CONFIG["no_overload"] = True
+    try:
+        for q in _random_queries(rng, arrays, 30):
+            want = O.evaluate(q, odb)
+            got = record(q, db)
+            assert same(got, want), (q, got.get("n"), want.get("n"))
+    finally:
+        pm.CONFIG["no_overload"] = O.CONFIG["no_overload"] = False

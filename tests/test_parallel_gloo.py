@@ -313,6 +313,10 @@ def _queries():
         ["And", [m(V("G"), V("B")), ["Not", m(V("G"), bp(1))]]],
         ["Or", [m(V("G"), bp(0)), m(V("G"), bp(2))]],
         ["Or", [i(V("B"), V("P")), ["Not", i(V("B"), bp(0))]]],
+        # Or with a Not of the positive term's own schema: rel_minus must
+        # subtract (pattern_matcher.py:681, term_answer - or_answer)
+        ["Or", [m(V("G"), bp(0)), ["Not", m(V("G"), bp(1))]]],
+        ["Or", [m(V("G"), bp(0)), m(V("G"), bp(2)), ["Not", m(V("G"), bp(0))]]],
         ["And", [i(V("A"), V("B")), i(V("B"), V("C")), i(V("C"), V("D"))]],
         ["And", [m(g(7), V("B")), i(V("X"), V("Y"))]],           # no shared variable
         ["Link", "*", True, [V("X"), bp(0)]],                     # global dedup path

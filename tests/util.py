@@ -66,6 +66,9 @@ def record(expr_spec, db):
 def same(got, want):
     if want.get("error") or got.get("error"):
         return got.get("error") == want.get("error")
+    # the device count (what bench.py reports) must equal the materialised set
+    if "count" in got and got["count"] != got["n"]:
+        return False
     return all(got[k] == want[k] for k in ("matched", "negation", "n", "sha256"))
 
 
