@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--load-rows", type=int, default=200_000)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-materialise", action="store_true")
+    ap.add_argument("--materialise-cap", type=int, default=2_000_000,
+                    help="largest answer whose Python objects the materialisation-inclusive figure builds")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
     return ap.parse_args()
 
@@ -88,9 +91,11 @@ def _L(t, *targets):
     return ["Link", t, True, list(targets)]
 
 
-def bio_specs(rank_genes, seed=17):
+def bio_specs(rank_genes, seed=17, anchor=0):
+    """Q1-Q4; `anchor` picks Q3's gene pair (each timed step uses its own,
+    so no step replays an anchored lookup of an earlier one)."""
     import numpy as np
-    rng = np.random.default_rng(seed)
+    rng = np.random.default_rng(seed + 7919 * anchor)
     ga, gb = (int(x) for x in rng.choice(rank_genes, 2, replace=False))
     g = lambda i: ["Node", "Gene", f"g{i}"]  # noqa: E731
     bp = lambda i: ["Node", "BiologicalProcess", f"bp{i}"]  # noqa: E731
@@ -153,7 +158,8 @@ def build_expr(pm, spec):
 
 
 def make_kb(args, rank, world, db):
-    """(AtomArrays for this rank, query specs, config dict, scaling)."""
+    """(AtomArrays for this rank, specs_of(step) -> query specs, config dict,
+    scaling).  Anchored queries take a different anchor every step."""
     import numpy as np
     from das_amd import parallel, synthetic
     if args.workload == "bio":
@@ -165,15 +171,19 @@ def make_kb(args, rank, world, db):
         cfg = {"workload": "config2 bio gene-level KB: single-Link + 2-clause And (Q1-Q4)",
                "genes_per_rank": int(len(rank_genes)), "bps": args.bps, "member_links_per_rank": args.members,
                "inheritance_links": args.inheritance}
-        return arrays, bio_specs(rank_genes), cfg, "weak"
+        return arrays, lambda i: bio_specs(rank_genes, anchor=i), cfg, "weak"
     if args.workload == "flybase":
         arrays = synthetic.flybase_kb(args.fb_genes, args.fb_schema, args.fb_rows)
-        # the gene's DO terms (cell 9 builds its Or from them), read off the arrays
-        do_terms = synthetic.flybase_do_terms(arrays, gene=7)
+        # one gene anchor per step; each gene's DO terms (cell 9 builds its Or
+        # from them), read off the arrays
+        n = args.warmup + args.steps + 2
+        genes = [(7 + 7919 * i) % args.fb_genes for i in range(n)]
+        do_terms = {g: synthetic.flybase_do_terms(arrays, gene=g) for g in genes}
         arrays = parallel.shard_arrays(arrays, rank, world)
         cfg = {"workload": "config3 FlyBase-shaped Execution KB: QueryFlyBase.ipynb And/And+Not/Or shapes",
-               "links": int(arrays.n_expr), "genes": args.fb_genes, "schemas": args.fb_schema}
-        return arrays, flybase_specs(7, do_terms), cfg, "strong"
+               "links": int(arrays.n_expr), "genes": args.fb_genes, "schemas": args.fb_schema,
+               "anchors": "a different gene per step"}
+        return arrays, lambda i: flybase_specs(genes[i % n], do_terms[genes[i % n]]), cfg, "strong"
     if args.gen == "device":
         # every rank holds the whole atom directory; rank r owns (indexes) the
         # global link range [r L / N, (r+1) L / N)
@@ -186,59 +196,148 @@ def make_kb(args, rank, world, db):
     cfg = {"workload": "config5 power-law hypergraph: 4-clause And on hub nodes",
            "links": args.hub_links, "nodes": args.hub_nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
            "generated": args.gen}
-    return arrays, hub_specs(), cfg, "strong"
+    return arrays, lambda i: hub_specs(), cfg, "strong"
+
+
+def cpu_cores():
+    """Host cores this process may use: the affinity set, capped by
+    OMP_NUM_THREADS (the GPU box exports its CPU share there; nproc and
+    os.cpu_count() show the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+def _cpu_sample(workload, args_d):
+    """(AtomArrays, query specs, description) of the bounded CPU sample of a
+    workload: the same generators and query shapes at reduced scale."""
+    from das_amd import synthetic
+    a = argparse.Namespace(**args_d)
+    if workload == "bio":
+        scale = 1000
+        genes, bps = max(a.genes // scale, 50), max(a.bps // scale, 20)
+        members, inh = max(a.members // scale, 500), max(a.inheritance // scale, 40)
+        arrays = synthetic.bio_kb(genes, bps, members, inh)
+        specs = [s for k in range(8) for _, s in bio_specs(range(1, genes), anchor=k)]
+        what = f"bio_kb(genes={genes}, bps={bps}, members={members}, inheritance={inh}) = 1/{scale} of the GPU workload"
+    elif workload == "flybase":
+        scale = 1000
+        arrays = synthetic.flybase_kb(max(a.fb_genes // scale, 100), max(a.fb_schema // 10, 4),
+                                      max(a.fb_rows // scale, 200), n_loc=50, n_do=40)
+        specs = [s for g in range(0, 96, 3) for _, s in flybase_specs(g, synthetic.flybase_do_terms(arrays, gene=g))]
+        what = f"flybase_kb at 1/{scale} of the GPU workload, 32 gene anchors"
+    else:
+        scale = max(a.hub_links // 30_000, 1)      # ~30 k links: a few oracle passes in the budget
+        arrays = synthetic.powerlaw_kb(max(a.hub_nodes // scale, 200), max(a.hub_links // scale, 2000),
+                                       link_types=4)
+        specs = [s for _, s in hub_specs()]
+        what = f"powerlaw_kb at 1/{scale} of the GPU workload"
+    return arrays, specs, what
+
+
+def _cpu_query_worker(job):
+    """One process of the CPU baseline: evaluates whole queries, one at a
+    time, round-robin from its offset, until the budget is spent."""
+    workload, args_d, wid, budget = job
+    from oracle import das_oracle as O
+    arrays, specs, _ = _cpu_sample(workload, args_d)
+    db = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    total, done, i = 0, 0, wid
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget:
+        total += O.evaluate(specs[i % len(specs)], db).get("n", 0)
+        done += 1
+        i += 1
+    return total, done, time.perf_counter() - t0
+
+
+def _cpu_build_worker(job):
+    """One process of the build CPU baseline: the oracle's ExpressionHasher
+    + key-value index restatement (canonical_parser.py:132-183) over its own
+    seeded power-law sample, repeated until the budget is spent."""
+    wid, n_links, n_nodes, budget = job
+    from das_amd import synthetic
+    from oracle import das_oracle as O
+    arrays = synthetic.powerlaw_kb(n_nodes, n_links, link_types=4, seed=1000 + wid)
+    links, reps = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        kb = O.KB.from_arrays(arrays)         # md5 handles + composite types of every atom
+        O.keyspace_lines(kb)                  # outgoing / incoming / pattern / template / name families
+        links += len(kb.links)
+        reps += 1
+        if time.perf_counter() - t0 > budget:
+            break
+    return links, reps, time.perf_counter() - t0
+
+
+def _calibration():
+    path = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        c = json.load(f)
+    return {"oracle_over_reference_time": c.get("ratio_all"), "source": "profiles/cpu_calibration.json",
+            "how": c.get("what")}
+
+
+def _pool_map(fn, jobs):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")       # fresh interpreters: nothing of this process's GPU state
+    with ctx.Pool(len(jobs)) as pool:
+        return pool.map(fn, jobs)
 
 
 def cpu_baseline(args, budget_s):
     """The oracle (CPU restatement keeping the reference's nested-loop join
-    complexity) on a bounded sample of the same workload, one core."""
-    from das_amd import synthetic
-    from oracle import das_oracle as O
-    if args.workload == "bio":
-        scale = 1000
-        genes, bps = max(args.genes // scale, 50), max(args.bps // scale, 20)
-        members, inh = max(args.members // scale, 500), max(args.inheritance // scale, 40)
-        arrays = synthetic.bio_kb(genes, bps, members, inh)
-        specs = [s for _, s in bio_specs(range(1, genes))]
-        what = f"bio_kb(genes={genes}, bps={bps}, members={members}, inheritance={inh}) = 1/{scale} of the GPU workload"
-    elif args.workload == "flybase":
-        scale = 1000
-        arrays = synthetic.flybase_kb(max(args.fb_genes // scale, 100), max(args.fb_schema // 10, 4),
-                                      max(args.fb_rows // scale, 200), n_loc=50, n_do=40)
-        specs = [s for _, s in flybase_specs(7, synthetic.flybase_do_terms(arrays, gene=7))]
-        what = f"flybase_kb at 1/{scale} of the GPU workload"
-    else:
-        scale = max(args.hub_links // 30_000, 1)      # ~30 k links: a few oracle passes in the budget
-        arrays = synthetic.powerlaw_kb(max(args.hub_nodes // scale, 200), max(args.hub_links // scale, 2000),
-                                       link_types=4)
-        specs = [s for _, s in hub_specs()]
-        what = f"powerlaw_kb at 1/{scale} of the GPU workload"
-    db = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
-    total, t0, passes = 0, time.perf_counter(), 0
-    while True:
-        for s in specs:
-            total += O.evaluate(s, db).get("n", 0)
-        passes += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": total / dt, "unit": "bindings/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (nested-loop And, reference complexity) on {what}, {len(specs)} queries, "
-                      f"{passes} passes in {dt:.1f} s"}
+    complexity; its speed against the reference itself is in
+    profiles/cpu_calibration.json) on a bounded sample of the same workload:
+    one process per host core, each evaluating whole queries one at a time
+    (SURVEY.md §8d(ii))."""
+    cores = cpu_cores()
+    args_d = vars(args)
+    _, specs, what = _cpu_sample(args.workload, args_d)
+    t0 = time.perf_counter()
+    res = _pool_map(_cpu_query_worker, [(args.workload, args_d, w, budget_s) for w in range(cores)])
+    wall = time.perf_counter() - t0
+    total = sum(r[0] for r in res)
+    done = sum(r[1] for r in res)
+    span = max(r[2] for r in res)
+    return {"value": total / span, "unit": "bindings/s", "cores": cores, "kind": "port",
+            "sample": f"oracle (nested-loop And, reference complexity) on {what}; {len(specs)} query instances, "
+                      f"{cores} processes x one whole query at a time, {done} queries in {span:.1f} s "
+                      f"({wall:.1f} s with interpreter start-up)",
+            "calibration": _calibration()}
 
 
-def roofline_of(stats, workload="bio"):
-    """Dominant single-kernel scope ("k_*") of the timed region -> roofline;
-    multi-launch phases (join_build, incoming_csr, ...) are reported under
-    "kernels" but are not a kernel's roofline."""
+def cpu_baseline_build(args, budget_s):
+    cores = cpu_cores()
+    n_links, n_nodes = 20_000, 4_000
+    t0 = time.perf_counter()
+    res = _pool_map(_cpu_build_worker, [(w, n_links, n_nodes, budget_s) for w in range(cores)])
+    span = max(r[2] for r in res)
+    links = sum(r[0] for r in res)
+    return {"value": links / span, "unit": "links/s", "cores": cores, "kind": "port",
+            "sample": f"oracle ExpressionHasher + key-value index restatement (KB.from_arrays + keyspace_lines) "
+                      f"of powerlaw_kb({n_nodes} nodes, {n_links} links) per process, {cores} processes, "
+                      f"{sum(r[1] for r in res)} builds in {span:.1f} s ({time.perf_counter() - t0:.1f} s wall)"}
+
+
+def roofline_of(stats, workload="bio", name=None):
+    """Dominant single-kernel scope ("k_*", one template instantiation) of
+    the timed region -> roofline; multi-launch phases (join_build,
+    incoming_csr, ...) are reported under "kernels" but are not a kernel's
+    roofline.  achieved = algorithmic bytes per launch / mean launch time."""
     single = {k: v for k, v in stats.items() if k.startswith("k_")}
     if not single:
         return None
-    name, st = max(single.items(), key=lambda kv: kv[1]["ms"])
+    if name is None or name not in single:
+        name = max(single.items(), key=lambda kv: kv[1]["ms"])[0]
+    st = single[name]
     achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9 if st["ms"] > 0 else 0.0
     traffic = None
     # per-kernel HBM bytes from this workload's rocprofv3 PMC passes (tools/profile_bench.sh)
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "bio" else f"pmc_traffic_{workload}.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get(name, {}).get("bytes_per_launch")
@@ -249,8 +348,11 @@ def roofline_of(stats, workload="bio"):
 
 
 def kernels_of(stats):
+    """Per scope: total ms, launches, mean launch us, algorithmic GB/s."""
     return {k: {"ms": round(v["ms"], 3), "launches": v["launches"],
-                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in stats.items()}
+                "avg_us": round(v["ms"] * 1e3 / max(v["launches"], 1), 2),
+                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+            for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
 
 
 # ---------------------------------------------------------------------------
@@ -301,20 +403,30 @@ def run_build(args, rank, world, dist, local_rank):
         links = int(n.item())
     # MD5 blocks hashed: a message of L bytes takes
     # ceil((L + 9) / 64) blocks; a composite message is K 32-hex handles joined
-    # by spaces (33 K - 1 bytes), a terminal one its "Type name" string
+    # by spaces (33 K - 1 bytes), a terminal one its "Type name" string; a
+    # link hashes two composites (its handle and its composite type)
     import numpy as np
     leaf_len = np.diff(arrays.leaf_off.astype(np.int64))
     blocks_leaf = int(((leaf_len + 9 + 63) // 64).sum())
     if getattr(arrays, "expr_on_device", False):
         nch = arrays.expr_off[1:] - arrays.expr_off[:-1]
-        blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum().item())
+        blocks_expr = 2 * int(((33 * nch - 1 + 9 + 63) // 64).sum().item())
         del nch
     else:
         nch = np.diff(arrays.expr_off.astype(np.int64))
-        blocks_expr = int(((33 * nch - 1 + 9 + 63) // 64).sum())
+        blocks_expr = 2 * int(((33 * nch - 1 + 9 + 63) // 64).sum())
     if rank == 0:
-        hs = stats.get("k_hash_group", {"ms": 0, "bytes": 0, "launches": 0})
+        hash_ks = {k: v for k, v in stats.items() if k.startswith("k_hash_group")}
+        hms = sum(v["ms"] for v in hash_ks.values())
         hl = stats.get("k_hash_strings", {"ms": 0, "bytes": 0, "launches": 0})
+        # §8d algorithmic bytes of the whole build: hash (arity*16 + 16) in +
+        # 16 out, CSR 2*arity*4 + 4 per link
+        n2, n3 = int(args.links * 0.7) // world, (args.links - int(args.links * 0.7)) // world
+        algo = n2 * (2 * 16 + 16 + 16 + 2 * 2 * 4 + 4) + n3 * (3 * 16 + 16 + 16 + 2 * 3 * 4 + 4)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline")
+            cpu = cpu_baseline_build(args, args.cpu_baseline_seconds)
         out = {"metric": "links indexed/s (bulk ExpressionHasher + intern + pattern/template/incoming CSR build)",
                "value": links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
                "ms_per_step": dev_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -324,14 +436,64 @@ def run_build(args, rank, world, dist, local_rank):
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
                           "parallelism": f"links partitioned x{world} (independent shards, nodes replicated)"},
-               "roofline": roofline_of(stats, "build"), "cpu_baseline": None,
-               "hash": {"ms": round(hs["ms"], 3), "GBps": round(hs["bytes"] / max(hs["ms"], 1e-9) / 1e6, 1),
-                        "md5_blocks_per_s": (blocks_leaf + blocks_expr) / max((hs["ms"] + hl["ms"]) * 1e-3, 1e-12),
-                        "md5_blocks": blocks_leaf + blocks_expr,
-                        "terminal_ms": round(hl["ms"], 3)},
+               "roofline": roofline_of(stats, "build"), "cpu_baseline": cpu,
+               "build_8d": {"algorithmic_bytes": algo, "achieved_GBps": round(algo / (dev_ms * 1e-3) / 1e9, 1),
+                            "frac": round(algo / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "note": "SURVEY.md §8d bytes of hash + CSR per link over the whole device build"},
+               "hash": {"ms": round(hms, 3), "md5_blocks_per_s": (blocks_leaf + blocks_expr) / max((hms + hl["ms"]) * 1e-3, 1e-12),
+                        "md5_blocks": blocks_leaf + blocks_expr, "terminal_ms": round(hl["ms"], 3),
+                        "valu": md5_valu(hash_ks)},
                "kernels": kernels_of(stats), "wall_incl_upload_s": round(wall, 3), "host_generate_s": round(t_gen, 2),
                "atoms": int(st.n_atoms), "device_bytes": int(st.device_bytes)}
         print(json.dumps(out))
+
+
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2   # CUs x SIMDs x clock / 2 cycles per wave64 VALU op (MI355X_MICROARCH.md)
+
+
+def md5_valu(hash_ks):
+    """k_hash_group<K> against the VALU issue peak: wave instructions issued
+    (static per-thread VALU count of the kernel, profiles/md5_isa.json from
+    tools/isa_count.py, x expressions / 64) over the launch time."""
+    path = os.path.join(ROOT, "profiles", "md5_isa.json")
+    if not os.path.exists(path) or not hash_ks:
+        return None
+    with open(path) as f:
+        isa = json.load(f)["kernels"]
+    out = {}
+    for k, v in hash_ks.items():
+        if k not in isa or v["ms"] <= 0:
+            continue
+        # bytes scope = expressions * (36 K + 44): recover the expression count
+        kk = int(k[k.index("<") + 1:-1])
+        n_expr = v["bytes"] / (36.0 * kk + 44.0)
+        wi = n_expr / 64.0 * isa[k]["valu"]
+        rate = wi / (v["ms"] * 1e-3)
+        out[k] = {"valu_per_expr": isa[k]["valu"], "wave_instr_per_s": rate, "peak": VALU_PEAK_WAVE_INSTR,
+                  "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4)}
+    return out
+
+
+def materialised_rate(pm, db, qs, cap):
+    """Bindings/s including Python object materialisation (the reference's
+    answer is a set of Assignment objects, distributed_atom_space.py:298-321):
+    each query of one step is evaluated and, when its answer has at most `cap`
+    bindings, `answer.assignments` is built; larger answers are listed apart
+    (their objects cost ~1 us each on the host, minutes per step)."""
+    done, skipped, n, t = [], [], 0, 0.0
+    for name, q in qs:
+        t0 = time.perf_counter()
+        ans = pm.PatternMatchingAnswer()
+        q.matched(db, ans)
+        c = ans.count()
+        if c > cap:
+            skipped.append([name, c])
+            continue
+        n += len(ans.assignments)
+        t += time.perf_counter() - t0
+        done.append(name)
+    return {"value": n / t if t > 0 else None, "unit": "bindings/s", "bindings": n, "seconds": round(t, 4),
+            "queries": done, "above_cap": skipped, "cap": cap}
 
 
 def log(msg):
@@ -438,7 +600,9 @@ def main():
     del arrays
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
-    qs = [(name, build_expr(pm, s)) for name, s in specs]
+    # one query set per step: anchored queries change their anchor every step
+    n_sets = args.warmup + args.steps + 1
+    qsets = [[(name, build_expr(pm, s)) for name, s in specs(i)] for i in range(n_sets)]
     if world > 1:
         from das_amd import parallel
         # bio_shard places a gene's Member links on the gene's rank
@@ -453,8 +617,8 @@ def main():
             q.matched(db, ans)
             return ans.count()
 
-    def step():
-        return sum(run(q) for _, q in qs)
+    def step(i):
+        return sum(run(q) for _, q in qsets[i])
 
     log("warmup")
     # the warmup steps record every kernel scope (the "kernels" table); the
@@ -465,11 +629,11 @@ def main():
         if i == args.warmup - 1:           # the last (warm) warmup step is the one profiled
             db.ctx.prof_reset()
             db.ctx.prof_enable(True)
-        step()
+        step(i)
     db.ctx.prof_enable(False)
     warm_stats = db.ctx.prof_stats()
     dominant = roofline_of(warm_stats, args.workload) if args.events == "dominant" else None
-    per_query = {name: run(q) for name, q in qs}
+    per_query = {name: run(q) for name, q in qsets[args.warmup]}
     db.ctx.prof_reset()
     db.ctx.prof_only(dominant["kernel"] if dominant else None)
     db.ctx.prof_enable(True)
@@ -479,8 +643,8 @@ def main():
     t0 = time.perf_counter()
     log("timed steps")
     bindings = 0
-    for _ in range(args.steps):
-        bindings += step()
+    for i in range(args.steps):
+        bindings += step(args.warmup + i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -493,8 +657,8 @@ def main():
         import pstats
         pr = cProfile.Profile()
         pr.enable()
-        for _ in range(3):
-            step()
+        for i in range(3):
+            step(i)
         pr.disable()
         with open(args.cprofile, "w") as f:
             pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
@@ -506,6 +670,9 @@ def main():
         dist.all_reduce(b)
         bindings = float(b.item())
     value = bindings / elapsed
+    incl = None
+    if world == 1 and not args.no_materialise:
+        incl = materialised_rate(pm, db, qsets[n_sets - 1], args.materialise_cap)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -521,8 +688,9 @@ def main():
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "u32", "data": data, "config": cfg,
-            "roofline": roofline_of(stats, args.workload),
+            "roofline": roofline_of(stats, args.workload, dominant["kernel"] if dominant else None),
             "cpu_baseline": cpu,
+            "incl_materialisation": incl,
             "kernels": kernels_of(warm_stats if dominant else stats),
             "kernels_from": "last warmup step (every scope)" if dominant else "timed steps (every scope)",
             "build_s": round(t_build, 2),

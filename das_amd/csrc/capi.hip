@@ -70,12 +70,20 @@ struct HostTrace {
   }
 };
 
+// The context a C-ABI call runs for, visible to KScope for its duration.
+struct ActiveCtx {
+  das::Ctx* prev;
+  explicit ActiveCtx(das::Ctx* c) : prev(das::active_ctx()) { das::active_ctx() = c; }
+  ~ActiveCtx() { das::active_ctx() = prev; }
+};
+
 template <typename F>
 int guarded(das_ctx_t* ctx, F&& f, const char* fn = __builtin_FUNCTION()) {
   HostTrace tr(fn);
   try {
     if (ctx) {
       std::lock_guard<std::mutex> lk(ctx->c.mu);
+      ActiveCtx act(&ctx->c);
       int cur = -1;
       if (hipGetDevice(&cur) != hipSuccess || cur != ctx->c.device) DAS_HIP(hipSetDevice(ctx->c.device));
       f();
@@ -640,6 +648,17 @@ int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap) {
 }  // extern "C"
 
 namespace das {
+Ctx*& active_ctx() {
+  thread_local Ctx* c = nullptr;
+  return c;
+}
+
+KScope::KScope(const char* name, double algorithmic_bytes) {
+  Ctx* c = active_ctx();
+  if (c && c->prof) impl = new ProfScope(*c, name, algorithmic_bytes);
+}
+KScope::~KScope() { delete static_cast<ProfScope*>(impl); }
+
 void prof_collect(Ctx& c) {
   if (c.pending.empty()) return;
   DAS_HIP(hipStreamSynchronize(c.s));

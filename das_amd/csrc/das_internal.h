@@ -152,13 +152,17 @@ struct Ctx {
   std::vector<uint64_t> leaf_off;
 };
 
+// Scope names are the kernel's name as rocprofv3 reports it, shortened the
+// way tools/pmc_traffic.py shortens it (namespaces dropped, integer template
+// arguments kept, unsigned int/long -> u32/u64), e.g. "k_dj_write<2,1,u32>",
+// so every launch size and time pairs with its rocprof row.
 struct ProfScope {
   Ctx& c;
-  const char* name;
+  std::string name;
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(Ctx& ctx, const char* n, double algorithmic_bytes) : c(ctx), name(n), bytes(algorithmic_bytes) {
-    if (!c.prof || (!c.prof_only.empty() && c.prof_only != n)) return;
+  ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
+    if (!c.prof || (!c.prof_only.empty() && c.prof_only != name)) return;
     a = c.take_event();
     b = c.take_event();
     DAS_HIP(hipEventRecord(a, c.s));
@@ -170,6 +174,8 @@ struct ProfScope {
   }
 };
 void prof_collect(Ctx& c);
+// The context whose C-ABI call runs on this thread (KScope's target).
+Ctx*& active_ctx();
 
 // hash.hip
 void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, Digest* out, hipStream_t s);

@@ -540,6 +540,7 @@ struct WidenU32 {
   const uint32_t* a;
   uint64_t n;
   __device__ uint64_t operator()(uint64_t i) const { return i < n ? (uint64_t)a[i] : 0ull; }
+  static std::string name() { return "WidenU32"; }
 };
 
 inline dim3 G(uint64_t n) { return dim3(grid_for(n, 256)); }
@@ -554,6 +555,7 @@ uint64_t compact_flags(const uint32_t* flag, uint64_t n, DBuf<uint32_t>& out, hi
   read_u32x2(scan.p + n - 1, flag + n - 1, s, last);
   const uint64_t m = (uint64_t)last[0] + last[1];
   out.alloc(m ? m : 1, s);
+  KScope ks("k_compact_index", 8.0 * n + 4.0 * m);
   hipLaunchKernelGGL(k_compact_index, G(n), dim3(B), 0, s, flag, (const uint32_t*)scan.p, n, out.p);
   DAS_HIP(hipGetLastError());
   return m;
@@ -629,6 +631,7 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
   for (uint64_t ty = 0; ty < n_types && ty + 1 < to.size(); ++ty) {
     const uint64_t b = to[ty], e = to[ty + 1];
     if (e <= b) continue;
+    KScope ks("k_seg_minmax", 4.0 * ncol * (e - b));
     hipLaunchKernelGGL(k_seg_minmax, dim3(grid_for(e - b, 256, 1024)), dim3(256), 0, s, (const uint32_t*)t.data,
                        t.ld, ncol, b, e, d.p + ty * ncol * 2);
   }
@@ -652,11 +655,17 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
 void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s) {
   if (n <= 1) return;
   DBuf<uint64_t> key(n, s);
-  hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
+  {
+    KScope ks("k_digest_key", 28.0 * n);           // index, gathered digest half (8 of 16 B), key out
+    hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
+  }
   radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
   DBuf<uint32_t> bad(1, s);
   fill_dev(bad.p, 0, 4, s);
-  hipLaunchKernelGGL(k_hi_ties, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, bad.p);
+  {
+    KScope ks("k_hi_ties", 20.0 * n);
+    hipLaunchKernelGGL(k_hi_ties, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, bad.p);
+  }
   if (read_u32(bad.p, s) == 0) return;
   // exact: LSD over (lo, hi)
   hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, false);
@@ -670,7 +679,9 @@ template <typename K>
 uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hipStream_t s) {
   DBuf<uint32_t> f(n ? n : 1, s), scan(n ? n : 1, s);
   uint64_t m = 0;
+  const std::string tag = key_tag<K>();
   if (n) {
+    KScope ks(("k_run_flags<" + tag + ">").c_str(), (sizeof(K) + 4.0) * n);
     hipLaunchKernelGGL((k_run_flags<K>), G(n), dim3(B), 0, s, key, n, f.p);
     exclusive_scan<uint32_t>(f.p, n, scan.p, s);
     m = (uint64_t)read_u32(scan.p + n - 1, s) + read_u32(f.p + n - 1, s);
@@ -678,6 +689,7 @@ uint64_t rle(const K* key, uint64_t n, K** ukey, uint64_t** uoff, Index& idx, hi
   *ukey = dalloc<K>(idx, m);
   *uoff = dalloc<uint64_t>(idx, m + 1);
   if (n) {
+    KScope ks(("k_run_emit<" + tag + ">").c_str(), (sizeof(K) + 8.0) * n + (sizeof(K) + 8.0) * m);
     hipLaunchKernelGGL((k_run_emit<K>), G(n), dim3(B), 0, s, key, (const uint32_t*)f.p, (const uint32_t*)scan.p, n,
                        *ukey, *uoff);
     DAS_HIP(hipGetLastError());
@@ -742,6 +754,7 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
     if (span > 2 * (khi - klo) + 4096) continue;
     uint32_t* d = dalloc<uint32_t>(idx, span);
     fill_dev(d, 0xFF, 4 * span, s);
+    KScope ks("k_dir_scatter", 12.0 * (khi - klo));
     hipLaunchKernelGGL(k_dir_scatter, dim3(grid_for(khi - klo, 256, 8192)), dim3(256), 0, s, (const uint64_t*)P.ukey,
                        klo, khi - klo, (uint32_t)tmin, d);
     DAS_HIP(hipGetLastError());
@@ -810,7 +823,10 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     ProfScope ps(c, "k_hash_strings", (double)n_bytes + 8.0 * nl + 16.0 * nl);
     hash_strings(d_bytes.p, d_loff.p, nl, dig.p, s);
   }
-  if (nl) hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)d_lct.p, ct.p, nl);
+  if (nl) {
+    KScope ks("k_leaf_ctype", 36.0 * nl);
+    hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)d_lct.p, ct.p, nl);
+  }
   for (uint32_t g = 0; g < a.n_levels; ++g) {
     const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
     if (e <= b) continue;
@@ -823,17 +839,24 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
       K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
     }
     // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
-    ProfScope ps(c, "k_hash_group", (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
+    ProfScope ps(c, K <= 9 ? "k_hash_group<" + std::to_string(K) + ">" : std::string("k_hash_group_dyn"),
+                 (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
     hash_group(dig.p, ct.p, p_child, p_eoff, p_ectl, nl, b, e - b, K, s);
   }
 
   // 2. which unified indices are atoms (nodes, links, link targets)
   DBuf<uint8_t> catl(nu, s);
   DBuf<uint32_t> flag(nu, s);
-  hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind, nl, ne,
-                     catl.p, flag.p);
-  if (ne) hipLaunchKernelGGL(k_mark_targets, G(ne), dim3(B), 0, s, (const uint8_t*)p_ekind, (const uint64_t*)p_eoff,
-                             (const uint32_t*)p_child, ne, flag.p);
+  {
+    KScope ks("k_init_cat", 1.0 * nu + 5.0 * nu);
+    hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind, nl, ne,
+                       catl.p, flag.p);
+  }
+  if (ne) {
+    KScope ks("k_mark_targets", 9.0 * ne + 8.0 * n_child);
+    hipLaunchKernelGGL(k_mark_targets, G(ne), dim3(B), 0, s, (const uint8_t*)p_ekind, (const uint64_t*)p_eoff,
+                       (const uint32_t*)p_child, ne, flag.p);
+  }
   DAS_HIP(hipGetLastError());
   DBuf<uint32_t> list;
   const uint64_t nc = compact_flags(flag.p, nu, list, s);
@@ -844,7 +867,10 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   DBuf<uint32_t> first(nc ? nc : 1, s), scan(nc ? nc : 1, s);
   uint64_t n_atoms = 0;
   if (nc) {
-    hipLaunchKernelGGL(k_first_flags, G(nc), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)list.p, nc, first.p);
+    {
+      KScope ks("k_first_flags", 24.0 * nc);
+      hipLaunchKernelGGL(k_first_flags, G(nc), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)list.p, nc, first.p);
+    }
     exclusive_scan<uint32_t>(first.p, nc, scan.p, s);
     n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
   }
@@ -854,13 +880,23 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   fill_dev(rep.p, 0xFF, 4 * rep.n, s);
   if (nc) {
     DBuf<uint8_t> cs(nc, s);
-    hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
-                       (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p, rep.p, cs.p);
-    hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
-                       (const uint32_t*)scan.p, nc, (const uint8_t*)cs.p, (const uint32_t*)catmax.p, rep.p);
+    {
+      // list, first, scan, catl in; local2id, sorted category out; catmax + rep per atom
+      KScope ks("k_assign_ids", 19.0 * nc + 8.0 * n_atoms);
+      hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
+                         (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p, rep.p, cs.p);
+    }
+    {
+      KScope ks("k_pick_rep", 13.0 * nc);
+      hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
+                         (const uint32_t*)scan.p, nc, (const uint8_t*)cs.p, (const uint32_t*)catmax.p, rep.p);
+    }
     DBuf<uint32_t> bad(1, s);
     fill_dev(bad.p, 0, 4, s);
-    hipLaunchKernelGGL(k_rep_missing, G(n_atoms), dim3(B), 0, s, (const uint32_t*)rep.p, n_atoms, bad.p);
+    {
+      KScope ks("k_rep_missing", 4.0 * n_atoms);
+      hipLaunchKernelGGL(k_rep_missing, G(n_atoms), dim3(B), 0, s, (const uint32_t*)rep.p, n_atoms, bad.p);
+    }
     DAS_HIP(hipGetLastError());
     DAS_CHECK(read_u32(bad.p, s) == 0, DAS_E_INTERNAL, "intern: a digest run has no representative");
   }
@@ -872,17 +908,24 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   {
     DBuf<uint32_t> tkey(n_atoms ? n_atoms : 1, s), perm(n_atoms ? n_atoms : 1, s);
     if (n_atoms) {
-      hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
-                         (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
-                         (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, tkey.p);
+      {
+        KScope ks("k_temp_type", 24.0 * n_atoms);    // rep, catmax, a type lookup, key out
+        hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
+                           (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
+                           (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, tkey.p);
+      }
       iota(perm.p, n_atoms, s);
       radix_sort_pairs<uint32_t>(tkey.p, perm.p, n_atoms, 0, std::max(1, bits_for(a.n_types)), s);
     }
     idx.by_digest = dalloc<uint32_t>(idx, n_atoms);
     DBuf<uint32_t> rep2(n_atoms ? n_atoms : 1, s), cat2(n_atoms ? n_atoms : 1, s);
     if (n_atoms) {
-      hipLaunchKernelGGL(k_apply_perm, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)perm.p,
-                         (const uint32_t*)rep.p, (const uint32_t*)catmax.p, rep2.p, cat2.p, idx.by_digest);
+      {
+        KScope ks("k_apply_perm", 24.0 * n_atoms);
+        hipLaunchKernelGGL(k_apply_perm, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)perm.p,
+                           (const uint32_t*)rep.p, (const uint32_t*)catmax.p, rep2.p, cat2.p, idx.by_digest);
+      }
+      KScope ks("k_remap_local", 8.0 * nu + 4.0 * n_atoms);
       hipLaunchKernelGGL(k_remap_local, G(nu), dim3(B), 0, s, nu, (const uint32_t*)idx.by_digest, local2id.p);
       DAS_HIP(hipGetLastError());
     }
@@ -902,6 +945,9 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   idx.name_leaf = dalloc<uint32_t>(idx, n_atoms);
   DBuf<Digest> a_ct(n_atoms ? n_atoms : 1, s);
   if (n_atoms) {
+    // rep + catmax in, digest + ctype digest gathered, type lookup; digest,
+    // cat, type, arity, ctype digest, name leaf out
+    KScope ks("k_fill_atoms", 8.0 * n_atoms + 32.0 * n_atoms + 8.0 * n_atoms + 16.0 * n_atoms + 29.0 * n_atoms);
     hipLaunchKernelGGL(k_fill_atoms, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                        (const uint32_t*)catmax.p, (const Digest*)dig.p, (const Digest*)ct.p, nl,
                        (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)p_eoff,
@@ -915,6 +961,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     exclusive_scan_fn<uint64_t>(WidenU32{idx.arity, n_atoms}, n_atoms + 1, idx.tgt_off, s);
     const uint64_t total = read_u64(idx.tgt_off + n_atoms, s);
     idx.tgt = dalloc<uint32_t>(idx, total);
+    KScope ks("k_fill_targets", 13.0 * n_atoms + 12.0 * total);     // per target: child in, id lookup, target out
     if (n_atoms)
       hipLaunchKernelGGL(k_fill_targets, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                          (const uint8_t*)idx.cat, (const uint64_t*)idx.tgt_off, nl, (const uint64_t*)p_eoff,
@@ -935,9 +982,13 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     idx.in_link = dalloc<uint32_t>(idx, total);
     if (total) {
       DBuf<uint32_t> key(total, s);
-      hipLaunchKernelGGL(k_owner_fill, G(n_atoms), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, n_atoms, idx.in_link);
+      {
+        KScope ks("k_owner_fill", 8.0 * n_atoms + 4.0 * total);
+        hipLaunchKernelGGL(k_owner_fill, G(n_atoms), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, n_atoms, idx.in_link);
+      }
       copy_dev(key.p, idx.tgt, 4 * total, s);
       radix_sort_pairs<uint32_t>(key.p, idx.in_link, total, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
+      KScope ks("k_bounds_u32", 4.0 * total + 4.0 * (n_atoms + 1));
       hipLaunchKernelGGL(k_bounds_u32, G(n_atoms + 1), dim3(B), 0, s, (const uint32_t*)key.p, total,
                          (uint32_t)n_atoms, idx.in_off);
     } else {
@@ -951,6 +1002,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   {
     DBuf<unsigned long long> h(64, s);
     fill_dev(h.p, 0, 64 * 8, s);
+    KScope ks("k_arity_hist", 5.0 * n_atoms);
     if (n_atoms) hipLaunchKernelGGL(k_arity_hist, dim3(grid_for(n_atoms, B, 2048)), dim3(B), 0, s, (const uint8_t*)idx.cat,
                                     (const uint32_t*)idx.arity, n_atoms, h.p);
     unsigned long long hh[64];
@@ -967,13 +1019,19 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   uint64_t n_ctypes = 0;
   {
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), lids;
-    if (n_atoms) hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+    if (n_atoms) {
+      KScope ks("k_link_flags", 9.0 * n_atoms);
+      hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
                                     (const uint32_t*)idx.arity, n_atoms, kNone, lf.p);
+    }
     const uint64_t nlk = compact_flags(lf.p, n_atoms, lids, s);
     if (nlk) {
       // sort link ids by ctype digest (hi, exact fallback)
       DBuf<uint64_t> key(nlk, s);
-      hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
+      {
+        KScope ks("k_ct_key", 28.0 * nlk);
+        hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, true);
+      }
       // composite types are few: order by the top 16 bits of hi (2 passes, not
       // 8); exact unless two different hi values share those bits, or two
       // different digests share hi -- either sends us to the full sort
@@ -989,11 +1047,17 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
       }
       DBuf<uint32_t> f(nlk, s), sc(nlk, s);
-      hipLaunchKernelGGL(k_first_flags, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, f.p);
+      {
+        KScope ks("k_first_flags", 24.0 * nlk);
+        hipLaunchKernelGGL(k_first_flags, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, f.p);
+      }
       exclusive_scan<uint32_t>(f.p, nlk, sc.p, s);
       n_ctypes = (uint64_t)read_u32(sc.p + nlk - 1, s) + read_u32(f.p + nlk - 1, s);
-      hipLaunchKernelGGL(k_set_ctype, G(nlk), dim3(B), 0, s, (const uint32_t*)lids.p, (const uint32_t*)f.p,
-                         (const uint32_t*)sc.p, nlk, idx.ctype);
+      {
+        KScope ks("k_set_ctype", 16.0 * nlk);
+        hipLaunchKernelGGL(k_set_ctype, G(nlk), dim3(B), 0, s, (const uint32_t*)lids.p, (const uint32_t*)f.p,
+                           (const uint32_t*)sc.p, nlk, idx.ctype);
+      }
       DBuf<Digest> u(n_ctypes, s);
       hipLaunchKernelGGL(k_ct_unique, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p,
                          (const uint32_t*)f.p, (const uint32_t*)sc.p, nlk, u.p);
@@ -1009,8 +1073,11 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   // 7. per-arity tables
   for (uint32_t ar = 1; ar <= (uint32_t)kMaxArity; ++ar) {
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), ids;
-    if (n_atoms) hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
-                                    (const uint32_t*)idx.arity, n_atoms, ar, lf.p);
+    if (n_atoms) {
+      KScope ks("k_link_flags", 9.0 * n_atoms);
+      hipLaunchKernelGGL(k_link_flags, G(n_atoms), dim3(B), 0, s, (const uint8_t*)idx.cat,
+                         (const uint32_t*)idx.arity, n_atoms, ar, lf.p);
+    }
     const uint64_t R = compact_flags(lf.p, n_atoms, ids, s);
     lf.release();
     if (!R) continue;
@@ -1019,15 +1086,22 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     {
       DBuf<uint32_t> key(R, s), perm(R, s);
       copy_dev(perm.p, ids.p, 4 * R, s);
-      hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint32_t*)perm.p, R, key.p);
+      {
+        KScope ks("k_u32_key", 12.0 * R);
+        hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint32_t*)perm.p, R, key.p);
+      }
       radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, tbits > 0 ? tbits : 1, s);
       RowTable& t = idx.ttab[ar];
       t.arity = (int)ar;
       t.rows = R;
       t.ld = col_stride(R);
       t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * t.ld);
-      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
-                         (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      {
+        // id in, its target offset and targets gathered, (id, targets) row out
+        KScope ks("k_gather_rows", 4.0 * R + 8.0 * R + 4.0 * ar * R + 4.0 * (ar + 1) * R);
+        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
+                           (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      }
       // host type offsets
       uint32_t* ukey; uint64_t* uoff;
       const uint64_t m = rle<uint32_t>(key.p, R, &ukey, &uoff, idx, s);
@@ -1050,7 +1124,10 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     {
       DBuf<uint32_t> key(R, s), perm(R, s);
       copy_dev(perm.p, ids.p, 4 * R, s);
-      hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.ctype, (const uint32_t*)perm.p, R, key.p);
+      {
+        KScope ks("k_u32_key", 12.0 * R);
+        hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.ctype, (const uint32_t*)perm.p, R, key.p);
+      }
       const int cbits = bits_for(n_ctypes ? n_ctypes - 1 : 0);
       radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, cbits > 0 ? cbits : 1, s);
       RowTable& t = idx.ctab[ar];
@@ -1058,8 +1135,12 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
       t.rows = R;
       t.ld = col_stride(R);
       t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * t.ld);
-      hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
-                         (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      {
+        // id in, its target offset and targets gathered, (id, targets) row out
+        KScope ks("k_gather_rows", 4.0 * R + 8.0 * R + 4.0 * ar * R + 4.0 * (ar + 1) * R);
+        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, t.ld, ar,
+                           (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, t.data);
+      }
       uint32_t* ukey; uint64_t* uoff;
       const uint64_t m = rle<uint32_t>(key.p, R, &ukey, &uoff, idx, s);
       std::vector<uint32_t> hk(m);
@@ -1082,12 +1163,18 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         for (int q = (int)ar - 1; q >= 0; --q) {
           if ((uint32_t)q == p) continue;
           DBuf<uint32_t> k2(R, s);
-          hipLaunchKernelGGL(k_tgt_key, G(R), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt,
-                             (const uint32_t*)perm.p, R, (uint32_t)q, k2.p);
+          {
+            KScope ks("k_tgt_key", 20.0 * R);
+            hipLaunchKernelGGL(k_tgt_key, G(R), dim3(B), 0, s, (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt,
+                               (const uint32_t*)perm.p, R, (uint32_t)q, k2.p);
+          }
           radix_sort_pairs<uint32_t>(k2.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
         }
-        hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,
-                           (const uint32_t*)idx.tgt, (const uint32_t*)perm.p, R, p, key.p);
+        {
+          KScope ks("k_pos_key", 28.0 * R);
+          hipLaunchKernelGGL(k_pos_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint64_t*)idx.tgt_off,
+                             (const uint32_t*)idx.tgt, (const uint32_t*)perm.p, R, p, key.p);
+        }
         // (type, t_p, t_q, id): sort by t_p, then (stable) by type
         radix_sort_pairs<uint64_t>(key.p, perm.p, R, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
         radix_sort_pairs<uint64_t>(key.p, perm.p, R, 32, 32 + std::max(1, tbits), s);
@@ -1096,8 +1183,11 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         P.t.rows = R;
         P.t.ld = col_stride(R);
         P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * P.t.ld);
-        hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, P.t.ld, ar,
-                           (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, P.t.data);
+        {
+          KScope ks("k_gather_rows", 4.0 * R + 8.0 * R + 4.0 * ar * R + 4.0 * (ar + 1) * R);
+          hipLaunchKernelGGL(k_gather_rows, G(R), dim3(B), 0, s, (const uint32_t*)perm.p, R, P.t.ld, ar,
+                             (const uint64_t*)idx.tgt_off, (const uint32_t*)idx.tgt, P.t.data);
+        }
         P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
         build_key_dir(P, idx, s);
       }

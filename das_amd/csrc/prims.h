@@ -10,6 +10,21 @@ namespace das {
 // ---------------------------------------------------------------------------
 // Exclusive scan (wave-level shuffles, 2048 items per 256-thread block)
 // ---------------------------------------------------------------------------
+// Timing scope for one kernel launch below the context layer (sorts, scans,
+// index build kernels): HIP events on the stream of the context whose C-ABI
+// call is running on this thread, when its profiling is on (das_prof_*).
+// Names follow ProfScope's convention (das_internal.h).
+struct KScope {
+  void* impl = nullptr;
+  KScope(const char* name, double algorithmic_bytes);
+  ~KScope();
+  KScope(const KScope&) = delete;
+  KScope& operator=(const KScope&) = delete;
+};
+template <typename K> constexpr const char* key_tag();
+template <> constexpr const char* key_tag<uint32_t>() { return "u32"; }
+template <> constexpr const char* key_tag<uint64_t>() { return "u64"; }
+
 constexpr int kScanBlock = 256;
 constexpr int kScanItems = 8;
 constexpr int kScanTile = kScanBlock * kScanItems;
@@ -142,6 +157,7 @@ template <typename T>
 struct PtrIn {
   const T* p;
   __device__ __forceinline__ T operator()(uint64_t i) const { return p[i]; }
+  static std::string name() { return std::string("PtrIn<") + key_tag<T>() + ">"; }
 };
 
 // out[i] = sum_{j<i} in(j).  Returns nothing; total = out[n-1] + in(n-1).
@@ -149,15 +165,21 @@ template <typename T, typename In>
 void exclusive_scan_fn(In in, uint64_t n, T* out, hipStream_t s) {
   if (n == 0) return;
   uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  const std::string targs = std::string("<") + key_tag<T>() + "," + In::name() + ">";
   if (tiles == 1) {
+    KScope ks(("k_scan_tiles" + targs).c_str(), 2.0 * sizeof(T) * n);
     hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3(1), dim3(kScanBlock), 0, s, in, n, (const T*)nullptr, out);
     DAS_HIP(hipGetLastError());
     return;
   }
   DBuf<T> sums(tiles, s), offs(tiles, s);
-  hipLaunchKernelGGL((k_scan_reduce<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n, sums.p);
+  {
+    KScope ks(("k_scan_reduce" + targs).c_str(), (double)sizeof(T) * n);
+    hipLaunchKernelGGL((k_scan_reduce<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n, sums.p);
+  }
   DAS_HIP(hipGetLastError());
   exclusive_scan_fn<T>(PtrIn<T>{sums.p}, tiles, offs.p, s);
+  KScope ks(("k_scan_tiles" + targs).c_str(), 2.0 * sizeof(T) * n);
   hipLaunchKernelGGL((k_scan_tiles<T, In>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, n,
                      (const T*)offs.p, out);
   DAS_HIP(hipGetLastError());
@@ -354,7 +376,9 @@ __global__ void k_copy_u32(uint32_t* dst, const uint32_t* src, uint64_t n);
 __global__ void k_copy_u128(uint4* dst, const uint4* src, uint64_t n);
 inline void copy_dev(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
   if (!bytes) return;
-  if (((((uintptr_t)dst) | ((uintptr_t)src) | bytes) & 15) == 0) {
+  const bool wide = ((((uintptr_t)dst) | ((uintptr_t)src) | bytes) & 15) == 0;
+  KScope ks(wide ? "k_copy_u128" : "k_copy_u32", 2.0 * bytes);
+  if (wide) {
     const uint64_t n = bytes / 16;
     hipLaunchKernelGGL(k_copy_u128, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, (uint4*)dst, (const uint4*)src, n);
   } else {
@@ -536,11 +560,18 @@ void radix_sort_pairs(K* keys, uint32_t* vals, uint64_t n, int begin_bit, int en
   K* ka = keys; K* kb = k2.p;
   uint32_t* va = vals; uint32_t* vb = v2.p;
   int passes = 0;
+  const std::string tag = key_tag<K>();
+  const double kv = (double)n * (sizeof(K) + (vals ? 4.0 : 0.0));    // one pass: keys (+ values) in and out
   for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
-    hipLaunchKernelGGL((k_radix_hist<K>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka, n, shift, hist.p, tiles);
+    {
+      KScope ks(("k_radix_hist<" + tag + ">").c_str(), (double)n * sizeof(K));
+      hipLaunchKernelGGL((k_radix_hist<K>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka, n, shift, hist.p, tiles);
+    }
     DAS_HIP(hipGetLastError());
     exclusive_scan<uint32_t>(hist.p, (uint64_t)tiles * 256, offs.p, s);
     static const bool lds = !(std::getenv("DAS_SORT_LDS") && std::getenv("DAS_SORT_LDS")[0] == '0');
+    KScope ks(((lds ? "k_radix_scatter_lds<" : "k_radix_scatter<") + tag + (vals ? ",true>" : ",false>")).c_str(),
+              2.0 * kv);
     if (lds && vals)
       hipLaunchKernelGGL((k_radix_scatter_lds<K, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
                          (const uint32_t*)va, kb, vb, n, shift, (const uint32_t*)hist.p, (const uint32_t*)offs.p,
@@ -579,11 +610,13 @@ __global__ void k_gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t*
 
 inline void iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (!n) return;
+  KScope ks("k_iota", 4.0 * n);
   hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n);
   DAS_HIP(hipGetLastError());
 }
 inline void gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t* dst, uint64_t n, hipStream_t s) {
   if (!n) return;
+  KScope ks("k_gather_u32", 12.0 * n);
   hipLaunchKernelGGL(k_gather_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, src, idx, dst, n);
   DAS_HIP(hipGetLastError());
 }
@@ -595,6 +628,7 @@ inline void fill_dev(void* dst, int byte, uint64_t bytes, hipStream_t s) {
   if (!bytes) return;
   const uint32_t b = (uint32_t)(byte & 0xFF);
   const uint64_t n = bytes / 4;
+  KScope ks("k_fill_u32", (double)bytes);
   hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, (uint32_t*)dst,
                      b | (b << 8) | (b << 16) | (b << 24), n);
   DAS_HIP(hipGetLastError());

@@ -653,7 +653,10 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
 template <int NP, int NB>
 void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
                      const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out,
-                     uint64_t cap, uint64_t total, bool balanced) {
+                     uint64_t cap, uint64_t total, bool balanced, double bytes) {
+  const bool wide = total >= (1ull << 32) - (1ull << 16);
+  KScope ks((std::string(balanced ? "k_dj_write_bal<" : "k_dj_write<") + std::to_string(NP) + "," +
+             std::to_string(NB) + (wide ? ",u64>" : ",u32>")).c_str(), bytes);
   if (balanced) {
     const unsigned g = grid_for((total + kBalChunk - 1) / kBalChunk, B / 64, 65535u * 4u);
     if (total < (1ull << 32) - (1ull << 16))
@@ -674,9 +677,11 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
 
 // dispatch on (probe cols, build cols); wide schemas use the 4 x 4 kernel in
 // column slices
+// bytes(np, nb): algorithmic bytes of a launch writing np probe and nb build columns
+template <typename Bytes>
 void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
               const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out, uint64_t cap,
-              uint64_t total, bool balanced) {
+              uint64_t total, bool balanced, const Bytes& bytes) {
   int pi = 0, bi = 0;
   do {
     JoinCols part{};
@@ -688,7 +693,8 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
     bi += part.nb;
 #define DJ(NPV, NBV)                                                                                  \
   if (part.np == NPV && part.nb == NBV) {                                                             \
-    launch_dj_write<NPV, NBV>(grid, s, pkey, np, kmin, range, lc, units, toff, part, out, cap, total, balanced); \
+    launch_dj_write<NPV, NBV>(grid, s, pkey, np, kmin, range, lc, units, toff, part, out, cap, total, balanced,      \
+                              bytes(part.np, part.nb));                                                            \
     continue;                                                                                         \
   }
     DJ(0, 1) DJ(0, 2) DJ(0, 3) DJ(0, 4)
@@ -1226,11 +1232,16 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
   auto out = new_table(c, DAS_TABLE_ORDERED, nu, uni, total);
   out->nrows = total;
   if (total) {
-    // algorithmic bytes: probe payload + build payload + output
-    ProfScope ps(c, balanced ? "k_dj_write_bal" : "k_dj_write",
-                 4.0 * P.nrows * P.ncols + build_bytes + 4.0 * total * nu);
+    // algorithmic bytes: probe payload + build payload +
+    // output, per launch (a schema wider than 4 + 4 columns is written by
+    // several launches, each reading the key and its own columns)
+    const bool one = jc.np <= 4 && jc.nb <= 4;
+    auto bytes = [&](int np, int nb) {
+      if (one) return 4.0 * P.nrows * P.ncols + build_bytes + 4.0 * total * nu;
+      return 4.0 * P.nrows * (np + 1) + (jc.nb ? build_bytes * nb / jc.nb : 0.0) + 4.0 * total * (np + nb);
+    };
     dj_write(grid, c.s, pkey, P.nrows, kmin, (uint32_t)range, lc, units, (const uint64_t*)toff.p, jc,
-             out->data, out->cap, total, balanced);
+             out->data, out->cap, total, balanced, bytes);
     DAS_HIP(hipGetLastError());
   }
   return out;

@@ -19,10 +19,16 @@ import sys
 
 
 def short(name):
+    """rocprof kernel name -> the HIP-event scope name bench.py reports
+    (das_internal.h ProfScope): namespaces and the parameter list dropped,
+    template arguments kept with unsigned int / long spelled u32 / u64, no
+    spaces, e.g. "k_dj_write<2,1,u32>", "k_radix_scatter_lds<u64,true>"."""
     n = name.replace("das::(anonymous namespace)::", "").replace("das::", "").replace("void ", "")
-    if n.startswith("k_tile_count<"):          # predicate kernels: scope names keep the predicate
-        return re.sub(r">.*", ">", n)
-    return re.sub(r"[<(].*", "", n)
+    n = n.split("(", 1)[0]
+    for a, b in (("unsigned long long", "u64"), ("unsigned long", "u64"), ("unsigned int", "u32"),
+                 ("unsigned char", "u8")):
+        n = n.replace(a, b)
+    return n.replace(" ", "")
 
 
 def per_kernel(db_dir, counter):

@@ -1,21 +1,30 @@
 #!/bin/bash
-# Profiles bench.py on the GPU box (run through gpurun from the repo root):
-#   1. rocprofv3 kernel trace + stats (csv) of the bench run
-#   2. HBM traffic PMC passes, FETCH_SIZE and WRITE_SIZE in separate runs
+# Measures one bench.py workload on the GPU box (run through gpurun from the
+# repo root); every step has its own time limit and the steps are chained, so
+# a failure ends the script.
+#   1. bench.py itself (the JSON line, with its cpu_baseline)
+#   2. rocprofv3 kernel trace + stats (csv) of the same bench command
+#   3. HBM traffic PMC passes, FETCH_SIZE and WRITE_SIZE in separate runs
 #      (MI355X_MICROARCH.md "HBM": one TCC counter group per pass)
-#   3. tools/pmc_traffic.py -> gpurun_out/pmc_traffic[_<workload>].json (per-kernel
-#      bytes per launch, gfx950 FETCH_SIZE correction applied)
-# WORKLOAD selects bench.py --workload (default bio); BENCH_ARGS adds flags.
-# Copy what is worth keeping into profiles/ afterwards.
+#   4. tools/pmc_traffic.py -> per-kernel bytes per launch (gfx950 FETCH_SIZE
+#      correction), tools/roofline_check.py -> the bench's roofline recomputed
+#      from the rocprof CSV
+# WORKLOAD selects bench.py --workload (default bio); BENCH_ARGS adds flags;
+# TAG names the outputs gpurun_out/<TAG>_<workload>*.  Copy what is worth
+# keeping into profiles/ afterwards.
 set -o pipefail
 W=${WORKLOAD:-bio}
-D=gpurun_out/prof_$W
+T=${TAG:-r2}
+D=gpurun_out/prof_${T}_$W
 mkdir -p $D
 export TMPDIR=/tmp
-ARGS="--workload $W --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
-OUT=pmc_traffic.json
-[ "$W" != bio ] && OUT=pmc_traffic_$W.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $ARGS > $D/kt.log 2>&1 &&
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/fetch -o run -- python bench.py $ARGS > $D/fetch.log 2>&1 &&
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $ARGS > $D/write.log 2>&1 &&
-python tools/pmc_traffic.py $D/fetch $D/write > gpurun_out/$OUT
+ARGS="--workload $W --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-}"
+PARGS="$ARGS --no-cpu-baseline --no-materialise"
+timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
+timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS > $D/kt.log 2>&1 &&
+cp "$(find $D/kt -name 'run_kernel_stats.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_stats.csv &&
+timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/fetch -o run -- python bench.py $PARGS > $D/fetch.log 2>&1 &&
+timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $PARGS > $D/write.log 2>&1 &&
+python tools/pmc_traffic.py $D/fetch $D/write > gpurun_out/${T}_pmc_traffic_$W.json &&
+python tools/roofline_check.py gpurun_out/${T}_bench_$W.json gpurun_out/${T}_${W}_kernel_stats.csv \
+    gpurun_out/${T}_pmc_traffic_$W.json > gpurun_out/${T}_roofline_check_$W.json
