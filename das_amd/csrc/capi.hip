@@ -352,8 +352,12 @@ int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out) {
 
 int das_lookup(das_ctx_t* ctx, const uint32_t* digests, uint64_t n, int64_t* ids, uint8_t* cat, uint32_t* arity,
                uint32_t* type) {
-  int rc = guarded(ctx, [&] { das::lookup_digests(ctx->c, (const Digest*)digests, n, ids); });
-  if (rc || (!cat && !arity && !type)) return rc;
+  bool done = false;
+  int rc = guarded(ctx, [&] {
+    done = das::lookup_small(ctx->c, (const Digest*)digests, n, ids, cat, arity, type);
+    if (!done) das::lookup_digests(ctx->c, (const Digest*)digests, n, ids);
+  });
+  if (rc || done || (!cat && !arity && !type)) return rc;
   std::vector<uint32_t> valid;
   std::vector<uint64_t> where;
   for (uint64_t i = 0; i < n; ++i) {

@@ -50,7 +50,10 @@ struct PosIndex {
   // span is at most 2x its key count (else dir[ty] == nullptr: binary search).
   std::vector<uint32_t*> dir;
   std::vector<uint32_t> dir_lo, dir_n;
+  // host mirror of ukey / uoff (nkeys <= kHostKeyMirror), else empty
+  std::vector<uint64_t> h_ukey, h_uoff;
 };
+constexpr uint64_t kHostKeyMirror = 1ull << 24;   // keys per P_{a,p} mirrored on the host (256 MB at most)
 
 struct CtypeRange {
   uint32_t arity;
@@ -191,6 +194,10 @@ void synth_powerlaw_links(uint32_t* d_child, uint64_t first, uint64_t n, uint32_
                           hipStream_t st);
 void free_index(Index& idx);
 void lookup_digests(Ctx& c, const Digest* h_digests, uint64_t n, int64_t* h_ids);
+// ids + category / arity / type of up to 4096 handles in one pinned round
+// trip (false: batch too large, use lookup_digests + das_atoms_info)
+bool lookup_small(Ctx& c, const Digest* h_digests, uint64_t n, int64_t* h_ids, uint8_t* cat, uint32_t* arity,
+                  uint32_t* type);
 
 // Column pointers of a table (kernel argument by value).
 struct ColSet {

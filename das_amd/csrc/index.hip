@@ -83,6 +83,21 @@ Slot& slot() {
 
 }  // namespace
 
+uint8_t* pinned_stage(uint64_t bytes) {
+  struct Stage {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0;
+    ~Stage() { if (p) (void)hipHostFree(p); }
+  };
+  thread_local Stage st;
+  if (bytes > st.cap) {
+    if (st.p) DAS_HIP(hipHostFree(st.p));
+    st.cap = std::max<uint64_t>(bytes, 1 << 16);
+    DAS_HIP(hipHostMalloc((void**)&st.p, st.cap, hipHostMallocCoherent | hipHostMallocMapped));
+  }
+  return st.p;
+}
+
 PubSlot pub_reserve() {
   Slot& sl = slot();
   const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;      // never 0 (the initial value)
@@ -1190,12 +1205,83 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         }
         P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
         build_key_dir(P, idx, s);
+        if (P.nkeys <= kHostKeyMirror) {
+          // host copy of the unique keys and offsets: an anchored scan finds
+          // its key range without a device round trip
+          P.h_ukey.resize(P.nkeys);
+          P.h_uoff.resize(P.nkeys + 1);
+          DAS_HIP(hipMemcpyAsync(P.h_ukey.data(), P.ukey, 8 * P.nkeys, hipMemcpyDeviceToHost, s));
+          DAS_HIP(hipMemcpyAsync(P.h_uoff.data(), P.uoff, 8 * (P.nkeys + 1), hipMemcpyDeviceToHost, s));
+          DAS_HIP(hipStreamSynchronize(s));
+        }
       }
     }
     DAS_HIP(hipGetLastError());
   }
   DAS_HIP(hipStreamSynchronize(s));
   idx.built = true;
+}
+
+namespace {
+// Handle lookups through pinned staging (one workgroup; small batches):
+// the request digests are read over the host mapping, each result is
+// stored to the host with system scope, then the slot is released.
+// out[2i] = id (-1: absent), out[2i + 1] = category | arity << 8 | type << 32
+__global__ void __launch_bounds__(256) k_lookup_pub(const Digest* dig, const uint32_t* by_digest, const uint8_t* cat,
+                                                    const uint32_t* arity, const uint32_t* type, uint64_t n_atoms,
+                                                    const Digest* q, uint64_t nq, int64_t* out, uint32_t* slot,
+                                                    uint32_t seq) {
+  for (uint64_t i = threadIdx.x; i < nq; i += blockDim.x) {
+    const uint64_t qh = q[i].hi(), ql = q[i].lo();
+    uint64_t lo = 0, hi = n_atoms;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const Digest d = dig[by_digest[mid]];
+      const uint64_t dh = d.hi(), dl = d.lo();
+      if (dh < qh || (dh == qh && dl < ql)) lo = mid + 1;
+      else hi = mid;
+    }
+    int64_t r = -1, info = (int64_t)kNone << 32;
+    if (lo < n_atoms) {
+      const uint32_t id = by_digest[lo];
+      const Digest d = dig[id];
+      if (d.hi() == qh && d.lo() == ql) {
+        r = (int64_t)id;
+        info = (int64_t)((uint64_t)cat[id] | ((uint64_t)(arity[id] & 0xFFFFFFu) << 8) | ((uint64_t)type[id] << 32));
+      }
+    }
+    __hip_atomic_store(&out[2 * i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&out[2 * i + 1], info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+bool lookup_small(Ctx& c, const Digest* h, uint64_t n, int64_t* out, uint8_t* cat, uint32_t* arity, uint32_t* type) {
+  DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
+  if (n > 4096) return false;
+  if (!n) return true;
+  uint8_t* st = pinned_stage(n * (sizeof(Digest) + 16));
+  Digest* q = reinterpret_cast<Digest*>(st);
+  int64_t* r = reinterpret_cast<int64_t*>(st + n * sizeof(Digest));
+  std::memcpy(q, h, n * sizeof(Digest));
+  const Index& x = c.idx;
+  const PubSlot ps = pub_reserve();
+  hipLaunchKernelGGL(k_lookup_pub, dim3(1), dim3(256), 0, c.s, (const Digest*)x.digest, (const uint32_t*)x.by_digest,
+                     (const uint8_t*)x.cat, (const uint32_t*)x.arity, (const uint32_t*)x.type, x.n_atoms,
+                     (const Digest*)q, n, r, ps.p, ps.seq);
+  DAS_HIP(hipGetLastError());
+  pub_wait(ps, c.s, nullptr, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    out[i] = r[2 * i];
+    const uint64_t info = (uint64_t)r[2 * i + 1];
+    if (cat) cat[i] = (uint8_t)(info & 0xFF);
+    if (arity) arity[i] = (uint32_t)((info >> 8) & 0xFFFFFF);
+    if (type) type[i] = (uint32_t)(info >> 32);
+  }
+  return true;
 }
 
 void lookup_digests(Ctx& c, const Digest* h, uint64_t n, int64_t* out) {

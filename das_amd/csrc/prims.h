@@ -205,6 +205,13 @@ struct PubSlot {
 };
 PubSlot pub_reserve();
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
+// Pinned, device-mapped staging memory for small request / reply calls
+// (handle lookups, index key ranges): the host writes the request, one
+// kernel reads it over the mapping and writes its reply back with
+// system-scope stores before releasing a PubSlot; the host spins on the
+// slot.  One launch per call, no runtime copies and no stream wait.  The
+// buffer is this thread's, reused by its next call.
+uint8_t* pinned_stage(uint64_t bytes);
 // Per-(device, stream) completion counter of the reduce pass; `base` = its
 // value before the next launch (the host advances it by the launch's tiles).
 struct ScanCtr {

@@ -16,6 +16,7 @@
 // order (deterministic) and no global atomics sit on the hot path.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <optional>
 
 #include "das_internal.h"
@@ -177,17 +178,23 @@ __global__ void __launch_bounds__(B) k_project(ScanSpec sp, uint64_t begin, uint
 }
 
 // Range lookup in a P_{a,p} key array: [lower_bound(lo), lower_bound(hi)) -> rows.
-__global__ void k_key_ranges(const uint64_t* ukey, const uint64_t* uoff, uint64_t nkeys, const uint64_t* qlo,
-                             const uint64_t* qhi, uint32_t nq, uint64_t* out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * nq) return;
-  const uint64_t q = (i & 1) ? qhi[i >> 1] : qlo[i >> 1];
-  uint64_t lo = 0, hi = nkeys;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (ukey[mid] < q) lo = mid + 1; else hi = mid;
+// Key ranges through pinned staging (das_internal: pinned_stage): requests
+// read over the host mapping, replies stored to the host, slot released.
+__global__ void __launch_bounds__(256) k_key_ranges_pub(const uint64_t* ukey, const uint64_t* uoff, uint64_t nkeys,
+                                                        const uint64_t* qlo, const uint64_t* qhi, uint32_t nq,
+                                                        uint64_t* out, uint32_t* slot, uint32_t seq) {
+  for (uint32_t i = threadIdx.x; i < 2 * nq; i += blockDim.x) {
+    const uint64_t q = (i & 1) ? qhi[i >> 1] : qlo[i >> 1];
+    uint64_t lo = 0, hi = nkeys;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (ukey[mid] < q) lo = mid + 1; else hi = mid;
+    }
+    __hip_atomic_store(&out[i], uoff[lo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  out[i] = uoff[lo];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1087,15 +1094,25 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
       }
       if (!qlo.empty()) {
         const uint32_t nq = (uint32_t)qlo.size();
-        DBuf<uint64_t> dq(2 * nq, c.s), dr(2 * nq, c.s);
-        DAS_HIP(hipMemcpyAsync(dq.p, qlo.data(), 8 * nq, hipMemcpyHostToDevice, c.s));
-        DAS_HIP(hipMemcpyAsync(dq.p + nq, qhi.data(), 8 * nq, hipMemcpyHostToDevice, c.s));
-        hipLaunchKernelGGL(k_key_ranges, dim3((2 * nq + 63) / 64), dim3(64), 0, c.s, (const uint64_t*)P.ukey,
-                           (const uint64_t*)P.uoff, P.nkeys, (const uint64_t*)dq.p, (const uint64_t*)dq.p + nq, nq, dr.p);
-        DAS_HIP(hipGetLastError());
         std::vector<uint64_t> hr(2 * nq);
-        DAS_HIP(hipMemcpyAsync(hr.data(), dr.p, 16 * nq, hipMemcpyDeviceToHost, c.s));
-        DAS_HIP(hipStreamSynchronize(c.s));
+        if (!P.h_ukey.empty() || P.nkeys == 0) {
+          // host mirror of the keys: no device round trip
+          for (uint32_t i = 0; i < 2 * nq; ++i) {
+            const uint64_t q = (i & 1) ? qhi[i >> 1] : qlo[i >> 1];
+            hr[i] = P.h_uoff[std::lower_bound(P.h_ukey.begin(), P.h_ukey.end(), q) - P.h_ukey.begin()];
+          }
+        } else {
+          uint64_t* st = reinterpret_cast<uint64_t*>(pinned_stage(32ull * nq));
+          std::memcpy(st, qlo.data(), 8 * nq);
+          std::memcpy(st + nq, qhi.data(), 8 * nq);
+          const PubSlot ps = pub_reserve();
+          hipLaunchKernelGGL(k_key_ranges_pub, dim3(1), dim3(256), 0, c.s, (const uint64_t*)P.ukey,
+                             (const uint64_t*)P.uoff, P.nkeys, (const uint64_t*)st, (const uint64_t*)st + nq, nq,
+                             st + 2 * nq, ps.p, ps.seq);
+          DAS_HIP(hipGetLastError());
+          pub_wait(ps, c.s, nullptr, 0);
+          std::memcpy(hr.data(), st + 2 * nq, 16 * nq);
+        }
         if (idx.range_cache.size() > (1u << 20)) idx.range_cache.clear();
         uint32_t j = 0;
         for (size_t i = 0; i < rr.size(); ++i)

@@ -62,6 +62,10 @@ class RelationalDB(DBInterface):
     def rel_local_tables(self, rel):
         return rel.tables
 
+    def prefetch_handles(self, handles) -> None:
+        """Resolves handles an expression is about to test, in one batch
+        (no reference counterpart: RedisMongoDB.prefetch caches types only)."""
+
 
 def _group(tables):
     g = {}
@@ -151,6 +155,9 @@ class HipDB(RelationalDB):
                 for (h, _), i, c, a in zip(good, ids.tolist(), cat.tolist(), ar.tolist()):
                     self._handle_cache[h] = (i, c, a)
         return [self._handle_cache[h] for h in handles]
+
+    def prefetch_handles(self, handles) -> None:
+        self._resolve(list(handles))
 
     def ids_of(self, handles: List[str]) -> np.ndarray:
         if not handles:

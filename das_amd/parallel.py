@@ -207,6 +207,10 @@ class ShardedDB(RelationalDB):
     def hex_of(self, ids):
         return self.local.hex_of(ids)
 
+    def prefetch_handles(self, handles):
+        if hasattr(self.local, "prefetch_handles"):
+            self.local.prefetch_handles(handles)
+
     # ------------------------------------------------------- matcher entries
     @staticmethod
     def _schema(var_ids, ordered):

@@ -616,6 +616,30 @@ class Not(LogicalExpression):
         return True
 
 
+def _nodes_of(expr, out):
+    if isinstance(expr, Node):
+        out.append(expr)
+    elif isinstance(expr, Link):
+        for t in expr.targets:
+            _nodes_of(t, out)
+    elif isinstance(expr, Not):
+        _nodes_of(expr.term, out)
+    elif isinstance(expr, (And, Or)):
+        for t in expr.terms:
+            _nodes_of(t, out)
+    return out
+
+
+def _prefetch(expr, db):
+    """One batched handle lookup for every grounded node under an And / Or
+    (instead of one device round trip per node_exists)."""
+    nodes = getattr(expr, '_nodes', None)
+    if nodes is None:
+        nodes = expr._nodes = _nodes_of(expr, [])
+    if nodes:
+        db.prefetch_handles([n.get_handle(db) for n in nodes])
+
+
 class Or(LogicalExpression):
 
     def __init__(self, terms: List[LogicalExpression]):
@@ -628,6 +652,7 @@ class Or(LogicalExpression):
         db = _hip(db)
         if not self.terms:
             return False
+        _prefetch(self, db)
         union = None
         any_matched = False
         negated = [t for t in self.terms if isinstance(t, Not)]
@@ -683,6 +708,7 @@ class And(LogicalExpression):
         if not getattr(self, '_planned', False):
             self._plan_orders()
             self._planned = True
+        _prefetch(self, db)
         acc = None
         forbidden = []
         for term in self.terms:
