@@ -69,6 +69,15 @@ class das_template_scan_t(C.Structure):
     ]
 
 
+class das_plan_node_t(C.Structure):
+    _fields_ = [
+        ("op", C.c_int32), ("nchild", C.c_uint32), ("value", C.c_uint32), ("dedup", C.c_uint32),
+        ("index_join", C.c_uint32), ("scan", das_link_scan_t), ("ij", das_link_scan_t),
+    ]
+
+
+PLAN_LINK, PLAN_CONST, PLAN_NOT, PLAN_AND, PLAN_OR = 1, 2, 3, 4, 5
+
 P = C.c_void_p
 DAS_BUILD_EXPR_ON_DEVICE = 1
 U32P = C.POINTER(C.c_uint32)
@@ -119,6 +128,8 @@ _SIGS = {
     "das_parsed_atoms": (C.c_int, [P, C.POINTER(das_atoms_t), C.POINTER(P)]),
     "das_parsed_type_name": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]),
     "das_parsed_free": (C.c_int, [P]),
+    "das_plan_execute": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32,
+                                   C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
@@ -412,6 +423,31 @@ class Context:
         out = C.c_int64()
         check(lib().das_ctype_lookup(self.h, ptr(d), C.byref(out)), self.h)
         return out.value
+
+    def plan_execute(self, nodes, no_overload=False):
+        """das_plan_execute over a das_plan_node_t array -> (matched, negation, [Table])."""
+        cap = 64
+        out = (P * cap)()
+        n_out, matched, neg = C.c_uint32(), C.c_int32(), C.c_int32()
+        check(lib().das_plan_execute(self.h, nodes, len(nodes), 1 if no_overload else 0, out, cap, C.byref(n_out),
+                                     C.byref(matched), C.byref(neg)), self.h)
+        return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
+
+    @staticmethod
+    def link_scan_struct(q, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False,
+                         order_pos=-1):
+        """Fills a das_link_scan_t (scan_link's argument layout)."""
+        q.order_pos = order_pos
+        q.arity = arity
+        q.type_id = DAS_NONE if type_id is None else type_id
+        for i in range(8):
+            q.target[i] = targets[i] if i < len(targets) else DAS_NONE
+            q.var[i] = var[i] if i < len(var) else -1
+        q.n_vars = n_vars
+        q.ordered = 1 if ordered else 0
+        q.no_overload = 1 if no_overload else 0
+        q.emit_link = 1 if emit_link else 0
+        return q
 
     def scan_link(self, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False,
                   order_pos=-1):

@@ -606,6 +606,18 @@ int das_set_minus(das_ctx_t* ctx, const das_table_t* const* a, uint32_t na, cons
   });
 }
 
+int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                     das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation) {
+  return guarded(ctx, [&] {
+    auto r = das::plan_execute(ctx->c, nodes, n, (int)no_overload);
+    DAS_CHECK(r.tables.size() <= cap, das::DAS_E_INVALID, "plan: more answer tables than `cap`");
+    for (size_t i = 0; i < r.tables.size(); ++i) out[i] = wrap(std::move(r.tables[i]));
+    *n_out = (uint32_t)r.tables.size();
+    *matched = r.matched ? 1 : 0;
+    *negation = r.negation ? 1 : 0;
+  });
+}
+
 int das_prof_enable(das_ctx_t* ctx, int on) {
   return guarded(ctx, [&] {
     das::prof_collect(ctx->c);

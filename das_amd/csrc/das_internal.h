@@ -239,6 +239,13 @@ void export_rows(Ctx& c, const Table& t, uint32_t* dst);
 std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
                                    const uint32_t* src, uint64_t n);
 
+// plan.hip: whole-expression evaluation (das_plan_execute)
+struct PlanOutput {
+  bool matched = false, negation = false;
+  std::vector<std::unique_ptr<Table>> tables;
+};
+PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload);
+
 // export.hip: Redis key-space files (canonical_parser.py:119-183)
 struct ExportCounts {
   uint64_t outgoing = 0, incoming = 0, patterns = 0, templates = 0, names = 0;

@@ -1,0 +1,260 @@
+// Whole-expression evaluation in one C-ABI call (das_plan_execute).
+//
+// The Python matcher (das_amd/pattern_matcher) lowers an And / Or / Not tree
+// of ordered, flat Links into a prefix-order node array: grounded nodes and
+// links are settled on the host (node_exists / link_exists become CONST
+// terms), every Link with a variable is one das_link_scan_t.  This file folds
+// that tree with the same rules as the Python classes -- which restate the
+// reference's -- so a query costs one host call instead of one per operator:
+//   And.matched  pattern_matcher.py:705-748  (failing term -> False; empty
+//                term skipped; Not terms -> forbidden; reset-on-empty; index
+//                join of a Link term against the running result; negation
+//                filter; set semantics)
+//   Or.matched   :644-687  (union of matched terms; Not terms -> And of their
+//                inner terms minus the union, negation flag set)
+//   Not.matched  :627-631
+// Tables of one relation are kept one per schema, rows distinct, empty tables
+// dropped (das_amd.database.hip_db.Relation).
+#include <memory>
+#include <vector>
+
+#include "das_internal.h"
+
+namespace das {
+namespace {
+
+using TablePtr = std::unique_ptr<Table>;
+
+struct Rel {
+  std::vector<TablePtr> t;
+  bool nonempty() const {
+    for (auto& x : t)
+      if (x->nrows) return true;
+    return false;
+  }
+  void push(TablePtr x) {
+    if (x && x->nrows) t.push_back(std::move(x));
+  }
+};
+
+struct Res {
+  bool matched = false;
+  Rel rel;
+  bool neg = false;
+};
+
+bool same_schema(const Table& a, const Table& b) {
+  if (a.kind != b.kind || a.ncols != b.ncols) return false;
+  for (int i = 0; i < a.ncols; ++i)
+    if (a.vars[i] != b.vars[i] || (a.kind == DAS_TABLE_COMPOSITE && a.member[i] != b.member[i])) return false;
+  return true;
+}
+
+struct Exec {
+  Ctx& c;
+  const das_plan_node_t* nd;
+  uint32_t n;
+  int no_overload;
+
+  uint32_t next(uint32_t i) const {
+    DAS_CHECK(i < n, DAS_E_INVALID, "plan: truncated node array");
+    const das_plan_node_t& x = nd[i];
+    if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_CONST) return i + 1;
+    if (x.op == DAS_PLAN_NOT) return next(i + 1);
+    DAS_CHECK(x.op == DAS_PLAN_AND || x.op == DAS_PLAN_OR, DAS_E_INVALID, "plan: bad node op");
+    uint32_t j = i + 1;
+    for (uint32_t k = 0; k < x.nchild; ++k) j = next(j);
+    return j;
+  }
+
+  std::vector<uint32_t> children(uint32_t i) const {
+    std::vector<uint32_t> out;
+    uint32_t j = i + 1;
+    for (uint32_t k = 0; k < nd[i].nchild; ++k) {
+      out.push_back(j);
+      j = next(j);
+    }
+    return out;
+  }
+
+  // rel_normalize: one table per schema (first-seen order), rows distinct
+  Rel normalize(Rel a) {
+    std::vector<std::vector<TablePtr>> groups;
+    for (auto& x : a.t) {
+      bool put = false;
+      for (auto& g : groups)
+        if (same_schema(*g[0], *x)) {
+          g.push_back(std::move(x));
+          put = true;
+          break;
+        }
+      if (!put) {
+        groups.emplace_back();
+        groups.back().push_back(std::move(x));
+      }
+    }
+    Rel out;
+    for (auto& g : groups) {
+      if (g.size() == 1) {
+        out.push(std::move(g[0]));
+        continue;
+      }
+      std::vector<const Table*> ts;
+      for (auto& x : g) ts.push_back(x.get());
+      auto cat = concat(c, ts.data(), (int)ts.size());
+      out.push(dedup(c, *cat));
+    }
+    return out;
+  }
+
+  Rel join_rel(const Rel& a, const Rel& b) {
+    Rel out;
+    for (auto& ta : a.t)
+      for (auto& tb : b.t) out.push(join(c, *ta, *tb, no_overload));
+    return out;
+  }
+
+  Rel antijoin_rel(Rel r, const Rel& f) {
+    for (auto& ft : f.t) {
+      Rel nx;
+      for (auto& t : r.t) nx.push(antijoin(c, *t, *ft));
+      r = std::move(nx);
+    }
+    return r;
+  }
+
+  Rel minus_rel(Rel a, const Rel& b) {
+    Rel out;
+    for (auto& t : a.t) {
+      TablePtr cur = std::move(t);
+      for (auto& f : b.t)
+        if (cur && cur->nrows && same_schema(*cur, *f)) cur = antijoin(c, *cur, *f);
+      out.push(std::move(cur));
+    }
+    return out;
+  }
+
+  Res eval(uint32_t i) {
+    const das_plan_node_t& x = nd[i];
+    Res r;
+    switch (x.op) {
+      case DAS_PLAN_CONST:
+        r.matched = x.value != 0;
+        return r;
+      case DAS_PLAN_LINK: {
+        DAS_CHECK(x.scan.ordered, DAS_E_UNSUPPORTED, "plan: unordered Link terms take the host path");
+        TablePtr t = scan_link(c, x.scan);
+        if (x.dedup && t->nrows) t = dedup(c, *t);
+        r.rel.push(std::move(t));
+        r.matched = r.rel.nonempty();
+        return r;
+      }
+      case DAS_PLAN_NOT:
+        r = eval(i + 1);
+        r.neg = !r.neg;
+        r.matched = true;
+        return r;
+      case DAS_PLAN_AND:
+        return eval_and(children(i));
+      case DAS_PLAN_OR:
+        return eval_or(children(i));
+      default:
+        throw Error(DAS_E_INVALID, "plan: bad node op");
+    }
+  }
+
+  Res eval_and(const std::vector<uint32_t>& terms) {
+    Res out;
+    if (terms.empty()) return out;
+    Rel acc;
+    bool have = false;
+    std::vector<Rel> forbidden;
+    for (uint32_t ti : terms) {
+      const das_plan_node_t& x = nd[ti];
+      if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
+        // the term's rows looked up from the running result's keys; an empty
+        // result takes the scan path, which tells a failing term (And ->
+        // False) from an empty join (reset-on-empty)
+        Rel r;
+        bool ok = true;
+        for (auto& t : acc.t) {
+          auto j = index_join(c, *t, x.ij);
+          if (!j) {
+            ok = false;
+            break;
+          }
+          r.push(std::move(j));
+        }
+        if (ok && r.nonempty()) {
+          acc = std::move(r);
+          continue;
+        }
+      }
+      Res s = eval(ti);
+      if (!s.matched) return Res{};
+      if (!s.rel.nonempty()) continue;
+      if (s.neg) {
+        forbidden.push_back(std::move(s.rel));
+        continue;
+      }
+      if (!have || !acc.nonempty()) {
+        acc = std::move(s.rel);
+        have = true;
+      } else {
+        acc = join_rel(acc, s.rel);
+      }
+    }
+    for (auto& f : forbidden)
+      if (acc.nonempty()) acc = antijoin_rel(std::move(acc), f);
+    out.rel = normalize(std::move(acc));
+    out.matched = out.rel.nonempty();
+    return out;
+  }
+
+  Res eval_or(const std::vector<uint32_t>& terms) {
+    Res out;
+    if (terms.empty()) return out;
+    Rel uni;
+    bool any = false;
+    std::vector<uint32_t> negated;
+    for (uint32_t ti : terms) {
+      if (nd[ti].op == DAS_PLAN_NOT) {
+        negated.push_back(ti + 1);
+        continue;
+      }
+      Res s = eval(ti);
+      if (!s.matched) continue;
+      any = true;
+      if (s.rel.nonempty()) {
+        for (auto& t : s.rel.t) uni.t.push_back(std::move(t));
+        uni = normalize(std::move(uni));
+      }
+    }
+    if (!negated.empty()) {
+      Res sub = eval_and(negated);
+      out.rel = minus_rel(std::move(sub.rel), uni);
+      out.neg = true;
+    } else {
+      out.rel = std::move(uni);
+    }
+    out.matched = any;
+    return out;
+  }
+};
+
+}  // namespace
+
+PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload) {
+  DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
+  DAS_CHECK(n > 0, DAS_E_INVALID, "plan: no nodes");
+  Exec ex{c, nodes, n, no_overload};
+  DAS_CHECK(ex.next(0) == n, DAS_E_INVALID, "plan: node array is not one expression tree");
+  Res r = ex.eval(0);
+  PlanOutput out;
+  out.matched = r.matched;
+  out.negation = r.neg;
+  for (auto& t : r.rel.t) out.tables.push_back(std::move(t));
+  return out;
+}
+
+}  // namespace das

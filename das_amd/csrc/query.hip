@@ -475,17 +475,24 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
 // wave keeps several loads in flight instead of one load -> store round trip
 // per 64 outputs.
 constexpr int kXUnroll = 4;
-template <int NP, int NB, typename T>
+template <int NP, int NB, typename T, int V = 1>
 __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
                                              uint64_t obase, int lane) {
   for (T o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+    // rounds of this iteration that hold outputs (wave-uniform): a group of
+    // 64 rows at fan-out ~2 fills 2 of the 4, and the owner searches of an
+    // empty round would be a third of the kernel's LDS instructions
+    const int nr = V == 0 ? kXUnroll : (re - o0) >= (T)(64 * kXUnroll) ? kXUnroll : (int)((re - o0 + 63) / 64);
     T o[kXUnroll];
     int l[kXUnroll];
     uint32_t br[kXUnroll];
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u) {
       o[u] = o0 + (T)(u * 64 + lane);
+      l[u] = 0;
+      br[u] = 0;
+      if (u >= nr) continue;
       int ll = 0;                                            // owner: max lane with pre <= o
 #pragma unroll
       for (int step = 32; step >= 1; step >>= 1) {
@@ -499,9 +506,10 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, con
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u)
 #pragma unroll
-      for (int i = 0; i < NB; ++i) bv[u][i] = o[u] < re ? bb[i][br[u]] : 0u;
+      for (int i = 0; i < NB; ++i) bv[u][i] = (u < nr && o[u] < re) ? bb[i][br[u]] : 0u;
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u) {
+      if (u >= nr) continue;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const uint32_t v = lane_get(pv[i], l[u]);
@@ -544,7 +552,7 @@ struct JoinCols {
   int np, nb;
 };
 
-template <int NP, int NB, typename T>
+template <int NP, int NB, typename T, int V>
 __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                 uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                 const uint64_t* __restrict__ unit_off, JoinCols jc,
@@ -584,7 +592,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
       const T inc = wave_inclusive_scan(c);
       const T tot = (T)__shfl(inc, 63, 64);
       const T pre = inc - c;                                 // this lane's first output
-      expand_group<NP, NB, T>((T)0, tot, pre, e[g].x, pv[g], bb, po, bo, base, lane);
+      expand_group<NP, NB, T, V>((T)0, tot, pre, e[g].x, pv[g], bb, po, bo, base, lane);
       base += tot;
     }
   }
@@ -662,8 +670,10 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
                      const uint2* lc, uint64_t units, const uint64_t* toff, const JoinCols& jc, uint32_t* out,
                      uint64_t cap, uint64_t total, bool balanced, double bytes) {
   const bool wide = total >= (1ull << 32) - (1ull << 16);
+  static const int fixed = std::getenv("DAS_DJ_FIXED") && std::getenv("DAS_DJ_FIXED")[0] == '1';
   KScope ks((std::string(balanced ? "k_dj_write_bal<" : "k_dj_write<") + std::to_string(NP) + "," +
-             std::to_string(NB) + (wide ? ",u64>" : ",u32>")).c_str(), bytes);
+             std::to_string(NB) + (wide ? ",u64" : ",u32") + (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
+                .c_str(), bytes);
   if (balanced) {
     const unsigned g = grid_for((total + kBalChunk - 1) / kBalChunk, B / 64, 65535u * 4u);
     if (total < (1ull << 32) - (1ull << 16))
@@ -674,12 +684,17 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
                          toff, jc, out, cap, total);
     return;
   }
-  if (total < (1ull << 32) - (1ull << 16))
-    hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+  if (total < (1ull << 32) - (1ull << 16)) {
+    if (fixed)
+      hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 0>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                         units, toff, jc, out, cap);
+    else
+      hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 1>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                         units, toff, jc, out, cap);
+  } else {
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint64_t, 1>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
                        toff, jc, out, cap);
-  else
-    hipLaunchKernelGGL((k_dj_write<NP, NB, uint64_t>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
-                       toff, jc, out, cap);
+  }
 }
 
 // dispatch on (probe cols, build cols); wide schemas use the 4 x 4 kernel in

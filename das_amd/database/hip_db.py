@@ -110,6 +110,7 @@ class HipDB(RelationalDB):
     def load_arrays(self, arrays: "_loader.AtomArrays"):
         """Hash + intern + index every atom on the GPU (replaces the Mongo
         insert / key-value files / Redis SADD of canonical_parser.py:111-240)."""
+        self.generation = getattr(self, "generation", 0) + 1      # invalidates lowered query plans
         self.ctx.build_index(arrays)
         self.arrays = arrays
         self.type_id = dict(arrays.type_id)
@@ -421,6 +422,18 @@ class HipDB(RelationalDB):
         var_ids: variable id per position in the Link's own target order;
         order_var: the variable the caller will join on -- a typed scan then
         returns its rows sorted by it (same answer, join-friendly order)."""
+        spec = self.link_scan_spec(link_type, handles, var_ids, ordered, no_overload, order_var)
+        if spec is None:
+            return Relation()
+        args, dedup = spec
+        t = self.ctx.scan_link(*args)
+        if dedup:
+            t = self.ctx.dedup(t)
+        return Relation([t])
+
+    def link_scan_spec(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
+        """(scan_link arguments, dedup) of match_link; None when the scan
+        matches nothing (unknown type or target, repeated unordered variable)."""
         if link_type in UNORDERED_LINK_TYPES:
             order = sorted(range(len(handles)), key=lambda i: handles[i])
             key_handles = [handles[i] for i in order]
@@ -430,7 +443,7 @@ class HipDB(RelationalDB):
         ttype = self._type_or_empty(link_type)
         tids = self._target_ids(key_handles)
         if ttype is False or tids is None or arity == 0 or arity > 8:
-            return Relation()
+            return None
         names = [v for v in var_ids if v is not None]
         repeated = len(set(names)) != len(names)
         if ordered:
@@ -438,17 +451,16 @@ class HipDB(RelationalDB):
             order_pos = -1
             if order_var is not None and order_var in var and link_type not in UNORDERED_LINK_TYPES:
                 order_pos = var.index(order_var)
-            t = self.ctx.scan_link(arity, ttype, tids, var, 0, True, no_overload, order_pos=order_pos)
+            args = (arity, ttype, tids, var, 0, True, no_overload, False, order_pos)
         else:
             if repeated:
-                return Relation()       # UnorderedAssignment.assign rejects a repeat (:196-197)
-            t = self.ctx.scan_link(arity, ttype, tids, names, len(names), False, no_overload)
+                return None             # UnorderedAssignment.assign rejects a repeat (:196-197)
+            args = (arity, ttype, tids, names, len(names), False, no_overload, False, -1)
         # rows are distinct links of one type unless a '*' type, a repeated
         # variable, an unordered value set or the sorted-key quirk of ordered
         # Similarity/Set queries can make two links bind the same values
-        if ttype is None or repeated or not ordered or link_type in UNORDERED_LINK_TYPES:
-            t = self.ctx.dedup(t)
-        return Relation([t])
+        dedup = ttype is None or repeated or not ordered or link_type in UNORDERED_LINK_TYPES
+        return args, dedup
 
     def match_template(self, link_type, target_types, var_ids, ordered, no_overload=False):
         """LinkTemplate.matched (pattern_matcher.py:603-614) over
@@ -496,12 +508,10 @@ class HipDB(RelationalDB):
                 out.append(self.ctx.join(ta, tb, CONFIG['no_overload']))
         return Relation(out)
 
-    def rel_index_join(self, acc, link_type, handles, var_ids):
-        """And's join of the running relation with one ordered Link term
-        through the pattern index (das_index_join): the rows of
-        rel_join(acc, match_link(...)) without scanning the term.  None when
-        it does not apply to every table of acc (the caller scans + joins)."""
-        if link_type in UNORDERED_LINK_TYPES or not acc.tables:
+    def index_join_spec(self, link_type, handles, var_ids):
+        """(arity, type id, target ids, variables) of das_index_join for one
+        ordered Link term, or None when the index join cannot apply."""
+        if link_type in UNORDERED_LINK_TYPES:
             return None
         ttype = self._type_or_empty(link_type)
         if ttype is None or ttype is False:
@@ -509,12 +519,23 @@ class HipDB(RelationalDB):
         tids = self._target_ids(list(handles))
         if tids is None:
             return None
-        var = [v if v is not None else -1 for v in var_ids]
+        return len(handles), ttype, tids, [v if v is not None else -1 for v in var_ids]
+
+    def rel_index_join(self, acc, link_type, handles, var_ids):
+        """And's join of the running relation with one ordered Link term
+        through the pattern index (das_index_join): the rows of
+        rel_join(acc, match_link(...)) without scanning the term.  None when
+        it does not apply to every table of acc (the caller scans + joins)."""
+        if not acc.tables:
+            return None
+        spec = self.index_join_spec(link_type, handles, var_ids)
+        if spec is None:
+            return None
         out = []
         for t in acc.tables:
             if t.kind != _lib.TABLE_ORDERED:
                 return None
-            r = self.ctx.index_join(t, len(handles), ttype, tids, var)
+            r = self.ctx.index_join(t, *spec)
             if r is None:
                 return None
             out.append(r)

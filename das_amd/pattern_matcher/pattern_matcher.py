@@ -19,6 +19,7 @@ for unordered (Similarity/Set) operands the reference's Unordered /
 CompositeAssignment algebra (:158-368: containment / coverage /
 compatibility checks, XOR set identity), das_amd/csrc/composite.hip.
 """
+import os
 from abc import ABC, abstractmethod
 from collections import Counter
 from copy import deepcopy
@@ -345,6 +346,110 @@ def _hip(db):
 
 
 # ---------------------------------------------------------------------------
+# Whole-expression plans: an And / Or / Not tree of ordered, flat Links is
+# lowered once per (expression, index) to das_plan_node_t records and folded
+# by das_plan_execute in a single native call (das_amd/csrc/plan.hip restates
+# the And / Or / Not rules below).  Anything else -- unordered links,
+# templates, nested link targets, sharded DBs -- takes the per-operator path.
+# ---------------------------------------------------------------------------
+
+
+class _Unsupported(Exception):
+    pass
+
+
+def _lower_link(link, db, out, no_overload):
+    if not link.ordered:
+        raise _Unsupported()
+    for t in link.targets:
+        if not (isinstance(t, Variable) or type(t) is Node):
+            raise _Unsupported()          # LinkTemplate / nested Link targets
+    # Link.matched (pattern_matcher.py:502-538): every target matched, then
+    # link_exists when nothing is a wildcard
+    if not all(t.matched(db, None) for t in link.targets):
+        out.append((_lib.PLAN_CONST, 0, 0, None, None))
+        return
+    handles = [t.get_handle(db) for t in link.targets]
+    if WILDCARD not in handles:
+        out.append((_lib.PLAN_CONST, 0, 1 if db.link_exists(link.atom_type, handles) else 0, None, None))
+        return
+    var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in link.targets]
+    hint = getattr(link, '_order_var', None)
+    spec = db.link_scan_spec(link.atom_type, handles, var_ids, True, no_overload,
+                             _vid(hint) if hint is not None else None)
+    if spec is None:
+        out.append((_lib.PLAN_CONST, 0, 0, None, None))
+        return
+    ij = None if no_overload else db.index_join_spec(link.atom_type, handles, var_ids)
+    out.append((_lib.PLAN_LINK, 0, 0, spec, ij))
+
+
+def _lower_into(expr, db, out, no_overload):
+    if isinstance(expr, (And, Or)):
+        if not expr.terms:
+            out.append((_lib.PLAN_CONST, 0, 0, None, None))
+            return
+        if isinstance(expr, And) and not getattr(expr, '_planned', False):
+            expr._plan_orders()
+            expr._planned = True
+        out.append((_lib.PLAN_AND if isinstance(expr, And) else _lib.PLAN_OR, len(expr.terms), 0, None, None))
+        for t in expr.terms:
+            _lower_into(t, db, out, no_overload)
+    elif isinstance(expr, Not):
+        out.append((_lib.PLAN_NOT, 1, 0, None, None))
+        _lower_into(expr.term, db, out, no_overload)
+    elif isinstance(expr, Link):
+        _lower_link(expr, db, out, no_overload)
+    elif type(expr) is Node:
+        out.append((_lib.PLAN_CONST, 0, 1 if expr.matched(db, None) else 0, None, None))
+    elif type(expr) is Variable:
+        out.append((_lib.PLAN_CONST, 0, 1, None, None))
+    else:
+        raise _Unsupported()
+
+
+def _lower(expr, db, no_overload):
+    recs = []
+    try:
+        _prefetch(expr, db)
+        _lower_into(expr, db, recs, no_overload)
+    except _Unsupported:
+        return None
+    arr = (_lib.das_plan_node_t * len(recs))()
+    for nd, (op, nchild, value, spec, ij) in zip(arr, recs):
+        nd.op, nd.nchild, nd.value = op, nchild, value
+        if spec is not None:
+            args, dedup = spec
+            _lib.Context.link_scan_struct(nd.scan, *args)
+            nd.dedup = 1 if dedup else 0
+        if ij is not None:
+            arity, ttype, tids, var = ij
+            _lib.Context.link_scan_struct(nd.ij, arity, ttype, tids, var, 0, True)
+            nd.index_join = 1
+    return arr
+
+
+def _try_plan(expr, db, answer):
+    """Evaluates `expr` with one das_plan_execute call when it can; returns
+    its matched() result, or None for the per-operator path."""
+    if type(db) is not HipDB or answer.negation or os.environ.get("DAS_PLAN") == "0":
+        return None
+    no_overload = bool(CONFIG['no_overload'])
+    key = (id(db), getattr(db, 'generation', 0), no_overload)
+    cached = getattr(expr, '_plan', None)
+    if cached is None or cached[0] != key:
+        cached = (key, _lower(expr, db, no_overload))
+        expr._plan = cached
+    nodes = cached[1]
+    if nodes is None:
+        return None
+    matched, negation, tables = db.ctx.plan_execute(nodes, no_overload)
+    answer._set(db, Relation(tables))
+    answer.negation = negation
+    return matched
+
+
+# ---------------------------------------------------------------------------
 # Answers
 # ---------------------------------------------------------------------------
 class PatternMatchingAnswer:
@@ -611,6 +716,9 @@ class Not(LogicalExpression):
         return f'NOT({self.term})'
 
     def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool:
+        r = _try_plan(self, db, answer)
+        if r is not None:
+            return r
         self.term.matched(db, answer)
         answer.negation = not answer.negation
         return True
@@ -652,6 +760,9 @@ class Or(LogicalExpression):
         db = _hip(db)
         if not self.terms:
             return False
+        r = _try_plan(self, db, answer)
+        if r is not None:
+            return r
         _prefetch(self, db)
         union = None
         any_matched = False
@@ -708,6 +819,9 @@ class And(LogicalExpression):
         if not getattr(self, '_planned', False):
             self._plan_orders()
             self._planned = True
+        r = _try_plan(self, db, answer)
+        if r is not None:
+            return r
         _prefetch(self, db)
         acc = None
         forbidden = []

@@ -253,6 +253,37 @@ int das_table_from_host(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32
                         const int32_t* member, const uint32_t* cols, uint64_t nrows, das_table_t** out);
 int das_table_free(das_table_t* t);
 
+/* ---- whole-expression plans --------------------------------------------- */
+/* An And / Or / Not tree of ordered Links, evaluated in one call with the
+ * folding rules of the pattern matcher (And.matched pattern_matcher.py:705-748,
+ * Or.matched :644-687, Not.matched :627-631) instead of one host call per
+ * operator.  Nodes are in prefix order: an AND / OR node is followed by its
+ * `nchild` subtrees, a NOT node by one.  Leaves: LINK = Link.matched's
+ * wildcard branch (`scan` as das_scan_link, ordered; `dedup` when the
+ * reference's set would merge rows: a '*' type, a repeated variable, the
+ * sorted key of an ordered Similarity/Set query); CONST = a term the host
+ * settled (node_exists / link_exists): matched = `value`, no assignments.
+ * `index_join` (LINK) allows And to evaluate the term as das_index_join(`ij`)
+ * against its running result, as the host path does.
+ * The answer's tables (one per schema, rows distinct) go to out[0..*n_out);
+ * DAS_ERR_INVALID if more than `cap`. */
+#define DAS_PLAN_LINK 1
+#define DAS_PLAN_CONST 2
+#define DAS_PLAN_NOT 3
+#define DAS_PLAN_AND 4
+#define DAS_PLAN_OR 5
+typedef struct {
+  int32_t op;
+  uint32_t nchild;
+  uint32_t value;
+  uint32_t dedup;
+  uint32_t index_join;
+  das_link_scan_t scan;
+  das_link_scan_t ij;
+} das_plan_node_t;
+int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                     das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation);
+
 /* ---- multi-GPU exchange (RCCL all-to-all of binding rows) ----- */
 /* Rows of `t` regrouped by destination = mix(key columns) % nparts (stable
  * inside a destination); counts[nparts] receives the group sizes.  nkey == 0

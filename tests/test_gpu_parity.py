@@ -174,13 +174,16 @@ def _random_queries(rng, arrays, n):
     return qs
 
 
-@pytest.mark.parametrize("sets", ["hash", "sort"])
+@pytest.mark.parametrize("sets", ["hash", "sort", "host"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw"])
 def test_gpu_synthetic_matches_oracle(gen, sets, monkeypatch):
     """Random Link / And / Or / Not queries; Or's dedup and Not's anti-join
     through the row hash sets and through the sort-based path (which also
-    turns the semi-join off, so one-variable And terms take the direct join)."""
+    turns the semi-join off, so one-variable And terms take the direct join);
+    "host": the per-operator path instead of the native plan."""
     from das_amd import synthetic
+    if sets == "host":
+        monkeypatch.setenv("DAS_PLAN", "0")
     if sets == "sort":
         monkeypatch.setenv("DAS_SET_SORT", "1")
         monkeypatch.setenv("DAS_SEMI_JOIN", "0")
