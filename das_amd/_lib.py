@@ -424,12 +424,14 @@ class Context:
         check(lib().das_ctype_lookup(self.h, ptr(d), C.byref(out)), self.h)
         return out.value
 
-    def plan_execute(self, nodes, no_overload=False):
-        """das_plan_execute over a das_plan_node_t array -> (matched, negation, [Table])."""
+    def plan_execute(self, words, n_nodes, no_overload=False):
+        """das_plan_execute over n_nodes das_plan_node_t records given as a
+        u32 array (51 words each) -> (matched, negation, [Table])."""
         cap = 64
         out = (P * cap)()
         n_out, matched, neg = C.c_uint32(), C.c_int32(), C.c_int32()
-        check(lib().das_plan_execute(self.h, nodes, len(nodes), 1 if no_overload else 0, out, cap, C.byref(n_out),
+        nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
+        check(lib().das_plan_execute(self.h, nodes, n_nodes, 1 if no_overload else 0, out, cap, C.byref(n_out),
                                      C.byref(matched), C.byref(neg)), self.h)
         return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
 

@@ -139,6 +139,49 @@ __global__ void __launch_bounds__(B) k_scan_write(ScanSpec sp, uint64_t begin, u
   }
 }
 
+// Single-workgroup scan of a small range (an anchored key range): count,
+// compaction and column writes in one launch, the row count published
+// straight into the pinned read-back slot (one launch + one round trip where
+// k_scan_count -> scan_total -> k_scan_write take three launches).  The
+// output table is sized by the range (an upper bound of the kept rows).
+constexpr int kSmallBlock = 1024;
+constexpr uint64_t kSmallScan = 16384;
+
+__device__ __forceinline__ void publish_u32(uint32_t* slot, uint32_t seq, uint32_t v) {
+  __hip_atomic_store(&slot[0], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kSmallBlock) k_scan_small(ScanSpec sp, uint64_t begin, uint64_t end, uint32_t* out,
+                                                            uint64_t cap, uint32_t* slot, uint32_t seq) {
+  constexpr int W = kSmallBlock / 64;
+  __shared__ uint32_t s_w[W];
+  __shared__ uint32_t s_run;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t lt = __lanemask_lt();
+  if (threadIdx.x == 0) s_run = 0;
+  __syncthreads();
+  for (uint64_t r0 = begin; r0 < end; r0 += kSmallBlock) {
+    const uint64_t r = r0 + threadIdx.x;
+    const bool keep = r < end && scan_keep(sp, r);
+    const uint64_t m = __ballot(keep);
+    if (__lane_id() == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t pos = s_run + __popcll(m & lt);
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+    if (keep) scan_emit(sp, r, out, cap, pos);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < W; ++w) t += s_w[w];
+      s_run += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) publish_u32(slot, seq, s_run);
+}
+
 // Pure projection (a scan with no predicate): out column c = source column
 // outpos[c] over [begin, end).  Output columns are 16-byte aligned (table
 // column strides are multiples of 64 rows); a source column is too when
@@ -980,6 +1023,20 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
     DAS_HIP(hipGetLastError());
     return t;
   }
+  if (n <= kSmallScan) {
+    auto t = new_table(c, kind, ncols, vars, n);
+    const PubSlot ps = pub_reserve();
+    {
+      ProfScope pf(c, "k_scan_small", 4.0 * n * (sp.arity + 1) + 4.0 * n * sp.nout);
+      hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kSmallBlock), 0, c.s, sp, begin, end, t->data, t->cap, ps.p,
+                         ps.seq);
+      DAS_HIP(hipGetLastError());
+    }
+    uint32_t m = 0;
+    pub_wait(ps, c.s, &m, 1);
+    t->nrows = m;
+    return t;
+  }
   DBuf<uint32_t> cnt(chunks, c.s), off(chunks + 1, c.s);
   {
     ProfScope ps(c, "k_scan_count", 4.0 * n * sp.arity);
@@ -1373,50 +1430,122 @@ struct IjGround {
   int n;
 };
 
-__global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, uint64_t n, uint64_t thi,
-                                             const uint64_t* __restrict__ ukey, const uint64_t* __restrict__ uoff,
-                                             uint64_t nkeys, const uint32_t* __restrict__ dir, uint32_t dlo,
-                                             uint32_t dn, IjGround g, uint2* __restrict__ lc,
-                                             uint32_t* __restrict__ rowid) {
+// (first row, count) in P_{a,p} of the links with t_p = t (and the grounded
+// prefix g): the key through the dense directory (one load) or a binary
+// search, then two binary searches per grounded prefix target.
+struct IjKeys {
+  uint64_t thi;
+  const uint64_t* ukey;
+  const uint64_t* uoff;
+  uint64_t nkeys;
+  const uint32_t* dir;
+  uint32_t dlo, dn;
+};
+
+__device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g) {
+  const uint64_t k = kx.thi | t;
+  uint64_t lo;
+  bool hit;
+  if (kx.dir) {                                  // dense directory: one load
+    const uint32_t d = t - kx.dlo;
+    const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
+    lo = j;
+    hit = j != 0xFFFFFFFFu;
+  } else {                                       // lower_bound
+    uint64_t l = 0, h = kx.nkeys;
+    while (l < h) {
+      const uint64_t mid = (l + h) >> 1;
+      if (kx.ukey[mid] < k) l = mid + 1; else h = mid;
+    }
+    lo = l;
+    hit = lo < kx.nkeys && kx.ukey[lo] == k;
+  }
+  uint2 e = make_uint2(0u, 0u);
+  if (hit) {
+    uint32_t b = (uint32_t)kx.uoff[lo], end = (uint32_t)kx.uoff[lo + 1];
+    // grounded targets that lead the range's secondary order: the rows
+    // equal to each value form a sub-range, found by two binary searches
+    for (int j = 0; j < g.n && b < end; ++j) {
+      const uint32_t* col = g.col[j];
+      const uint32_t v = g.val[j];
+      uint32_t l = b, h = end;
+      while (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
+      uint32_t l2 = l, h2 = end;
+      while (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if (col[m] <= v) l2 = m + 1; else h2 = m; }
+      b = l;
+      end = l2;
+    }
+    if (end > b) e = make_uint2(b, end - b);
+  }
+  return e;
+}
+
+__global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, uint64_t n, IjKeys kx, IjGround g,
+                                             uint2* __restrict__ lc, uint32_t* __restrict__ rowid) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t t = key[i];
-    const uint64_t k = thi | t;
-    uint64_t lo;
-    bool hit;
-    if (dir) {                                   // dense directory: one load
-      const uint32_t d = t - dlo;
-      const uint32_t j = d < dn ? dir[d] : 0xFFFFFFFFu;
-      lo = j;
-      hit = j != 0xFFFFFFFFu;
-    } else {                                     // lower_bound
-      uint64_t l = 0, h = nkeys;
-      while (l < h) {
-        const uint64_t mid = (l + h) >> 1;
-        if (ukey[mid] < k) l = mid + 1; else h = mid;
-      }
-      lo = l;
-      hit = lo < nkeys && ukey[lo] == k;
-    }
-    uint2 e = make_uint2(0u, 0u);
-    if (hit) {
-      uint32_t b = (uint32_t)uoff[lo], end = (uint32_t)uoff[lo + 1];
-      // grounded targets that lead the range's secondary order: the rows
-      // equal to each value form a sub-range, found by two binary searches
-      for (int j = 0; j < g.n && b < end; ++j) {
-        const uint32_t* col = g.col[j];
-        const uint32_t v = g.val[j];
-        uint32_t l = b, h = end;
-        while (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
-        uint32_t l2 = l, h2 = end;
-        while (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if (col[m] <= v) l2 = m + 1; else h2 = m; }
-        b = l;
-        end = l2;
-      }
-      if (end > b) e = make_uint2(b, end - b);
-    }
-    lc[i] = e;
+    lc[i] = ij_lookup(key[i], kx, g);
     rowid[i] = (uint32_t)i;
   }
+}
+
+// Single-workgroup index join of a small probe table: lookups, a block scan
+// of the match counts, and -- when the total fits the output table the host
+// allocated speculatively (`cap` rows) -- the expansion, each thread taking
+// outputs o, o + 1024, ... and finding its probe row by a binary search over
+// the LDS prefix; the total is published to the pinned slot either way (the
+// host redoes a larger join through the multi-launch path).
+constexpr uint32_t kIjSmall = 2048;
+constexpr uint64_t kIjSmallCap = 32768;
+
+__global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __restrict__ key, uint32_t n, IjKeys kx,
+                                                          IjGround g, JoinCols jc, uint32_t* __restrict__ out,
+                                                          uint64_t cap, uint32_t* slot, uint32_t seq) {
+  constexpr int W = kSmallBlock / 64;
+  __shared__ uint32_t s_pre[kIjSmall + 1];
+  __shared__ uint32_t s_lo[kIjSmall];
+  __shared__ uint32_t s_w[W];
+  for (uint32_t r = threadIdx.x; r < n; r += kSmallBlock) {
+    const uint2 e = ij_lookup(key[r], kx, g);
+    s_lo[r] = e.x;
+    s_pre[r] = e.y;
+  }
+  __syncthreads();
+  // exclusive scan of s_pre[0..n): rows in rounds of 1024
+  const int wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += kSmallBlock) {
+    const uint32_t r = r0 + threadIdx.x;
+    const uint32_t v = r < n ? s_pre[r] : 0u;
+    const uint32_t inc = wave_incl_sum_u32(v);
+    if (__lane_id() == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t pre = carry + inc - v, all = 0;
+    for (int w = 0; w < W; ++w) {
+      if (w < wave) pre += s_w[w];
+      all += s_w[w];
+    }
+    __syncthreads();
+    if (r < n) s_pre[r] = pre;
+    carry += all;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) s_pre[n] = carry;
+  __syncthreads();
+  const uint32_t total = carry;
+  if ((uint64_t)total <= cap) {
+    for (uint32_t o = threadIdx.x; o < total; o += kSmallBlock) {
+      uint32_t l = 0, h = n;                       // last row r with s_pre[r] <= o
+      while (h - l > 1) {
+        const uint32_t m = (l + h) >> 1;
+        if (s_pre[m] <= o) l = m; else h = m;
+      }
+      const uint32_t br = s_lo[l] + (o - s_pre[l]);
+      for (int i = 0; i < jc.np; ++i) out[(uint64_t)jc.po[i] * cap + o] = jc.p[i][l];
+      for (int i = 0; i < jc.nb; ++i) out[(uint64_t)jc.bo[i] * cap + o] = jc.b[i][br];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) publish_u32(slot, seq, total);
 }
 
 std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
@@ -1490,20 +1619,41 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
     for (auto& f : fresh)
       if (f.first == uni[k]) { jc.b[jc.nb] = PI.t.col(1 + (int)f.second); jc.bo[jc.nb++] = k; }
   }
-  DBuf<uint2> lc(A.nrows, c.s);
-  DBuf<uint32_t> rowid(A.nrows, c.s);
-  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !std::getenv("DAS_NO_KEY_DIR");
-  const uint32_t* dir = use_dir ? PI.dir[q.type_id] : nullptr;
-  const uint32_t dlo = use_dir ? PI.dir_lo[q.type_id] : 0, dn = use_dir ? PI.dir_n[q.type_id] : 0;
-  {
-    ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
-    hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, (const uint32_t*)A.col(colof(A, q.var[bp])), A.nrows,
-                       (uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-                       (const uint32_t*)dir, dlo, dn, g, lc.p, rowid.p);
-    DAS_HIP(hipGetLastError());
+  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
+  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
+  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
+            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
+            use_dir ? PI.dir_n[q.type_id] : 0u};
+  const uint32_t* akey = A.col(colof(A, q.var[bp]));
+  std::unique_ptr<Table> out;
+  if (A.nrows <= kIjSmall) {
+    // one launch when the output fits a speculative table
+    auto t = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), kIjSmallCap);
+    const PubSlot ps = pub_reserve();
+    {
+      ProfScope pf(c, "k_ij_small", 16.0 * A.nrows + 4.0 * A.nrows * A.ncols);
+      hipLaunchKernelGGL(k_ij_small, dim3(1), dim3(kSmallBlock), 0, c.s, akey, (uint32_t)A.nrows, kx, g, jc, t->data,
+                         t->cap, ps.p, ps.seq);
+      DAS_HIP(hipGetLastError());
+    }
+    uint32_t total = 0;
+    pub_wait(ps, c.s, &total, 1);
+    if (total <= t->cap) {
+      t->nrows = total;
+      out = std::move(t);
+    }
   }
-  // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
-  auto out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, jc, nu, uni.data(), 0.0);
+  if (!out) {
+    DBuf<uint2> lc(A.nrows, c.s);
+    DBuf<uint32_t> rowid(A.nrows, c.s);
+    {
+      ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
+      hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, akey, A.nrows, kx, g, lc.p, rowid.p);
+      DAS_HIP(hipGetLastError());
+    }
+    // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
+    out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, jc, nu, uni.data(), 0.0);
+  }
   out->sorted_col = A.sorted_col >= 0 ? colof(*out, A.vars[A.sorted_col]) : -1;
   const uint32_t ncol = ar + 1;
   const auto& tb = idx.tbound[ar];

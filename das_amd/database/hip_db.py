@@ -100,6 +100,7 @@ class HipDB(RelationalDB):
         self.type_id = {}
         self._hex_cache = {}
         self._handle_cache = {}
+        self._node_handles = {}
         self._mirror = None
         self.pattern_black_list = []
 
@@ -213,7 +214,7 @@ class HipDB(RelationalDB):
     # ------------------------------------------------- DBInterface (reference)
     def node_exists(self, node_type: str, node_name: str) -> bool:
         """redis_mongo_db.py:204-208"""
-        return self._exists(ExpressionHasher.terminal_hash(node_type, node_name), 0)
+        return self._exists(self.get_node_handle(node_type, node_name), 0)
 
     def link_exists(self, link_type: str, target_handles: List[str]) -> bool:
         """redis_mongo_db.py:210-213 (no sorting for unordered types, as the reference)"""
@@ -221,8 +222,14 @@ class HipDB(RelationalDB):
         return self._exists(h, len(target_handles))
 
     def get_node_handle(self, node_type: str, node_name: str) -> str:
-        """redis_mongo_db.py:215-216"""
-        return ExpressionHasher.terminal_hash(node_type, node_name)
+        """redis_mongo_db.py:215-216 (memoised: a query names few nodes, often again)"""
+        key = (node_type, node_name)
+        h = self._node_handles.get(key)
+        if h is None:
+            if len(self._node_handles) > (1 << 20):
+                self._node_handles.clear()
+            h = self._node_handles[key] = ExpressionHasher.terminal_hash(node_type, node_name)
+        return h
 
     def get_link_handle(self, link_type: str, target_handles: List[str]) -> str:
         """redis_mongo_db.py:218-220"""
@@ -408,12 +415,20 @@ class HipDB(RelationalDB):
 
     def _target_ids(self, handles):
         """ids for grounded handles (DAS_NONE for '*'); None if one is unknown."""
-        grounded = [h for h in handles if h != WILDCARD]
-        ids = self.ids_of(grounded) if grounded else np.zeros(0, np.int64)
-        if (ids < 0).any():
-            return None
-        it = iter(ids.tolist())
-        return [_lib.DAS_NONE if h == WILDCARD else next(it) for h in handles]
+        cache = self._handle_cache
+        miss = [h for h in handles if h != WILDCARD and h not in cache]
+        if miss:
+            self._resolve(miss)
+        out = []
+        for h in handles:
+            if h == WILDCARD:
+                out.append(_lib.DAS_NONE)
+                continue
+            i = cache[h][0]
+            if i < 0:
+                return None
+            out.append(i)
+        return out
 
     def match_link(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         """Link.matched's wildcard branch fused with _assign_variables

@@ -408,25 +408,37 @@ def _lower_into(expr, db, out, no_overload):
         raise _Unsupported()
 
 
+_NO_SCAN = [0] * 23
+
+
+def _scan_words(arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False, order_pos=-1):
+    """das_link_scan_t as 23 words (field order of include/das_mi355x.h)."""
+    t = list(targets) + [_lib.DAS_NONE] * (8 - len(targets))
+    v = list(var) + [-1] * (8 - len(var))
+    return [arity, _lib.DAS_NONE if type_id is None else type_id] + t + v + \
+        [n_vars, 1 if ordered else 0, 1 if no_overload else 0, 1 if emit_link else 0, order_pos]
+
+
 def _lower(expr, db, no_overload):
+    """The das_plan_node_t array (51 u32 words per node) of `expr`, or None."""
     recs = []
     try:
         _prefetch(expr, db)
         _lower_into(expr, db, recs, no_overload)
     except _Unsupported:
         return None
-    arr = (_lib.das_plan_node_t * len(recs))()
-    for nd, (op, nchild, value, spec, ij) in zip(arr, recs):
-        nd.op, nd.nchild, nd.value = op, nchild, value
-        if spec is not None:
-            args, dedup = spec
-            _lib.Context.link_scan_struct(nd.scan, *args)
-            nd.dedup = 1 if dedup else 0
-        if ij is not None:
-            arity, ttype, tids, var = ij
-            _lib.Context.link_scan_struct(nd.ij, arity, ttype, tids, var, 0, True)
-            nd.index_join = 1
-    return arr
+    words = []
+    for op, nchild, value, spec, ij in recs:
+        if spec is None:
+            words += [op, nchild, value, 0, 0]
+            words += _NO_SCAN
+            words += _NO_SCAN
+            continue
+        args, dedup = spec
+        words += [op, nchild, value, 1 if dedup else 0, 0 if ij is None else 1]
+        words += _scan_words(*args)
+        words += _NO_SCAN if ij is None else _scan_words(ij[0], ij[1], ij[2], ij[3], 0, True)
+    return np.array(words, dtype=np.int64).astype(np.uint32)
 
 
 def _try_plan(expr, db, answer):
@@ -443,7 +455,7 @@ def _try_plan(expr, db, answer):
     nodes = cached[1]
     if nodes is None:
         return None
-    matched, negation, tables = db.ctx.plan_execute(nodes, no_overload)
+    matched, negation, tables = db.ctx.plan_execute(nodes, len(nodes) // 51, no_overload)
     answer._set(db, Relation(tables))
     answer.negation = negation
     return matched
