@@ -101,6 +101,8 @@ class HipDB(RelationalDB):
         self._hex_cache = {}
         self._handle_cache = {}
         self._node_handles = {}
+        self._plan_records = {}
+        self.generation = 0
         self._mirror = None
         self.pattern_black_list = []
 
@@ -112,6 +114,7 @@ class HipDB(RelationalDB):
         """Hash + intern + index every atom on the GPU (replaces the Mongo
         insert / key-value files / Redis SADD of canonical_parser.py:111-240)."""
         self.generation = getattr(self, "generation", 0) + 1      # invalidates lowered query plans
+        self._plan_records = {}
         self.ctx.build_index(arrays)
         self.arrays = arrays
         self.type_id = dict(arrays.type_id)

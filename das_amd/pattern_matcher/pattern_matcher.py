@@ -358,57 +358,17 @@ class _Unsupported(Exception):
     pass
 
 
-def _lower_link(link, db, out, no_overload):
-    if not link.ordered:
-        raise _Unsupported()
-    for t in link.targets:
-        if not (isinstance(t, Variable) or type(t) is Node):
-            raise _Unsupported()          # LinkTemplate / nested Link targets
-    # Link.matched (pattern_matcher.py:502-538): every target matched, then
-    # link_exists when nothing is a wildcard
-    if not all(t.matched(db, None) for t in link.targets):
-        out.append((_lib.PLAN_CONST, 0, 0, None, None))
-        return
-    handles = [t.get_handle(db) for t in link.targets]
-    if WILDCARD not in handles:
-        out.append((_lib.PLAN_CONST, 0, 1 if db.link_exists(link.atom_type, handles) else 0, None, None))
-        return
-    var_ids = [_vid(t.name) if isinstance(t, Variable) else None for t in link.targets]
-    hint = getattr(link, '_order_var', None)
-    spec = db.link_scan_spec(link.atom_type, handles, var_ids, True, no_overload,
-                             _vid(hint) if hint is not None else None)
-    if spec is None:
-        out.append((_lib.PLAN_CONST, 0, 0, None, None))
-        return
-    ij = None if no_overload else db.index_join_spec(link.atom_type, handles, var_ids)
-    out.append((_lib.PLAN_LINK, 0, 0, spec, ij))
-
-
-def _lower_into(expr, db, out, no_overload):
-    if isinstance(expr, (And, Or)):
-        if not expr.terms:
-            out.append((_lib.PLAN_CONST, 0, 0, None, None))
-            return
-        if isinstance(expr, And) and not getattr(expr, '_planned', False):
-            expr._plan_orders()
-            expr._planned = True
-        out.append((_lib.PLAN_AND if isinstance(expr, And) else _lib.PLAN_OR, len(expr.terms), 0, None, None))
-        for t in expr.terms:
-            _lower_into(t, db, out, no_overload)
-    elif isinstance(expr, Not):
-        out.append((_lib.PLAN_NOT, 1, 0, None, None))
-        _lower_into(expr.term, db, out, no_overload)
-    elif isinstance(expr, Link):
-        _lower_link(expr, db, out, no_overload)
-    elif type(expr) is Node:
-        out.append((_lib.PLAN_CONST, 0, 1 if expr.matched(db, None) else 0, None, None))
-    elif type(expr) is Variable:
-        out.append((_lib.PLAN_CONST, 0, 1, None, None))
-    else:
-        raise _Unsupported()
-
-
-_NO_SCAN = [0] * 23
+def _node_record(op, nchild=0, value=0, spec=None, ij=None):
+    """One das_plan_node_t as 204 bytes (51 u32 words, include/das_mi355x.h)."""
+    words = [op, nchild, value, 0, 0] + [0] * 46
+    if spec is not None:
+        args, dedup = spec
+        words[3] = 1 if dedup else 0
+        words[5:28] = _scan_words(*args)
+    if ij is not None:
+        words[4] = 1
+        words[28:51] = _scan_words(ij[0], ij[1], ij[2], ij[3], 0, True)
+    return np.array(words, dtype=np.int64).astype(np.uint32).tobytes()
 
 
 def _scan_words(arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False, order_pos=-1):
@@ -419,26 +379,112 @@ def _scan_words(arity, type_id, targets, var, n_vars, ordered, no_overload=False
         [n_vars, 1 if ordered else 0, 1 if no_overload else 0, 1 if emit_link else 0, order_pos]
 
 
+_HEADERS = {}
+
+
+def _header(op, nchild=0, value=0):
+    key = (op, nchild, value)
+    r = _HEADERS.get(key)
+    if r is None:
+        r = _HEADERS[key] = _node_record(op, nchild, value)
+    return r
+
+
+def _link_signature(link):
+    """What a Link's plan record depends on besides the index: its type,
+    targets (variable names / node type and name) and join-order hint."""
+    sig = [link.atom_type, getattr(link, '_order_var', None)]
+    for t in link.targets:
+        k = t._k
+        if k == 'v':
+            sig.append(t.name)
+        elif k == 'n':
+            sig.append((t.atom_type, t.name))
+        else:
+            raise _Unsupported()          # LinkTemplate / nested Link / typed targets
+    return tuple(sig)
+
+
+def _link_record(link, db, no_overload):
+    """Link.matched (pattern_matcher.py:502-538) as one plan record: every
+    target matched (node_exists), link_exists when nothing is a wildcard,
+    else the match_link scan (+ the index-join form And may use)."""
+    if not all(t.matched(db, None) for t in link.targets):
+        return _header(_lib.PLAN_CONST, 0, 0)
+    handles = [t.get_handle(db) for t in link.targets]
+    if WILDCARD not in handles:
+        return _header(_lib.PLAN_CONST, 0, 1 if db.link_exists(link.atom_type, handles) else 0)
+    var_ids = [_vid(t.name) if t._k == 'v' else None for t in link.targets]
+    hint = getattr(link, '_order_var', None)
+    spec = db.link_scan_spec(link.atom_type, handles, var_ids, True, no_overload,
+                             _vid(hint) if hint is not None else None)
+    if spec is None:
+        return _header(_lib.PLAN_CONST, 0, 0)
+    ij = None if no_overload else db.index_join_spec(link.atom_type, handles, var_ids)
+    return _node_record(_lib.PLAN_LINK, 0, 0, spec, ij)
+
+
+def _walk(expr, out, links):
+    """Prefix-order skeleton of `expr`: header records and Link slots."""
+    k = expr._k
+    if k == 'a' or k == 'o':
+        if not expr.terms:
+            out.append(_header(_lib.PLAN_CONST, 0, 0))
+            return
+        if k == 'a' and not getattr(expr, '_planned', False):
+            expr._plan_orders()
+            expr._planned = True
+        out.append(_header(_lib.PLAN_AND if k == 'a' else _lib.PLAN_OR, len(expr.terms)))
+        for t in expr.terms:
+            _walk(t, out, links)
+    elif k == 'x':
+        out.append(_header(_lib.PLAN_NOT, 1))
+        _walk(expr.term, out, links)
+    elif k == 'l':
+        if not expr.ordered:
+            raise _Unsupported()
+        links.append((len(out), expr, _link_signature(expr)))
+        out.append(None)
+    elif k == 'n' or k == 'v':
+        links.append((len(out), expr, None))
+        out.append(None)
+    else:
+        raise _Unsupported()
+
+
 def _lower(expr, db, no_overload):
-    """The das_plan_node_t array (51 u32 words per node) of `expr`, or None."""
-    recs = []
+    """The das_plan_node_t array (51 u32 words per node) of `expr`, or None.
+    Link records are cached per (index, signature), so a repeated query
+    shape re-lowers only the links whose anchors changed; their handles are
+    resolved in one batched lookup."""
+    out, links = [], []
     try:
-        _prefetch(expr, db)
-        _lower_into(expr, db, recs, no_overload)
+        _walk(expr, out, links)
     except _Unsupported:
         return None
-    words = []
-    for op, nchild, value, spec, ij in recs:
-        if spec is None:
-            words += [op, nchild, value, 0, 0]
-            words += _NO_SCAN
-            words += _NO_SCAN
-            continue
-        args, dedup = spec
-        words += [op, nchild, value, 1 if dedup else 0, 0 if ij is None else 1]
-        words += _scan_words(*args)
-        words += _NO_SCAN if ij is None else _scan_words(ij[0], ij[1], ij[2], ij[3], 0, True)
-    return np.array(words, dtype=np.int64).astype(np.uint32)
+    cache = db.__dict__.setdefault('_plan_records', {})
+    if len(cache) > (1 << 16):
+        cache.clear()
+    todo = []
+    for pos, e, sig in links:
+        if sig is not None:
+            r = cache.get((no_overload, sig))
+            if r is not None:
+                out[pos] = r
+                continue
+        todo.append((pos, e, sig))
+    if todo:
+        nodes = [t for _, e, _ in todo for t in (e.targets if e._k == 'l' else [e]) if t._k == 'n']
+        if nodes:
+            db.prefetch_handles([n.get_handle(db) for n in nodes])
+        for pos, e, sig in todo:
+            if e._k == 'n':
+                out[pos] = _header(_lib.PLAN_CONST, 0, 1 if e.matched(db, None) else 0)
+            elif e._k == 'v':
+                out[pos] = _header(_lib.PLAN_CONST, 0, 1)
+            else:
+                out[pos] = cache[(no_overload, sig)] = _link_record(e, db, no_overload)
+    return np.frombuffer(b"".join(out), dtype=np.uint32)
 
 
 def _try_plan(expr, db, answer):
@@ -447,7 +493,7 @@ def _try_plan(expr, db, answer):
     if type(db) is not HipDB or answer.negation or os.environ.get("DAS_PLAN") == "0":
         return None
     no_overload = bool(CONFIG['no_overload'])
-    key = (id(db), getattr(db, 'generation', 0), no_overload)
+    key = (id(db), db.generation, no_overload)
     cached = getattr(expr, '_plan', None)
     if cached is None or cached[0] != key:
         cached = (key, _lower(expr, db, no_overload))
@@ -563,6 +609,10 @@ def _unordered(names, hexcols, cols, i):
 # Expressions
 # ---------------------------------------------------------------------------
 class LogicalExpression(ABC):
+    # class tag for the hot lowering / planning walks (isinstance through
+    # ABCMeta costs ~0.5 us per call): 'n' Node, 'l' Link, 'v' Variable,
+    # 'tv' TypedVariable, 't' LinkTemplate, 'a' And, 'o' Or, 'x' Not
+    _k = ''
 
     @abstractmethod
     def matched(self, db: DBInterface, answer: PatternMatchingAnswer) -> bool: ...
@@ -585,6 +635,7 @@ class Atom(LogicalExpression, ABC):
 
 
 class Node(Atom):
+    _k = 'n'
 
     def __init__(self, node_type: str, node_name: str):
         super().__init__(node_type)
@@ -612,6 +663,7 @@ def _variables_last(t1, t2):
 
 
 class Link(Atom):
+    _k = 'l'
 
     def __init__(self, link_type: str, targets: List[Atom], ordered: bool):
         assert not any(isinstance(target, TypedVariable) for target in targets)
@@ -674,6 +726,7 @@ class Link(Atom):
 
 
 class Variable(Atom):
+    _k = 'v'
 
     def __init__(self, variable_name: str):
         super().__init__('ANY')
@@ -690,6 +743,7 @@ class Variable(Atom):
 
 
 class TypedVariable(Variable):
+    _k = 'tv'
 
     def __init__(self, variable_name: str, variable_type: str):
         super().__init__(variable_name)
@@ -700,6 +754,7 @@ class TypedVariable(Variable):
 
 
 class LinkTemplate(LogicalExpression):
+    _k = 't'
 
     def __init__(self, link_type: str, targets: List[TypedVariable], ordered: bool):
         assert all(isinstance(target, TypedVariable) for target in targets)
@@ -720,6 +775,7 @@ class LinkTemplate(LogicalExpression):
 
 
 class Not(LogicalExpression):
+    _k = 'x'
 
     def __init__(self, term: LogicalExpression):
         self.term = term
@@ -737,14 +793,15 @@ class Not(LogicalExpression):
 
 
 def _nodes_of(expr, out):
-    if isinstance(expr, Node):
+    k = expr._k
+    if k == 'n':
         out.append(expr)
-    elif isinstance(expr, Link):
+    elif k == 'l':
         for t in expr.targets:
             _nodes_of(t, out)
-    elif isinstance(expr, Not):
+    elif k == 'x':
         _nodes_of(expr.term, out)
-    elif isinstance(expr, (And, Or)):
+    elif k == 'a' or k == 'o':
         for t in expr.terms:
             _nodes_of(t, out)
     return out
@@ -761,6 +818,7 @@ def _prefetch(expr, db):
 
 
 class Or(LogicalExpression):
+    _k = 'o'
 
     def __init__(self, terms: List[LogicalExpression]):
         self.terms = terms
@@ -801,6 +859,7 @@ class Or(LogicalExpression):
 
 
 class And(LogicalExpression):
+    _k = 'a'
 
     def __init__(self, terms: List[LogicalExpression]):
         self.terms = terms
@@ -816,10 +875,10 @@ class And(LogicalExpression):
         sorted by its first variable that another term also binds (the join
         key), so joins probe sorted keys.  Answers are unchanged."""
         def names(t):
-            return [x.name for x in t.targets if isinstance(x, Variable)] if isinstance(t, Link) else []
+            return [x.name for x in t.targets if x._k == 'v' or x._k == 'tv'] if t._k == 'l' else []
         vs = [set(names(t)) for t in self.terms]
         for i, t in enumerate(self.terms):
-            if not isinstance(t, Link):
+            if t._k != 'l':
                 continue
             others = set().union(*(v for j, v in enumerate(vs) if j != i)) if len(vs) > 1 else set()
             t._order_var = next((n for n in names(t) if n in others), None)
