@@ -218,6 +218,9 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q);
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q);
 std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
 std::unique_ptr<Table> index_join(Ctx& c, const Table& a, const das_link_scan_t& q);   // nullptr: not applicable
+// rows of a whose link (q's grounded targets + a's values of q's variables)
+// does not exist; nullptr when a does not bind every variable position
+std::unique_ptr<Table> anti_index_join(Ctx& c, const Table& a, const das_link_scan_t& q);
 std::unique_ptr<Table> antijoin(Ctx& c, const Table& a, const Table& t);
 std::unique_ptr<Table> dedup(Ctx& c, const Table& a);
 std::unique_ptr<Table> concat(Ctx& c, const Table* const* ts, int n);

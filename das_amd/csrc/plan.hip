@@ -169,8 +169,16 @@ struct Exec {
     Rel acc;
     bool have = false;
     std::vector<Rel> forbidden;
+    std::vector<uint32_t> anti;        // Not(Link) terms applied as anti index joins
     for (uint32_t ti : terms) {
       const das_plan_node_t& x = nd[ti];
+      if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) {
+        // Not.matched is always True and its rows only ever filter the final
+        // result (:720-724, :741-746): instead of scanning the term, each
+        // result row's link is looked up in the index at the end
+        anti.push_back(ti + 1);
+        continue;
+      }
       if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
         // the term's rows looked up from the running result's keys; an empty
         // result takes the scan path, which tells a failing term (And ->
@@ -206,6 +214,17 @@ struct Exec {
     }
     for (auto& f : forbidden)
       if (acc.nonempty()) acc = antijoin_rel(std::move(acc), f);
+    for (uint32_t li : anti) {
+      if (!acc.nonempty()) break;
+      Rel nx;
+      for (auto& t : acc.t) {
+        // a table that does not bind every variable of the term: no row is
+        // covered by a negated row (check_negation, :112-117) -- kept whole
+        auto r = anti_index_join(c, *t, nd[li].ij);
+        nx.push(r ? std::move(r) : std::move(t));
+      }
+      acc = std::move(nx);
+    }
     out.rel = normalize(std::move(acc));
     out.matched = out.rel.nonempty();
     return out;

@@ -890,11 +890,56 @@ struct FlagPred {
   __device__ __forceinline__ bool operator()(uint64_t i) const { return keep[i] != 0; }
 };
 
+// Single-workgroup compaction of a small table (the result of an anchored
+// query's filter): predicate, in-order ranks and column writes in one launch,
+// the kept count published to the pinned slot.
+template <typename Pred>
+__global__ void __launch_bounds__(kSmallBlock) k_compact_small(Pred pred, uint64_t n, ColSet src, uint32_t* out,
+                                                               uint64_t cap, uint32_t* slot, uint32_t seq) {
+  constexpr int W = kSmallBlock / 64;
+  __shared__ uint32_t s_w[W];
+  __shared__ uint32_t s_run;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t lt = __lanemask_lt();
+  if (threadIdx.x == 0) s_run = 0;
+  __syncthreads();
+  for (uint64_t r0 = 0; r0 < n; r0 += kSmallBlock) {
+    const uint64_t r = r0 + threadIdx.x;
+    const bool keep = r < n && pred(r);
+    const uint64_t m = __ballot(keep);
+    if (__lane_id() == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t pos = s_run + __popcll(m & lt);
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+    if (keep)
+      for (int k = 0; k < src.n; ++k) out[(uint64_t)k * cap + pos] = src.c[k][r];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < W; ++w) t += s_w[w];
+      s_run += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) publish_u32(slot, seq, s_run);
+}
+
 template <typename Pred>
 std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const char* prof = nullptr,
                                     double pred_bytes = 4.0) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
+  if (n <= kSmallScan) {
+    auto t = new_table_like(c, a, n);
+    const PubSlot ps = pub_reserve();
+    hipLaunchKernelGGL((k_compact_small<Pred>), dim3(1), dim3(kSmallBlock), 0, c.s, pred, n, cols_of(a), t->data,
+                       t->cap, ps.p, ps.seq);
+    DAS_HIP(hipGetLastError());
+    uint32_t m = 0;
+    pub_wait(ps, c.s, &m, 1);
+    t->nrows = m;
+    return t;
+  }
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
   DAS_CHECK(tiles < (1ull << 31), DAS_E_UNSUPPORTED, "compaction: too many rows");
   DBuf<uint32_t> tcnt(tiles, c.s), toff(tiles + 1, c.s);
@@ -1427,6 +1472,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
 struct IjGround {
   const uint32_t* col[kMaxArity];   // P_{a,p} columns of grounded targets, in the table's secondary order
   uint32_t val[kMaxArity];
+  const uint32_t* src[kMaxArity];   // per-row value column instead of val (anti index join), or nullptr
   int n;
 };
 
@@ -1442,7 +1488,7 @@ struct IjKeys {
   uint32_t dlo, dn;
 };
 
-__device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g) {
+__device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g, uint64_t row = 0) {
   const uint64_t k = kx.thi | t;
   uint64_t lo;
   bool hit;
@@ -1467,7 +1513,7 @@ __device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const I
     // equal to each value form a sub-range, found by two binary searches
     for (int j = 0; j < g.n && b < end; ++j) {
       const uint32_t* col = g.col[j];
-      const uint32_t v = g.val[j];
+      const uint32_t v = g.src[j] ? g.src[j][row] : g.val[j];
       uint32_t l = b, h = end;
       while (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
       uint32_t l2 = l, h2 = end;
@@ -1546,6 +1592,70 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
   }
   __syncthreads();
   if (threadIdx.x == 0) publish_u32(slot, seq, total);
+}
+
+// Anti index join: keep row r of A when the link whose targets are the
+// grounded targets and A's values of the term's variables does NOT exist --
+// And's negation filter (pattern_matcher.py:741-746) for a Not(Link) term
+// whose variables A binds, without scanning the term.  One key lookup plus
+// one binary search per other position (P_{a,p}'s secondary order).
+__global__ void __launch_bounds__(B) k_anti_ij(const uint32_t* __restrict__ key, uint64_t n, IjKeys kx, IjGround g,
+                                               uint32_t* __restrict__ keep) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    keep[i] = ij_lookup(key[i], kx, g, i).y == 0 ? 1u : 0u;
+}
+
+std::unique_ptr<Table> anti_index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+  Index& idx = c.idx;
+  DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
+  const uint32_t ar = q.arity;
+  if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
+      ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
+    return nullptr;
+  auto colof = [](const Table& t, int32_t v) {
+    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+    return -1;
+  };
+  // every position grounded or bound by A (else the filter is not a lookup)
+  int bp = -1;
+  for (uint32_t p = 0; p < ar; ++p) {
+    if (q.target[p] != kNone) continue;
+    if (q.var[p] < 0 || colof(A, q.var[p]) < 0) return nullptr;
+    if (bp < 0) bp = (int)p;
+  }
+  if (bp < 0) return nullptr;
+  if (A.nrows == 0) return new_table_like(c, A, 0);
+  const PosIndex& PI = idx.pidx[ar][bp];
+  if (PI.nkeys == 0) {
+    DBuf<uint32_t> all(A.nrows, c.s);
+    iota(all.p, A.nrows, c.s);
+    return gather_table(c, A, all.p, A.nrows);
+  }
+  IjGround g{};
+  for (uint32_t p = 0; p < ar; ++p) {
+    if ((int)p == bp) continue;
+    g.col[g.n] = PI.t.col(1 + (int)p);
+    if (q.target[p] != kNone) {
+      g.val[g.n] = q.target[p];
+      g.src[g.n] = nullptr;
+    } else {
+      g.src[g.n] = A.col(colof(A, q.var[p]));
+    }
+    ++g.n;
+  }
+  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
+  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
+  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
+            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
+            use_dir ? PI.dir_n[q.type_id] : 0u};
+  DBuf<uint32_t> keep(A.nrows, c.s);
+  {
+    ProfScope ps(c, "k_anti_ij", 4.0 * A.nrows * (ar + 1));
+    hipLaunchKernelGGL(k_anti_ij, G(A.nrows), dim3(B), 0, c.s, (const uint32_t*)A.col(colof(A, q.var[bp])), A.nrows,
+                       kx, g, keep.p);
+    DAS_HIP(hipGetLastError());
+  }
+  return compact_table(c, A, keep.p);
 }
 
 std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {

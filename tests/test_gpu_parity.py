@@ -158,7 +158,16 @@ def _random_queries(rng, arrays, n):
     def link(a, b):
         return ["Link", types[rng.integers(len(types))], True, [a, b]]
     for _ in range(n):
-        k = rng.integers(6)
+        k = rng.integers(9)
+        if k == 6:      # Not term on variables the result binds only partly: no row is covered
+            qs.append(["And", [link(V("A"), node()), link(V("A"), V("B")), ["Not", link(V("B"), V("C"))]]])
+            continue
+        if k == 7:      # Not term on both bound variables, reversed (anti index join, two lookups)
+            qs.append(["And", [link(V("A"), V("B")), ["Not", link(V("B"), V("A"))]]])
+            continue
+        if k == 8:      # Not term on an unbound variable only
+            qs.append(["And", [link(V("A"), V("B")), ["Not", link(V("C"), node())]]])
+            continue
         if k == 0:
             qs.append(link(V("A"), node()))
         elif k == 1:
