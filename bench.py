@@ -591,6 +591,10 @@ def main():
     # ---- knowledge base (per-rank partition for N > 1) ----
     t_build = time.perf_counter()
     log(f"generating {args.workload} KB")
+    # one non-null stream shared by torch (collectives, staging buffers) and
+    # the native context: exchanges are then ordered on the stream, with no
+    # host synchronisation around each collective (parallel.HipLocal)
+    torch.cuda.set_stream(torch.cuda.Stream(device=local_rank))
     db = HipDB(device=local_rank)
     arrays, specs, cfg, scaling = make_kb(args, rank, world, db)
     log(f"building the device index ({arrays.n_expr} expressions)")

@@ -121,6 +121,7 @@ _SIGS = {
     "das_table_from_host": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_table_free": (C.c_int, [P]),
     "das_partition": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P), P]),
+    "das_table_gather": (C.c_int, [P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_table_export_rows": (C.c_int, [P, P, P]),
     "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_parse_canonical": (C.c_int, [P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
@@ -538,6 +539,11 @@ class Context:
         out = P()
         check(lib().das_partition(self.h, t.h, kv, len(key_vars), nparts, C.byref(out), ptr(counts)), self.h)
         return Table(self, out), counts
+
+    def gather(self, t, idx):
+        """Rows idx (host indices) of table t as a new table."""
+        idx = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
+        return self._table(lib().das_table_gather, t.h, ptr(idx), idx.shape[0])
 
     def export_rows(self, t, dptr):
         check(lib().das_table_export_rows(self.h, t.h, dptr), self.h)

@@ -558,6 +558,16 @@ int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars,
   return guarded(ctx, [&] { *out = wrap(das::partition(ctx->c, t->t, key_vars, nkey, nparts, counts)); });
 }
 
+int das_table_gather(das_ctx_t* ctx, const das_table_t* t, const uint32_t* idx, uint64_t n, das_table_t** out) {
+  return guarded(ctx, [&] {
+    for (uint64_t i = 0; i < n; ++i) DAS_CHECK(idx[i] < t->t.nrows, das::DAS_E_INVALID, "gather index out of range");
+    das::DBuf<uint32_t> d(n ? n : 1, ctx->c.s);
+    if (n) DAS_HIP(hipMemcpyAsync(d.p, idx, 4 * n, hipMemcpyHostToDevice, ctx->c.s));
+    *out = wrap(das::gather_table(ctx->c, t->t, d.p, n));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));      // `idx` is caller memory
+  });
+}
+
 int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst) {
   return guarded(ctx, [&] { das::export_rows(ctx->c, t->t, d_dst); });
 }

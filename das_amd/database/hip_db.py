@@ -95,6 +95,7 @@ class HipDB(RelationalDB):
             except ImportError:
                 stream = None
         self.ctx = _lib.Context(device, stream)
+        self.stream = stream
         self.tuple_targets = tuple_targets
         self.arrays = None
         self.type_id = {}

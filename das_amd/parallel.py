@@ -104,9 +104,12 @@ class ShardedDB(RelationalDB):
         self.rank = dist.get_rank(group)
         self.tuple_targets = local.tuple_targets
         self.spec = dict(partition_spec or {})
-        self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0}   # join placements taken
+        self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0, "heavy": 0}   # join placements taken
         # DAS_JOIN_PLACEMENT=exchange|broadcast forces one placement (tests)
         self.force = os.environ.get("DAS_JOIN_PLACEMENT", "")
+        # a key bucket is heavy when its rows (both sides) exceed this fraction
+        # of one rank's fair share of the join's rows (DAS_HEAVY_FRAC, tests)
+        self.heavy_frac = float(os.environ.get("DAS_HEAVY_FRAC", "1.0"))
 
     # ------------------------------------------------------------ collectives
     def _allreduce_sum(self, values):
@@ -345,8 +348,54 @@ class ShardedDB(RelationalDB):
             return _with_part(self.local.join(ta, self._gather_all(tb), no_overload), pa)
         key = tuple(shared)
         self.plan_stats["exchange"] += 1
+        skewed = self._join_skewed(ta, tb, shared, no_overload)
+        if skewed is not None:
+            return skewed
         return _with_part(self.local.join(self._exchange(ta, shared), self._exchange(tb, shared), no_overload),
                           ("hash", key))
+
+    HEAVY_BUCKETS = 4096
+
+    def _join_skewed(self, ta, tb, shared, no_overload):
+        """Heavy-hitter handling of an exchanged join (SURVEY §8e, config 5's
+        hub keys): both sides are bucketed by hash(shared) and the global
+        bucket histogram is all-reduced.  A bucket holding more than
+        heavy_frac x (join rows / world) is heavy: hashing it would send all
+        its rows to one rank.  In a heavy bucket the side with more rows stays
+        where it is (split across ranks) and the other side is all-gathered
+        to every rank; light buckets take the usual all-to-all.  Returns None
+        when no bucket is heavy."""
+        nb = self.HEAVY_BUCKETS
+        pa, ca = self.local.partition(ta, list(shared), nb)
+        pb, cb = self.local.partition(tb, list(shared), nb)
+        g = self._allreduce_sum(np.concatenate([ca.astype(np.int64), cb.astype(np.int64)]))
+        ga, gb = g[:nb], g[nb:]
+        load = ga + gb
+        fair = max(load.sum() / self.world, 1)
+        heavy = (load > self.heavy_frac * fair) & (ga > 0) & (gb > 0)
+        if not heavy.any():
+            return None
+        self.plan_stats["heavy"] += 1
+        a_stays = heavy & (ga >= gb)                      # a split in place, b gathered
+        b_stays = heavy & ~a_stays
+        offa = np.concatenate([[0], np.cumsum(ca.astype(np.int64))])
+        offb = np.concatenate([[0], np.cumsum(cb.astype(np.int64))])
+
+        def rows(off, mask):
+            idx = [np.arange(off[k], off[k + 1]) for k in np.nonzero(mask)[0]]
+            return np.concatenate(idx).astype(np.uint32) if idx else np.zeros(0, np.uint32)
+        light = ~heavy
+        a_light, b_light = self.local.gather_rows(pa, rows(offa, light)), self.local.gather_rows(pb, rows(offb, light))
+        out = [self.local.join(self._exchange(a_light, shared), self._exchange(b_light, shared), no_overload),
+               self.local.join(self.local.gather_rows(pa, rows(offa, a_stays)),
+                               self._gather_all(self.local.gather_rows(pb, rows(offb, a_stays))), no_overload),
+               self.local.join(self._gather_all(self.local.gather_rows(pa, rows(offa, b_stays))),
+                               self.local.gather_rows(pb, rows(offb, b_stays)), no_overload)]
+        out = [t for t in out if t.nrows]
+        if not out:
+            return self.local.join(self.local.gather_rows(pa, np.zeros(0, np.uint32)),
+                                   self.local.gather_rows(pb, np.zeros(0, np.uint32)), no_overload)
+        return _with_part(out[0] if len(out) == 1 else self.local.concat(out), None)
 
     def rel_antijoin(self, rel, forbidden):
         tables = rel.tables
@@ -403,13 +452,20 @@ class HipLocal:
 
     def __init__(self, db, cpu_staging=False):
         """cpu_staging: collective buffers on the host (gloo backend; used to
-        rehearse several ranks on one GPU).  Default: device buffers (RCCL)."""
+        rehearse several ranks on one GPU).  Default: device buffers (RCCL).
+        When the context runs on torch's current stream (HipDB's default),
+        staging copies and collectives are ordered by the stream itself: no
+        host synchronisation around them."""
         import torch
         self.db = db
         self.torch = torch
         self.gpu = torch.device("cuda", torch.cuda.current_device())
         self.dev = torch.device("cpu") if cpu_staging else self.gpu
         self.tuple_targets = db.tuple_targets
+        # (the null stream does not count: the context then runs on a stream
+        # of its own)
+        self.stream_ordered = (not cpu_staging and bool(db.stream) and
+                               db.stream == torch.cuda.current_stream().cuda_stream)
 
     def __getattr__(self, name):     # DBInterface passthrough
         return getattr(self.db, name)
@@ -442,8 +498,10 @@ class HipLocal:
         return self.db.ctx.set_minus(a, b)
 
     def slice(self, t, lo, hi):
-        rows = self.rows_out(t)[lo:hi]
-        return self.rows_in(t.kind, t.vars, rows, hi - lo, t.members)
+        return self.db.ctx.gather(t, np.arange(lo, hi, dtype=np.uint32))
+
+    def gather_rows(self, t, idx):
+        return self.db.ctx.gather(t, idx)
 
     def xfer_tensor(self, arr):
         return self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.dev)
@@ -456,6 +514,12 @@ class HipLocal:
 
     def rows_out(self, t):
         buf = self.torch.empty((t.nrows, max(len(t.vars), 1)), dtype=self.torch.int32, device=self.gpu)
+        if self.stream_ordered:
+            # one stream: the allocation, the export and the collective that
+            # reads the buffer are ordered without the host
+            if t.nrows:
+                self.db.ctx.export_rows(t, buf.data_ptr())
+            return buf
         # torch's allocation must be ready before the ctx stream writes it, and
         # the ctx stream (its own, when torch runs on the null stream) must be
         # done before torch / the collective reads it
@@ -474,6 +538,11 @@ class HipLocal:
 
     def rows_in(self, kind, vars_, buf, n, members=None):
         buf = buf.to(self.gpu).contiguous()
+        if self.stream_ordered:
+            # the import kernel follows the collective on the stream; torch's
+            # caching allocator does not reuse `buf` before work queued on the
+            # stream that uses it has run
+            return self.db.ctx.import_rows(kind, list(vars_), buf.data_ptr() if n else None, n, members)
         self.torch.cuda.current_stream().synchronize()     # copy / collective landed
         t = self.db.ctx.import_rows(kind, list(vars_), buf.data_ptr() if n else None, n, members)
         self.db.ctx.sync()                                  # before `buf` can be freed / reused
@@ -539,6 +608,31 @@ def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
     return arrays, np.arange(rank * n_genes, (rank + 1) * n_genes)
 
 
+def content_owner(arrays, world):
+    """Owning rank of every expression, by content: a repeated expression
+    (same type and targets, stored twice, possibly over distinct copies of a
+    nested child) maps to one canonical id first -- children before parents
+    -- so all copies of one handle land on one rank."""
+    nl, ne = arrays.n_leaf, arrays.n_expr
+    off = arrays.expr_off.astype(np.int64)
+    child = arrays.expr_child.astype(np.int64)
+    canon = np.arange(nl + ne, dtype=np.int64)
+    own = np.zeros(ne, dtype=np.int64)
+    nested = np.zeros(ne, dtype=bool)
+    nested[child[child >= nl] - nl] = True
+    for g in range(len(arrays.level_off) - 1):
+        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
+        if e <= b:
+            continue
+        k = int(off[b + 1] - off[b])
+        ch = canon[child[off[b]:off[e]].reshape(e - b, k)]
+        if nested[b:e].any():          # only a contained expression's id reaches a parent's hash
+            _, first, inv = np.unique(ch, axis=0, return_index=True, return_inverse=True)
+            canon[nl + b:nl + e] = nl + b + first[inv.ravel()]
+        own[b:e] = owner_of(ch, world)
+    return own
+
+
 def shard_arrays(arrays, rank, world):
     """Generic link sharding for a fixed KB (strong scaling): every rank keeps
     the whole atom directory; a link's pattern-index rows stay on the rank its
@@ -547,45 +641,32 @@ def shard_arrays(arrays, rank, world):
     if world == 1:
         return arrays
     kinds = arrays.expr_kind.copy()
-    off = arrays.expr_off
-    for g in range(len(arrays.level_off) - 1):
-        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
-        if e <= b:
-            continue
-        k = int(off[b + 1] - off[b])
-        ch = arrays.expr_child[int(off[b]):int(off[e])].reshape(e - b, k).astype(np.int64)
-        own = owner_of(ch, world)
-        seg = kinds[b:e]
-        seg[(seg == 1) & (own != rank)] = 3
-        kinds[b:e] = seg
+    kinds[(kinds == 1) & (content_owner(arrays, world) != rank)] = 3
     arrays.expr_kind = kinds
     return arrays
 
 
 def partition_arrays(arrays, rank, world):
-    """Independent shards for the bulk build (config 4 at N GPUs): rank r keeps
-    only the links its content hash selects, plus the nested expressions they
-    contain and every leaf; it hashes and indexes nothing else.  Atom ids are
-    then local to the shard (the reference's sharded Redis keys, not the
-    replicated directory ShardedDB queries need)."""
+    """Independent shards for the bulk build (config 4 at N GPUs): rank r
+    indexes only the links its content hash selects (nested or not), keeps the
+    expressions those links contain so their handles hash, and every leaf.  A
+    contained link owned by another rank stays directory-only (kind 3): each
+    link is indexed on exactly one rank.  Atom ids are then local to the shard
+    (the reference's sharded Redis keys, not the replicated directory
+    ShardedDB queries need)."""
     from .loader import AtomArrays
     if world == 1:
         return arrays
     nl, ne = arrays.n_leaf, arrays.n_expr
     off = arrays.expr_off.astype(np.int64)
     child = arrays.expr_child.astype(np.int64)
-    nested = np.zeros(ne, dtype=bool)
-    nested[child[child >= nl] - nl] = True
     keep = np.zeros(ne, dtype=bool)
     groups = [(int(arrays.level_off[g]), int(arrays.level_off[g + 1])) for g in range(len(arrays.level_off) - 1)]
+    own = content_owner(arrays, world) == rank
     for b, e in groups:
         if e <= b:
             continue
-        k = int(off[b + 1] - off[b])
-        ch = child[off[b]:off[e]].reshape(e - b, k)
-        top = ~nested[b:e]
-        own = owner_of(ch, world) == rank
-        keep[b:e] = (top & own) | (arrays.expr_kind[b:e] == 2)
+        keep[b:e] = own[b:e] & (arrays.expr_kind[b:e] == 1)
     for b, e in reversed(groups):          # parents before children: close over nesting
         if e <= b:
             continue
@@ -593,6 +674,8 @@ def partition_arrays(arrays, rank, world):
         ch = child[off[b]:off[e]].reshape(e - b, k)[keep[b:e]]
         sub = ch[ch >= nl] - nl
         keep[sub] = True
+    kinds = arrays.expr_kind.copy()
+    kinds[(kinds == 1) & ~own] = 3
     newpos = np.cumsum(keep) - 1
     nch = np.diff(off)[keep]
     expr_off = np.zeros(int(keep.sum()) + 1, dtype=np.uint64)
@@ -609,5 +692,5 @@ def partition_arrays(arrays, rank, world):
     for b, e in groups:
         level_off.append(level_off[-1] + int(keep[b:e].sum()))
     return AtomArrays(arrays.leaf_bytes, arrays.leaf_off, arrays.leaf_kind, arrays.leaf_ctype, arrays.leaf_type_id,
-                      arrays.name_start, expr_off, ch.astype(np.uint32), arrays.expr_kind[keep],
+                      arrays.name_start, expr_off, ch.astype(np.uint32), kinds[keep],
                       arrays.expr_ctype_leaf[keep], np.array(level_off, dtype=np.uint64), arrays.type_names)

@@ -290,6 +290,9 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
  * keys on every column (global dedup / set difference). */
 int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars, uint32_t nkey,
                   uint32_t nparts, das_table_t** out, uint64_t* counts);
+/* Rows idx[0..n) of `t` (host indices) as a new table, same schema: the
+ * heavy / light split of a skewed join's buckets. */
+int das_table_gather(das_ctx_t* ctx, const das_table_t* t, const uint32_t* idx, uint64_t n, das_table_t** out);
 /* Row-major (n x ncols u32) device copies for the collective buffers. */
 int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst);
 int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,

@@ -243,28 +243,24 @@ def test_gpu_facade_readme_examples():
         [h for h, _ in das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"])])
 
 
-def _sharded_worker(rank, world, port, out_path):
+def _sharded_worker(rank, world, port, out_path, mode):
     import os as _os
     import torch
     import torch.distributed as dist
+    if mode == "heavy":          # exchanged joins with skewed buckets split
+        _os.environ["DAS_JOIN_PLACEMENT"] = "exchange"
+        _os.environ["DAS_HEAVY_FRAC"] = "0.05"
     _os.environ["MASTER_ADDR"] = "127.0.0.1"
     _os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
-    from das_amd.parallel import HipLocal, ShardedDB, owner_of
+    from das_amd.parallel import HipLocal, ShardedDB, shard_arrays
     from das_amd.pattern_matcher import pattern_matcher as pm
     from tests.test_parallel_gloo import _queries
-    arrays = synthetic.bio_kb(60, 25, 600, 80, seed=3)
-    # mark links not owned by this rank as remote (kind 3): same directory, split index
-    n_leaf = arrays.n_leaf
-    kinds = arrays.expr_kind.copy()
-    for j in range(arrays.n_expr):
-        ch = np.array(arrays.children(j)[1:], dtype=np.int64)[None, :]
-        if owner_of(ch, world)[0] != rank:
-            kinds[j] = 3
-    arrays.expr_kind = kinds
+    # links not owned by this rank are remote (kind 3): same directory, split index
+    arrays = shard_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3), rank, world)
     db = HipDB(device=0)
     db.load_arrays(arrays)
     sdb = ShardedDB(HipLocal(db, cpu_staging=True), dist)
@@ -275,12 +271,14 @@ def _sharded_worker(rank, world, port, out_path):
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
         res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
                     "local": sdb.rel_local_count(ans._relation())})
+    res.append(sdb.plan_stats)
     with open(f"{out_path}.{rank}", "w") as f:
         json.dump(res, f)
     dist.destroy_process_group()
 
 
-def test_gpu_sharded_two_ranks_one_gpu():
+@pytest.mark.parametrize("mode", ["default", "heavy"])
+def test_gpu_sharded_two_ranks_one_gpu(mode):
     """The multi-GPU path (partition / export / import kernels + exchange) with
     two ranks sharing cuda:0 over gloo, against the single-process oracle."""
     import socket
@@ -295,8 +293,10 @@ def test_gpu_sharded_two_ranks_one_gpu():
     odb = O.RedisMongoSemantics(O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)))
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.spawn(_sharded_worker, args=(2, port, out), nprocs=2, join=True)
+        mp.spawn(_sharded_worker, args=(2, port, out, mode), nprocs=2, join=True)
         per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    if mode == "heavy":
+        assert per_rank[0][-1]["heavy"] > 0, per_rank[0][-1]
     for qi, q in enumerate(_queries()):
         want = O.evaluate(q, odb)
         want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])

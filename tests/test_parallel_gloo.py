@@ -110,10 +110,11 @@ class NumpyLocal:
 
     tuple_targets = False
 
-    def __init__(self, kb_full, rank, world, by_target=None):
+    def __init__(self, kb_full, rank, world, by_target=None, local_kb=None):
         """by_target {link type: position}: those links live on the rank that
         owns the atom at that position (hash of its handle), the rest by the
-        link's own handle -- the layout ShardedDB's partition_spec describes."""
+        link's own handle -- the layout ShardedDB's partition_spec describes.
+        local_kb: this rank's links given directly (parallel.shard_arrays)."""
         handles = set(kb_full.nodes) | set(kb_full.links)
         for _, (_, tg, _) in kb_full.links.items():
             handles.update(tg)
@@ -126,7 +127,8 @@ class NumpyLocal:
         def owner(h, v):
             key = v[1][by_target[v[0]]] if v[0] in by_target else h
             return int(key[:8], 16) % world
-        local.links = {h: v for h, v in kb_full.links.items() if owner(h, v) == rank}
+        local.links = {h: v for h, v in kb_full.links.items() if owner(h, v) == rank} if local_kb is None \
+            else dict(local_kb.links)
         self.odb = O.RedisMongoSemantics(local)
         self.full = O.RedisMongoSemantics(kb_full)
 
@@ -242,6 +244,9 @@ class NumpyLocal:
     def slice(self, t, lo, hi):
         return NTable(t.kind, t.vars, t.rows[lo:hi], t.members)
 
+    def gather_rows(self, t, idx):
+        return NTable(t.kind, t.vars, t.rows[np.asarray(idx, dtype=np.int64)], t.members)
+
     def join(self, a, b, no_overload=False):
         if a.kind != ORDERED or b.kind != ORDERED:
             vars_, members = _join_schema(a, b)
@@ -347,16 +352,48 @@ def _composite_queries():
     ]
 
 
+def _fly_queries():
+    import bench
+    from das_amd import synthetic
+    from tests.golden import make_synthetic as MS
+    arrays = MS.make_arrays("flybase")
+    return [q for g in (0, 42) for _, q in bench.flybase_specs(g, synthetic.flybase_do_terms(arrays, g))]
+
+
+def _hub_queries():
+    import bench
+    V = lambda n: ["Var", n]  # noqa: E731
+    n = lambda i: ["Node", "Concept", f"n{i}"]  # noqa: E731
+    L = lambda t, a, b: ["Link", t, True, [a, b]]  # noqa: E731
+    return [q for _, q in bench.hub_specs()] + [
+        ["And", [L("T0", V("V1"), n(0)), L("T0", V("V1"), V("V2")), L("T0", V("V2"), n(1))]],
+        ["And", [L("T1", V("V1"), V("V2")), L("T1", V("V2"), n(0)), ["Not", L("T2", V("V1"), n(1))]]]]
+
+
+# kind -> (DAS_JOIN_PLACEMENT, DAS_HEAVY_FRAC)
+_ENV = {"bio_exchange": ("exchange", ""), "bio_broadcast": ("broadcast", ""), "bio_heavy": ("exchange", "0.05"),
+        "hub": ("exchange", "0.05"), "flybase": ("exchange", "0.2")}
+
+
 def _kb(kind):
     from das_amd import synthetic
-    if kind in ("bio", "bio_part", "bio_exchange", "bio_broadcast"):
+    if kind in ("bio", "bio_part", "bio_exchange", "bio_broadcast", "bio_heavy"):
         return O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)), _queries()
+    if kind == "flybase":
+        from tests.golden import make_synthetic as MS
+        return O.KB.from_arrays(MS.make_arrays("flybase")), _fly_queries()
+    if kind == "hub":
+        from tests.golden import make_synthetic as MS
+        return O.KB.from_arrays(MS.make_arrays("hub")), _hub_queries()
     return O.KB.from_arrays(synthetic.similarity_kb(n_nodes=20, n_inh=90, n_sim=45, n_set=20, seed=9)), \
         _composite_queries()
 
 
 def _worker(rank, world, port, out_path, kind):
-    os.environ["DAS_JOIN_PLACEMENT"] = {"bio_exchange": "exchange", "bio_broadcast": "broadcast"}.get(kind, "")
+    place, heavy = _ENV.get(kind, ("", ""))
+    os.environ["DAS_JOIN_PLACEMENT"] = place
+    if heavy:
+        os.environ["DAS_HEAVY_FRAC"] = heavy
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -365,7 +402,13 @@ def _worker(rank, world, port, out_path, kind):
     from das_amd.pattern_matcher import pattern_matcher as pm
     kb, queries = _kb(kind)
     spec = {"Member": 0} if kind == "bio_part" else None
-    sdb = ShardedDB(NumpyLocal(kb, rank, world, by_target=spec), dist, partition_spec=spec)
+    local_kb = None
+    if kind == "flybase":
+        # the bench's strong-scaling layout: links sharded by content hash
+        from das_amd.parallel import shard_arrays
+        from tests.golden import make_synthetic as MS
+        local_kb = O.KB.from_arrays(shard_arrays(MS.make_arrays("flybase"), rank, world))
+    sdb = ShardedDB(NumpyLocal(kb, rank, world, by_target=spec, local_kb=local_kb), dist, partition_spec=spec)
     res = []
     for q in queries:
         ans = pm.PatternMatchingAnswer()
@@ -392,7 +435,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world", [2])
-@pytest.mark.parametrize("kind", ["bio", "bio_part", "bio_exchange", "bio_broadcast", "composite"])
+@pytest.mark.parametrize("kind", ["bio", "bio_part", "bio_exchange", "bio_broadcast", "bio_heavy", "hub",
+                                  "flybase", "composite"])
 def test_sharded_matcher_equals_single_process_oracle(world, kind):
     kb, queries = _kb(kind)
     odb = O.RedisMongoSemantics(kb)
@@ -405,6 +449,8 @@ def test_sharded_matcher_equals_single_process_oracle(world, kind):
         assert stats["colocated"] > 0 and stats["broadcast"] > 0, stats    # both placements exercised
     if kind in ("bio_exchange", "bio_broadcast"):
         assert stats[kind[4:]] > 0 and stats["colocated"] == 0, stats
+    if _ENV.get(kind, ("", ""))[1]:
+        assert stats["heavy"] > 0, stats                                  # skewed buckets split
     for qi, q in enumerate(queries):
         want = O.evaluate(q, odb)
         if "error" in want:
@@ -419,3 +465,28 @@ def test_sharded_matcher_equals_single_process_oracle(world, kind):
             assert got["rows"] == want_rows, q
             locals_ += got["local"]
         assert locals_ == want["n"], (q, locals_, want["n"])      # partitions are disjoint
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["bio_full", "hub"])
+def test_partition_arrays_build_union_equals_single_build(world, name):
+    """Config 4 at N GPUs: each rank indexes only its partition_arrays shard.
+    The shards' key-value families (outgoing / incoming sets, pattern and
+    template keys, names -- canonical_parser.py:119-183) must union to the
+    single build's, and every link (nested ones too) is indexed on exactly
+    one rank."""
+    from das_amd.parallel import partition_arrays
+    from tests.golden import make_synthetic as MS
+    full_kb = O.KB.from_arrays(MS.make_arrays(name))
+    full = O.keyspace_lines(full_kb)
+    union = {k: set() for k in full}
+    owners = {}
+    for r in range(world):
+        kb = O.KB.from_arrays(partition_arrays(MS.make_arrays(name), r, world))
+        for k, lines in O.keyspace_lines(kb).items():
+            union[k] |= set(lines)
+        for h in kb.links:
+            owners[h] = owners.get(h, 0) + 1
+    for k in full:
+        assert union[k] == set(full[k]), k
+    assert owners == {h: 1 for h in full_kb.links}
