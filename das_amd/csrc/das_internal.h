@@ -54,6 +54,7 @@ struct PosIndex {
   std::vector<uint64_t> h_ukey, h_uoff;
 };
 constexpr uint64_t kHostKeyMirror = 1ull << 24;   // keys per P_{a,p} mirrored on the host (256 MB at most)
+constexpr uint64_t kHostNodeMirror = 1ull << 24;  // nodes mirrored on the host (384 MB at most)
 
 struct CtypeRange {
   uint32_t arity;
@@ -91,6 +92,11 @@ struct Index {
   std::vector<Digest> type_digest;                             // host: md5(type name) per named type
   std::vector<uint32_t> type_name_len;                         // host: bytes of each type name
   std::vector<CtypeRange> ctype_range;                         // host
+  // host mirror of the nodes in handle order (n_nodes <= kHostNodeMirror):
+  // digest, id and named type -- an anchored query resolves its grounded
+  // nodes without a device round trip
+  std::vector<Digest> h_node_dig;
+  std::vector<uint32_t> h_node_id, h_node_type;
   std::vector<void*> owned;                                    // device allocations
   std::map<std::array<uint64_t, 4>, std::pair<uint64_t, uint64_t>> range_cache;   // P lookups
   uint64_t device_bytes = 0;

@@ -370,6 +370,23 @@ __global__ void k_temp_type(uint64_t n_atoms, const uint32_t* rep, const uint32_
   }
 }
 
+// host node mirror: nodes in by_digest (handle) order
+__global__ void k_node_flags(uint64_t n, const uint32_t* by_digest, const uint8_t* cat, uint32_t* flag) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    flag[i] = cat[by_digest[i]] == CAT_NODE ? 1u : 0u;
+}
+__global__ void k_node_pack(uint64_t n, const uint32_t* by_digest, const uint8_t* cat, const uint32_t* pos,
+                            const Digest* dig, const uint32_t* type, Digest* o_dig, uint32_t* o_id, uint32_t* o_type) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = by_digest[i];
+    if (cat[id] != CAT_NODE) continue;
+    const uint32_t o = pos[i];
+    o_dig[o] = dig[id];
+    o_id[o] = id;
+    o_type[o] = type[id];
+  }
+}
+
 // final id f <- temp perm[f]; by_digest[temp] = f
 __global__ void k_apply_perm(uint64_t n, const uint32_t* perm, const uint32_t* rep, const uint32_t* catmax,
                              uint32_t* rep2, uint32_t* cat2, uint32_t* by_digest) {
@@ -1218,6 +1235,36 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     }
     DAS_HIP(hipGetLastError());
   }
+  idx.h_node_dig.clear();
+  idx.h_node_id.clear();
+  idx.h_node_type.clear();
+  if (idx.n_nodes && idx.n_nodes <= kHostNodeMirror && idx.n_atoms < 0xFFFFFFFFull) {
+    const uint64_t n = idx.n_atoms;
+    DBuf<uint32_t> flag(n, s), pos(n + 1, s);
+    {
+      KScope ks("k_node_flags", 9.0 * n);
+      hipLaunchKernelGGL(k_node_flags, G(n), dim3(B), 0, s, n, (const uint32_t*)idx.by_digest,
+                         (const uint8_t*)idx.cat, flag.p);
+    }
+    const uint64_t nn = scan_total<uint32_t>(SpanIn<uint32_t>{flag.p}, n, pos.p, s);
+    if (nn) {
+      DBuf<Digest> od(nn, s);
+      DBuf<uint32_t> oi(nn, s), ot(nn, s);
+      {
+        KScope ks("k_node_pack", 9.0 * n + 24.0 * nn);
+        hipLaunchKernelGGL(k_node_pack, G(n), dim3(B), 0, s, n, (const uint32_t*)idx.by_digest,
+                           (const uint8_t*)idx.cat, (const uint32_t*)pos.p, (const Digest*)idx.digest,
+                           (const uint32_t*)idx.type, od.p, oi.p, ot.p);
+      }
+      idx.h_node_dig.resize(nn);
+      idx.h_node_id.resize(nn);
+      idx.h_node_type.resize(nn);
+      DAS_HIP(hipMemcpyAsync(idx.h_node_dig.data(), od.p, sizeof(Digest) * nn, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipMemcpyAsync(idx.h_node_id.data(), oi.p, 4 * nn, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipMemcpyAsync(idx.h_node_type.data(), ot.p, 4 * nn, hipMemcpyDeviceToHost, s));
+      DAS_HIP(hipStreamSynchronize(s));
+    }
+  }
   DAS_HIP(hipStreamSynchronize(s));
   idx.built = true;
 }
@@ -1263,6 +1310,23 @@ bool lookup_small(Ctx& c, const Digest* h, uint64_t n, int64_t* out, uint8_t* ca
   DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
   if (n > 4096) return false;
   if (!n) return true;
+  {
+    // every digest a node of the host mirror: answered on the host
+    const auto& nd = c.idx.h_node_dig;
+    auto less = [](const Digest& a, const Digest& b) {
+      return a.hi() < b.hi() || (a.hi() == b.hi() && a.lo() < b.lo());
+    };
+    uint64_t i = 0;
+    for (; i < n && !nd.empty(); ++i) {
+      const size_t j = std::lower_bound(nd.begin(), nd.end(), h[i], less) - nd.begin();
+      if (j == nd.size() || nd[j].hi() != h[i].hi() || nd[j].lo() != h[i].lo()) break;
+      out[i] = c.idx.h_node_id[j];
+      if (cat) cat[i] = CAT_NODE;
+      if (arity) arity[i] = 0;
+      if (type) type[i] = c.idx.h_node_type[j];
+    }
+    if (i == n) return true;
+  }
   uint8_t* st = pinned_stage(n * (sizeof(Digest) + 16));
   Digest* q = reinterpret_cast<Digest*>(st);
   int64_t* r = reinterpret_cast<int64_t*>(st + n * sizeof(Digest));

@@ -1478,7 +1478,11 @@ struct IjGround {
 
 // (first row, count) in P_{a,p} of the links with t_p = t (and the grounded
 // prefix g): the key through the dense directory (one load) or a binary
-// search, then two binary searches per grounded prefix target.
+// search, then an equal-range search per grounded prefix target.  Ranged
+// mode (fixed): the rows of one grounded key (type, t_q = v) of P_{a,q},
+// known on the host, narrowed by the targets in P_{a,q}'s secondary order --
+// the probe's own value among them (g.src) -- a search over one small,
+// cache-resident range instead of random key ranges of the whole table.
 struct IjKeys {
   uint64_t thi;
   const uint64_t* ukey;
@@ -1486,13 +1490,18 @@ struct IjKeys {
   uint64_t nkeys;
   const uint32_t* dir;
   uint32_t dlo, dn;
+  uint32_t flo, fhi;    // ranged mode: rows [flo, fhi)
+  int fixed;
 };
 
 __device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g, uint64_t row = 0) {
   const uint64_t k = kx.thi | t;
   uint64_t lo;
   bool hit;
-  if (kx.dir) {                                  // dense directory: one load
+  if (kx.fixed) {
+    lo = 0;
+    hit = kx.fhi > kx.flo;
+  } else if (kx.dir) {                           // dense directory: one load
     const uint32_t d = t - kx.dlo;
     const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
     lo = j;
@@ -1508,16 +1517,18 @@ __device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const I
   }
   uint2 e = make_uint2(0u, 0u);
   if (hit) {
-    uint32_t b = (uint32_t)kx.uoff[lo], end = (uint32_t)kx.uoff[lo + 1];
-    // grounded targets that lead the range's secondary order: the rows
-    // equal to each value form a sub-range, found by two binary searches
+    uint32_t b = kx.fixed ? kx.flo : (uint32_t)kx.uoff[lo], end = kx.fixed ? kx.fhi : (uint32_t)kx.uoff[lo + 1];
+    // targets that lead the range's secondary order: the rows equal to each
+    // value form a sub-range; its two bounds are searched in lockstep (two
+    // independent load chains per step)
     for (int j = 0; j < g.n && b < end; ++j) {
       const uint32_t* col = g.col[j];
       const uint32_t v = g.src[j] ? g.src[j][row] : g.val[j];
-      uint32_t l = b, h = end;
-      while (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
-      uint32_t l2 = l, h2 = end;
-      while (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if (col[m] <= v) l2 = m + 1; else h2 = m; }
+      uint32_t l = b, h = end, l2 = b, h2 = end;
+      while (l < h || l2 < h2) {
+        if (l < h) { const uint32_t m = (l + h) >> 1; if (col[m] < v) l = m + 1; else h = m; }
+        if (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if (col[m] <= v) l2 = m + 1; else h2 = m; }
+      }
       b = l;
       end = l2;
     }
@@ -1529,7 +1540,7 @@ __device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const I
 __global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, uint64_t n, IjKeys kx, IjGround g,
                                              uint2* __restrict__ lc, uint32_t* __restrict__ rowid) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    lc[i] = ij_lookup(key[i], kx, g);
+    lc[i] = ij_lookup(key[i], kx, g, i);
     rowid[i] = (uint32_t)i;
   }
 }
@@ -1551,7 +1562,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
   __shared__ uint32_t s_lo[kIjSmall];
   __shared__ uint32_t s_w[W];
   for (uint32_t r = threadIdx.x; r < n; r += kSmallBlock) {
-    const uint2 e = ij_lookup(key[r], kx, g);
+    const uint2 e = ij_lookup(key[r], kx, g, r);
     s_lo[r] = e.x;
     s_pre[r] = e.y;
   }
@@ -1647,7 +1658,7 @@ std::unique_ptr<Table> anti_index_join(Ctx& c, const Table& A, const das_link_sc
   const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
   IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
             use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
-            use_dir ? PI.dir_n[q.type_id] : 0u};
+            use_dir ? PI.dir_n[q.type_id] : 0u, 0u, 0u, 0};
   DBuf<uint32_t> keep(A.nrows, c.s);
   {
     ProfScope ps(c, "k_anti_ij", 4.0 * A.nrows * (ar + 1));
@@ -1722,19 +1733,73 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
   DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
   const int nu = (int)uni.size();
   if (A.nrows == 0 || PI.nkeys == 0) return new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), 0);
+  const uint32_t* akey = A.col(colof(A, q.var[bp]));
+  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
+  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
+  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
+            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
+            use_dir ? PI.dir_n[q.type_id] : 0u, 0u, 0u, 0};
+  const RowTable* T = &PI.t;                     // the table the expansion reads
+  {
+    // ranged mode: the rows of a grounded key (type, t_q = v) of P_{a,q},
+    // when they are few (found in the host key mirror) and ordered by the
+    // probe's position once the grounded targets before it are fixed
+    const char* f = std::getenv("DAS_IJ_RANGED");          // tests: 1 whenever possible, 0 never
+    uint64_t best = ~0ull;
+    IjGround gb{};
+    uint32_t blo = 0, bhi = 0, bq = 0;
+    for (uint32_t qq = 0; qq < ar && !(f && f[0] == '0'); ++qq) {
+      if (q.target[qq] == kNone) continue;
+      const PosIndex& PQ = idx.pidx[ar][qq];
+      if (PQ.h_ukey.empty() || PQ.t.rows >= 0xFFFFFFFFull) continue;
+      IjGround gq{};
+      bool stop = false, ok = true, probe = false;
+      for (uint32_t r = 0; r < ar && ok; ++r) {
+        if (r == qq) continue;
+        if (q.target[r] != kNone) {
+          if (stop) ok = false;
+          gq.col[gq.n] = PQ.t.col(1 + (int)r);
+          gq.val[gq.n] = q.target[r];
+          gq.src[gq.n++] = nullptr;
+        } else if ((int)r == bp) {
+          if (stop) ok = false;
+          gq.col[gq.n] = PQ.t.col(1 + (int)r);
+          gq.src[gq.n++] = akey;
+          probe = true;
+        } else {
+          stop = true;
+        }
+      }
+      if (!ok || !probe) continue;
+      const uint64_t k = ((uint64_t)q.type_id << 32) | q.target[qq];
+      const size_t i = std::lower_bound(PQ.h_ukey.begin(), PQ.h_ukey.end(), k) - PQ.h_ukey.begin();
+      const bool has = i < PQ.h_ukey.size() && PQ.h_ukey[i] == k;
+      const uint64_t lo = has ? PQ.h_uoff[i] : 0, hi = has ? PQ.h_uoff[i + 1] : 0;
+      if (hi - lo < best) {
+        best = hi - lo;
+        gb = gq;
+        blo = (uint32_t)lo;
+        bhi = (uint32_t)hi;
+        bq = qq;
+      }
+    }
+    const bool take = best != ~0ull &&
+                      ((f && f[0] == '1') || (best <= (1ull << 22) && best <= 64ull * A.nrows));
+    if (take) {
+      g = gb;
+      kx.fixed = 1;
+      kx.flo = blo;
+      kx.fhi = bhi;
+      T = &idx.pidx[ar][bq].t;
+    }
+  }
   JoinCols jc{};
   for (int k = 0; k < nu; ++k) {
     const int ia = colof(A, uni[k]);
     if (ia >= 0) { jc.p[jc.np] = A.col(ia); jc.po[jc.np++] = k; continue; }
     for (auto& f : fresh)
-      if (f.first == uni[k]) { jc.b[jc.nb] = PI.t.col(1 + (int)f.second); jc.bo[jc.nb++] = k; }
+      if (f.first == uni[k]) { jc.b[jc.nb] = T->col(1 + (int)f.second); jc.bo[jc.nb++] = k; }
   }
-  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
-  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
-  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
-            use_dir ? PI.dir_n[q.type_id] : 0u};
-  const uint32_t* akey = A.col(colof(A, q.var[bp]));
   std::unique_ptr<Table> out;
   if (A.nrows <= kIjSmall) {
     // one launch when the output fits a speculative table

@@ -545,17 +545,21 @@ def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
 
 # ------------------------------------------------------------ index join
 
-@pytest.mark.parametrize("mode", ["1", "1-bsearch", "0"])
+@pytest.mark.parametrize("mode", ["1", "1-bsearch", "1-ranged", "0"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw", "flybase"])
 def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
     """And with das_index_join forced on every eligible term (1: keys found
     through the dense per-type key directory; 1-bsearch: by binary search
     over the unique keys) and never (0): the same answers as the oracle,
     incl. grounded-prefix terms (FlyBase Execution(Schema s, V, V)), hub
-    keys and empty joins that fall back to the scan path (reset-on-empty)."""
+    keys and empty joins that fall back to the scan path (reset-on-empty).
+    1-ranged: grounded-key terms searched within the (type, t_q = v) rows of
+    P_{a,q} (ranged mode) wherever the shape allows it; the other modes
+    never take it."""
     import bench
     from das_amd import synthetic
     monkeypatch.setenv("DAS_INDEX_JOIN", mode[0])
+    monkeypatch.setenv("DAS_IJ_RANGED", "1" if mode == "1-ranged" else "0")
     if mode == "1-bsearch":
         monkeypatch.setenv("DAS_NO_KEY_DIR", "1")
     if gen == "bio":

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--schema", type=int, default=60)
     ap.add_argument("--rows", type=int, default=450_000)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--kernels", action="store_true", help="also: per-query kernel scopes (plan path, one run each)")
     args = ap.parse_args()
     import torch
     import bench
@@ -52,6 +53,23 @@ def main():
                 ts.sort()
                 res[f"{name} {'fresh' if fresh else 'reused'}"] = round(ts[len(ts) // 2] * 1e6, 1)
         out[f"plan={mode}"] = res if f"plan={mode}" not in out else {k: [out[f'plan={mode}'][k], v] for k, v in res.items()}
+    if args.kernels:
+        os.environ["DAS_PLAN"] = "1"
+        specs = bench.flybase_specs(genes[1], do[genes[1]])
+        for name, s in specs:
+            q = bench.build_expr(pm, s)
+            a = pm.PatternMatchingAnswer()
+            q.matched(db, a)                      # warm
+            q = bench.build_expr(pm, bench.flybase_specs(genes[2], do[genes[2]])[[n for n, _ in specs].index(name)][1])
+            db.ctx.prof_reset()
+            db.ctx.prof_enable(True)
+            a = pm.PatternMatchingAnswer()
+            q.matched(db, a)
+            n = a.count()
+            db.ctx.prof_enable(False)
+            st = db.ctx.prof_stats()
+            out[f"kernels {name} (n={n})"] = {k: [v["launches"], round(v["ms"] * 1e3, 1)]
+                                             for k, v in sorted(st.items(), key=lambda kv: -kv[1]["ms"])}
     print(json.dumps(out, indent=1))
 
 

@@ -4,9 +4,13 @@ HIP-event scopes use.
 
     python tools/pmc_traffic.py <fetch-dir> <write-dir> [steps]
 
-FETCH_SIZE and WRITE_SIZE are reported in KiB.  On gfx950 FETCH_SIZE counts half
-the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM), so
-fetched bytes are taken as 2 x FETCH_SIZE; WRITE_SIZE is used as is.
+FETCH_SIZE and WRITE_SIZE are reported in KiB.  FETCH_SIZE counts 64 B per
+memory request (profiles/fetch_calibration.json, tools/ubench/fetch_cal.hip):
+a wide coalesced stream issues 128-B requests tallied at 64 B, so streaming
+kernels' reads are 2 x FETCH_SIZE (MI355X_MICROARCH.md, HBM); an isolated
+4-B load is one 64-B request counted exactly, so the random-probe kernels
+(RANDOM below) take FETCH_SIZE as is.  The raw figure is reported beside the
+corrected one.  WRITE_SIZE is used as is.
 TOPK=k (env) averages only each kernel's k largest launches (the timed
 full-size launches of a run whose warm-up step is a small KB, e.g. the build).
 """
@@ -29,6 +33,15 @@ def short(name):
                  ("unsigned char", "u8")):
         n = n.replace(a, b)
     return n.replace(" ", "")
+
+
+# kernels whose reads are dominated by isolated random loads (x1)
+RANDOM = {"k_tile_count<BitsPred>", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
+          "k_hset_first", "k_hset_anti", "k_lookup", "k_lookup_pub"}
+
+
+def fetch_factor(kernel):
+    return 1.0 if kernel in RANDOM else 2.0
 
 
 def per_kernel(db_dir, counter):
@@ -54,11 +67,14 @@ def main():
         wb, wn = write.get(k, (0.0, 0))
         if not fn or not wn:
             continue
-        rd = 2.0 * fb / fn
+        f = fetch_factor(k)
+        rd = f * fb / fn
         wr = wb / wn
         res[k] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                  "fetch_size_raw_per_launch": fb / fn, "fetch_factor": f,
                   "launches_fetch_pass": fn, "launches_write_pass": wn,
-                  "note": "read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; mean over "
+                  "note": f"read = {f:g} x FETCH_SIZE ({'random probes' if f == 1 else 'streaming'}), "
+                          "write = WRITE_SIZE; mean over "
                           + (f"the {os.environ['TOPK']} largest launches" if os.environ.get("TOPK") else "all launches")}
     print(json.dumps(res, indent=1, sort_keys=True))
 
