@@ -682,6 +682,34 @@ Ctx*& active_ctx() {
 KScope::KScope(const char* name, double algorithmic_bytes) {
   Ctx* c = active_ctx();
   if (c && c->prof) impl = new ProfScope(*c, name, algorithmic_bytes);
+  else if (trace_on()) trace_mark("kernel", name);
+}
+
+namespace {
+struct TraceEv {
+  const char* what;
+  std::string name;
+  double us;
+};
+thread_local std::vector<TraceEv> t_trace;
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+bool trace_on() {
+  static const bool on = std::getenv("DAS_TRACE") != nullptr;
+  return on;
+}
+void trace_mark(const char* what, const std::string& name) {
+  if (trace_on()) t_trace.push_back({what, name, now_us()});
+}
+void trace_dump(const char* title) {
+  if (!trace_on() || t_trace.empty()) return;
+  const double t0 = t_trace.front().us;
+  std::fprintf(stderr, "[trace] %s\n", title);
+  for (auto& e : t_trace) std::fprintf(stderr, "[trace] %9.1f %s %s\n", e.us - t0, e.what, e.name.c_str());
+  t_trace.clear();
 }
 KScope::~KScope() { delete static_cast<ProfScope*>(impl); }
 

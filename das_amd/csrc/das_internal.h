@@ -165,12 +165,20 @@ struct Ctx {
 // way tools/pmc_traffic.py shortens it (namespaces dropped, integer template
 // arguments kept, unsigned int/long -> u32/u64), e.g. "k_dj_write<2,1,u32>",
 // so every launch size and time pairs with its rocprof row.
+// Host timeline (DAS_TRACE=1, tools): marks on a monotonic microsecond clock
+// -- kernel scopes, read-back waits, plan nodes -- printed to stderr by
+// das_plan_execute.
+bool trace_on();
+void trace_mark(const char* what, const std::string& name = std::string());
+void trace_dump(const char* title);
+
 struct ProfScope {
   Ctx& c;
   std::string name;
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
+    if (trace_on()) trace_mark("kernel", name);
     if (!c.prof || (!c.prof_only.empty() && c.prof_only != name)) return;
     a = c.take_event();
     b = c.take_event();
@@ -254,6 +262,13 @@ struct PlanOutput {
   std::vector<std::unique_ptr<Table>> tables;
 };
 PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload);
+// query.hip: an And of ordered Links (terms) and Not(Link) filters (anti)
+// evaluated by one single-workgroup launch when its running result stays
+// small.  0: not taken (the caller evaluates it operator by operator);
+// 1: evaluated -- `matched`, and the result table when matched.
+int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+              const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
+              std::unique_ptr<Table>& out);
 
 // export.hip: Redis key-space files (canonical_parser.py:119-183)
 struct ExportCounts {

@@ -105,6 +105,7 @@ PubSlot pub_reserve() {
 }
 
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
+  trace_mark("wait");
   for (uint64_t it = 1;; ++it) {
     if (__atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq) break;
     if ((it & 255) == 0) {
@@ -120,6 +121,7 @@ void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
     __builtin_ia32_pause();
   }
   for (uint32_t i = 0; i < n; ++i) out[i] = __atomic_load_n(&ps.p[i], __ATOMIC_RELAXED);
+  trace_mark("woke");
 }
 
 ScanCtr& scan_ctr(hipStream_t s) {

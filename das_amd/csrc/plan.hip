@@ -136,6 +136,8 @@ struct Exec {
 
   Res eval(uint32_t i) {
     const das_plan_node_t& x = nd[i];
+    static const char* const kOp[] = {"?", "LINK", "CONST", "NOT", "AND", "OR"};
+    if (trace_on()) trace_mark("node", x.op <= 5 ? kOp[x.op] : "?");
     Res r;
     switch (x.op) {
       case DAS_PLAN_CONST:
@@ -166,6 +168,24 @@ struct Exec {
   Res eval_and(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
+    {
+      // an And of Links (and Not(Link) filters): one fused launch when small
+      std::vector<const das_plan_node_t*> pos, neg;
+      bool flat = true;
+      for (uint32_t ti : terms) {
+        const das_plan_node_t& x = nd[ti];
+        if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) neg.push_back(&nd[ti + 1]);
+        else if (x.op == DAS_PLAN_LINK) pos.push_back(&x);
+        else flat = false;
+      }
+      bool m = false;
+      TablePtr t;
+      if (flat && fused_and(c, pos, neg, no_overload, m, t)) {
+        out.matched = m;
+        if (m) out.rel.push(std::move(t));
+        return out;
+      }
+    }
     Rel acc;
     bool have = false;
     std::vector<Rel> forbidden;
@@ -268,7 +288,10 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   DAS_CHECK(n > 0, DAS_E_INVALID, "plan: no nodes");
   Exec ex{c, nodes, n, no_overload};
   DAS_CHECK(ex.next(0) == n, DAS_E_INVALID, "plan: node array is not one expression tree");
+  trace_mark("plan");
   Res r = ex.eval(0);
+  trace_mark("done");
+  trace_dump("das_plan_execute");
   PlanOutput out;
   out.matched = r.matched;
   out.negation = r.neg;

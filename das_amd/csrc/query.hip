@@ -15,6 +15,7 @@
 // per-block two-pass (count -> scan -> write) so output order is the input
 // order (deterministic) and no global atomics sit on the hot path.
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <optional>
@@ -1107,20 +1108,35 @@ void set_cols(ScanSpec& sp, const RowTable& rt) {
 
 }  // namespace
 
-std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
+namespace {
+// A Link scan resolved on the host: the spec, the row range(s) of the index
+// table it reads, the output schema and order (scan_link runs it; the fused
+// small-And chain embeds it as a stage).
+struct ScanPrep {
+  ScanSpec sp{};
+  int32_t vars[kMaxCols] = {0};
+  int ncols = 0;
+  int kind = DAS_TABLE_ORDERED;
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;
+  int sorted_pos = -1;
+  bool empty = false;
+};
+
+void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
   Index& idx = c.idx;
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
   DAS_CHECK(ar <= 8, DAS_E_INVALID, "arity > 8");
   // output schema
-  int32_t vars[kMaxCols];
-  int ncols = 0;
-  ScanSpec sp{};
+  int32_t* vars = P.vars;
+  int& ncols = P.ncols;
+  ScanSpec& sp = P.sp;
   sp.arity = ar;
   sp.no_overload = q.no_overload;
   sp.emit_link = q.emit_link;
   sp.unordered = q.ordered ? 0 : 1;
-  int kind = q.ordered ? DAS_TABLE_ORDERED : DAS_TABLE_UNORDERED;
+  int& kind = P.kind;
+  kind = q.ordered ? DAS_TABLE_ORDERED : DAS_TABLE_UNORDERED;
   bool any_wild = false;
   for (uint32_t p = 0; p < ar; ++p) {
     sp.fixed[p] = q.target[p];
@@ -1157,19 +1173,19 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
     DAS_CHECK(sp.nupos == q.n_vars, DAS_E_INVALID, "unordered scan: variables != wildcard positions");
     sp.nout = ncols;
   }
-  auto empty = [&]() { return new_table(c, kind, ncols, vars, 0); };
+  auto empty = [&]() { P.empty = true; };
   if (ar == 0 || ar > (uint32_t)kMaxArity || idx.ttab[ar].rows == 0) return empty();
   if (q.type_id != kNone && q.type_id >= idx.n_types) return empty();
   // Families the reference indexes (canonical_parser.py:144-178)
   if (ar > (uint32_t)kMaxPosArity) {
     if (q.type_id != kNone || any_wild) return empty();   // only [*, e0..en]
   }
-  std::vector<std::pair<uint64_t, uint64_t>> ranges;     // row ranges of rt to scan
+  auto& ranges = P.ranges;                                // row ranges of rt to scan
   const RowTable* rt = nullptr;
   std::vector<uint32_t> grounded;
   for (uint32_t p = 0; p < ar; ++p)
     if (q.target[p] != kNone) grounded.push_back(p);
-  int sorted_pos = -1;                                    // output comes sorted by this position
+  int& sorted_pos = P.sorted_pos;                         // output comes sorted by this position
   if (grounded.empty() || ar > (uint32_t)kMaxPosArity) {
     const bool typed = q.type_id != kNone;
     if (typed && ar <= (uint32_t)kMaxPosArity && q.order_pos >= 0 && (uint32_t)q.order_pos < ar &&
@@ -1270,21 +1286,29 @@ std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
   for (uint32_t p = 0; p < ar; ++p) filt |= sp.fixed[p] != kNone;
   sp.all_keep = !filt && sp.neq == 0 && !(sp.unordered && sp.nupos > 1) && !(!sp.unordered && sp.no_overload && sp.nout > 1);
   if (ranges.empty()) return empty();
+}
+}  // namespace
+
+std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
+  ScanPrep P;
+  scan_prepare(c, q, P);
+  if (P.empty) return new_table(c, P.kind, P.ncols, P.vars, 0);
+  ScanSpec& sp = P.sp;
   std::unique_ptr<Table> t;
-  if (ranges.size() == 1) {
-    t = run_scan(c, sp, ranges[0].first, ranges[0].second, kind, ncols, vars, q.type_id);
+  if (P.ranges.size() == 1) {
+    t = run_scan(c, sp, P.ranges[0].first, P.ranges[0].second, P.kind, P.ncols, P.vars, q.type_id);
   } else {
     std::vector<std::unique_ptr<Table>> parts;
     std::vector<const Table*> pp;
-    for (auto& r : ranges) {
-      parts.push_back(run_scan(c, sp, r.first, r.second, kind, ncols, vars, q.type_id));
+    for (auto& r : P.ranges) {
+      parts.push_back(run_scan(c, sp, r.first, r.second, P.kind, P.ncols, P.vars, q.type_id));
       pp.push_back(parts.back().get());
     }
     t = concat(c, pp.data(), (int)pp.size());
   }
-  if (sorted_pos >= 0 && q.ordered)
+  if (P.sorted_pos >= 0 && q.ordered)
     for (int k = 0; k < t->ncols; ++k)
-      if (sp.outpos[k] == sorted_pos) t->sorted_col = k;
+      if (sp.outpos[k] == P.sorted_pos) t->sorted_col = k;
   return t;
 }
 
@@ -1616,97 +1640,113 @@ __global__ void __launch_bounds__(B) k_anti_ij(const uint32_t* __restrict__ key,
     keep[i] = ij_lookup(key[i], kx, g, i).y == 0 ? 1u : 0u;
 }
 
-std::unique_ptr<Table> anti_index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+namespace {
+int colof_t(const Table& t, int32_t v) {
+  for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
+  return -1;
+}
+
+IjKeys ij_keys(const PosIndex& PI, uint32_t type_id) {
+  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
+  const bool use_dir = type_id < PI.dir.size() && PI.dir[type_id] && !no_dir;
+  return IjKeys{(uint64_t)type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
+                use_dir ? PI.dir[type_id] : nullptr, use_dir ? PI.dir_lo[type_id] : 0u,
+                use_dir ? PI.dir_n[type_id] : 0u, 0u, 0u, 0};
+}
+
+// Anti index join of A by a Not(Link) term, resolved on the host.
+struct AntiPlan {
+  IjKeys kx{};
+  IjGround g{};
+  const uint32_t* key = nullptr;
+  bool keep_all = false;       // no link of that arity is indexed: nothing is forbidden
+};
+
+// false: the term does not reduce to a lookup per row of A (a variable of
+// the term that A does not bind: the caller keeps A whole)
+bool anti_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, AntiPlan& pl) {
   Index& idx = c.idx;
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
   if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
       ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
-    return nullptr;
-  auto colof = [](const Table& t, int32_t v) {
-    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
-    return -1;
-  };
+    return false;
   // every position grounded or bound by A (else the filter is not a lookup)
   int bp = -1;
   for (uint32_t p = 0; p < ar; ++p) {
     if (q.target[p] != kNone) continue;
-    if (q.var[p] < 0 || colof(A, q.var[p]) < 0) return nullptr;
+    if (q.var[p] < 0 || colof_t(A, q.var[p]) < 0) return false;
     if (bp < 0) bp = (int)p;
   }
-  if (bp < 0) return nullptr;
-  if (A.nrows == 0) return new_table_like(c, A, 0);
+  if (bp < 0) return false;
   const PosIndex& PI = idx.pidx[ar][bp];
   if (PI.nkeys == 0) {
-    DBuf<uint32_t> all(A.nrows, c.s);
-    iota(all.p, A.nrows, c.s);
-    return gather_table(c, A, all.p, A.nrows);
+    pl.keep_all = true;
+    return true;
   }
-  IjGround g{};
   for (uint32_t p = 0; p < ar; ++p) {
     if ((int)p == bp) continue;
-    g.col[g.n] = PI.t.col(1 + (int)p);
+    pl.g.col[pl.g.n] = PI.t.col(1 + (int)p);
     if (q.target[p] != kNone) {
-      g.val[g.n] = q.target[p];
-      g.src[g.n] = nullptr;
+      pl.g.val[pl.g.n] = q.target[p];
+      pl.g.src[pl.g.n] = nullptr;
     } else {
-      g.src[g.n] = A.col(colof(A, q.var[p]));
+      pl.g.src[pl.g.n] = A.col(colof_t(A, q.var[p]));
     }
-    ++g.n;
+    ++pl.g.n;
   }
-  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
-  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
-  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
-            use_dir ? PI.dir_n[q.type_id] : 0u, 0u, 0u, 0};
-  DBuf<uint32_t> keep(A.nrows, c.s);
-  {
-    ProfScope ps(c, "k_anti_ij", 4.0 * A.nrows * (ar + 1));
-    hipLaunchKernelGGL(k_anti_ij, G(A.nrows), dim3(B), 0, c.s, (const uint32_t*)A.col(colof(A, q.var[bp])), A.nrows,
-                       kx, g, keep.p);
-    DAS_HIP(hipGetLastError());
-  }
-  return compact_table(c, A, keep.p);
+  pl.kx = ij_keys(PI, q.type_id);
+  pl.key = A.col(colof_t(A, q.var[bp]));
+  return true;
 }
 
-std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+// Index join of A with a Link term, resolved on the host.  `rows` = A's row
+// count, or an upper bound of it (the fused chain), for the cost choices.
+struct IjPlan {
+  IjKeys kx{};
+  IjGround g{};
+  JoinCols jc{};
+  const uint32_t* akey = nullptr;
+  std::vector<int32_t> uni;
+  uint32_t lo[kMaxCols] = {0}, hi[kMaxCols] = {0};
+  bool empty = false;          // no output row possible
+};
+
+// false: not an index join of A (the caller scans the term and joins)
+bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows, IjPlan& pl) {
   Index& idx = c.idx;
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
   if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
-      ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
-    return nullptr;
-  auto colof = [](const Table& t, int32_t v) {
-    for (int i = 0; i < t.ncols; ++i) if (t.vars[i] == v) return i;
-    return -1;
-  };
+      ar == 0 || ar > (uint32_t)kMaxPosArity || rows >= 0xFFFFFFFFull)
+    return false;
   // one bound position; every other position a fresh, distinct variable or
   // a grounded target that leads P_{a,p}'s secondary order
   int bp = -1;
   std::vector<std::pair<int32_t, uint32_t>> fresh;   // (var, position)
   for (uint32_t p = 0; p < ar; ++p) {
     if (q.target[p] != kNone) {
-      if (q.var[p] >= 0) return nullptr;
+      if (q.var[p] >= 0) return false;
       continue;
     }
-    if (q.var[p] < 0) return nullptr;
-    if (colof(A, q.var[p]) >= 0) {
-      if (bp >= 0) return nullptr;
+    if (q.var[p] < 0) return false;
+    if (colof_t(A, q.var[p]) >= 0) {
+      if (bp >= 0) return false;
       bp = (int)p;
     } else {
-      for (auto& f : fresh) if (f.first == q.var[p]) return nullptr;
+      for (auto& f : fresh) if (f.first == q.var[p]) return false;
       fresh.push_back({q.var[p], p});
     }
   }
-  if (bp < 0) return nullptr;
+  if (bp < 0) return false;
   const PosIndex& PI = idx.pidx[ar][bp];
-  IjGround g{};
+  IjGround& g = pl.g;
   {
     bool prefix = true;                          // still inside the grounded prefix
     for (uint32_t p = 0; p < ar; ++p) {
       if ((int)p == bp) continue;
       if (q.target[p] != kNone) {
-        if (!prefix) return nullptr;             // a grounded target after a free one: rows not contiguous
+        if (!prefix) return false;               // a grounded target after a free one: rows not contiguous
         g.col[g.n] = PI.t.col(1 + (int)p);
         g.val[g.n++] = q.target[p];
       } else {
@@ -1717,28 +1757,49 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
   // cost: a search per row of A against a scan of the Link's type segment
   {
     const char* f = std::getenv("DAS_INDEX_JOIN");          // tests: 1 always, 0 never
-    if (f && f[0] == '0') return nullptr;
+    if (f && f[0] == '0') return false;
     const uint64_t seg = idx.type_off[ar].size() > q.type_id + 1
                              ? idx.type_off[ar][q.type_id + 1] - idx.type_off[ar][q.type_id] : 0;
     // (with grounded targets the scan reads one key range, of unknown size
     // here: index-join only small probes)
-    const bool cheap = g.n == 0 ? 4 * A.nrows <= seg : A.nrows <= (1ull << 20);
-    if (!(f && f[0] == '1') && !cheap) return nullptr;
+    const bool cheap = g.n == 0 ? 4 * rows <= seg : rows <= (1ull << 20);
+    if (!(f && f[0] == '1') && !cheap) return false;
   }
   DAS_CHECK(PI.t.rows < 0xFFFFFFFFull, DAS_E_UNSUPPORTED, "index join: P table too large");
   // output schema: A's variables and the fresh ones, ascending
-  std::vector<int32_t> uni(A.vars, A.vars + A.ncols);
+  std::vector<int32_t>& uni = pl.uni;
+  uni.assign(A.vars, A.vars + A.ncols);
   for (auto& f : fresh) uni.push_back(f.first);
   std::sort(uni.begin(), uni.end());
   DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
   const int nu = (int)uni.size();
-  if (A.nrows == 0 || PI.nkeys == 0) return new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), 0);
-  const uint32_t* akey = A.col(colof(A, q.var[bp]));
-  static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
-  const bool use_dir = q.type_id < PI.dir.size() && PI.dir[q.type_id] && !no_dir;
-  IjKeys kx{(uint64_t)q.type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-            use_dir ? PI.dir[q.type_id] : nullptr, use_dir ? PI.dir_lo[q.type_id] : 0u,
-            use_dir ? PI.dir_n[q.type_id] : 0u, 0u, 0u, 0};
+  // output column bounds: A's columns, and the type's bounds for fresh ones
+  {
+    const uint32_t ncol = ar + 1;
+    const auto& tb = idx.tbound[ar];
+    for (int k = 0; k < nu; ++k) {
+      const int ia = colof_t(A, uni[k]);
+      if (ia >= 0) {
+        pl.lo[k] = A.lo[ia];
+        pl.hi[k] = A.hi[ia];
+        continue;
+      }
+      pl.lo[k] = 0;
+      pl.hi[k] = kNone;
+      for (auto& f : fresh)
+        if (f.first == uni[k] && (uint64_t)(q.type_id + 1) * ncol * 2 <= tb.size()) {
+          pl.lo[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2];
+          pl.hi[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2 + 1];
+        }
+    }
+  }
+  if (rows == 0 || PI.nkeys == 0) {
+    pl.empty = true;
+    return true;
+  }
+  const uint32_t* akey = pl.akey = A.col(colof_t(A, q.var[bp]));
+  IjKeys& kx = pl.kx;
+  kx = ij_keys(PI, q.type_id);
   const RowTable* T = &PI.t;                     // the table the expansion reads
   {
     // ranged mode: the rows of a grounded key (type, t_q = v) of P_{a,q},
@@ -1784,7 +1845,7 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
       }
     }
     const bool take = best != ~0ull &&
-                      ((f && f[0] == '1') || (best <= (1ull << 22) && best <= 64ull * A.nrows));
+                      ((f && f[0] == '1') || (best <= (1ull << 22) && best <= 64ull * rows));
     if (take) {
       g = gb;
       kx.fixed = 1;
@@ -1793,61 +1854,412 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
       T = &idx.pidx[ar][bq].t;
     }
   }
-  JoinCols jc{};
+  JoinCols& jc = pl.jc;
   for (int k = 0; k < nu; ++k) {
-    const int ia = colof(A, uni[k]);
+    const int ia = colof_t(A, uni[k]);
     if (ia >= 0) { jc.p[jc.np] = A.col(ia); jc.po[jc.np++] = k; continue; }
     for (auto& f : fresh)
       if (f.first == uni[k]) { jc.b[jc.nb] = T->col(1 + (int)f.second); jc.bo[jc.nb++] = k; }
   }
+  return true;
+}
+}  // namespace
+
+std::unique_ptr<Table> anti_index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+  AntiPlan pl;
+  if (!anti_prepare(c, A, q, pl)) return nullptr;
+  if (A.nrows == 0) return new_table_like(c, A, 0);
+  if (pl.keep_all) {
+    DBuf<uint32_t> all(A.nrows, c.s);
+    iota(all.p, A.nrows, c.s);
+    return gather_table(c, A, all.p, A.nrows);
+  }
+  DBuf<uint32_t> keep(A.nrows, c.s);
+  {
+    ProfScope ps(c, "k_anti_ij", 4.0 * A.nrows * (q.arity + 1));
+    hipLaunchKernelGGL(k_anti_ij, G(A.nrows), dim3(B), 0, c.s, pl.key, A.nrows, pl.kx, pl.g, keep.p);
+    DAS_HIP(hipGetLastError());
+  }
+  return compact_table(c, A, keep.p);
+}
+
+std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t& q) {
+  IjPlan pl;
+  if (!ij_prepare(c, A, q, A.nrows, pl)) return nullptr;
+  const int nu = (int)pl.uni.size();
   std::unique_ptr<Table> out;
-  if (A.nrows <= kIjSmall) {
-    // one launch when the output fits a speculative table
-    auto t = new_table(c, DAS_TABLE_ORDERED, nu, uni.data(), kIjSmallCap);
-    const PubSlot ps = pub_reserve();
-    {
-      ProfScope pf(c, "k_ij_small", 16.0 * A.nrows + 4.0 * A.nrows * A.ncols);
-      hipLaunchKernelGGL(k_ij_small, dim3(1), dim3(kSmallBlock), 0, c.s, akey, (uint32_t)A.nrows, kx, g, jc, t->data,
-                         t->cap, ps.p, ps.seq);
-      DAS_HIP(hipGetLastError());
-    }
-    uint32_t total = 0;
-    pub_wait(ps, c.s, &total, 1);
-    if (total <= t->cap) {
-      t->nrows = total;
-      out = std::move(t);
-    }
-  }
-  if (!out) {
-    DBuf<uint2> lc(A.nrows, c.s);
-    DBuf<uint32_t> rowid(A.nrows, c.s);
-    {
-      ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
-      hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, akey, A.nrows, kx, g, lc.p, rowid.p);
-      DAS_HIP(hipGetLastError());
-    }
-    // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
-    out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, jc, nu, uni.data(), 0.0);
-  }
-  out->sorted_col = A.sorted_col >= 0 ? colof(*out, A.vars[A.sorted_col]) : -1;
-  const uint32_t ncol = ar + 1;
-  const auto& tb = idx.tbound[ar];
-  for (int k = 0; k < nu; ++k) {
-    const int ia = colof(A, uni[k]);
-    if (ia >= 0) {
-      out->lo[k] = A.lo[ia];
-      out->hi[k] = A.hi[ia];
-      continue;
-    }
-    out->lo[k] = 0;
-    out->hi[k] = kNone;
-    for (auto& f : fresh)
-      if (f.first == uni[k] && (uint64_t)(q.type_id + 1) * ncol * 2 <= tb.size()) {
-        out->lo[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2];
-        out->hi[k] = tb[((uint64_t)q.type_id * ncol + 1 + f.second) * 2 + 1];
+  if (pl.empty) {
+    out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), 0);
+  } else {
+    if (A.nrows <= kIjSmall) {
+      // one launch when the output fits a speculative table
+      auto t = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), kIjSmallCap);
+      const PubSlot ps = pub_reserve();
+      {
+        ProfScope pf(c, "k_ij_small", 16.0 * A.nrows + 4.0 * A.nrows * A.ncols);
+        hipLaunchKernelGGL(k_ij_small, dim3(1), dim3(kSmallBlock), 0, c.s, pl.akey, (uint32_t)A.nrows, pl.kx, pl.g,
+                           pl.jc, t->data, t->cap, ps.p, ps.seq);
+        DAS_HIP(hipGetLastError());
       }
+      uint32_t total = 0;
+      pub_wait(ps, c.s, &total, 1);
+      if (total <= t->cap) {
+        t->nrows = total;
+        out = std::move(t);
+      }
+    }
+    if (!out) {
+      DBuf<uint2> lc(A.nrows, c.s);
+      DBuf<uint32_t> rowid(A.nrows, c.s);
+      {
+        ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
+        hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, pl.akey, A.nrows, pl.kx, pl.g, lc.p, rowid.p);
+        DAS_HIP(hipGetLastError());
+      }
+      // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
+      out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, pl.jc, nu, pl.uni.data(), 0.0);
+    }
+  }
+  out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
+  for (int k = 0; k < nu; ++k) {
+    out->lo[k] = pl.lo[k];
+    out->hi[k] = pl.hi[k];
   }
   return out;
+}
+
+// ---------------------------------------------------------------------------
+// Fused small And (das_plan_execute).  An anchored And of ordered Links --
+// the FlyBase shapes: a grounded scan, index joins, a small cross join, anti
+// index joins for its Not terms -- keeps its running result at a few rows,
+// so each operator is one small launch and one read-back round trip.  Here
+// the whole chain runs in ONE workgroup of ONE launch, with one read-back:
+// the stages (compiled on the host from the same prepare steps as the
+// per-operator path: scan_prepare, ij_prepare, anti_prepare) are read from
+// pinned memory into LDS, each stage's row count stays in LDS, every
+// intermediate table is allocated up front at a speculative capacity.  The
+// chain gives up ("bail") when a result outgrows its table or an index join
+// comes out empty (And's reset-on-empty path, pattern_matcher.py:720-733):
+// the caller then evaluates the And operator by operator.  A scan term with
+// no rows makes the And fail (:712-713), as on the host path.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kChainStages = 8;
+constexpr uint32_t kChainCap = 32768;                 // rows per speculative table
+constexpr uint64_t kChainJoinPairs = 1ull << 22;      // cross-join work bound (pairs)
+
+enum : uint32_t { CH_SCAN = 1, CH_IJ = 2, CH_JOIN = 3, CH_ANTI = 4 };
+enum : uint32_t { CHS_OK = 0, CHS_EMPTY_SCAN = 1, CHS_BAIL = 2 };
+
+struct ChainStage {
+  uint32_t op, in, rel, cap;     // input stage (running result), scanned stage (JOIN), output capacity
+  uint32_t begin, end;           // SCAN: row range of the index table
+  uint32_t* dst;                 // output table (ncols columns of `cap` rows)
+  const uint32_t* key;           // IJ / ANTI: the probe key column
+  ScanSpec sp;                   // SCAN
+  IjKeys kx;                     // IJ / ANTI
+  IjGround g;
+  JoinCols jc;                   // IJ: output columns; JOIN: p = columns of `in`, b = of `rel`
+  uint32_t nsh;                  // JOIN: shared-variable column pairs
+  const uint32_t* sha[kMaxCols];
+  const uint32_t* shb[kMaxCols];
+  uint32_t ncopy;                // ANTI: the input's columns, copied
+  const uint32_t* copy[kMaxCols];
+};
+struct ChainDesc {
+  uint32_t nstage, pad;
+  ChainStage st[kChainStages];
+};
+
+// Block-wide ordered compaction step: this thread's output position among
+// the kept rows of the round (keep order = thread order); advances *run.
+__device__ __forceinline__ uint32_t chain_rank(bool keep, uint32_t* s_w, uint32_t* run) {
+  constexpr int W = kSmallBlock / 64;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(keep);
+  if (__lane_id() == 0) s_w[wave] = __popcll(m);
+  __syncthreads();
+  uint32_t pos = *run + __popcll(m & __lanemask_lt());
+  uint32_t all = 0;
+  for (int w = 0; w < W; ++w) {
+    if (w < wave) pos += s_w[w];
+    all += s_w[w];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *run += all;
+  __syncthreads();
+  return pos;
+}
+
+__global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restrict__ hdesc, uint32_t nwords,
+                                                       uint32_t* slot, uint32_t seq) {
+  constexpr int W = kSmallBlock / 64;
+  __shared__ ChainDesc d;
+  __shared__ uint32_t s_cnt[kChainStages];
+  __shared__ uint32_t s_pre[kIjSmall + 1];
+  __shared__ uint32_t s_lo[kIjSmall];
+  __shared__ uint32_t s_w[W];
+  __shared__ uint32_t s_run, s_state;
+  uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
+  for (uint32_t i = threadIdx.x; i < nwords; i += kSmallBlock) dw[i] = hdesc[i];
+  if (threadIdx.x == 0) s_state = CHS_OK;
+  __syncthreads();
+  uint32_t last = 0;
+  for (uint32_t si = 0; si < d.nstage && s_state == CHS_OK; ++si) {
+    const ChainStage& st = d.st[si];
+    if (threadIdx.x == 0) s_run = 0;
+    __syncthreads();
+    uint32_t n = 0;
+    if (st.op == CH_SCAN) {
+      for (uint32_t r0 = st.begin; r0 < st.end; r0 += kSmallBlock) {
+        const uint32_t r = r0 + threadIdx.x;
+        const bool keep = r < st.end && scan_keep(st.sp, r);
+        const uint32_t pos = chain_rank(keep, s_w, &s_run);
+        if (keep) scan_emit(st.sp, r, st.dst, st.cap, pos);
+      }
+      n = s_run;
+      if (n == 0 && threadIdx.x == 0) s_state = CHS_EMPTY_SCAN;
+    } else if (st.op == CH_IJ) {
+      const uint32_t nin = s_cnt[st.in];
+      if (nin > kIjSmall) {
+        if (threadIdx.x == 0) s_state = CHS_BAIL;
+      } else {
+        for (uint32_t r = threadIdx.x; r < nin; r += kSmallBlock) {
+          const uint2 e = ij_lookup(st.key[r], st.kx, st.g, r);
+          s_lo[r] = e.x;
+          s_pre[r] = e.y;
+        }
+        __syncthreads();
+        // exclusive scan of s_pre[0..nin) in rounds of 1024
+        const int wave = threadIdx.x >> 6;
+        uint32_t carry = 0;
+        for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
+          const uint32_t r = r0 + threadIdx.x;
+          const uint32_t v = r < nin ? s_pre[r] : 0u;
+          const uint32_t inc = wave_incl_sum_u32(v);
+          if (__lane_id() == 63) s_w[wave] = inc;
+          __syncthreads();
+          uint32_t pre = carry + inc - v, all = 0;
+          for (int w = 0; w < W; ++w) {
+            if (w < wave) pre += s_w[w];
+            all += s_w[w];
+          }
+          __syncthreads();
+          if (r < nin) s_pre[r] = pre;
+          carry += all;
+          __syncthreads();
+        }
+        if (threadIdx.x == 0) s_pre[nin] = carry;
+        __syncthreads();
+        n = carry;
+        if (n == 0 || n > st.cap) {
+          if (threadIdx.x == 0) s_state = CHS_BAIL;
+        } else {
+          for (uint32_t o = threadIdx.x; o < n; o += kSmallBlock) {
+            uint32_t l = 0, h = nin;                   // last row r with s_pre[r] <= o
+            while (h - l > 1) {
+              const uint32_t m = (l + h) >> 1;
+              if (s_pre[m] <= o) l = m; else h = m;
+            }
+            const uint32_t br = s_lo[l] + (o - s_pre[l]);
+            for (int i = 0; i < st.jc.np; ++i) st.dst[(uint64_t)st.jc.po[i] * st.cap + o] = st.jc.p[i][l];
+            for (int i = 0; i < st.jc.nb; ++i) st.dst[(uint64_t)st.jc.bo[i] * st.cap + o] = st.jc.b[i][br];
+          }
+        }
+      }
+    } else if (st.op == CH_JOIN) {
+      const uint32_t na = s_cnt[st.in], nb = s_cnt[st.rel];
+      const uint64_t pairs = (uint64_t)na * nb;
+      if (pairs > kChainJoinPairs) {
+        if (threadIdx.x == 0) s_state = CHS_BAIL;
+      } else {
+        for (uint64_t k0 = 0; k0 < pairs; k0 += kSmallBlock) {
+          const uint64_t k = k0 + threadIdx.x;
+          const uint32_t i = k < pairs ? (uint32_t)(k / nb) : 0u, j = k < pairs ? (uint32_t)(k % nb) : 0u;
+          bool keep = k < pairs;
+          for (uint32_t x = 0; x < st.nsh && keep; ++x) keep = st.sha[x][i] == st.shb[x][j];
+          const uint32_t pos = chain_rank(keep, s_w, &s_run);
+          if (keep && pos < st.cap) {
+            for (int c = 0; c < st.jc.np; ++c) st.dst[(uint64_t)st.jc.po[c] * st.cap + pos] = st.jc.p[c][i];
+            for (int c = 0; c < st.jc.nb; ++c) st.dst[(uint64_t)st.jc.bo[c] * st.cap + pos] = st.jc.b[c][j];
+          }
+        }
+        n = s_run;
+        if ((n == 0 || n > st.cap) && threadIdx.x == 0) s_state = CHS_BAIL;
+      }
+    } else {   // CH_ANTI
+      const uint32_t nin = s_cnt[st.in];
+      for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
+        const uint32_t r = r0 + threadIdx.x;
+        const bool keep = r < nin && ij_lookup(st.key[r], st.kx, st.g, r).y == 0;
+        const uint32_t pos = chain_rank(keep, s_w, &s_run);
+        if (keep)
+          for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+      }
+      n = s_run;
+    }
+    if (threadIdx.x == 0) s_cnt[si] = n;
+    last = si;
+    __syncthreads();
+  }
+  // every store of the chain is made visible before the host reads the
+  // counts and (later, through other launches) the tables
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&slot[0], s_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&slot[1], s_cnt[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&slot[2], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace
+
+int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+              const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
+              std::unique_ptr<Table>& out) {
+  const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
+  if ((f && f[0] == '0') || no_overload || terms.empty()) return 0;
+  Index& idx = c.idx;
+  ChainDesc d{};
+  std::vector<std::unique_ptr<Table>> tabs;                  // one output table per stage
+  auto add = [&](uint32_t op) -> ChainStage* {
+    if (d.nstage >= (uint32_t)kChainStages) return nullptr;
+    ChainStage& st = d.st[d.nstage++];
+    st.op = op;
+    return &st;
+  };
+  int acc = -1;                                               // stage holding the running result
+  for (const das_plan_node_t* x : terms) {
+    if (x->op != DAS_PLAN_LINK || !x->scan.ordered || x->dedup) return 0;
+    if (acc >= 0 && x->index_join) {
+      IjPlan pl;
+      const Table& A = *tabs[acc];
+      if (ij_prepare(c, A, x->ij, kIjSmall, pl)) {
+        if (pl.empty) return 0;
+        ChainStage* st = add(CH_IJ);
+        if (!st) return 0;
+        auto t = new_table(c, DAS_TABLE_ORDERED, (int)pl.uni.size(), pl.uni.data(), kChainCap);
+        for (size_t k = 0; k < pl.uni.size(); ++k) {
+          t->lo[k] = pl.lo[k];
+          t->hi[k] = pl.hi[k];
+        }
+        st->in = (uint32_t)acc;
+        st->cap = (uint32_t)t->cap;
+        st->dst = t->data;
+        st->key = pl.akey;
+        st->kx = pl.kx;
+        st->g = pl.g;
+        st->jc = pl.jc;
+        tabs.push_back(std::move(t));
+        acc = (int)d.nstage - 1;
+        continue;
+      }
+    }
+    ScanPrep P;
+    scan_prepare(c, x->scan, P);
+    if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) return 0;
+    const uint64_t b = P.ranges[0].first, e = P.ranges[0].second;
+    if (e - b > kSmallScan || e >= 0xFFFFFFFFull) return 0;
+    ChainStage* st = add(CH_SCAN);
+    if (!st) return 0;
+    auto t = new_table(c, P.kind, P.ncols, P.vars, e - b);
+    scan_bounds(idx, P.sp, x->scan.type_id, *t);
+    st->sp = P.sp;
+    st->begin = (uint32_t)b;
+    st->end = (uint32_t)e;
+    st->cap = (uint32_t)t->cap;
+    st->dst = t->data;
+    tabs.push_back(std::move(t));
+    const int rel = (int)d.nstage - 1;
+    if (acc < 0) {
+      acc = rel;
+      continue;
+    }
+    // And's join of the running result with the scanned term (join(), the
+    // natural join on the shared variables; a cross join when none)
+    const Table& A = *tabs[acc];
+    const Table& R = *tabs[rel];
+    std::vector<int32_t> va(A.vars, A.vars + A.ncols), vb(R.vars, R.vars + R.ncols), shared, uni;
+    std::set_intersection(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(shared));
+    std::set_union(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(uni));
+    if ((int)uni.size() > kMaxCols) return 0;
+    ChainStage* js = add(CH_JOIN);
+    if (!js) return 0;
+    auto jt = new_table(c, DAS_TABLE_ORDERED, (int)uni.size(), uni.data(), kChainCap);
+    js->in = (uint32_t)acc;
+    js->rel = (uint32_t)rel;
+    js->cap = (uint32_t)jt->cap;
+    js->dst = jt->data;
+    for (int32_t v : shared) {
+      js->sha[js->nsh] = A.col(colof_t(A, v));
+      js->shb[js->nsh++] = R.col(colof_t(R, v));
+    }
+    for (int k = 0; k < (int)uni.size(); ++k) {
+      const int ia = colof_t(A, uni[k]), ib = colof_t(R, uni[k]);
+      uint32_t lo = 0, hi = kNone;
+      if (ia >= 0) { lo = std::max(lo, A.lo[ia]); hi = std::min(hi, A.hi[ia]); }
+      if (ib >= 0) { lo = std::max(lo, R.lo[ib]); hi = std::min(hi, R.hi[ib]); }
+      jt->lo[k] = lo;
+      jt->hi[k] = hi;
+      if (ia >= 0) { js->jc.p[js->jc.np] = A.col(ia); js->jc.po[js->jc.np++] = k; }
+      else { js->jc.b[js->jc.nb] = R.col(ib); js->jc.bo[js->jc.nb++] = k; }
+    }
+    tabs.push_back(std::move(jt));
+    acc = (int)d.nstage - 1;
+  }
+  for (const das_plan_node_t* x : anti) {
+    AntiPlan ap;
+    const Table& A = *tabs[acc];
+    if (!anti_prepare(c, A, x->ij, ap) || ap.keep_all) continue;   // nothing forbidden / not a lookup: A whole
+    ChainStage* st = add(CH_ANTI);
+    if (!st) return 0;
+    auto t = new_table_like(c, A, A.cap);
+    for (int k = 0; k < A.ncols; ++k) {
+      t->lo[k] = A.lo[k];
+      t->hi[k] = A.hi[k];
+    }
+    st->in = (uint32_t)acc;
+    st->cap = (uint32_t)t->cap;
+    st->dst = t->data;
+    st->key = ap.key;
+    st->kx = ap.kx;
+    st->g = ap.g;
+    st->ncopy = (uint32_t)A.ncols;
+    for (int k = 0; k < A.ncols; ++k) st->copy[k] = A.col(k);
+    tabs.push_back(std::move(t));
+    acc = (int)d.nstage - 1;
+  }
+  if (d.nstage < 2) return 0;                                 // one operator: nothing to fuse
+  // only the stages in use travel (the kernel copies them into LDS)
+  const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
+  static_assert(sizeof(ChainStage) % 4 == 0 && offsetof(ChainDesc, st) % 4 == 0, "word copy");
+  uint8_t* hd = pinned_stage(bytes);
+  std::memcpy(hd, &d, bytes);
+  // algorithmic bytes known up front: the scanned index rows
+  double sbytes = 0;
+  for (uint32_t i = 0; i < d.nstage; ++i)
+    if (d.st[i].op == CH_SCAN) sbytes += 4.0 * (d.st[i].end - d.st[i].begin) * (d.st[i].sp.arity + 1);
+  const PubSlot ps = pub_reserve();
+  {
+    ProfScope pf(c, "k_chain", sbytes);
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
+                       ps.seq);
+    DAS_HIP(hipGetLastError());
+  }
+  uint32_t w[3] = {0, 0, 0};
+  pub_wait(ps, c.s, w, 3);
+  if (w[0] == CHS_BAIL) return 0;
+  matched = false;
+  out.reset();
+  if (w[0] == CHS_EMPTY_SCAN || w[1] == 0) return 1;          // a failing term, or nothing left after Not
+  DAS_CHECK(w[2] == d.nstage - 1, DAS_E_INTERNAL, "fused chain stopped early");
+  tabs[acc]->nrows = w[1];
+  matched = true;
+  out = std::move(tabs[acc]);
+  return 1;
 }
 
 // ---------------------------------------------------------------------------
