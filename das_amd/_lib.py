@@ -393,6 +393,16 @@ class Context:
             check(lib().das_lookup(self.h, ptr(d), n, ptr(ids), ptr(cat), ptr(ar), ptr(ty)), self.h)
         return ids, cat, ar, ty
 
+    def lookup_hex(self, hexes):
+        """Handle strings -> (ids, categories, arities) as lists: lookup()
+        without numpy, for the few handles of one query."""
+        n = len(hexes)
+        buf = (C.c_uint32 * (4 * n)).from_buffer_copy(bytes.fromhex("".join(hexes)))
+        ids, cat = (C.c_int64 * n)(), (C.c_uint8 * n)()
+        ar, ty = (C.c_uint32 * n)(), (C.c_uint32 * n)()
+        check(lib().das_lookup(self.h, buf, n, ids, cat, ar, ty), self.h)
+        return list(ids), list(cat), list(ar)
+
     def atoms_info(self, ids):
         ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint32))
         n = ids.shape[0]

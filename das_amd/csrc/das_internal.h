@@ -265,10 +265,12 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
 // query.hip: an And of ordered Links (terms) and Not(Link) filters (anti)
 // evaluated by one single-workgroup launch when its running result stays
 // small.  0: not taken (the caller evaluates it operator by operator);
-// 1: evaluated -- `matched`, and the result table when matched.
+// 1: evaluated -- `matched`, and the result table when matched; 2: partial
+// -- `out` is the (non-empty) running result after the first *consumed
+// terms, no Not filter applied: the caller continues the And from there.
 int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
-              std::unique_ptr<Table>& out);
+              std::unique_ptr<Table>& out, uint32_t* consumed);
 
 // export.hip: Redis key-space files (canonical_parser.py:119-183)
 struct ExportCounts {

@@ -168,28 +168,37 @@ struct Exec {
   Res eval_and(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
-    {
-      // an And of Links (and Not(Link) filters): one fused launch when small
-      std::vector<const das_plan_node_t*> pos, neg;
-      bool flat = true;
-      for (uint32_t ti : terms) {
-        const das_plan_node_t& x = nd[ti];
-        if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) neg.push_back(&nd[ti + 1]);
-        else if (x.op == DAS_PLAN_LINK) pos.push_back(&x);
-        else flat = false;
-      }
-      bool m = false;
-      TablePtr t;
-      if (flat && fused_and(c, pos, neg, no_overload, m, t)) {
-        out.matched = m;
-        if (m) out.rel.push(std::move(t));
-        return out;
-      }
-    }
     Rel acc;
     bool have = false;
     std::vector<Rel> forbidden;
     std::vector<uint32_t> anti;        // Not(Link) terms applied as anti index joins
+    uint32_t skip = 0;                 // positive terms the fused chain already folded into acc
+    {
+      // the leading Link terms of the And (and its Not(Link) filters): one
+      // fused launch while the running result stays small
+      std::vector<const das_plan_node_t*> pos, neg;
+      for (uint32_t ti : terms) {
+        const das_plan_node_t& x = nd[ti];
+        if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) neg.push_back(&nd[ti + 1]);
+        else pos.push_back(&x);
+      }
+      bool m = false;
+      TablePtr t;
+      const int r = fused_and(c, pos, neg, no_overload, m, t, &skip);
+      if (r == 1) {
+        out.matched = m;
+        if (m) out.rel.push(std::move(t));
+        return out;
+      }
+      if (r == 2) {
+        // the chain folded the first `skip` Link terms: continue from there
+        acc.push(std::move(t));
+        have = true;
+      } else {
+        skip = 0;
+      }
+    }
+    uint32_t seen = 0;                 // Link / other positive terms met so far
     for (uint32_t ti : terms) {
       const das_plan_node_t& x = nd[ti];
       if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) {
@@ -199,6 +208,7 @@ struct Exec {
         anti.push_back(ti + 1);
         continue;
       }
+      if (seen++ < skip) continue;
       if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
         // the term's rows looked up from the running result's keys; an empty
         // result takes the scan path, which tells a failing term (And ->

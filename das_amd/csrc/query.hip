@@ -1569,6 +1569,132 @@ __global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, u
   }
 }
 
+// Few probe rows are latency-bound (a key directory load, its offsets, then
+// an equal-range search per grounded target: ~16 dependent loads per probe,
+// one thread at a time).  With few probes a group of G lanes serves each
+// probe and searches G+1-ary: one round of G loads and a ballot narrows a
+// range G+1-fold, so a ~100-row range takes one round.
+// First index in [lo, hi) whose value is >= v (strict = false) or > v
+// (strict = true), hi if none, by the G lanes of a group (all with the same
+// arguments): a G+1-ary search, one round of G loads per step.
+template <int G>
+__device__ __forceinline__ void group_bounds(const uint32_t* __restrict__ col, uint32_t& lo, uint32_t& hi,
+                                             uint32_t v) {
+  const uint32_t gl = __lane_id() & (G - 1);
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << (__lane_id() & ~(uint32_t)(G - 1) & 63);
+  const int gbase = (int)(__lane_id() & ~(uint32_t)(G - 1));
+  // lower bound (>= v) over [a0, a1), upper bound (> v) over [b0, b1): lockstep
+  uint32_t a0 = lo, a1 = hi, b0 = lo, b1 = hi;
+  bool da = false, db = false;
+  while (!(da && db)) {
+    const uint32_t la = a1 - a0, lb = b1 - b0;
+    // sample positions: the range itself when it fits the group, else G
+    // evenly spaced interior points
+    const uint32_t pa = la <= G ? a0 + gl : a0 + (uint32_t)(((uint64_t)(gl + 1) * la) / (G + 1));
+    const uint32_t pb = lb <= G ? b0 + gl : b0 + (uint32_t)(((uint64_t)(gl + 1) * lb) / (G + 1));
+    const bool ina = !da && (la > G || gl < la), inb = !db && (lb > G || gl < lb);
+    const uint32_t xa = ina ? col[pa] : 0u, xb = inb ? col[pb] : 0u;
+    const uint32_t ca = (uint32_t)__popcll((__ballot(ina && xa < v) & gmask) >> gbase);
+    const uint32_t cb = (uint32_t)__popcll((__ballot(inb && xb <= v) & gmask) >> gbase);
+    if (!da) {
+      if (la <= G) {
+        a0 += ca;
+        da = true;
+      } else {
+        const uint32_t n0 = ca == 0 ? a0 : a0 + (uint32_t)(((uint64_t)ca * la) / (G + 1)) + 1;
+        const uint32_t n1 = ca == G ? a1 : a0 + (uint32_t)(((uint64_t)(ca + 1) * la) / (G + 1));
+        a0 = n0;
+        a1 = n1;
+        if (a0 >= a1) da = true;
+      }
+    }
+    if (!db) {
+      if (lb <= G) {
+        b0 += cb;
+        db = true;
+      } else {
+        const uint32_t n0 = cb == 0 ? b0 : b0 + (uint32_t)(((uint64_t)cb * lb) / (G + 1)) + 1;
+        const uint32_t n1 = cb == G ? b1 : b0 + (uint32_t)(((uint64_t)(cb + 1) * lb) / (G + 1));
+        b0 = n0;
+        b1 = n1;
+        if (b0 >= b1) db = true;
+      }
+    }
+  }
+  lo = a0;
+  hi = b0;
+}
+
+// ij_lookup by the G lanes of a group (same arguments, same result).
+template <int G>
+__device__ __forceinline__ uint2 ij_lookup_group(uint32_t t, const IjKeys& kx, const IjGround& g, uint64_t row) {
+  uint32_t b = 0, end = 0;
+  if (kx.fixed) {
+    b = kx.flo;
+    end = kx.fhi;
+  } else {
+    uint64_t lo;
+    bool hit;
+    if (kx.dir) {
+      const uint32_t d = t - kx.dlo;
+      const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
+      lo = j;
+      hit = j != 0xFFFFFFFFu;
+    } else {
+      const uint64_t k = kx.thi | t;
+      uint64_t l = 0, h = kx.nkeys;
+      while (l < h) {
+        const uint64_t mid = (l + h) >> 1;
+        if (kx.ukey[mid] < k) l = mid + 1; else h = mid;
+      }
+      lo = l;
+      hit = lo < kx.nkeys && kx.ukey[lo] == k;
+    }
+    if (hit) {
+      b = (uint32_t)kx.uoff[lo];
+      end = (uint32_t)kx.uoff[lo + 1];
+    }
+  }
+  for (int j = 0; j < g.n && b < end; ++j) {
+    const uint32_t v = g.src[j] ? g.src[j][row] : g.val[j];
+    group_bounds<G>(g.col[j], b, end, v);
+  }
+  return end > b ? make_uint2(b, end - b) : make_uint2(0u, 0u);
+}
+
+// Lookups of rows [0, nin) into s_lo / s_pre (x, y of ij_lookup), by groups
+// of G lanes (G = 1: one row per thread).
+template <int G>
+__device__ __forceinline__ void lookups_into(const uint32_t* key, const IjKeys& kx, const IjGround& g, uint32_t nin,
+                                             uint32_t* s_lo, uint32_t* s_pre) {
+  if (G == 1) {
+    for (uint32_t r = threadIdx.x; r < nin; r += kSmallBlock) {
+      const uint2 e = ij_lookup(key[r], kx, g, r);
+      s_lo[r] = e.x;
+      s_pre[r] = e.y;
+    }
+  } else {
+    const uint32_t groups = kSmallBlock / G, gid = threadIdx.x / G;
+    for (uint32_t r0 = 0; r0 < nin; r0 += groups) {      // uniform trip count: every lane of a group searches
+      const uint32_t r = r0 + gid;
+      const uint32_t rr = r < nin ? r : nin - 1;
+      const uint2 e = ij_lookup_group<G>(key[rr], kx, g, rr);
+      if (r < nin && (threadIdx.x & (G - 1)) == 0) {
+        s_lo[r] = e.x;
+        s_pre[r] = e.y;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void lookups_small(const uint32_t* key, const IjKeys& kx, const IjGround& g, uint32_t nin,
+                                              uint32_t* s_lo, uint32_t* s_pre) {
+  if (nin <= kSmallBlock / 64) lookups_into<64>(key, kx, g, nin, s_lo, s_pre);
+  else if (nin <= kSmallBlock / 16) lookups_into<16>(key, kx, g, nin, s_lo, s_pre);
+  else if (nin <= kSmallBlock / 4) lookups_into<4>(key, kx, g, nin, s_lo, s_pre);
+  else lookups_into<1>(key, kx, g, nin, s_lo, s_pre);
+}
+
 // Single-workgroup index join of a small probe table: lookups, a block scan
 // of the match counts, and -- when the total fits the output table the host
 // allocated speculatively (`cap` rows) -- the expansion, each thread taking
@@ -1585,11 +1711,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
   __shared__ uint32_t s_pre[kIjSmall + 1];
   __shared__ uint32_t s_lo[kIjSmall];
   __shared__ uint32_t s_w[W];
-  for (uint32_t r = threadIdx.x; r < n; r += kSmallBlock) {
-    const uint2 e = ij_lookup(key[r], kx, g, r);
-    s_lo[r] = e.x;
-    s_pre[r] = e.y;
-  }
+  lookups_small(key, kx, g, n, s_lo, s_pre);
   __syncthreads();
   // exclusive scan of s_pre[0..n): rows in rounds of 1024
   const int wave = threadIdx.x >> 6;
@@ -1937,11 +2059,16 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
 // the stages (compiled on the host from the same prepare steps as the
 // per-operator path: scan_prepare, ij_prepare, anti_prepare) are read from
 // pinned memory into LDS, each stage's row count stays in LDS, every
-// intermediate table is allocated up front at a speculative capacity.  The
-// chain gives up ("bail") when a result outgrows its table or an index join
-// comes out empty (And's reset-on-empty path, pattern_matcher.py:720-733):
-// the caller then evaluates the And operator by operator.  A scan term with
-// no rows makes the And fail (:712-713), as on the host path.
+// intermediate table is allocated up front at a speculative capacity.
+//
+// A stage that cannot run here -- its input is too large for the LDS
+// prefix, its output outgrows its table, or an index join comes out empty
+// (And's reset-on-empty path, pattern_matcher.py:720-733) -- ends the chain
+// at the last complete running result ("partial"): the caller continues the
+// And from the next term operator by operator.  A scan term with no rows
+// makes the And fail (:712-713), as on the host path.
+//
+// Lookups of few probe rows go through groups of lanes (lookups_small).
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kChainStages = 8;
@@ -1949,10 +2076,11 @@ constexpr uint32_t kChainCap = 32768;                 // rows per speculative ta
 constexpr uint64_t kChainJoinPairs = 1ull << 22;      // cross-join work bound (pairs)
 
 enum : uint32_t { CH_SCAN = 1, CH_IJ = 2, CH_JOIN = 3, CH_ANTI = 4 };
-enum : uint32_t { CHS_OK = 0, CHS_EMPTY_SCAN = 1, CHS_BAIL = 2 };
+enum : uint32_t { CHS_OK = 0, CHS_EMPTY_SCAN = 1, CHS_PARTIAL = 2 };
 
 struct ChainStage {
   uint32_t op, in, rel, cap;     // input stage (running result), scanned stage (JOIN), output capacity
+  uint32_t done;                 // the running result is complete after this stage
   uint32_t begin, end;           // SCAN: row range of the index table
   uint32_t* dst;                 // output table (ncols columns of `cap` rows)
   const uint32_t* key;           // IJ / ANTI: the probe key column
@@ -1999,17 +2127,20 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
   __shared__ uint32_t s_pre[kIjSmall + 1];
   __shared__ uint32_t s_lo[kIjSmall];
   __shared__ uint32_t s_w[W];
-  __shared__ uint32_t s_run, s_state;
+  __shared__ uint32_t s_run, s_state, s_acc;
   uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
   for (uint32_t i = threadIdx.x; i < nwords; i += kSmallBlock) dw[i] = hdesc[i];
-  if (threadIdx.x == 0) s_state = CHS_OK;
+  if (threadIdx.x == 0) {
+    s_state = CHS_OK;
+    s_acc = 0;
+  }
   __syncthreads();
-  uint32_t last = 0;
   for (uint32_t si = 0; si < d.nstage && s_state == CHS_OK; ++si) {
     const ChainStage& st = d.st[si];
     if (threadIdx.x == 0) s_run = 0;
     __syncthreads();
     uint32_t n = 0;
+    bool ok = true;                // uniform: the stage produced its full result
     if (st.op == CH_SCAN) {
       for (uint32_t r0 = st.begin; r0 < st.end; r0 += kSmallBlock) {
         const uint32_t r = r0 + threadIdx.x;
@@ -2022,13 +2153,9 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
     } else if (st.op == CH_IJ) {
       const uint32_t nin = s_cnt[st.in];
       if (nin > kIjSmall) {
-        if (threadIdx.x == 0) s_state = CHS_BAIL;
+        ok = false;
       } else {
-        for (uint32_t r = threadIdx.x; r < nin; r += kSmallBlock) {
-          const uint2 e = ij_lookup(st.key[r], st.kx, st.g, r);
-          s_lo[r] = e.x;
-          s_pre[r] = e.y;
-        }
+        lookups_small(st.key, st.kx, st.g, nin, s_lo, s_pre);
         __syncthreads();
         // exclusive scan of s_pre[0..nin) in rounds of 1024
         const int wave = threadIdx.x >> 6;
@@ -2053,7 +2180,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
         __syncthreads();
         n = carry;
         if (n == 0 || n > st.cap) {
-          if (threadIdx.x == 0) s_state = CHS_BAIL;
+          ok = false;
         } else {
           for (uint32_t o = threadIdx.x; o < n; o += kSmallBlock) {
             uint32_t l = 0, h = nin;                   // last row r with s_pre[r] <= o
@@ -2071,7 +2198,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
       const uint32_t na = s_cnt[st.in], nb = s_cnt[st.rel];
       const uint64_t pairs = (uint64_t)na * nb;
       if (pairs > kChainJoinPairs) {
-        if (threadIdx.x == 0) s_state = CHS_BAIL;
+        ok = false;
       } else {
         for (uint64_t k0 = 0; k0 < pairs; k0 += kSmallBlock) {
           const uint64_t k = k0 + threadIdx.x;
@@ -2085,21 +2212,36 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
           }
         }
         n = s_run;
-        if ((n == 0 || n > st.cap) && threadIdx.x == 0) s_state = CHS_BAIL;
+        if (n == 0 || n > st.cap) ok = false;
       }
     } else {   // CH_ANTI
       const uint32_t nin = s_cnt[st.in];
-      for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
-        const uint32_t r = r0 + threadIdx.x;
-        const bool keep = r < nin && ij_lookup(st.key[r], st.kx, st.g, r).y == 0;
-        const uint32_t pos = chain_rank(keep, s_w, &s_run);
-        if (keep)
-          for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+      if (nin <= kIjSmall) {
+        lookups_small(st.key, st.kx, st.g, nin, s_lo, s_pre);   // s_pre[r] = matches of row r's link (0 or 1)
+        __syncthreads();
+        for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
+          const uint32_t r = r0 + threadIdx.x;
+          const bool keep = r < nin && s_pre[r] == 0;
+          const uint32_t pos = chain_rank(keep, s_w, &s_run);
+          if (keep)
+            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+        }
+      } else {
+        for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
+          const uint32_t r = r0 + threadIdx.x;
+          const bool keep = r < nin && ij_lookup(st.key[r], st.kx, st.g, r).y == 0;
+          const uint32_t pos = chain_rank(keep, s_w, &s_run);
+          if (keep)
+            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+        }
       }
       n = s_run;
     }
-    if (threadIdx.x == 0) s_cnt[si] = n;
-    last = si;
+    if (threadIdx.x == 0) {
+      s_cnt[si] = n;
+      if (!ok) s_state = CHS_PARTIAL;
+      else if (st.done) s_acc = si;
+    }
     __syncthreads();
   }
   // every store of the chain is made visible before the host reads the
@@ -2108,8 +2250,8 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_store(&slot[0], s_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&slot[1], s_cnt[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&slot[2], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&slot[1], s_cnt[s_acc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&slot[2], s_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
     __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2119,34 +2261,40 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
 
 int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
-              std::unique_ptr<Table>& out) {
+              std::unique_ptr<Table>& out, uint32_t* consumed) {
   const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
   if ((f && f[0] == '0') || no_overload || terms.empty()) return 0;
   Index& idx = c.idx;
   ChainDesc d{};
   std::vector<std::unique_ptr<Table>> tabs;                  // one output table per stage
+  std::vector<uint32_t> terms_done;                           // positive terms folded after each stage
   auto add = [&](uint32_t op) -> ChainStage* {
     if (d.nstage >= (uint32_t)kChainStages) return nullptr;
     ChainStage& st = d.st[d.nstage++];
     st.op = op;
     return &st;
   };
+  // a chain ending early (too many stages) still folds the terms compiled so
+  // far; the caller continues from there
   int acc = -1;                                               // stage holding the running result
+  uint32_t nterm = 0;
+  bool all_terms = true;
   for (const das_plan_node_t* x : terms) {
-    if (x->op != DAS_PLAN_LINK || !x->scan.ordered || x->dedup) return 0;
+    if (x->op != DAS_PLAN_LINK || !x->scan.ordered || x->dedup) { all_terms = false; break; }
     if (acc >= 0 && x->index_join) {
       IjPlan pl;
       const Table& A = *tabs[acc];
       if (ij_prepare(c, A, x->ij, kIjSmall, pl)) {
-        if (pl.empty) return 0;
+        if (pl.empty) { all_terms = false; break; }
         ChainStage* st = add(CH_IJ);
-        if (!st) return 0;
+        if (!st) { all_terms = false; break; }
         auto t = new_table(c, DAS_TABLE_ORDERED, (int)pl.uni.size(), pl.uni.data(), kChainCap);
         for (size_t k = 0; k < pl.uni.size(); ++k) {
           t->lo[k] = pl.lo[k];
           t->hi[k] = pl.hi[k];
         }
         st->in = (uint32_t)acc;
+        st->done = 1;
         st->cap = (uint32_t)t->cap;
         st->dst = t->data;
         st->key = pl.akey;
@@ -2154,17 +2302,20 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
         st->g = pl.g;
         st->jc = pl.jc;
         tabs.push_back(std::move(t));
+        terms_done.push_back(++nterm);
         acc = (int)d.nstage - 1;
         continue;
       }
     }
     ScanPrep P;
     scan_prepare(c, x->scan, P);
-    if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) return 0;
+    if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) { all_terms = false; break; }
     const uint64_t b = P.ranges[0].first, e = P.ranges[0].second;
-    if (e - b > kSmallScan || e >= 0xFFFFFFFFull) return 0;
+    if (e - b > kSmallScan || e >= 0xFFFFFFFFull || d.nstage + (acc >= 0 ? 2 : 1) > (uint32_t)kChainStages) {
+      all_terms = false;
+      break;
+    }
     ChainStage* st = add(CH_SCAN);
-    if (!st) return 0;
     auto t = new_table(c, P.kind, P.ncols, P.vars, e - b);
     scan_bounds(idx, P.sp, x->scan.type_id, *t);
     st->sp = P.sp;
@@ -2172,12 +2323,15 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     st->end = (uint32_t)e;
     st->cap = (uint32_t)t->cap;
     st->dst = t->data;
+    st->done = acc < 0 ? 1 : 0;
     tabs.push_back(std::move(t));
     const int rel = (int)d.nstage - 1;
     if (acc < 0) {
+      terms_done.push_back(++nterm);
       acc = rel;
       continue;
     }
+    terms_done.push_back(nterm);
     // And's join of the running result with the scanned term (join(), the
     // natural join on the shared variables; a cross join when none)
     const Table& A = *tabs[acc];
@@ -2185,12 +2339,12 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     std::vector<int32_t> va(A.vars, A.vars + A.ncols), vb(R.vars, R.vars + R.ncols), shared, uni;
     std::set_intersection(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(shared));
     std::set_union(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(uni));
-    if ((int)uni.size() > kMaxCols) return 0;
+    DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
     ChainStage* js = add(CH_JOIN);
-    if (!js) return 0;
     auto jt = new_table(c, DAS_TABLE_ORDERED, (int)uni.size(), uni.data(), kChainCap);
     js->in = (uint32_t)acc;
     js->rel = (uint32_t)rel;
+    js->done = 1;
     js->cap = (uint32_t)jt->cap;
     js->dst = jt->data;
     for (int32_t v : shared) {
@@ -2208,31 +2362,46 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
       else { js->jc.b[js->jc.nb] = R.col(ib); js->jc.bo[js->jc.nb++] = k; }
     }
     tabs.push_back(std::move(jt));
+    terms_done.push_back(++nterm);
     acc = (int)d.nstage - 1;
   }
-  for (const das_plan_node_t* x : anti) {
-    AntiPlan ap;
-    const Table& A = *tabs[acc];
-    if (!anti_prepare(c, A, x->ij, ap) || ap.keep_all) continue;   // nothing forbidden / not a lookup: A whole
-    ChainStage* st = add(CH_ANTI);
-    if (!st) return 0;
-    auto t = new_table_like(c, A, A.cap);
-    for (int k = 0; k < A.ncols; ++k) {
-      t->lo[k] = A.lo[k];
-      t->hi[k] = A.hi[k];
+  if (acc < 0) return 0;
+  const uint32_t n_anti_stage0 = d.nstage;
+  bool anti_ok = all_terms;
+  if (all_terms)
+    for (const das_plan_node_t* x : anti) {
+      AntiPlan ap;
+      const Table& A = *tabs[acc];
+      if (!anti_prepare(c, A, x->ij, ap) || ap.keep_all) continue;   // nothing forbidden / not a lookup: A whole
+      ChainStage* st = add(CH_ANTI);
+      if (!st) {                                                     // the caller applies them all
+        d.nstage = n_anti_stage0;
+        tabs.resize(n_anti_stage0);
+        terms_done.resize(n_anti_stage0);
+        acc = (int)n_anti_stage0 - 1;
+        anti_ok = false;
+        break;
+      }
+      auto t = new_table_like(c, A, A.cap);
+      for (int k = 0; k < A.ncols; ++k) {
+        t->lo[k] = A.lo[k];
+        t->hi[k] = A.hi[k];
+      }
+      st->in = (uint32_t)acc;
+      st->done = 1;
+      st->cap = (uint32_t)t->cap;
+      st->dst = t->data;
+      st->key = ap.key;
+      st->kx = ap.kx;
+      st->g = ap.g;
+      st->ncopy = (uint32_t)A.ncols;
+      for (int k = 0; k < A.ncols; ++k) st->copy[k] = A.col(k);
+      tabs.push_back(std::move(t));
+      terms_done.push_back(nterm);
+      acc = (int)d.nstage - 1;
     }
-    st->in = (uint32_t)acc;
-    st->cap = (uint32_t)t->cap;
-    st->dst = t->data;
-    st->key = ap.key;
-    st->kx = ap.kx;
-    st->g = ap.g;
-    st->ncopy = (uint32_t)A.ncols;
-    for (int k = 0; k < A.ncols; ++k) st->copy[k] = A.col(k);
-    tabs.push_back(std::move(t));
-    acc = (int)d.nstage - 1;
-  }
   if (d.nstage < 2) return 0;                                 // one operator: nothing to fuse
+  const bool complete = all_terms && anti_ok;
   // only the stages in use travel (the kernel copies them into LDS)
   const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
   static_assert(sizeof(ChainStage) % 4 == 0 && offsetof(ChainDesc, st) % 4 == 0, "word copy");
@@ -2251,15 +2420,25 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   }
   uint32_t w[3] = {0, 0, 0};
   pub_wait(ps, c.s, w, 3);
-  if (w[0] == CHS_BAIL) return 0;
   matched = false;
   out.reset();
-  if (w[0] == CHS_EMPTY_SCAN || w[1] == 0) return 1;          // a failing term, or nothing left after Not
-  DAS_CHECK(w[2] == d.nstage - 1, DAS_E_INTERNAL, "fused chain stopped early");
-  tabs[acc]->nrows = w[1];
-  matched = true;
-  out = std::move(tabs[acc]);
-  return 1;
+  if (w[0] == CHS_EMPTY_SCAN) return 1;                       // a failing term: And is False
+  DAS_CHECK(w[2] < d.nstage && d.st[w[2]].done, DAS_E_INTERNAL, "fused chain: bad running result");
+  const uint32_t last = w[2];
+  if (w[0] == CHS_OK && last == d.nstage - 1 && complete) {
+    if (w[1] == 0) return 1;                                  // nothing left after the Not filters
+    tabs[last]->nrows = w[1];
+    matched = true;
+    out = std::move(tabs[last]);
+    return 1;
+  }
+  // partial: the running result after terms_done[last] positive terms, no
+  // Not filter applied yet (anti stages never stop a chain)
+  if (d.st[last].op == CH_ANTI) return 0;                     // cannot happen (anti stages never stop); be safe
+  tabs[last]->nrows = w[1];
+  out = std::move(tabs[last]);
+  *consumed = terms_done[last];
+  return 2;
 }
 
 // ---------------------------------------------------------------------------

@@ -149,6 +149,15 @@ class HipDB(RelationalDB):
         """handle -> (id, category, arity) through a host cache of the device
         index (handles are immutable once the index is built)."""
         miss = [h for h in dict.fromkeys(handles) if h not in self._handle_cache]
+        if miss and all(type(h) is str and len(h) == 32 for h in miss):
+            try:
+                ids, cat, ar = self.ctx.lookup_hex(miss)
+            except ValueError:          # not hex: the per-handle path below sorts it out
+                pass
+            else:
+                for h, i, c, a in zip(miss, ids, cat, ar):
+                    self._handle_cache[h] = (i, c, a)
+                miss = []
         if miss:
             good = []
             for h in miss:

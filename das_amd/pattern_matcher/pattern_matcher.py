@@ -20,6 +20,7 @@ CompositeAssignment algebra (:158-368: containment / coverage /
 compatibility checks, XOR set identity), das_amd/csrc/composite.hip.
 """
 import os
+import struct
 from abc import ABC, abstractmethod
 from collections import Counter
 from copy import deepcopy
@@ -358,6 +359,9 @@ class _Unsupported(Exception):
     pass
 
 
+_RECORD = struct.Struct("<51I")
+
+
 def _node_record(op, nchild=0, value=0, spec=None, ij=None):
     """One das_plan_node_t as 204 bytes (51 u32 words, include/das_mi355x.h)."""
     words = [op, nchild, value, 0, 0] + [0] * 46
@@ -368,7 +372,7 @@ def _node_record(op, nchild=0, value=0, spec=None, ij=None):
     if ij is not None:
         words[4] = 1
         words[28:51] = _scan_words(ij[0], ij[1], ij[2], ij[3], 0, True)
-    return np.array(words, dtype=np.int64).astype(np.uint32).tobytes()
+    return _RECORD.pack(*[w & 0xFFFFFFFF for w in words])
 
 
 def _scan_words(arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False, order_pos=-1):
