@@ -271,6 +271,10 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
 int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
               std::unique_ptr<Table>& out, uint32_t* consumed);
+// query.hip: an Or of ordered Links with one schema (no Not terms): the
+// scans and the union's dedup in one launch.  0: not taken; 1: evaluated.
+int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
+             std::unique_ptr<Table>& out);
 
 // export.hip: Redis key-space files (canonical_parser.py:119-183)
 struct ExportCounts {

@@ -263,6 +263,18 @@ struct Exec {
   Res eval_or(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
+    {
+      // an Or of Links of one schema: scans and union in one launch
+      std::vector<const das_plan_node_t*> links;
+      for (uint32_t ti : terms) links.push_back(&nd[ti]);
+      bool m = false;
+      TablePtr t;
+      if (fused_or(c, links, no_overload, m, t)) {
+        out.matched = m;
+        if (m) out.rel.push(std::move(t));
+        return out;
+      }
+    }
     Rel uni;
     bool any = false;
     std::vector<uint32_t> negated;

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <optional>
+#include <string>
 
 #include "das_internal.h"
 
@@ -1569,6 +1570,11 @@ __global__ void __launch_bounds__(B) k_ij_lc(const uint32_t* __restrict__ key, u
   }
 }
 
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {   // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+
 // Few probe rows are latency-bound (a key directory load, its offsets, then
 // an equal-range search per grounded target: ~16 dependent loads per probe,
 // one thread at a time).  With few probes a group of G lanes serves each
@@ -1581,7 +1587,7 @@ template <int G>
 __device__ __forceinline__ void group_bounds(const uint32_t* __restrict__ col, uint32_t& lo, uint32_t& hi,
                                              uint32_t v) {
   const uint32_t gl = __lane_id() & (G - 1);
-  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << (__lane_id() & ~(uint32_t)(G - 1) & 63);
+  const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << (G & 63)) - 1)) << (__lane_id() & ~(uint32_t)(G - 1) & 63);
   const int gbase = (int)(__lane_id() & ~(uint32_t)(G - 1));
   // lower bound (>= v) over [a0, a1), upper bound (> v) over [b0, b1): lockstep
   uint32_t a0 = lo, a1 = hi, b0 = lo, b1 = hi;
@@ -2075,12 +2081,16 @@ constexpr int kChainStages = 8;
 constexpr uint32_t kChainCap = 32768;                 // rows per speculative table
 constexpr uint64_t kChainJoinPairs = 1ull << 22;      // cross-join work bound (pairs)
 
-enum : uint32_t { CH_SCAN = 1, CH_IJ = 2, CH_JOIN = 3, CH_ANTI = 4 };
+enum : uint32_t { CH_SCAN = 1, CH_IJ = 2, CH_JOIN = 3, CH_ANTI = 4, CH_DEDUP = 5 };
+constexpr uint32_t kChainHash = 2 * kIjSmall;         // LDS hash slots of the dedup stage (power of two)
+constexpr uint32_t kChainNoStage = 0xFFFFFFFFu;
 enum : uint32_t { CHS_OK = 0, CHS_EMPTY_SCAN = 1, CHS_PARTIAL = 2 };
 
 struct ChainStage {
   uint32_t op, in, rel, cap;     // input stage (running result), scanned stage (JOIN), output capacity
   uint32_t done;                 // the running result is complete after this stage
+  uint32_t append;               // SCAN: append to this stage's table (Or's union), or kChainNoStage
+  uint32_t empty_ok;             // SCAN: no rows is not a failing term (Or)
   uint32_t begin, end;           // SCAN: row range of the index table
   uint32_t* dst;                 // output table (ncols columns of `cap` rows)
   const uint32_t* key;           // IJ / ANTI: the probe key column
@@ -2120,12 +2130,14 @@ __device__ __forceinline__ uint32_t chain_rank(bool keep, uint32_t* s_w, uint32_
 }
 
 __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restrict__ hdesc, uint32_t nwords,
-                                                       uint32_t* slot, uint32_t seq) {
+                                                       uint32_t* slot, uint32_t seq, uint64_t* tstamp) {
+  if (tstamp && threadIdx.x == 0) tstamp[0] = wall_clock64();
   constexpr int W = kSmallBlock / 64;
   __shared__ ChainDesc d;
   __shared__ uint32_t s_cnt[kChainStages];
-  __shared__ uint32_t s_pre[kIjSmall + 1];
-  __shared__ uint32_t s_lo[kIjSmall];
+  __shared__ uint32_t s_buf[kChainHash + 1];             // IJ prefix + ranges, or the dedup hash slots
+  uint32_t* s_pre = s_buf;
+  uint32_t* s_lo = s_buf + kIjSmall + 1;
   __shared__ uint32_t s_w[W];
   __shared__ uint32_t s_run, s_state, s_acc;
   uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
@@ -2135,6 +2147,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
     s_acc = 0;
   }
   __syncthreads();
+  if (tstamp && threadIdx.x == 0) tstamp[1] = wall_clock64();
   for (uint32_t si = 0; si < d.nstage && s_state == CHS_OK; ++si) {
     const ChainStage& st = d.st[si];
     if (threadIdx.x == 0) s_run = 0;
@@ -2142,6 +2155,9 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
     uint32_t n = 0;
     bool ok = true;                // uniform: the stage produced its full result
     if (st.op == CH_SCAN) {
+      const bool app = st.append != kChainNoStage;
+      if (app && threadIdx.x == 0) s_run = s_cnt[st.append];
+      __syncthreads();
       for (uint32_t r0 = st.begin; r0 < st.end; r0 += kSmallBlock) {
         const uint32_t r = r0 + threadIdx.x;
         const bool keep = r < st.end && scan_keep(st.sp, r);
@@ -2149,7 +2165,47 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
         if (keep) scan_emit(st.sp, r, st.dst, st.cap, pos);
       }
       n = s_run;
-      if (n == 0 && threadIdx.x == 0) s_state = CHS_EMPTY_SCAN;
+      if (app) {
+        if (threadIdx.x == 0) s_cnt[st.append] = n;
+        n = 0;
+      } else if (n == 0 && !st.empty_ok && threadIdx.x == 0) {
+        s_state = CHS_EMPTY_SCAN;
+      }
+    } else if (st.op == CH_DEDUP) {
+      // distinct rows of the input (Python set semantics of Or's union):
+      // an LDS open-addressing set of row indices, full-row equality
+      const uint32_t nin = s_cnt[st.in];
+      if (nin > kChainHash / 2) {
+        ok = false;
+      } else {
+        for (uint32_t i = threadIdx.x; i < kChainHash; i += kSmallBlock) s_buf[i] = 0u;
+        __syncthreads();
+        bool first[(kChainHash / 2 + kSmallBlock - 1) / kSmallBlock];
+        for (uint32_t k = 0, r = threadIdx.x; r < kChainHash / 2; ++k, r += kSmallBlock) {
+          first[k] = false;
+          if (r >= nin) continue;
+          uint32_t h = 0x9e3779b9u;
+          for (uint32_t c = 0; c < st.ncopy; ++c) h = mix32(h ^ (st.copy[c][r] + 0x7f4a7c15u * (c + 1)));
+          for (uint32_t probe = h & (kChainHash - 1);; probe = (probe + 1) & (kChainHash - 1)) {
+            const uint32_t cur = atomicCAS(&s_buf[probe], 0u, r + 1);
+            if (cur == 0u) {
+              first[k] = true;
+              break;
+            }
+            bool same = true;
+            for (uint32_t c = 0; c < st.ncopy && same; ++c) same = st.copy[c][cur - 1] == st.copy[c][r];
+            if (same) break;
+          }
+        }
+        for (uint32_t k = 0, r0 = 0; r0 < nin; ++k, r0 += kSmallBlock) {
+          const uint32_t r = r0 + threadIdx.x;
+          const bool keep = r < nin && first[k];
+          const uint32_t pos = chain_rank(keep, s_w, &s_run);
+          if (keep)
+            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+        }
+        n = s_run;
+      }
     } else if (st.op == CH_IJ) {
       const uint32_t nin = s_cnt[st.in];
       if (nin > kIjSmall) {
@@ -2241,6 +2297,7 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
       s_cnt[si] = n;
       if (!ok) s_state = CHS_PARTIAL;
       else if (st.done) s_acc = si;
+      if (tstamp) tstamp[2 + si] = wall_clock64();
     }
     __syncthreads();
   }
@@ -2272,6 +2329,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     if (d.nstage >= (uint32_t)kChainStages) return nullptr;
     ChainStage& st = d.st[d.nstage++];
     st.op = op;
+    st.append = kChainNoStage;
     return &st;
   };
   // a chain ending early (too many stages) still folds the terms compiled so
@@ -2405,8 +2463,12 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   // only the stages in use travel (the kernel copies them into LDS)
   const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
   static_assert(sizeof(ChainStage) % 4 == 0 && offsetof(ChainDesc, st) % 4 == 0, "word copy");
-  uint8_t* hd = pinned_stage(bytes);
+  // (DAS_TRACE: stage timestamps of the device clock after the descriptors)
+  const uint64_t tsoff = (bytes + 63) & ~63ull;
+  uint8_t* hd = pinned_stage(tsoff + 8 * (kChainStages + 2));
   std::memcpy(hd, &d, bytes);
+  uint64_t* ts = trace_on() ? reinterpret_cast<uint64_t*>(hd + tsoff) : nullptr;
+  if (ts) std::memset(ts, 0, 8 * (kChainStages + 2));
   // algorithmic bytes known up front: the scanned index rows
   double sbytes = 0;
   for (uint32_t i = 0; i < d.nstage; ++i)
@@ -2415,11 +2477,18 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   {
     ProfScope pf(c, "k_chain", sbytes);
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
-                       ps.seq);
+                       ps.seq, ts);
     DAS_HIP(hipGetLastError());
   }
   uint32_t w[3] = {0, 0, 0};
   pub_wait(ps, c.s, w, 3);
+  if (ts) {
+    static const char* const kOp[] = {"?", "scan", "ij", "join", "anti"};
+    trace_mark("chain copy", std::to_string((ts[1] - ts[0]) / 100.0) + " us");
+    for (uint32_t i = 0; i < d.nstage && ts[2 + i]; ++i)
+      trace_mark("chain stage", std::string(kOp[d.st[i].op < 5 ? d.st[i].op : 0]) + " " +
+                                    std::to_string((ts[2 + i] - (i ? ts[1 + i] : ts[1])) / 100.0) + " us");
+  }
   matched = false;
   out.reset();
   if (w[0] == CHS_EMPTY_SCAN) return 1;                       // a failing term: And is False
@@ -2439,6 +2508,86 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   out = std::move(tabs[last]);
   *consumed = terms_done[last];
   return 2;
+}
+
+int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
+             std::unique_ptr<Table>& out) {
+  const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
+  if ((f && f[0] == '0') || no_overload || terms.size() < 2 || terms.size() + 1 > (size_t)kChainStages) return 0;
+  Index& idx = c.idx;
+  std::vector<ScanPrep> preps(terms.size());
+  uint64_t total = 0;
+  for (size_t i = 0; i < terms.size(); ++i) {
+    const das_plan_node_t* x = terms[i];
+    if (x->op != DAS_PLAN_LINK || !x->scan.ordered) return 0;
+    ScanPrep& P = preps[i];
+    scan_prepare(c, x->scan, P);
+    if (P.kind != DAS_TABLE_ORDERED) return 0;
+    if (i && (P.ncols != preps[0].ncols || !std::equal(P.vars, P.vars + P.ncols, preps[0].vars))) return 0;
+    if (P.empty) continue;
+    if (P.ranges.size() != 1) return 0;
+    total += P.ranges[0].second - P.ranges[0].first;
+  }
+  if (total > kChainHash / 2 || total == 0) return 0;
+  ChainDesc d{};
+  auto cat = new_table(c, DAS_TABLE_ORDERED, preps[0].ncols, preps[0].vars, total);
+  auto res = new_table(c, DAS_TABLE_ORDERED, preps[0].ncols, preps[0].vars, total);
+  // column bounds: the union of the terms' bounds
+  for (int k = 0; k < res->ncols; ++k) {
+    res->lo[k] = kNone;
+    res->hi[k] = 0;
+  }
+  bool any = false;
+  for (size_t i = 0; i < terms.size(); ++i) {
+    ScanPrep& P = preps[i];
+    if (P.empty) continue;
+    Table tb;
+    tb.ncols = P.ncols;
+    scan_bounds(idx, P.sp, terms[i]->scan.type_id, tb);
+    for (int k = 0; k < res->ncols; ++k) {
+      res->lo[k] = std::min(res->lo[k], tb.lo[k]);
+      res->hi[k] = std::max(res->hi[k], tb.hi[k]);
+    }
+    ChainStage& st = d.st[d.nstage++];
+    st.op = CH_SCAN;
+    st.sp = P.sp;
+    st.begin = (uint32_t)P.ranges[0].first;
+    st.end = (uint32_t)P.ranges[0].second;
+    st.cap = (uint32_t)cat->cap;
+    st.dst = cat->data;
+    st.empty_ok = 1;
+    st.append = any ? 0u : kChainNoStage;
+    st.done = any ? 0u : 1u;
+    any = true;
+  }
+  ChainStage& dd = d.st[d.nstage++];
+  dd.op = CH_DEDUP;
+  dd.in = 0;
+  dd.done = 1;
+  dd.cap = (uint32_t)res->cap;
+  dd.dst = res->data;
+  dd.ncopy = (uint32_t)cat->ncols;
+  for (int k = 0; k < cat->ncols; ++k) dd.copy[k] = cat->col(k);
+  const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
+  uint8_t* hd = pinned_stage(bytes);
+  std::memcpy(hd, &d, bytes);
+  const PubSlot ps = pub_reserve();
+  {
+    ProfScope pf(c, "k_chain", 4.0 * total * (terms[0]->scan.arity + 1));
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
+                       ps.seq, (uint64_t*)nullptr);
+    DAS_HIP(hipGetLastError());
+  }
+  uint32_t w[3] = {0, 0, 0};
+  pub_wait(ps, c.s, w, 3);
+  DAS_CHECK(w[0] == CHS_OK && w[2] == d.nstage - 1, DAS_E_INTERNAL, "fused union: incomplete");
+  matched = w[1] > 0;
+  out.reset();
+  if (matched) {
+    res->nrows = w[1];
+    out = std::move(res);
+  }
+  return 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -2707,10 +2856,6 @@ std::unique_ptr<Table> dedup(Ctx& c, const Table& A) {
 // Exchange helpers (multi-GPU): destination by key hash, row-major staging
 // ---------------------------------------------------------------------------
 namespace {
-__device__ __forceinline__ uint32_t mix32(uint32_t h) {   // murmur3 finaliser
-  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
-  return h;
-}
 __global__ void k_dest(ColSet key, uint64_t n, uint32_t nparts, uint32_t* dest) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t h = 0x9e3779b9u;
