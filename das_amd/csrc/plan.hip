@@ -286,11 +286,11 @@ struct Exec {
       Res s = eval(ti);
       if (!s.matched) continue;
       any = true;
-      if (s.rel.nonempty()) {
-        for (auto& t : s.rel.t) uni.t.push_back(std::move(t));
-        uni = normalize(std::move(uni));
-      }
+      // (the union is normalised once at the end: the same set as after
+      // every term, one dedup per schema instead of one per term)
+      for (auto& t : s.rel.t) uni.push(std::move(t));
     }
+    uni = normalize(std::move(uni));
     if (!negated.empty()) {
       Res sub = eval_and(negated);
       out.rel = minus_rel(std::move(sub.rel), uni);

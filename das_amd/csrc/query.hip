@@ -141,6 +141,64 @@ __global__ void __launch_bounds__(B) k_scan_write(ScanSpec sp, uint64_t begin, u
   }
 }
 
+// Several scans with one output schema in one pass (Or's union of Link
+// terms): segment s = (spec, row range), its chunks numbered from chunk0;
+// block b scans chunk b of the segment that holds it.  Specs by value.
+constexpr int kMultiSeg = 6;
+struct MultiScan {
+  uint32_t nseg;
+  struct Seg {
+    ScanSpec sp;
+    uint64_t begin, end, chunk0;
+  } seg[kMultiSeg];
+};
+
+__device__ __forceinline__ const MultiScan::Seg& seg_of(const MultiScan& ms, uint32_t b) {
+  uint32_t s = 0;
+  while (s + 1 < ms.nseg && ms.seg[s + 1].chunk0 <= b) ++s;
+  return ms.seg[s];
+}
+
+__global__ void __launch_bounds__(B) k_scan_count_multi(MultiScan ms, uint32_t* chunk_cnt) {
+  __shared__ uint32_t s_w[B / 64];
+  const MultiScan::Seg& sg = seg_of(ms, blockIdx.x);
+  const uint64_t cb = sg.begin + (uint64_t)(blockIdx.x - sg.chunk0) * kChunk;
+  uint32_t cnt = 0;
+  for (int it = 0; it < kChunkIters; ++it) {
+    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
+    if (r < sg.end && scan_keep(sg.sp, r)) ++cnt;
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (__lane_id() == 0) s_w[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ void __launch_bounds__(B) k_scan_write_multi(MultiScan ms, const uint32_t* chunk_off, uint32_t* out,
+                                                        uint64_t cap) {
+  __shared__ uint32_t s_w[B / 64];
+  __shared__ uint32_t s_run;
+  const MultiScan::Seg& sg = seg_of(ms, blockIdx.x);
+  const uint64_t cb = sg.begin + (uint64_t)(blockIdx.x - sg.chunk0) * kChunk;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t lt = __lanemask_lt();
+  if (threadIdx.x == 0) s_run = chunk_off[blockIdx.x];
+  __syncthreads();
+  for (int it = 0; it < kChunkIters; ++it) {
+    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
+    const bool keep = r < sg.end && scan_keep(sg.sp, r);
+    const uint64_t m = __ballot(keep);
+    if (__lane_id() == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t pos = s_run + __popcll(m & lt);
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+    if (keep) scan_emit(sg.sp, r, out, cap, pos);
+    __syncthreads();
+    if (threadIdx.x == 0) s_run += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+}
+
 // Single-workgroup scan of a small range (an anchored key range): count,
 // compaction and column writes in one launch, the row count published
 // straight into the pinned read-back slot (one launch + one round trip where
@@ -2528,7 +2586,68 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
     if (P.ranges.size() != 1) return 0;
     total += P.ranges[0].second - P.ranges[0].first;
   }
-  if (total > kChainHash / 2 || total == 0) return 0;
+  if (total == 0) return 0;
+  bool single = true;
+  for (auto& P : preps) single = single && (P.empty || P.ranges.size() == 1);
+  const char* fm = std::getenv("DAS_UNION_MULTI");            // tests: 1 = always the multi-launch form
+  if (total > kChainHash / 2 || !single || (fm && fm[0] == '1')) {
+    // larger: every range of every term counted in one launch, written in
+    // one, then one dedup of the concatenation
+    MultiScan ms{};
+    uint64_t chunks = 0;
+    for (auto& P : preps) {
+      if (P.empty) continue;
+      for (auto& r : P.ranges) {
+        if (r.second <= r.first) continue;
+        if (ms.nseg == (uint32_t)kMultiSeg) return 0;
+        MultiScan::Seg& sg = ms.seg[ms.nseg++];
+        sg.sp = P.sp;
+        sg.begin = r.first;
+        sg.end = r.second;
+        sg.chunk0 = chunks;
+        chunks += (r.second - r.first + kChunk - 1) / kChunk;
+      }
+    }
+    if (!ms.nseg || chunks >= (1ull << 31)) return 0;
+    uint64_t scanned = 0;
+    for (uint32_t i = 0; i < ms.nseg; ++i) scanned += ms.seg[i].end - ms.seg[i].begin;
+    DBuf<uint32_t> cnt(chunks, c.s), off(chunks + 1, c.s);
+    {
+      ProfScope pf(c, "k_scan_count_multi", 4.0 * scanned * terms[0]->scan.arity);
+      hipLaunchKernelGGL(k_scan_count_multi, dim3((unsigned)chunks), dim3(B), 0, c.s, ms, cnt.p);
+      DAS_HIP(hipGetLastError());
+    }
+    const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{cnt.p}, chunks, off.p, c.s);
+    matched = false;
+    out.reset();
+    if (!m) return 1;
+    auto cat = new_table(c, DAS_TABLE_ORDERED, preps[0].ncols, preps[0].vars, m);
+    cat->nrows = m;
+    {
+      ProfScope pf(c, "k_scan_write_multi", 4.0 * scanned * (terms[0]->scan.arity + 1) + 4.0 * m * cat->ncols);
+      hipLaunchKernelGGL(k_scan_write_multi, dim3((unsigned)chunks), dim3(B), 0, c.s, ms, (const uint32_t*)off.p,
+                         cat->data, cat->cap);
+      DAS_HIP(hipGetLastError());
+    }
+    for (int k = 0; k < cat->ncols; ++k) {
+      cat->lo[k] = kNone;
+      cat->hi[k] = 0;
+    }
+    for (size_t i = 0; i < terms.size(); ++i) {
+      if (preps[i].empty) continue;
+      Table tb;
+      tb.ncols = preps[i].ncols;
+      scan_bounds(idx, preps[i].sp, terms[i]->scan.type_id, tb);
+      for (int k = 0; k < cat->ncols; ++k) {
+        cat->lo[k] = std::min(cat->lo[k], tb.lo[k]);
+        cat->hi[k] = std::max(cat->hi[k], tb.hi[k]);
+      }
+    }
+    out = dedup(c, *cat);
+    matched = out->nrows > 0;
+    if (!matched) out.reset();
+    return 1;
+  }
   ChainDesc d{};
   auto cat = new_table(c, DAS_TABLE_ORDERED, preps[0].ncols, preps[0].vars, total);
   auto res = new_table(c, DAS_TABLE_ORDERED, preps[0].ncols, preps[0].vars, total);

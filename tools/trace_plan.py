@@ -29,7 +29,9 @@ def main():
     db = HipDB(device=0)
     db.load_arrays(arrays)
     torch.cuda.synchronize()
-    warm, fresh = 7, 7 + 7919 * 3
+    warm = 7
+    # a fresh anchor with several DO terms (F9's Or has one term per term)
+    fresh = next(g for g in range(7 + 7919 * 3, args.genes, 7919) if len(synthetic.flybase_do_terms(arrays, g)) >= 3)
     for gene, tag in ((warm, "warm-up"), (warm, "warm"), (fresh, "fresh anchor")):
         for name, spec in bench.flybase_specs(gene, synthetic.flybase_do_terms(arrays, gene)):
             q = bench.build_expr(pm, spec)
