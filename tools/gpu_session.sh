@@ -1,6 +1,18 @@
+#!/bin/bash
+# One GPU session (run through gpurun from the repo root): the GPU parity
+# suite, then the bench + rocprof + PMC passes of the workloads named in
+# WORKLOADS (default: bio).  Steps are chained with &&, each under its own
+# time limit, so a failure ends the session.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread --durations=10 > gpurun_out/tests.txt 2>&1 &&
-timeout -k 10 400 python tools/plan_ab.py > gpurun_out/plan_ab.json 2> gpurun_out/plan_ab.err &&
-timeout -k 10 300 python bench.py --workload flybase --steps 20 --warmup 3 --no-cpu-baseline --no-materialise > gpurun_out/fb.json 2> gpurun_out/fb.err &&
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-materialise > gpurun_out/bio.json 2> gpurun_out/bio.err
+export TMPDIR=/tmp
+run_tests() {
+    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 150 \
+        --timeout-method thread --durations=15 > gpurun_out/tests.txt 2>&1
+}
+run_profiles() {
+    for w in ${WORKLOADS:-bio}; do
+        WORKLOAD=$w bash tools/profile_bench.sh || return 1
+    done
+}
+if [ "${SKIP_TESTS:-0}" = "1" ]; then run_profiles; else run_tests && run_profiles; fi
