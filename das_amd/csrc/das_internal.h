@@ -231,6 +231,9 @@ void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_s
 std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q);
 std::unique_ptr<Table> scan_template(Ctx& c, const das_template_scan_t& q);
 std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
+// rows of p whose value of the one shared variable lies in EVERY qs[i]'s key
+// set (each qs[i] one column, distinct keys); nullptr when not applicable
+std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& p, const std::vector<const Table*>& qs);
 std::unique_ptr<Table> index_join(Ctx& c, const Table& a, const das_link_scan_t& q);   // nullptr: not applicable
 // rows of a whose link (q's grounded targets + a's values of q's variables)
 // does not exist; nullptr when a does not bind every variable position

@@ -165,6 +165,39 @@ struct Exec {
     }
   }
 
+  // The variable of a Link term with exactly one variable position and every
+  // other target grounded (its scan is one column of distinct keys), or -1.
+  int32_t one_var(uint32_t ti) const {
+    const das_plan_node_t& x = nd[ti];
+    if (x.op != DAS_PLAN_LINK || !x.scan.ordered || x.scan.emit_link || x.scan.type_id == kNone) return -1;
+    int32_t v = -1;
+    for (uint32_t p = 0; p < x.scan.arity && p < 8; ++p) {
+      if (x.scan.target[p] != kNone) continue;
+      if (x.scan.var[p] < 0 || v >= 0) return -1;
+      v = x.scan.var[p];
+    }
+    return v;
+  }
+
+  // End (exclusive) of the run of terms from k that semi_join_multi can fold
+  // at once: Link terms with one variable, the same one, bound by the running
+  // result's single table of more than 2^20 rows (smaller results take the
+  // index join term by term).  DAS_SEMI_MULTI=1 drops the size floor, 0
+  // disables the run (tests).
+  size_t semi_run(const std::vector<uint32_t>& terms, size_t k, const Rel& acc) const {
+    const char* f = std::getenv("DAS_SEMI_MULTI");
+    if ((f && f[0] == '0') || acc.t.size() != 1) return k;
+    const Table& a = *acc.t[0];
+    if (a.kind != DAS_TABLE_ORDERED || (!(f && f[0] == '1') && a.nrows <= (1ull << 20))) return k;
+    const int32_t v = one_var(terms[k]);
+    bool bound = false;
+    for (int i = 0; i < a.ncols; ++i) bound |= a.vars[i] == v;
+    if (v < 0 || !bound) return k;
+    size_t e = k + 1;
+    while (e < terms.size() && one_var(terms[e]) == v) ++e;
+    return e;
+  }
+
   Res eval_and(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
@@ -199,7 +232,8 @@ struct Exec {
       }
     }
     uint32_t seen = 0;                 // Link / other positive terms met so far
-    for (uint32_t ti : terms) {
+    for (size_t k = 0; k < terms.size(); ++k) {
+      const uint32_t ti = terms[k];
       const das_plan_node_t& x = nd[ti];
       if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) {
         // Not.matched is always True and its rows only ever filter the final
@@ -209,6 +243,35 @@ struct Exec {
         continue;
       }
       if (seen++ < skip) continue;
+      if (have && acc.nonempty()) {
+        const size_t e = semi_run(terms, k, acc);
+        if (e >= k + 2) {
+          // consecutive one-variable terms on one variable of a large running
+          // result: each term scanned (a failing term fails the And,
+          // :712-713), then ONE filter by the intersection of their key sets
+          std::vector<Rel> rs;
+          for (size_t j = k; j < e; ++j) {
+            Res s = eval(terms[j]);
+            if (!s.matched) return Res{};
+            rs.push_back(std::move(s.rel));
+          }
+          std::vector<const Table*> qs;
+          for (auto& r : rs) qs.push_back(r.t[0].get());
+          TablePtr f = semi_join_multi(c, *acc.t[0], qs);
+          if (f && f->nrows) {
+            // non-empty: every prefix of the term-by-term fold is non-empty
+            // too (the fold's rows project onto each prefix), so no
+            // reset-on-empty step was skipped and the rows are the same
+            acc = Rel{};
+            acc.push(std::move(f));
+          } else {
+            for (auto& r : rs) acc = acc.nonempty() ? join_rel(acc, r) : std::move(r);
+          }
+          seen += (uint32_t)(e - k - 1);
+          k = e - 1;
+          continue;
+        }
+      }
       if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
         // the term's rows looked up from the running result's keys; an empty
         // result takes the scan path, which tells a failing term (And ->

@@ -2769,6 +2769,72 @@ std::unique_ptr<Table> semi_join(Ctx& c, const Table& P, const Table& Q) {
                       "k_tile_count<BitsPred>", 4.0);
 }
 
+// Several one-variable build sides on the same variable (consecutive terms of
+// an And, e.g. T2(V2, h1), T3(V2, h0) of the hub query): their key sets are
+// intersected as bitmaps first -- one set pass per term into its own bitmap
+// (duplicates detected as in semi_join), one AND per extra term -- and P is
+// filtered ONCE by the intersection, instead of one probe + compaction pass
+// per term.  The bitmap spans the intersection of the columns' id bounds: a
+// key outside it is in no intersection.  nullptr when a side does not fit
+// (the caller joins term by term); the plan executor checks that the result
+// is non-empty before taking it (And's reset-on-empty rule).
+__global__ void k_bits_and(uint32_t* __restrict__ acc, const uint32_t* __restrict__ b, uint64_t words) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
+    acc[i] &= b[i];
+}
+
+std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector<const Table*>& Qs) {
+  if (Qs.empty() || P.kind != DAS_TABLE_ORDERED || !P.nrows) return nullptr;
+  const int32_t var = Qs[0]->vars[0];
+  int pk = -1;
+  for (int i = 0; i < P.ncols; ++i) if (P.vars[i] == var) pk = i;
+  if (pk < 0) return nullptr;
+  uint64_t lo = 0, hi = c.idx.n_atoms ? c.idx.n_atoms - 1 : 0;
+  auto clip = [&](uint32_t l, uint32_t h) {
+    if (h == kNone || l > h) return;                       // unknown bound
+    lo = std::max<uint64_t>(lo, l);
+    hi = std::min<uint64_t>(hi, h);
+  };
+  clip(P.lo[pk], P.hi[pk]);
+  for (const Table* Q : Qs) {
+    if (Q->kind != DAS_TABLE_ORDERED || Q->ncols != 1 || Q->vars[0] != var || Q->nrows >= 0xFFFFFFFFull) return nullptr;
+    clip(Q->lo[0], Q->hi[0]);
+  }
+  if (lo > hi) return new_table_like(c, P, 0);              // disjoint bounds: nothing passes
+  const uint64_t range = hi - lo + 1;
+  if (range > (1ull << 31)) return nullptr;
+  const uint64_t words = (range + 31) / 32;
+  DBuf<uint32_t> acc(words + 1, c.s), one(words + 1, c.s);  // + the duplicate flag
+  for (size_t i = 0; i < Qs.size(); ++i) {
+    uint32_t* bits = i == 0 ? acc.p : one.p;
+    fill_dev(bits, 0, 4 * (words + 1), c.s);
+    {
+      ProfScope ps(c, "join_build", 4.0 * Qs[i]->nrows + 4.0 * words);
+      hipLaunchKernelGGL(k_bits_set, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0), Qs[i]->nrows,
+                         (uint32_t)lo, (uint32_t)range, bits, bits + words);
+      DAS_HIP(hipGetLastError());
+    }
+    if (read_u32(bits + words, c.s)) return nullptr;        // duplicate keys: counts matter
+    if (i) {
+      KScope ks("k_bits_and", 12.0 * words);
+      hipLaunchKernelGGL(k_bits_and, G(words), dim3(B), 0, c.s, acc.p, (const uint32_t*)one.p, words);
+      DAS_HIP(hipGetLastError());
+    }
+  }
+  one.release();
+  auto out = compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), (uint32_t)lo, (uint32_t)range,
+                                         (const uint32_t*)acc.p},
+                          "k_tile_count<BitsPred>", 4.0);
+  out->sorted_col = P.sorted_col;
+  for (int k = 0; k < out->ncols; ++k) {
+    out->lo[k] = P.lo[k];
+    out->hi[k] = P.hi[k];
+  }
+  out->lo[pk] = (uint32_t)lo;
+  out->hi[pk] = (uint32_t)hi;
+  return out;
+}
+
 std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_overload) {
   if (A.kind != DAS_TABLE_ORDERED || Bt.kind != DAS_TABLE_ORDERED) return theta_join(c, A, Bt, no_overload);
   // schemas

@@ -465,6 +465,43 @@ def test_gpu_hub_four_clause_matches_oracle(semi, monkeypatch):
         assert same(got, want), (name, got.get("n"), want.get("n"))
 
 
+@pytest.mark.parametrize("multi", ["1", "0"])
+def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
+    """Runs of one-variable hub clauses on one variable (T2(V2,a), T3(V2,b),
+    ...) folded by ONE filter with the intersection of their key sets
+    (semi_join_multi, forced below its size floor with DAS_SEMI_MULTI=1)
+    against the term-by-term fold (0).  Random anchors make some
+    intersections empty: then the plan executor folds term by term, which
+    keeps And's reset-on-empty rule (pattern_matcher.py:725-729) -- a
+    running result emptied by T2 is replaced by T3's rows."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_SEMI_MULTI", multi)
+    arrays = synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    n = lambda i: ["Node", "Concept", f"n{i}"]  # noqa: E731
+    V, L = bench._V, bench._L
+    rng = np.random.default_rng(33)
+    specs = [q for _, q in bench.hub_specs()]
+    specs.append(["And", [L("T0", V("V1"), n(0)), L("T1", V("V1"), V("V2")), L("T2", V("V2"), n(1)),
+                          L("T3", V("V2"), n(0)), L("T0", V("V2"), n(2))]])
+    for _ in range(24):
+        a, b, c = (int(x) for x in rng.integers(0, 200, 3))
+        t = [f"T{int(x)}" for x in rng.integers(0, 4, 4)]
+        run = [L(t[1], V("V2"), n(a)), L(t[2], V("V2"), n(b))]
+        if rng.random() < 0.4:
+            run.append(L(t[3], n(c), V("V2")))
+        specs.append(["And", [L(t[0], V("V1"), n(int(rng.integers(0, 4)))), L("T1", V("V1"), V("V2"))] + run])
+    nonempty = 0
+    for q in specs:
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
+        nonempty += want.get("n", 0) > 0
+    assert nonempty >= 4
+
+
 def test_gpu_native_canonical_load_matches_oracle():
     """Canonical text -> native reader (canonical.cpp) -> device index: the
     queries answer as the oracle over the Python reader's atoms; nested
