@@ -533,6 +533,70 @@ __global__ void k_gather_rows(const uint32_t* ids, uint64_t R, uint64_t ld, uint
   }
 }
 
+// P_{a,p} of one named type's segment [b, b + n) of T_a (rows sorted by
+// (type, id)): the rows ordered by (t_p, the other targets in position
+// order, id) through ONE stable sort of a packed key -- each field is the
+// target minus the segment's column minimum (tbound), in bits_for(max - min)
+// bits, t_p most significant -- with the link id (or the T row) as payload.
+// The P table's columns then come back out of the key by a streaming unpack
+// instead of gathers through a permutation into tgt_off / tgt.
+struct PackKey {
+  uint32_t n;                  // fields in the key
+  uint32_t pos[3];             // target position of field k (k = 0 most significant)
+  uint32_t lo[3];              // segment minimum of that column
+  uint32_t sh[3];              // bit offset of field k in the key
+  uint32_t bits[3];
+};
+
+// key of T row b + (rsel ? rsel[i] : i); val = the row's link id (rsel null) or keeps rsel
+__global__ void k_pack_key(const uint32_t* __restrict__ T, uint64_t ld, uint64_t b, uint64_t n, PackKey f,
+                           const uint32_t* __restrict__ rsel, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = b + (rsel ? rsel[i] : i);
+    uint64_t k = 0;
+    for (uint32_t j = 0; j < f.n; ++j) k |= (uint64_t)(T[(uint64_t)(1 + f.pos[j]) * ld + r] - f.lo[j]) << f.sh[j];
+    key[i] = k;
+    if (!rsel) val[i] = T[r];
+  }
+}
+
+// stage 1 of a key wider than 64 bits (arity 3): the least significant
+// target alone, payload = the row inside the segment
+__global__ void k_pack_key32(const uint32_t* __restrict__ col, uint64_t b, uint64_t n, uint32_t lo,
+                             uint32_t* __restrict__ key, uint32_t* __restrict__ row) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    key[i] = col[b + i] - lo;
+    row[i] = (uint32_t)i;
+  }
+}
+
+// sorted (key, val) -> P rows [ob, ob + n): id, the key's targets, and the
+// target left out of the key (pos_rest, read at T row b + val; val is then a
+// row, else the link id); pk = type << 32 | t_p for the key directory
+__global__ void k_unpack_key(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n,
+                             PackKey f, int32_t pos_rest, const uint32_t* __restrict__ T, uint64_t tld, uint64_t b,
+                             uint32_t ty, uint32_t* __restrict__ out, uint64_t ld, uint64_t ob,
+                             uint64_t* __restrict__ pk) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key[i];
+    const uint32_t v = val[i];
+    uint32_t tp = 0;
+    for (uint32_t j = 0; j < f.n; ++j) {
+      const uint32_t t = (uint32_t)((k >> f.sh[j]) & ((1ull << f.bits[j]) - 1)) + f.lo[j];
+      out[(uint64_t)(1 + f.pos[j]) * ld + ob + i] = t;
+      if (j == 0) tp = t;
+    }
+    if (pos_rest >= 0) {
+      const uint64_t r = b + v;
+      out[ob + i] = T[r];
+      out[(uint64_t)(1 + pos_rest) * ld + ob + i] = T[(uint64_t)(1 + pos_rest) * tld + r];
+    } else {
+      out[ob + i] = v;
+    }
+    pk[ob + i] = ((uint64_t)ty << 32) | tp;
+  }
+}
+
 template <typename K>
 __global__ void k_run_flags(const K* key, uint64_t n, uint32_t* f) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -1185,7 +1249,86 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
       for (uint64_t r = 0; r < m; ++r) idx.ctype_range[hk[r]] = CtypeRange{ar, ho[r], ho[r + 1]};
     }
     // P_{a,p}
-    if (ar <= (uint32_t)kMaxPosArity) {
+    const bool packed = !(std::getenv("DAS_PIDX_PERM") && std::getenv("DAS_PIDX_PERM")[0] == '1') &&
+                        idx.type_off[ar].size() == a.n_types + 1 && idx.type_off[ar][a.n_types] == R;
+    if (ar <= (uint32_t)kMaxPosArity && packed) {
+      const RowTable& T = idx.ttab[ar];
+      const auto& to = idx.type_off[ar];
+      const auto& tb = idx.tbound[ar];
+      const uint32_t ncol = ar + 1;
+      for (uint32_t p = 0; p < ar; ++p) {
+        PosIndex& P = idx.pidx[ar][p];
+        P.t.arity = (int)ar;
+        P.t.rows = R;
+        P.t.ld = col_stride(R);
+        P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * P.t.ld);
+        DBuf<uint64_t> pk(R, s);
+        for (uint32_t ty = 0; ty < a.n_types; ++ty) {
+          const uint64_t b = to[ty], n = to[ty + 1] - to[ty];
+          if (!n) continue;
+          // fields: t_p, then the other positions in order
+          uint32_t pos[3], nf = 0;
+          pos[nf++] = p;
+          for (uint32_t q = 0; q < ar; ++q)
+            if (q != p) pos[nf++] = q;
+          uint32_t lo[3], bits[3], total = 0;
+          for (uint32_t j = 0; j < nf; ++j) {
+            lo[j] = tb[((uint64_t)ty * ncol + 1 + pos[j]) * 2];
+            bits[j] = (uint32_t)bits_for(tb[((uint64_t)ty * ncol + 1 + pos[j]) * 2 + 1] - lo[j]);
+            total += bits[j];
+          }
+          // a key wider than 64 bits (arity 3): the last field is sorted
+          // first on its own (LSD), the rest carry the segment row
+          const bool force_two = std::getenv("DAS_PIDX_TWO") && std::getenv("DAS_PIDX_TWO")[0] == '1';
+          const bool two = total > 64 || (nf == 3 && force_two);      // (tests: DAS_PIDX_TWO=1)
+          PackKey f{};
+          f.n = two ? nf - 1 : nf;
+          uint32_t sh = 0;
+          for (int j = (int)f.n - 1; j >= 0; --j) {
+            f.pos[j] = pos[j];
+            f.lo[j] = lo[j];
+            f.bits[j] = bits[j];
+            f.sh[j] = sh;
+            sh += bits[j];
+          }
+          DBuf<uint64_t> key(n, s);
+          DBuf<uint32_t> val(n, s);
+          if (two) {
+            DBuf<uint32_t> k32(n, s);
+            {
+              KScope ks("k_pack_key32", 12.0 * n);
+              hipLaunchKernelGGL(k_pack_key32, G(n), dim3(B), 0, s, (const uint32_t*)T.col(1 + pos[nf - 1]), b, n,
+                                 lo[nf - 1], k32.p, val.p);
+            }
+            radix_sort_pairs<uint32_t>(k32.p, val.p, n, 0, std::max(1u, bits[nf - 1]), s);
+          }
+          {
+            // fields in, key (+ link id) out; stage 2 gathers its fields at the sorted rows
+            KScope ks("k_pack_key", (two ? 12.0 : 12.0) * n + 4.0 * f.n * n);
+            hipLaunchKernelGGL(k_pack_key, G(n), dim3(B), 0, s, (const uint32_t*)T.data, T.ld, b, n, f,
+                               two ? (const uint32_t*)val.p : nullptr, key.p, val.p);
+          }
+          if (sh) radix_sort_pairs<uint64_t>(key.p, val.p, n, 0, (int)sh, s);
+          {
+            KScope ks("k_unpack_key", 12.0 * n + 4.0 * (ar + 1) * n + 8.0 * n);
+            hipLaunchKernelGGL(k_unpack_key, G(n), dim3(B), 0, s, (const uint64_t*)key.p, (const uint32_t*)val.p, n,
+                               f, two ? (int32_t)pos[nf - 1] : -1, (const uint32_t*)T.data, T.ld, b, ty, P.t.data,
+                               P.t.ld, b, pk.p);
+          }
+          DAS_HIP(hipGetLastError());
+        }
+        P.nkeys = rle<uint64_t>(pk.p, R, &P.ukey, &P.uoff, idx, s);
+        build_key_dir(P, idx, s);
+        if (P.nkeys <= kHostKeyMirror) {
+          P.h_ukey.resize(P.nkeys);
+          P.h_uoff.resize(P.nkeys + 1);
+          DAS_HIP(hipMemcpyAsync(P.h_ukey.data(), P.ukey, 8 * P.nkeys, hipMemcpyDeviceToHost, s));
+          DAS_HIP(hipMemcpyAsync(P.h_uoff.data(), P.uoff, 8 * (P.nkeys + 1), hipMemcpyDeviceToHost, s));
+          DAS_HIP(hipStreamSynchronize(s));
+        }
+      }
+    } else if (ar <= (uint32_t)kMaxPosArity) {
+      // permutation path (links of no named type present, or DAS_PIDX_PERM=1)
       for (uint32_t p = 0; p < ar; ++p) {
         DBuf<uint64_t> key(R, s);
         DBuf<uint32_t> perm(R, s);

@@ -775,7 +775,8 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
   const bool wide = total >= (1ull << 32) - (1ull << 16);
   static const int fixed = std::getenv("DAS_DJ_FIXED") && std::getenv("DAS_DJ_FIXED")[0] == '1';
   KScope ks((std::string(balanced ? "k_dj_write_bal<" : "k_dj_write<") + std::to_string(NP) + "," +
-             std::to_string(NB) + (wide ? ",u64" : ",u32") + (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
+             std::to_string(NB) + (wide ? ",u64" : ",u32") +
+             (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
                 .c_str(), bytes);
   if (balanced) {
     const unsigned g = grid_for((total + kBalChunk - 1) / kBalChunk, B / 64, 65535u * 4u);
@@ -1453,6 +1454,8 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
     // output, per launch (a schema wider than 4 + 4 columns is written by
     // several launches, each reading the key and its own columns)
     const bool one = jc.np <= 4 && jc.nb <= 4;
+    // build_bytes < 0: -(bytes per output) -- an index join reads one P row per output
+    if (build_bytes < 0) build_bytes = -build_bytes * (double)total;
     auto bytes = [&](int np, int nb) {
       if (one) return 4.0 * P.nrows * P.ncols + build_bytes + 4.0 * total * nu;
       return 4.0 * P.nrows * (np + 1) + (jc.nb ? build_bytes * nb / jc.nb : 0.0) + 4.0 * total * (np + nb);
@@ -2102,8 +2105,9 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
         hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, pl.akey, A.nrows, pl.kx, pl.g, lc.p, rowid.p);
         DAS_HIP(hipGetLastError());
       }
-      // build bytes: the P_{a,p} rows each output reads (4 B per fresh column)
-      out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, pl.jc, nu, pl.uni.data(), 0.0);
+      // build bytes: the P_{a,p} rows each output reads (4 B per fresh column;
+      // every output is its own P row, so the expansion sizes them)
+      out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, pl.jc, nu, pl.uni.data(), -4.0 * pl.jc.nb);
     }
   }
   out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;

@@ -44,16 +44,37 @@ def fetch_factor(kernel):
     return 1.0 if kernel in RANDOM else 2.0
 
 
+def _last_counts():
+    """LAST_FROM=<bench.json> (the build bench: one timed build after a small
+    warm-up build): kernel -> its launch count in the timed region, so only
+    the last that many dispatches of each kernel are averaged."""
+    path = os.environ.get("LAST_FROM")
+    if not path:
+        return None
+    with open(path) as f:
+        line = [l for l in f if l.startswith("{")][-1]
+    return {k: v["launches"] for k, v in json.loads(line).get("kernels", {}).items()}
+
+
 def per_kernel(db_dir, counter):
     dbs = glob.glob(os.path.join(db_dir, "**", "*.db"), recursive=True)
     out = {}
     for db in dbs:
         c = sqlite3.connect(db)
-        for name, v in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
-                                 (counter,)):
-            out.setdefault(short(name), []).append(float(v) * 1024.0)
+        for name, v, d in c.execute("select kernel_name, value, dispatch_id from counters_collection "
+                                    "where counter_name = ?", (counter,)):
+            out.setdefault(short(name), []).append((int(d), float(v) * 1024.0))
     k = int(os.environ.get("TOPK", "0"))
-    return {s: (sum(sorted(v)[-k:] if k else v), min(k, len(v)) if k else len(v)) for s, v in out.items()}
+    last = _last_counts()
+    res = {}
+    for s, dv in out.items():
+        v = [x[1] for x in sorted(dv)]                      # dispatch order
+        if last is not None and last.get(s):
+            v = v[-last[s]:]
+        elif k:
+            v = sorted(v)[-k:]
+        res[s] = (sum(v), len(v))
+    return res
 
 
 def main():
@@ -75,7 +96,9 @@ def main():
                   "launches_fetch_pass": fn, "launches_write_pass": wn,
                   "note": f"read = {f:g} x FETCH_SIZE ({'random probes' if f == 1 else 'streaming'}), "
                           "write = WRITE_SIZE; mean over "
-                          + (f"the {os.environ['TOPK']} largest launches" if os.environ.get("TOPK") else "all launches")}
+                          + ("the timed build's launches (the last dispatches)" if os.environ.get("LAST_FROM")
+                             else f"the {os.environ['TOPK']} largest launches" if os.environ.get("TOPK")
+                             else "all launches")}
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
