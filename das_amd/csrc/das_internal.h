@@ -234,6 +234,10 @@ std::unique_ptr<Table> join(Ctx& c, const Table& a, const Table& b, int flags);
 // rows of p whose value of the one shared variable lies in EVERY qs[i]'s key
 // set (each qs[i] one column, distinct keys); nullptr when not applicable
 std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& p, const std::vector<const Table*>& qs);
+// index_join(a, q) restricted to the rows whose fresh variable fvar lies in
+// every qs[i]'s key set, filtered during the expansion; nullptr: not applicable
+std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& a, const das_link_scan_t& q, int32_t fvar,
+                                           const std::vector<const Table*>& qs);
 std::unique_ptr<Table> index_join(Ctx& c, const Table& a, const das_link_scan_t& q);   // nullptr: not applicable
 // rows of a whose link (q's grounded targets + a's values of q's variables)
 // does not exist; nullptr when a does not bind every variable position

@@ -267,6 +267,23 @@ __global__ void k_prefix_ties(const uint64_t* key, uint64_t n, int shift, uint32
   if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
 }
 
+// Same checks on the sorted high halves: only adjacent entries whose high
+// halves tie gather their digests (duplicate atoms and hi collisions).
+__global__ void k_hi_ties_key(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+  uint32_t b = 0;
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (key[i] == key[i - 1]) b |= dig[idx[i - 1]].lo() != dig[idx[i]].lo();
+  if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+__global__ void k_first_flags_key(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n,
+                                  uint32_t* first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t f = 1;
+    if (i > 0 && key[i] == key[i - 1]) f = dig[idx[i - 1]].lo() != dig[idx[i]].lo();
+    first[i] = f;
+  }
+}
+
 __global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* first) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t f = 1;
@@ -749,10 +766,14 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
   idx.gbound[t.arity] = std::move(g);
 }
 
-// Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact fallback).
-void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s) {
-  if (n <= 1) return;
-  DBuf<uint64_t> key(n, s);
+// Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact
+// fallback); key[i] = the high half of entry i's digest, sorted.
+void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>& key, hipStream_t s) {
+  key.alloc(n ? n : 1, s);
+  if (n <= 1) {
+    if (n) hipLaunchKernelGGL(k_digest_key, dim3(1), dim3(64), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
+    return;
+  }
   {
     KScope ks("k_digest_key", 28.0 * n);           // index, gathered digest half (8 of 16 B), key out
     hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
@@ -761,8 +782,8 @@ void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, hipStream_t s)
   DBuf<uint32_t> bad(1, s);
   fill_dev(bad.p, 0, 4, s);
   {
-    KScope ks("k_hi_ties", 20.0 * n);
-    hipLaunchKernelGGL(k_hi_ties, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, bad.p);
+    KScope ks("k_hi_ties_key", 8.0 * n);          // sorted keys; digests only where they tie
+    hipLaunchKernelGGL(k_hi_ties_key, G(n), dim3(B), 0, s, (const uint64_t*)key.p, dig, (const uint32_t*)idx, n, bad.p);
   }
   if (read_u32(bad.p, s) == 0) return;
   // exact: LSD over (lo, hi)
@@ -961,14 +982,17 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   flag.release();
 
   // 3. intern: sort by digest, one id per distinct digest
-  sort_by_digest(dig.p, list.p, nc, s);
+  DBuf<uint64_t> skey;
+  sort_by_digest(dig.p, list.p, nc, skey, s);
   DBuf<uint32_t> first(nc ? nc : 1, s), scan(nc ? nc : 1, s);
   uint64_t n_atoms = 0;
   if (nc) {
     {
-      KScope ks("k_first_flags", 24.0 * nc);
-      hipLaunchKernelGGL(k_first_flags, G(nc), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)list.p, nc, first.p);
+      KScope ks("k_first_flags_key", 12.0 * nc);   // sorted keys in, flags out; digests only where keys tie
+      hipLaunchKernelGGL(k_first_flags_key, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, (const Digest*)dig.p,
+                         (const uint32_t*)list.p, nc, first.p);
     }
+    skey.release();
     exclusive_scan<uint32_t>(first.p, nc, scan.p, s);
     n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
   }

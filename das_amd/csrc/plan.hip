@@ -198,6 +198,65 @@ struct Exec {
     return e;
   }
 
+  // And's fold of one positive term into the running result; false when the
+  // term fails the And (:712-713).
+  bool step(uint32_t ti, Rel& acc, bool& have, std::vector<Rel>& forbidden) {
+    const das_plan_node_t& x = nd[ti];
+    if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
+      // the term's rows looked up from the running result's keys; an empty
+      // result takes the scan path, which tells a failing term (And ->
+      // False) from an empty join (reset-on-empty)
+      Rel r;
+      bool ok = true;
+      for (auto& t : acc.t) {
+        auto j = index_join(c, *t, x.ij);
+        if (!j) {
+          ok = false;
+          break;
+        }
+        r.push(std::move(j));
+      }
+      if (ok && r.nonempty()) {
+        acc = std::move(r);
+        return true;
+      }
+    }
+    Res s = eval(ti);
+    if (!s.matched) return false;
+    if (!s.rel.nonempty()) return true;
+    if (s.neg) {
+      forbidden.push_back(std::move(s.rel));
+      return true;
+    }
+    if (!have || !acc.nonempty()) {
+      acc = std::move(s.rel);
+      have = true;
+    } else {
+      acc = join_rel(acc, s.rel);
+    }
+    return true;
+  }
+
+  // End (exclusive) of the one-variable filter terms that follow the
+  // index-joined Link term k on one of its fresh variables (*v), or k.  The
+  // running result must have more than 4096 rows (DAS_SEMI_MULTI as above).
+  size_t filt_run(const std::vector<uint32_t>& terms, size_t k, const Table& a, int32_t& v) const {
+    const char* f = std::getenv("DAS_SEMI_MULTI");
+    if ((f && f[0] == '0') || a.kind != DAS_TABLE_ORDERED || (!(f && f[0] == '1') && a.nrows <= 4096) ||
+        k + 1 >= terms.size())
+      return k;
+    v = one_var(terms[k + 1]);
+    if (v < 0) return k;
+    const das_link_scan_t& q = nd[terms[k]].ij;
+    bool fresh = false;
+    for (uint32_t p = 0; p < q.arity && p < 8; ++p) fresh |= q.target[p] == kNone && q.var[p] == v;
+    for (int i = 0; i < a.ncols; ++i) fresh &= a.vars[i] != v;
+    if (!fresh) return k;
+    size_t e = k + 2;
+    while (e < terms.size() && one_var(terms[e]) == v) ++e;
+    return e;
+  }
+
   Res eval_and(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
@@ -272,38 +331,38 @@ struct Exec {
           continue;
         }
       }
-      if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
-        // the term's rows looked up from the running result's keys; an empty
-        // result takes the scan path, which tells a failing term (And ->
-        // False) from an empty join (reset-on-empty)
-        Rel r;
-        bool ok = true;
-        for (auto& t : acc.t) {
-          auto j = index_join(c, *t, x.ij);
-          if (!j) {
-            ok = false;
-            break;
+      if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.t.size() == 1 && acc.nonempty()) {
+        int32_t v = -1;
+        const size_t e = filt_run(terms, k, *acc.t[0], v);
+        if (e >= k + 2) {
+          // an index-joined term whose fresh variable the next one-variable
+          // terms filter (the hub And's T1(V1,V2) | T2(V2,h1) T3(V2,h0)):
+          // the filter terms are scanned (a failing term fails the And), and
+          // the join is expanded with their key-set intersection applied
+          std::vector<Rel> rs;
+          for (size_t j = k + 1; j < e; ++j) {
+            Res s = eval(terms[j]);
+            if (!s.matched) return Res{};
+            rs.push_back(std::move(s.rel));
           }
-          r.push(std::move(j));
-        }
-        if (ok && r.nonempty()) {
-          acc = std::move(r);
+          std::vector<const Table*> qs;
+          for (auto& r : rs) qs.push_back(r.t[0].get());
+          TablePtr f = index_join_filtered(c, *acc.t[0], x.ij, v, qs);
+          if (f && f->nrows) {
+            // non-empty: no prefix of the term-by-term fold was empty (see
+            // semi_join_multi above), so the rows are the fold's
+            acc = Rel{};
+            acc.push(std::move(f));
+          } else {
+            if (!step(ti, acc, have, forbidden)) return Res{};
+            for (auto& r : rs) acc = acc.nonempty() ? join_rel(acc, r) : std::move(r);
+          }
+          seen += (uint32_t)(e - k - 1);
+          k = e - 1;
           continue;
         }
       }
-      Res s = eval(ti);
-      if (!s.matched) return Res{};
-      if (!s.rel.nonempty()) continue;
-      if (s.neg) {
-        forbidden.push_back(std::move(s.rel));
-        continue;
-      }
-      if (!have || !acc.nonempty()) {
-        acc = std::move(s.rel);
-        have = true;
-      } else {
-        acc = join_rel(acc, s.rel);
-      }
+      if (!step(ti, acc, have, forbidden)) return Res{};
     }
     for (auto& f : forbidden)
       if (acc.nonempty()) acc = antijoin_rel(std::move(acc), f);

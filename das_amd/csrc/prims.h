@@ -475,14 +475,17 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter(const K* kin, cons
 // (tile-local offsets from the tile's histogram), then written out by
 // consecutive threads, so each digit's run of the tile (~16 keys at 256
 // digits) leaves as one contiguous store instead of 64 lanes hitting up to
-// 64 buckets per wave store.  Same stable order as k_radix_scatter.
+// 64 buckets per wave store.  Values follow in a second phase through the
+// SAME LDS buffer (each item's tile position and each output slot's global
+// position stay in registers), so a block holds one tile of keys, not keys
+// plus values: twice the resident blocks for 64-bit keys.  Same stable order
+// as k_radix_scatter.
 template <typename K, bool kHasVals>
 __global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, const uint32_t* vin, K* kout,
                                                                  uint32_t* vout, uint64_t n, int shift,
                                                                  const uint32_t* hist, const uint32_t* offs,
                                                                  uint32_t n_tiles) {
   __shared__ K s_key[kSortTile];
-  __shared__ uint32_t s_val[kHasVals ? kSortTile : 1];
   __shared__ uint32_t s_gbase[256], s_loff[256], s_run[256];
   __shared__ uint32_t s_cnt[kSortBlock / 64][256];
   __shared__ uint32_t s_wsum[kSortBlock / 64];
@@ -513,6 +516,7 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, 
     __syncthreads();
   }
   const uint64_t lt = __lanemask_lt();
+  uint32_t lpos[kHasVals ? kSortItems : 1];             // tile position of this thread's item r
 #pragma unroll
   for (int r = 0; r < kSortItems; ++r) {
     const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
@@ -532,7 +536,7 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, 
       uint32_t pos = s_loff[d] + s_run[d] + rank;
       for (int w = 0; w < wave; ++w) pos += s_cnt[w][d];
       s_key[pos] = kr[r];
-      if (kHasVals) s_val[pos] = vr[r];
+      if (kHasVals) lpos[r] = pos;
     }
     __syncthreads();
     uint32_t add = 0;
@@ -545,12 +549,30 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, 
     __syncthreads();
   }
   const uint32_t valid_n = (uint32_t)(n - base < (uint64_t)kSortTile ? n - base : (uint64_t)kSortTile);
-  for (uint32_t j = tid; j < valid_n; j += kSortBlock) {
-    const K k = s_key[j];
-    const uint32_t d = (uint32_t)(k >> shift) & 255u;
-    const uint64_t g = (uint64_t)s_gbase[d] + (j - s_loff[d]);
-    kout[g] = k;
-    if (kHasVals) vout[g] = s_val[j];
+  uint32_t gpos[kHasVals ? kSortItems : 1];             // global slot of tile position tid + k * kSortBlock
+#pragma unroll
+  for (int k = 0; k < kSortItems; ++k) {
+    const uint32_t j = (uint32_t)tid + (uint32_t)k * kSortBlock;
+    if (j < valid_n) {
+      const K key = s_key[j];
+      const uint32_t d = (uint32_t)(key >> shift) & 255u;
+      const uint32_t g = s_gbase[d] + (j - s_loff[d]);    // < n < 2^32
+      kout[g] = key;
+      if (kHasVals) gpos[k] = g;
+    }
+  }
+  if (kHasVals) {
+    uint32_t* s_val = reinterpret_cast<uint32_t*>(s_key);
+    __syncthreads();                                   // every key read out of the buffer
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r)
+      if (base + (uint64_t)r * kSortBlock + tid < n) s_val[lpos[r]] = vr[r];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)k * kSortBlock;
+      if (j < valid_n) vout[gpos[k]] = s_val[j];
+    }
   }
 }
 

@@ -563,7 +563,10 @@ __global__ void k_pack_lc(const uint32_t* off, uint32_t range, uint2* lc) {
 // (ds_bpermute), takes the probe values from the owner lane and gathers the
 // build payload at (bucket lo + rank inside the bucket).  Stores are one
 // coalesced 256-byte column segment per chunk.
-constexpr int kXGroups = 4;
+#ifndef DAS_DJ_GROUPS
+#define DAS_DJ_GROUPS 2
+#endif
+constexpr int kXGroups = DAS_DJ_GROUPS;
 constexpr uint64_t kXRows = 64ull * kXGroups;
 constexpr uint64_t kHeavyUnit = 1ull << 16;   // outputs above which a unit is expanded output-balanced
 
@@ -577,7 +580,10 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
 // outputs are resolved first and their build loads issued together, so a
 // wave keeps several loads in flight instead of one load -> store round trip
 // per 64 outputs.
-constexpr int kXUnroll = 4;
+#ifndef DAS_DJ_UNROLL
+#define DAS_DJ_UNROLL 4
+#endif
+constexpr int kXUnroll = DAS_DJ_UNROLL;
 template <int NP, int NB, typename T, int V = 1>
 __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
@@ -830,6 +836,144 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
     DJ(4, 0) DJ(4, 1) DJ(4, 2) DJ(4, 3) DJ(4, 4)
 #undef DJ
   } while (pi < jc.np || bi < jc.nb);
+}
+
+// ---------------------------------------------------------------------------
+// Filtered expansion: a join whose fresh build column is then filtered by
+// semi-join terms (T0(V1,h0) T1(V1,V2) | T2(V2,h1) T3(V2,h0) of the hub And:
+// the key bitmap holds T2's and T3's keys).  The join's outputs are expanded
+// virtually, in output-balanced chunks, twice: MODE 0 tests each output's
+// build value against the bitmap (one flag byte per output, the chunk's kept
+// count); MODE 1 writes only the kept outputs, in output order, at the
+// chunk's scanned offset.  The unfiltered join is never materialised.
+// ---------------------------------------------------------------------------
+struct FiltKey {
+  const uint32_t* col;     // build column holding the filtered variable
+  uint32_t lo, range;
+  const uint32_t* bits;
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                               uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                               const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
+                                               uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
+                                               const uint32_t* __restrict__ coff, JoinCols jc,
+                                               uint32_t* __restrict__ out, uint64_t cap) {
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  const uint64_t lt = __lanemask_lt();
+  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
+    const uint64_t ob = w * kBalChunk;
+    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+    uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
+    while (hi - lo > 1) {
+      const uint64_t step = (hi - lo + 63) / 64;
+      const uint64_t idx = lo + (uint64_t)lane * step;
+      const bool ok = idx < hi && unit_off[idx] <= ob;
+      const uint64_t m = __ballot(ok);
+      const uint64_t nlo = lo + (uint64_t)(63 - __clzll((long long)m)) * step;
+      hi = nlo + step < hi ? nlo + step : hi;
+      lo = nlo;
+    }
+    uint32_t run = 0;                                  // kept outputs of this chunk so far
+    const uint32_t obase = MODE == 1 ? coff[w] : 0u;
+    for (uint64_t u = lo; u < units; ++u) {
+      uint64_t base = unit_off[u];
+      if (base >= oe) break;
+      const uint64_t r0 = u * kXRows;
+      uint2 e[kXGroups];
+#pragma unroll
+      for (int g = 0; g < kXGroups; ++g) {
+        const uint64_t r = r0 + g * 64 + lane;
+        const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+        e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int g = 0; g < kXGroups; ++g) {
+        const uint32_t c = e[g].y;
+        const uint32_t inc = wave_inclusive_scan(c);
+        const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+        const uint32_t pre = inc - c;
+        const uint64_t gb = base, ge = base + tot;
+        base = ge;
+        if (ge <= ob || gb >= oe) continue;
+        const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
+        const uint64_t r = r0 + g * 64 + lane;
+        uint32_t pv[4] = {0u, 0u, 0u, 0u};
+        if (MODE == 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < jc.np) pv[i] = r < np ? jc.p[i][r] : 0u;
+        }
+        // kXUnroll rounds of 64 outputs resolved before their loads issue
+        for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+          const int nr = (re - o0) >= 64u * kXUnroll ? kXUnroll : (int)((re - o0 + 63) / 64);
+          uint32_t o[kXUnroll], br[kXUnroll];
+          int ll[kXUnroll];
+#pragma unroll
+          for (int q = 0; q < kXUnroll; ++q) {
+            o[q] = o0 + (uint32_t)(q * 64 + lane);
+            ll[q] = 0;
+            br[q] = 0;
+            if (q >= nr) continue;
+            int l = 0;                                 // owner: max lane with pre <= o
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1) {
+              const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
+              if (l + st < 64 && pl <= o[q]) l += st;
+            }
+            ll[q] = l;
+            br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+          }
+          if (MODE == 0) {
+            uint32_t v[kXUnroll];
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+            uint32_t wd[kXUnroll];
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) {
+              if (q >= nr) continue;
+              const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
+              if (o[q] < re) fl[gb + o[q]] = f ? 1 : 0;
+              run += (uint32_t)__popcll(__ballot(f));
+            }
+          } else {
+            bool f[kXUnroll];
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
+            uint32_t bv[kXUnroll][4];
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) bv[q][i] = (i < jc.nb && f[q]) ? jc.b[i][br[q]] : 0u;
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) {
+              if (q >= nr) continue;
+              const uint64_t m = __ballot(f[q]);
+              const uint64_t pos = (uint64_t)obase + run + __popcll(m & lt);
+              run += (uint32_t)__popcll(m);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (i >= jc.np) break;
+                const uint32_t x = lane_get(pv[i], ll[q]);
+                if (f[q]) out[(uint64_t)jc.po[i] * cap + pos] = x;
+              }
+              if (f[q]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  if (i < jc.nb) out[(uint64_t)jc.bo[i] * cap + pos] = bv[q][i];
+              }
+            }
+          }
+        }
+      }
+    }
+    if (MODE == 0 && lane == 0) ccnt[w] = run;
+  }
 }
 
 }  // namespace
@@ -1275,6 +1419,13 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
       uint64_t total = 0;
       for (uint32_t ty : types) {
         const uint64_t k = ((uint64_t)ty << 32) | q.target[p];
+        if (!P.h_ukey.empty()) {
+          // host mirror of the keys: one binary search, no cache to consult
+          const size_t i = std::lower_bound(P.h_ukey.begin(), P.h_ukey.end(), k) - P.h_ukey.begin();
+          const bool has = i < P.h_ukey.size() && P.h_ukey[i] == k;
+          rr.push_back(has ? std::pair<uint64_t, uint64_t>{P.h_uoff[i], P.h_uoff[i + 1]} : std::pair<uint64_t, uint64_t>{0, 0});
+          continue;
+        }
         const std::array<uint64_t, 4> ck{ar, p, k, 0};
         auto hit = idx.range_cache.find(ck);
         if (hit != idx.range_cache.end()) {
@@ -1733,10 +1884,10 @@ __device__ __forceinline__ uint2 ij_lookup_group(uint32_t t, const IjKeys& kx, c
 // of G lanes (G = 1: one row per thread).
 template <int G>
 __device__ __forceinline__ void lookups_into(const uint32_t* key, const IjKeys& kx, const IjGround& g, uint32_t nin,
-                                             uint32_t* s_lo, uint32_t* s_pre) {
+                                             uint32_t* s_lo, uint32_t* s_pre, uint32_t base) {
   if (G == 1) {
     for (uint32_t r = threadIdx.x; r < nin; r += kSmallBlock) {
-      const uint2 e = ij_lookup(key[r], kx, g, r);
+      const uint2 e = ij_lookup(key[base + r], kx, g, base + r);
       s_lo[r] = e.x;
       s_pre[r] = e.y;
     }
@@ -1745,7 +1896,7 @@ __device__ __forceinline__ void lookups_into(const uint32_t* key, const IjKeys& 
     for (uint32_t r0 = 0; r0 < nin; r0 += groups) {      // uniform trip count: every lane of a group searches
       const uint32_t r = r0 + gid;
       const uint32_t rr = r < nin ? r : nin - 1;
-      const uint2 e = ij_lookup_group<G>(key[rr], kx, g, rr);
+      const uint2 e = ij_lookup_group<G>(key[base + rr], kx, g, base + rr);
       if (r < nin && (threadIdx.x & (G - 1)) == 0) {
         s_lo[r] = e.x;
         s_pre[r] = e.y;
@@ -1754,12 +1905,13 @@ __device__ __forceinline__ void lookups_into(const uint32_t* key, const IjKeys& 
   }
 }
 
+// rows [base, base + nin) of the probe; results at s_lo / s_pre [0, nin)
 __device__ __forceinline__ void lookups_small(const uint32_t* key, const IjKeys& kx, const IjGround& g, uint32_t nin,
-                                              uint32_t* s_lo, uint32_t* s_pre) {
-  if (nin <= kSmallBlock / 64) lookups_into<64>(key, kx, g, nin, s_lo, s_pre);
-  else if (nin <= kSmallBlock / 16) lookups_into<16>(key, kx, g, nin, s_lo, s_pre);
-  else if (nin <= kSmallBlock / 4) lookups_into<4>(key, kx, g, nin, s_lo, s_pre);
-  else lookups_into<1>(key, kx, g, nin, s_lo, s_pre);
+                                              uint32_t* s_lo, uint32_t* s_pre, uint32_t base = 0) {
+  if (nin <= kSmallBlock / 64) lookups_into<64>(key, kx, g, nin, s_lo, s_pre, base);
+  else if (nin <= kSmallBlock / 16) lookups_into<16>(key, kx, g, nin, s_lo, s_pre, base);
+  else if (nin <= kSmallBlock / 4) lookups_into<4>(key, kx, g, nin, s_lo, s_pre, base);
+  else lookups_into<1>(key, kx, g, nin, s_lo, s_pre, base);
 }
 
 // Single-workgroup index join of a small probe table: lookups, a block scan
@@ -2269,18 +2421,21 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
         n = s_run;
       }
     } else if (st.op == CH_IJ) {
+      // the probe in chunks of kIjSmall rows (the LDS prefix): lookups, a
+      // block scan of the match counts, the chunk's outputs appended in
+      // probe order
       const uint32_t nin = s_cnt[st.in];
-      if (nin > kIjSmall) {
-        ok = false;
-      } else {
-        lookups_small(st.key, st.kx, st.g, nin, s_lo, s_pre);
+      const int wave = threadIdx.x >> 6;
+      uint32_t outn = 0;
+      for (uint32_t c0 = 0; c0 < nin && ok; c0 += kIjSmall) {
+        const uint32_t cn = nin - c0 < kIjSmall ? nin - c0 : kIjSmall;
+        lookups_small(st.key, st.kx, st.g, cn, s_lo, s_pre, c0);
         __syncthreads();
-        // exclusive scan of s_pre[0..nin) in rounds of 1024
-        const int wave = threadIdx.x >> 6;
+        // exclusive scan of s_pre[0..cn) in rounds of 1024
         uint32_t carry = 0;
-        for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
+        for (uint32_t r0 = 0; r0 < cn; r0 += kSmallBlock) {
           const uint32_t r = r0 + threadIdx.x;
-          const uint32_t v = r < nin ? s_pre[r] : 0u;
+          const uint32_t v = r < cn ? s_pre[r] : 0u;
           const uint32_t inc = wave_incl_sum_u32(v);
           if (__lane_id() == 63) s_w[wave] = inc;
           __syncthreads();
@@ -2290,28 +2445,31 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
             all += s_w[w];
           }
           __syncthreads();
-          if (r < nin) s_pre[r] = pre;
+          if (r < cn) s_pre[r] = pre;
           carry += all;
           __syncthreads();
         }
-        if (threadIdx.x == 0) s_pre[nin] = carry;
+        if (threadIdx.x == 0) s_pre[cn] = carry;
         __syncthreads();
-        n = carry;
-        if (n == 0 || n > st.cap) {
+        if ((uint64_t)outn + carry > st.cap) {
           ok = false;
         } else {
-          for (uint32_t o = threadIdx.x; o < n; o += kSmallBlock) {
-            uint32_t l = 0, h = nin;                   // last row r with s_pre[r] <= o
+          for (uint32_t o = threadIdx.x; o < carry; o += kSmallBlock) {
+            uint32_t l = 0, h = cn;                    // last row r with s_pre[r] <= o
             while (h - l > 1) {
               const uint32_t m = (l + h) >> 1;
               if (s_pre[m] <= o) l = m; else h = m;
             }
             const uint32_t br = s_lo[l] + (o - s_pre[l]);
-            for (int i = 0; i < st.jc.np; ++i) st.dst[(uint64_t)st.jc.po[i] * st.cap + o] = st.jc.p[i][l];
-            for (int i = 0; i < st.jc.nb; ++i) st.dst[(uint64_t)st.jc.bo[i] * st.cap + o] = st.jc.b[i][br];
+            for (int i = 0; i < st.jc.np; ++i) st.dst[(uint64_t)st.jc.po[i] * st.cap + outn + o] = st.jc.p[i][c0 + l];
+            for (int i = 0; i < st.jc.nb; ++i) st.dst[(uint64_t)st.jc.bo[i] * st.cap + outn + o] = st.jc.b[i][br];
           }
+          outn += carry;
         }
+        __syncthreads();                               // s_lo / s_pre are reused by the next chunk
       }
+      n = outn;
+      if (n == 0) ok = false;
     } else if (st.op == CH_JOIN) {
       const uint32_t na = s_cnt[st.in], nb = s_cnt[st.rel];
       const uint64_t pairs = (uint64_t)na * nb;
@@ -2404,11 +2562,14 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     if (acc >= 0 && x->index_join) {
       IjPlan pl;
       const Table& A = *tabs[acc];
-      if (ij_prepare(c, A, x->ij, kIjSmall, pl)) {
+      const bool ijok = ij_prepare(c, A, x->ij, kIjSmall, pl);
+      if (trace_on()) trace_mark("prep ij_prepare");
+      if (ijok) {
         if (pl.empty) { all_terms = false; break; }
         ChainStage* st = add(CH_IJ);
         if (!st) { all_terms = false; break; }
         auto t = new_table(c, DAS_TABLE_ORDERED, (int)pl.uni.size(), pl.uni.data(), kChainCap);
+        if (trace_on()) trace_mark("prep new_table");
         for (size_t k = 0; k < pl.uni.size(); ++k) {
           t->lo[k] = pl.lo[k];
           t->hi[k] = pl.hi[k];
@@ -2429,6 +2590,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     }
     ScanPrep P;
     scan_prepare(c, x->scan, P);
+    if (trace_on()) trace_mark("prep scan_prepare");
     if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) { all_terms = false; break; }
     const uint64_t b = P.ranges[0].first, e = P.ranges[0].second;
     if (e - b > kSmallScan || e >= 0xFFFFFFFFull || d.nstage + (acc >= 0 ? 2 : 1) > (uint32_t)kChainStages) {
@@ -2438,6 +2600,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     ChainStage* st = add(CH_SCAN);
     auto t = new_table(c, P.kind, P.ncols, P.vars, e - b);
     scan_bounds(idx, P.sp, x->scan.type_id, *t);
+    if (trace_on()) trace_mark("prep scan table");
     st->sp = P.sp;
     st->begin = (uint32_t)b;
     st->end = (uint32_t)e;
@@ -2535,7 +2698,9 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   double sbytes = 0;
   for (uint32_t i = 0; i < d.nstage; ++i)
     if (d.st[i].op == CH_SCAN) sbytes += 4.0 * (d.st[i].end - d.st[i].begin) * (d.st[i].sp.arity + 1);
+  if (trace_on()) trace_mark("prep staged");
   const PubSlot ps = pub_reserve();
+  if (trace_on()) trace_mark("prep slot");
   {
     ProfScope pf(c, "k_chain", sbytes);
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
@@ -2787,28 +2952,27 @@ __global__ void k_bits_and(uint32_t* __restrict__ acc, const uint32_t* __restric
     acc[i] &= b[i];
 }
 
-std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector<const Table*>& Qs) {
-  if (Qs.empty() || P.kind != DAS_TABLE_ORDERED || !P.nrows) return nullptr;
-  const int32_t var = Qs[0]->vars[0];
-  int pk = -1;
-  for (int i = 0; i < P.ncols; ++i) if (P.vars[i] == var) pk = i;
-  if (pk < 0) return nullptr;
-  uint64_t lo = 0, hi = c.idx.n_atoms ? c.idx.n_atoms - 1 : 0;
+// The intersection of the key sets of Qs (one column each, variable `var`) as
+// a bitmap over [lo, hi] (narrowed here to the Qs' bounds); false when a Q
+// does not qualify, the range is too wide or a Q repeats a key.  lo > hi on
+// return: the bounds are disjoint, no key is in every set.
+bool key_bits(Ctx& c, const std::vector<const Table*>& Qs, int32_t var, uint64_t& lo, uint64_t& hi,
+              DBuf<uint32_t>& acc) {
   auto clip = [&](uint32_t l, uint32_t h) {
     if (h == kNone || l > h) return;                       // unknown bound
     lo = std::max<uint64_t>(lo, l);
     hi = std::min<uint64_t>(hi, h);
   };
-  clip(P.lo[pk], P.hi[pk]);
   for (const Table* Q : Qs) {
-    if (Q->kind != DAS_TABLE_ORDERED || Q->ncols != 1 || Q->vars[0] != var || Q->nrows >= 0xFFFFFFFFull) return nullptr;
+    if (Q->kind != DAS_TABLE_ORDERED || Q->ncols != 1 || Q->vars[0] != var || Q->nrows >= 0xFFFFFFFFull) return false;
     clip(Q->lo[0], Q->hi[0]);
   }
-  if (lo > hi) return new_table_like(c, P, 0);              // disjoint bounds: nothing passes
+  if (lo > hi) return true;
   const uint64_t range = hi - lo + 1;
-  if (range > (1ull << 31)) return nullptr;
+  if (range > (1ull << 31)) return false;
   const uint64_t words = (range + 31) / 32;
-  DBuf<uint32_t> acc(words + 1, c.s), one(words + 1, c.s);  // + the duplicate flag
+  acc.alloc(words + 1, c.s);                                // + the duplicate flag
+  DBuf<uint32_t> one(Qs.size() > 1 ? words + 1 : 1, c.s);
   for (size_t i = 0; i < Qs.size(); ++i) {
     uint32_t* bits = i == 0 ? acc.p : one.p;
     fill_dev(bits, 0, 4 * (words + 1), c.s);
@@ -2818,14 +2982,31 @@ std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector
                          (uint32_t)lo, (uint32_t)range, bits, bits + words);
       DAS_HIP(hipGetLastError());
     }
-    if (read_u32(bits + words, c.s)) return nullptr;        // duplicate keys: counts matter
+    if (read_u32(bits + words, c.s)) return false;          // duplicate keys: counts matter
     if (i) {
       KScope ks("k_bits_and", 12.0 * words);
       hipLaunchKernelGGL(k_bits_and, G(words), dim3(B), 0, c.s, acc.p, (const uint32_t*)one.p, words);
       DAS_HIP(hipGetLastError());
     }
   }
-  one.release();
+  return true;
+}
+
+std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector<const Table*>& Qs) {
+  if (Qs.empty() || P.kind != DAS_TABLE_ORDERED || !P.nrows) return nullptr;
+  const int32_t var = Qs[0]->vars[0];
+  int pk = -1;
+  for (int i = 0; i < P.ncols; ++i) if (P.vars[i] == var) pk = i;
+  if (pk < 0) return nullptr;
+  uint64_t lo = 0, hi = c.idx.n_atoms ? c.idx.n_atoms - 1 : 0;
+  if (P.hi[pk] != kNone && P.lo[pk] <= P.hi[pk]) {
+    lo = P.lo[pk];
+    hi = std::min<uint64_t>(hi, P.hi[pk]);
+  }
+  DBuf<uint32_t> acc;
+  if (!key_bits(c, Qs, var, lo, hi, acc)) return nullptr;
+  if (lo > hi) return new_table_like(c, P, 0);              // disjoint bounds: nothing passes
+  const uint64_t range = hi - lo + 1;
   auto out = compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), (uint32_t)lo, (uint32_t)range,
                                          (const uint32_t*)acc.p},
                           "k_tile_count<BitsPred>", 4.0);
@@ -2836,6 +3017,85 @@ std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector
   }
   out->lo[pk] = (uint32_t)lo;
   out->hi[pk] = (uint32_t)hi;
+  return out;
+}
+
+// index_join(A, q) followed by the semi-join of every Qs[i] on q's fresh
+// variable fvar, with the join's outputs filtered while they are expanded
+// (k_dj_filt) -- the unfiltered join is never written.  nullptr when it does
+// not apply; the plan executor takes a non-empty result only.
+std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_link_scan_t& q, int32_t fvar,
+                                           const std::vector<const Table*>& Qs) {
+  IjPlan pl;
+  if (Qs.empty() || !ij_prepare(c, A, q, A.nrows, pl) || pl.empty) return nullptr;
+  const JoinCols& jc = pl.jc;
+  if (jc.np > 4 || jc.nb > 4) return nullptr;
+  int fb = -1;
+  for (int i = 0; i < jc.nb; ++i)
+    if (pl.uni[jc.bo[i]] == fvar) fb = i;
+  if (fb < 0) return nullptr;
+  const int nu = (int)pl.uni.size();
+  const int fo = jc.bo[fb];
+  uint64_t lo = 0, hi = c.idx.n_atoms ? c.idx.n_atoms - 1 : 0;
+  if (pl.hi[fo] != kNone && pl.lo[fo] <= pl.hi[fo]) {
+    lo = pl.lo[fo];
+    hi = std::min<uint64_t>(hi, pl.hi[fo]);
+  }
+  DBuf<uint32_t> bits;
+  if (!key_bits(c, Qs, fvar, lo, hi, bits)) return nullptr;
+  if (lo > hi) return new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), 0);
+  DBuf<uint2> lc(A.nrows, c.s);
+  DBuf<uint32_t> rowid(A.nrows, c.s);
+  {
+    ProfScope ps(c, "k_ij_lc", 4.0 * A.nrows + 8.0 * A.nrows + 4.0 * A.nrows);
+    hipLaunchKernelGGL(k_ij_lc, G(A.nrows), dim3(B), 0, c.s, pl.akey, A.nrows, pl.kx, pl.g, lc.p, rowid.p);
+    DAS_HIP(hipGetLastError());
+  }
+  const uint64_t units = (A.nrows + kXRows - 1) / kXRows;
+  const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
+  DBuf<uint64_t> tot(units, c.s), toff(units + 1, c.s);
+  {
+    ProfScope ps(c, "k_dj_count", 4.0 * A.nrows);
+    hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
+                       (uint32_t)A.nrows, (const uint2*)lc.p, units, tot.p);
+    DAS_HIP(hipGetLastError());
+  }
+  const uint64_t total = scan_total<uint64_t>(SpanIn<uint64_t>{tot.p}, units, toff.p, c.s);
+  if (!total) return new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), 0);
+  if (total >= (1ull << 32) - (1ull << 16)) return nullptr;
+  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const unsigned fgrid = grid_for(chunks, B / 64, 65535u * 4u);
+  const FiltKey fk{jc.b[fb], (uint32_t)lo, (uint32_t)(hi - lo + 1), (const uint32_t*)bits.p};
+  DBuf<uint8_t> fl(total, c.s);
+  DBuf<uint32_t> ccnt(chunks, c.s), coff(chunks + 1, c.s);
+  {
+    // per probe row its row id and (first, count); per output its build
+    // value (a P row) and its flag byte
+    ProfScope ps(c, "k_dj_filt<flag>", 12.0 * A.nrows + 5.0 * total);
+    hipLaunchKernelGGL(k_dj_filt<0>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
+                       (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p,
+                       (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
+    DAS_HIP(hipGetLastError());
+  }
+  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, chunks, coff.p, c.s);
+  auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
+  out->nrows = m;
+  if (m) {
+    // + the probe columns, the flags, the kept outputs' build rows and their columns out
+    ProfScope ps(c, "k_dj_filt<write>",
+                 (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
+    hipLaunchKernelGGL(k_dj_filt<1>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
+                       (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,
+                       (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
+  for (int k = 0; k < nu; ++k) {
+    out->lo[k] = pl.lo[k];
+    out->hi[k] = pl.hi[k];
+  }
+  out->lo[fo] = (uint32_t)lo;
+  out->hi[fo] = (uint32_t)hi;
   return out;
 }
 

@@ -486,6 +486,12 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     specs = [q for _, q in bench.hub_specs()]
     specs.append(["And", [L("T0", V("V1"), n(0)), L("T1", V("V1"), V("V2")), L("T2", V("V2"), n(1)),
                           L("T3", V("V2"), n(0)), L("T0", V("V2"), n(2))]])
+    # one filter term after the index-joined term, then a term on the filtered variable
+    specs.append(["And", [L("T0", V("V1"), n(0)), L("T0", V("V1"), V("V2")), L("T0", V("V2"), n(1)),
+                          L("T0", V("V2"), V("V3"))]])
+    # a filter term whose key set misses every joined row: term-by-term fold (reset-on-empty)
+    specs.append(["And", [L("T0", V("V1"), n(0)), L("T1", V("V1"), V("V2")), L("T2", V("V2"), n(132)),
+                          L("T3", V("V2"), n(0))]])
     for _ in range(24):
         a, b, c = (int(x) for x in rng.integers(0, 200, 3))
         t = [f"T{int(x)}" for x in rng.integers(0, 4, 4)]
@@ -500,6 +506,47 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
         assert same(got, want), (q, got.get("n"), want.get("n"))
         nonempty += want.get("n", 0) > 0
     assert nonempty >= 4
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_gpu_chain_large_index_join_stage(fused, monkeypatch):
+    """Fused single-launch And (k_chain) whose index-join stages probe more
+    rows than one LDS prefix (kIjSmall = 2048): the stage runs in chunks and
+    appends their outputs in probe order; against the oracle and the
+    per-operator path (DAS_FUSED=0)."""
+    from das_amd import loader
+    monkeypatch.setenv("DAS_FUSED", fused)
+    rng = np.random.default_rng(12)
+    b = loader.AtomBuilder()
+    hub = b.terminal("Concept", "hub", True)
+    xs = [b.terminal("Concept", f"x{i}", True) for i in range(2100)]
+    ys = [b.terminal("Concept", f"y{i}", True) for i in range(300)]
+    for x in xs:
+        b.expr("Rel", [hub, x])
+        for y in rng.choice(len(ys), int(rng.integers(1, 3)), replace=False):
+            b.expr("Rel2", [x, ys[int(y)]])
+    for y in ys[:150]:
+        b.expr("Rel3", [y, xs[int(rng.integers(0, 2100))]])
+    arrays = b.finish()
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    V = lambda x: ["Var", x]  # noqa: E731
+    h = ["Node", "Concept", "hub"]
+    for q in (["And", [["Link", "Rel", True, [h, V("A")]], ["Link", "Rel2", True, [V("A"), V("B")]]]],
+              ["And", [["Link", "Rel", True, [h, V("A")]], ["Link", "Rel2", True, [V("A"), V("B")]],
+                       ["Link", "Rel3", True, [V("B"), V("C")]]]],
+              ["And", [["Link", "Rel", True, [h, V("A")]], ["Link", "Rel2", True, [V("A"), V("B")]],
+                       ["Not", ["Link", "Rel3", True, [V("B"), V("A")]]]]]):
+        key = json.dumps(q)
+        if key not in _CHAIN_WANT:                        # the oracle's nested loop: once per query
+            _CHAIN_WANT[key] = O.evaluate(q, odb)
+        want = _CHAIN_WANT[key]
+        got = record(q, db)
+        assert want.get("n", 0) > 1000                 # (stage inputs: 2100 and ~3150 rows)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+_CHAIN_WANT = {}
 
 
 def test_gpu_native_canonical_load_matches_oracle():

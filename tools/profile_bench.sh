@@ -23,8 +23,10 @@ PARGS="$ARGS --no-cpu-baseline --no-materialise"
 timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
 timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS > $D/kt.log 2>&1 &&
 cp "$(find $D/kt -name 'run_kernel_stats.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_stats.csv &&
+cp "$(find $D/kt -name 'run_kernel_trace.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_trace.csv &&
 timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/fetch -o run -- python bench.py $PARGS > $D/fetch.log 2>&1 &&
 timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $PARGS > $D/write.log 2>&1 &&
+if [ "$W" = build ]; then export LAST_FROM=gpurun_out/${T}_bench_$W.json; fi &&
 python tools/pmc_traffic.py $D/fetch $D/write > gpurun_out/${T}_pmc_traffic_$W.json &&
 python tools/roofline_check.py gpurun_out/${T}_bench_$W.json gpurun_out/${T}_${W}_kernel_stats.csv \
     gpurun_out/${T}_pmc_traffic_$W.json > gpurun_out/${T}_roofline_check_$W.json
