@@ -269,6 +269,32 @@ __global__ void k_prefix_ties(const uint64_t* key, uint64_t n, int shift, uint32
 
 // Same checks on the sorted high halves: only adjacent entries whose high
 // halves tie gather their digests (duplicate atoms and hi collisions).
+// The digest sort's key with the entry's category priority (2 bits) in place
+// of the high half's two lowest bits: equal digests stay adjacent (ordered by
+// category inside their run); entries whose keys agree above those bits but
+// whose digests differ are caught by k_prio_ties (then the exact sort runs).
+__global__ void k_digest_key_prio(const Digest* dig, const uint32_t* idx, const uint8_t* prio, uint64_t n,
+                                  uint64_t* key) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = idx[i];
+    key[i] = (dig[u].hi() & ~3ull) | (uint64_t)(prio[u] & 3u);
+  }
+}
+__global__ void k_prio_ties(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+  uint32_t b = 0;
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if ((key[i] >> 2) == (key[i - 1] >> 2)) {
+      const Digest a = dig[idx[i - 1]], c = dig[idx[i]];
+      b |= a.hi() != c.hi() || a.lo() != c.lo();
+    }
+  if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+// tie-free category-carrying keys: a run starts where the digest bits change
+__global__ void k_first_flags_prio(const uint64_t* key, uint64_t n, uint32_t* first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    first[i] = i == 0 || (key[i] >> 2) != (key[i - 1] >> 2);
+}
+
 __global__ void k_hi_ties_key(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
   uint32_t b = 0;
   for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -309,8 +335,9 @@ __device__ __forceinline__ bool wave_run_tail(uint32_t id) {
 }
 
 __global__ void __launch_bounds__(256) k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan,
-                                                    uint64_t n, const uint8_t* catl, uint32_t* local2id,
-                                                    uint32_t* catmax, uint32_t* rep, uint8_t* cat_sorted) {
+                                                    uint64_t n, const uint8_t* catl, const uint64_t* pkey,
+                                                    uint32_t* local2id, uint32_t* catmax, uint32_t* rep,
+                                                    uint8_t* cat_sorted) {
   const int lane = __lane_id();
   for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = base + threadIdx.x;           // block-uniform trip count: the whole wave shuffles
@@ -320,7 +347,7 @@ __global__ void __launch_bounds__(256) k_assign_ids(const uint32_t* idx, const u
     if (act) {
       id = scan[i] + first[i] - 1;
       const uint32_t u = idx[i];
-      const uint8_t c = catl[u];
+      const uint8_t c = pkey ? (uint8_t)(pkey[i] & 3u) : catl[u];   // pkey: the category rode in the sort key
       local2id[u] = id;
       cat_sorted[i] = c;
       single = first[i] && (i + 1 == n || first[i + 1]);
@@ -767,30 +794,49 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
 }
 
 // Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact
-// fallback); key[i] = the high half of entry i's digest, sorted.
-void sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>& key, hipStream_t s) {
+// fallback); key[i] = the high half of entry i's digest, sorted.  With
+// `prio` (category per unified index) the fast path carries it in the key's
+// two lowest bits and returns true: then key >> 2 separates digests and
+// key & 3 is the entry's category.  false: exact order, key = high halves.
+bool sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>& key, hipStream_t s,
+                    const uint8_t* prio = nullptr) {
   key.alloc(n ? n : 1, s);
   if (n <= 1) {
     if (n) hipLaunchKernelGGL(k_digest_key, dim3(1), dim3(64), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
-    return;
+    return false;
+  }
+  DBuf<uint32_t> bad(1, s);
+  fill_dev(bad.p, 0, 4, s);
+  if (prio) {
+    {
+      KScope ks("k_digest_key", 29.0 * n);         // index, gathered digest half, category, key out
+      hipLaunchKernelGGL(k_digest_key_prio, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, prio, n, key.p);
+    }
+    radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+    {
+      KScope ks("k_prio_ties", 8.0 * n);            // sorted keys; digests only where the digest bits tie
+      hipLaunchKernelGGL(k_prio_ties, G(n), dim3(B), 0, s, (const uint64_t*)key.p, dig, (const uint32_t*)idx, n,
+                         bad.p);
+    }
+    if (read_u32(bad.p, s) == 0) return true;
+    fill_dev(bad.p, 0, 4, s);
   }
   {
     KScope ks("k_digest_key", 28.0 * n);           // index, gathered digest half (8 of 16 B), key out
     hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
   }
   radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
-  DBuf<uint32_t> bad(1, s);
-  fill_dev(bad.p, 0, 4, s);
   {
     KScope ks("k_hi_ties_key", 8.0 * n);          // sorted keys; digests only where they tie
     hipLaunchKernelGGL(k_hi_ties_key, G(n), dim3(B), 0, s, (const uint64_t*)key.p, dig, (const uint32_t*)idx, n, bad.p);
   }
-  if (read_u32(bad.p, s) == 0) return;
+  if (read_u32(bad.p, s) == 0) return false;
   // exact: LSD over (lo, hi)
   hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, false);
   radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
   hipLaunchKernelGGL(k_digest_key, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, n, key.p, true);
   radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+  return false;
 }
 
 // Run-length encoding of sorted keys: unique keys + n_runs+1 offsets (device).
@@ -882,6 +928,25 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
     P.dir_n[ty] = (uint32_t)span;
   }
 }
+
+namespace {
+__global__ void k_unsorted(const uint32_t* key, uint64_t n, uint32_t* bad) {
+  uint32_t b = 0;
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    b |= key[i] < key[i - 1];
+  if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+// keys[0..n) already non-decreasing (one read pass; a sort by them would be a no-op)
+bool keys_sorted(const uint32_t* key, uint64_t n, hipStream_t s) {
+  if (n <= 1) return true;
+  DBuf<uint32_t> bad(1, s);
+  fill_dev(bad.p, 0, 4, s);
+  KScope ks("k_unsorted", 4.0 * n);
+  hipLaunchKernelGGL(k_unsorted, G(n), dim3(B), 0, s, key, n, bad.p);
+  DAS_HIP(hipGetLastError());
+  return read_u32(bad.p, s) == 0;
+}
+}  // namespace
 
 void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   // DAS_BUILD_EXPR_ON_DEVICE: expr_off / expr_child / expr_kind /
@@ -983,16 +1048,18 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
 
   // 3. intern: sort by digest, one id per distinct digest
   DBuf<uint64_t> skey;
-  sort_by_digest(dig.p, list.p, nc, skey, s);
+  const bool prio_key = sort_by_digest(dig.p, list.p, nc, skey, s, catl.p);
   DBuf<uint32_t> first(nc ? nc : 1, s), scan(nc ? nc : 1, s);
   uint64_t n_atoms = 0;
   if (nc) {
-    {
+    if (prio_key) {
+      KScope ks("k_first_flags_prio", 12.0 * nc);  // sorted keys in, flags out
+      hipLaunchKernelGGL(k_first_flags_prio, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, nc, first.p);
+    } else {
       KScope ks("k_first_flags_key", 12.0 * nc);   // sorted keys in, flags out; digests only where keys tie
       hipLaunchKernelGGL(k_first_flags_key, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, (const Digest*)dig.p,
                          (const uint32_t*)list.p, nc, first.p);
     }
-    skey.release();
     exclusive_scan<uint32_t>(first.p, nc, scan.p, s);
     n_atoms = (uint64_t)read_u32(scan.p + nc - 1, s) + read_u32(first.p + nc - 1, s);
   }
@@ -1006,8 +1073,10 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
       // list, first, scan, catl in; local2id, sorted category out; catmax + rep per atom
       KScope ks("k_assign_ids", 19.0 * nc + 8.0 * n_atoms);
       hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
-                         (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p, local2id.p, catmax.p, rep.p, cs.p);
+                         (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p,
+                         prio_key ? (const uint64_t*)skey.p : nullptr, local2id.p, catmax.p, rep.p, cs.p);
     }
+    skey.release();
     {
       KScope ks("k_pick_rep", 13.0 * nc);
       hipLaunchKernelGGL(k_pick_rep, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
@@ -1212,7 +1281,10 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         KScope ks("k_u32_key", 12.0 * R);
         hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.type, (const uint32_t*)perm.p, R, key.p);
       }
-      radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, tbits > 0 ? tbits : 1, s);
+      // no sort: final ids are clustered by named type (step 3b) and T_a
+      // holds links only, so the arity's link ids in ascending order are
+      // already in (type, id) order (a kNone type would sort last: none is a link)
+      (void)tbits;
       RowTable& t = idx.ttab[ar];
       t.arity = (int)ar;
       t.rows = R;
@@ -1251,7 +1323,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
         hipLaunchKernelGGL(k_u32_key, G(R), dim3(B), 0, s, (const uint32_t*)idx.ctype, (const uint32_t*)perm.p, R, key.p);
       }
       const int cbits = bits_for(n_ctypes ? n_ctypes - 1 : 0);
-      radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, cbits > 0 ? cbits : 1, s);
+      if (!keys_sorted(key.p, R, s)) radix_sort_pairs<uint32_t>(key.p, perm.p, R, 0, cbits > 0 ? cbits : 1, s);
       RowTable& t = idx.ctab[ar];
       t.arity = (int)ar;
       t.rows = R;

@@ -2293,6 +2293,7 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
 namespace {
 constexpr int kChainStages = 8;
 constexpr uint32_t kChainCap = 32768;                 // rows per speculative table
+constexpr uint32_t kChainIjRows = kIjSmall;           // probe rows an index-join stage takes in the chain
 constexpr uint64_t kChainJoinPairs = 1ull << 22;      // cross-join work bound (pairs)
 
 enum : uint32_t { CH_SCAN = 1, CH_IJ = 2, CH_JOIN = 3, CH_ANTI = 4, CH_DEDUP = 5 };
@@ -2423,10 +2424,13 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
     } else if (st.op == CH_IJ) {
       // the probe in chunks of kIjSmall rows (the LDS prefix): lookups, a
       // block scan of the match counts, the chunk's outputs appended in
-      // probe order
+      // probe order.  Inputs above kChainIjRows end the chain instead: one
+      // workgroup expanding them lost to the multi-workgroup index join
+      // (FlyBase F5 / F7 at hub genes, profiles/r2_flybase_host_split.json)
       const uint32_t nin = s_cnt[st.in];
       const int wave = threadIdx.x >> 6;
       uint32_t outn = 0;
+      if (nin > kChainIjRows) ok = false;
       for (uint32_t c0 = 0; c0 < nin && ok; c0 += kIjSmall) {
         const uint32_t cn = nin - c0 < kIjSmall ? nin - c0 : kIjSmall;
         lookups_small(st.key, st.kx, st.g, cn, s_lo, s_pre, c0);
@@ -3071,7 +3075,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
-    ProfScope ps(c, "k_dj_filt<flag>", 12.0 * A.nrows + 5.0 * total);
+    ProfScope ps(c, "k_dj_filt<0>", 12.0 * A.nrows + 5.0 * total);
     hipLaunchKernelGGL(k_dj_filt<0>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
                        (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p,
                        (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
@@ -3082,7 +3086,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   out->nrows = m;
   if (m) {
     // + the probe columns, the flags, the kept outputs' build rows and their columns out
-    ProfScope ps(c, "k_dj_filt<write>",
+    ProfScope ps(c, "k_dj_filt<1>",
                  (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
     hipLaunchKernelGGL(k_dj_filt<1>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
                        (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,

@@ -104,3 +104,37 @@ def test_gpu_hub_fullsize_counts():
     assert want["H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)"] > 10_000_000
     for name, spec in bench.hub_specs():
         assert _count(db, spec) == want[name], name
+
+
+def test_gpu_build_fullsize_incoming_sets():
+    """Config 4 at BASELINE size (10^9 links generated in HBM): the incoming
+    CSR (`incomming_set:<target>`, canonical_parser.py:141-143) of nodes
+    sampled across the Zipf ranks equals what the generator's arrays imply --
+    one entry per (distinct link, position) holding the node -- comes out
+    sorted by link id, and every listed link targets the node."""
+    import torch
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    n_nodes, n_links = 1 << 27, 1_000_000_000
+    db = HipDB(device=0)
+    arrays = synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links)
+    db.load_arrays(arrays)
+    base = len(arrays.type_names)
+    c2 = int(arrays.level_off[1])
+    ch2 = arrays.expr_child[:3 * c2].view(-1, 3)
+    ch3 = arrays.expr_child[3 * c2:].view(-1, 4)
+    for rank in (3, 10, 100, 1000, 100_000, 10_000_000, n_nodes - 1):
+        x = base + rank
+        want = 0
+        for ch in (ch2, ch3):
+            rows = ch[(ch[:, 1:] == x).any(dim=1)]
+            if rows.shape[0]:
+                rows = torch.unique(rows, dim=0)               # one atom per distinct link
+                want += int((rows[:, 1:] == x).sum())
+        nid = int(db.ids_of([db.get_node_handle("Concept", f"n{rank}")])[0])
+        assert nid >= 0, rank
+        got = db.ctx.incoming(nid)
+        assert got.shape[0] == want, (rank, got.shape[0], want)
+        assert np.all(got[1:] >= got[:-1]), rank                # sorted by link id
+        for lid in got[np.linspace(0, len(got) - 1, min(len(got), 200)).astype(np.int64)] if len(got) else []:
+            assert nid in db.ctx.link_targets(int(lid)), (rank, int(lid))

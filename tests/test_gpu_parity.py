@@ -511,8 +511,9 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
 @pytest.mark.parametrize("fused", ["1", "0"])
 def test_gpu_chain_large_index_join_stage(fused, monkeypatch):
     """Fused single-launch And (k_chain) whose index-join stages probe more
-    rows than one LDS prefix (kIjSmall = 2048): the stage runs in chunks and
-    appends their outputs in probe order; against the oracle and the
+    rows than one LDS prefix (kIjSmall = 2048): the chain ends after the
+    last stage it completed and the host continues the And operator by
+    operator (the partial-chain path); against the oracle and the
     per-operator path (DAS_FUSED=0)."""
     from das_amd import loader
     monkeypatch.setenv("DAS_FUSED", fused)

@@ -1,9 +1,7 @@
 #!/bin/bash
-# Scratch session (run through gpurun): the whole GPU suite, then one bench
-# line per workload (no profiler).  Each GPU step has its own time limit.
+# Scratch session (run through gpurun): FlyBase host profile.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread --durations=10 > gpurun_out/t_all.txt 2>&1 &&
-for w in hub bio flybase build; do
-  timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline --no-materialise > gpurun_out/b_$w.json 2> gpurun_out/b_$w.err || exit 1
-done
+timeout -k 10 300 python bench.py --workload flybase --steps 20 --warmup 3 --no-cpu-baseline --no-materialise --cprofile gpurun_out/fb_cprofile.txt > gpurun_out/fb_cp.json 2> gpurun_out/fb_cp.err &&
+timeout -k 10 300 python tools/host_split.py > gpurun_out/host_split.json 2> gpurun_out/host_split.err &&
+DAS_TRACE=1 timeout -k 10 300 python tools/trace_plan.py > gpurun_out/trace_plan.out 2> gpurun_out/trace_plan.txt
