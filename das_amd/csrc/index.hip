@@ -403,7 +403,7 @@ __global__ void k_rep_missing(const uint32_t* rep, uint64_t n, uint32_t* bad) {
 // named-type cluster key of a temp (digest-order) id; kNone types last
 __global__ void k_temp_type(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, uint64_t n_leaf,
                             const uint32_t* leaf_ctype, const uint32_t* leaf_type_id, const uint64_t* expr_off,
-                            const uint32_t* expr_child, uint32_t n_types, uint32_t* key) {
+                            const uint32_t* expr_child, uint32_t n_types, uint32_t degree_bits, uint32_t* key) {
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n_atoms; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = rep[t];
     uint32_t ty = kNone;
@@ -412,7 +412,51 @@ __global__ void k_temp_type(uint64_t n_atoms, const uint32_t* rep, const uint32_
     } else if (catmax[t] == PRIO_LINK || catmax[t] == PRIO_REMOTE) {
       ty = leaf_type_id[expr_child[expr_off[u - n_leaf]]];
     }
-    key[t] = ty == kNone ? n_types : ty;
+    const uint32_t k = ty == kNone ? n_types : ty;
+    // degree_bits = 5: (type, 31) -- the bucket of an atom with no sampled
+    // reference; k_run_bucket lowers it for the referenced ones
+    key[t] = degree_bits ? (k << 5) | 31u : k;
+  }
+}
+
+// References to each unified index from link expressions (kinds 1 and 3:
+// every rank of a sharded KB holds all of them, so all ranks count alike),
+// counted without same-address atomics (a hub is referenced 10^8 times):
+// every stride-th link writes its targets into fixed slots (kNone padding),
+// the slots are radix-sorted, and each run of equal targets adds its length
+// once (one atomic per run end and per run start).
+__global__ void k_ref_sample(const uint8_t* expr_kind, const uint64_t* off, const uint32_t* child, uint64_t n_expr,
+                             uint64_t stride, uint64_t n_samp, uint32_t* slots) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n_samp; s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = s * stride;
+    uint32_t* o = slots + s * kMaxArity;
+    uint32_t k = 0;
+    if (j < n_expr && (expr_kind[j] == 1 || expr_kind[j] == 3)) {
+      const uint64_t b = off[j] + 1, e = off[j + 1];
+      for (uint64_t c = b; c < e && k < (uint32_t)kMaxArity; ++c) o[k++] = child[c];
+    }
+    for (; k < (uint32_t)kMaxArity; ++k) o[k] = kNone;
+  }
+}
+// after k_temp_type: each sampled run's atom (temp id through local2id) takes
+// the bucket 31 - floor(log2(count + 1)) in its key's low 5 bits; copies of
+// one atom keep the largest count (atomicMin: deterministic)
+__global__ void k_run_bucket(const uint32_t* key, uint64_t n, const uint32_t* cnt, const uint32_t* local2id,
+                             uint32_t* tkey) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = key[i];
+    if (u == kNone || (i + 1 < n && key[i + 1] == u)) continue;    // run ends only
+    const uint32_t t = local2id[u];
+    if (t == kNone) continue;
+    atomicMin(&tkey[t], (tkey[t] & ~31u) | (uint32_t)__clz((int)(cnt[u] + 1u)));
+  }
+}
+__global__ void k_run_count(const uint32_t* key, uint64_t n, uint32_t* cnt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = key[i];
+    if (k == kNone) continue;
+    if (i == 0 || key[i - 1] != k) atomicSub(&cnt[k], (uint32_t)i);
+    if (i + 1 == n || key[i + 1] != k) atomicAdd(&cnt[k], (uint32_t)(i + 1));
   }
 }
 
@@ -1093,20 +1137,57 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
   }
   first.release(); scan.release(); list.release();
 
-  // 3b. final ids clustered by named type (digest order inside a type), so a
-  // variable's bindings occupy a compact id range (direct-address joins);
-  // by_digest keeps the digest order for handle lookups.
+  // 3b. final ids clustered by named type, so a variable's bindings occupy a
+  // compact id range (direct-address joins); inside a type, atoms referenced
+  // more often come first (a power-of-two bucket of their reference count,
+  // then digest order), so the hot keys of a power-law KB share a few cache
+  // lines of any id-indexed bitmap or directory.  by_digest keeps the digest
+  // order for handle lookups.  DAS_DEGREE_ORDER=0: digest order inside a type.
   {
     DBuf<uint32_t> tkey(n_atoms ? n_atoms : 1, s), perm(n_atoms ? n_atoms : 1, s);
+    const char* dg = std::getenv("DAS_DEGREE_ORDER");
+    const bool degree = !(dg && dg[0] == '0') && ne > 0;
     if (n_atoms) {
+      DBuf<uint32_t> cnt, slots;
+      uint64_t n_slots = 0;
+      if (degree) {
+        // every link below 2^22 targets, else every 64th link (the bucket only
+        // orders; a hub stays a hub in any sample)
+        const uint64_t stride = n_child < (1ull << 22) ? 1 : 64;
+        const uint64_t n_samp = (ne + stride - 1) / stride;
+        n_slots = n_samp * kMaxArity;
+        cnt.alloc(nu, s);
+        fill_dev(cnt.p, 0, 4 * nu, s);
+        slots.alloc(n_slots, s);
+        {
+          KScope ks("k_ref_sample", 21.0 * n_samp + 4.0 * n_slots);
+          hipLaunchKernelGGL(k_ref_sample, G(n_samp), dim3(B), 0, s, (const uint8_t*)p_ekind, (const uint64_t*)p_eoff,
+                             (const uint32_t*)p_child, ne, stride, n_samp, slots.p);
+        }
+        radix_sort_pairs<uint32_t>(slots.p, nullptr, n_slots, 0, 32, s);
+        {
+          KScope ks("k_run_count", 8.0 * n_slots);
+          hipLaunchKernelGGL(k_run_count, G(n_slots), dim3(B), 0, s, (const uint32_t*)slots.p, n_slots, cnt.p);
+        }
+        DAS_HIP(hipGetLastError());
+      }
       {
         KScope ks("k_temp_type", 24.0 * n_atoms);    // rep, catmax, a type lookup, key out
         hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                            (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
-                           (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, tkey.p);
+                           (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, degree ? 5u : 0u, tkey.p);
       }
+      if (degree) {
+        KScope ks("k_run_bucket", 8.0 * n_slots);
+        hipLaunchKernelGGL(k_run_bucket, G(n_slots), dim3(B), 0, s, (const uint32_t*)slots.p, n_slots,
+                           (const uint32_t*)cnt.p, (const uint32_t*)local2id.p, tkey.p);
+        DAS_HIP(hipGetLastError());
+        slots.release();
+        cnt.release();
+      }
+      const int kbits = std::max(1, bits_for(a.n_types)) + (degree ? 5 : 0);
       iota(perm.p, n_atoms, s);
-      radix_sort_pairs<uint32_t>(tkey.p, perm.p, n_atoms, 0, std::max(1, bits_for(a.n_types)), s);
+      radix_sort_pairs<uint32_t>(tkey.p, perm.p, n_atoms, 0, kbits, s);
     }
     idx.by_digest = dalloc<uint32_t>(idx, n_atoms);
     DBuf<uint32_t> rep2(n_atoms ? n_atoms : 1, s), cat2(n_atoms ? n_atoms : 1, s);
@@ -1124,7 +1205,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
     catmax = std::move(cat2);
   }
 
-  // 4. atom arrays (id order: named type, then handle)
+  // 4. atom arrays (id order: named type, reference bucket, handle)
   idx.n_atoms = n_atoms;
   idx.n_types = a.n_types;
   idx.digest = dalloc<Digest>(idx, n_atoms);

@@ -853,7 +853,9 @@ struct FiltKey {
   const uint32_t* bits;
 };
 
-template <int MODE>
+// NPC / NBC: the probe / build output column counts when specialised (the
+// pointers then live in registers), -1 = read from jc at run time
+template <int MODE, int NPC = -1, int NBC = -1>
 __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
@@ -864,6 +866,18 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
+  const uint32_t* pp[4];
+  const uint32_t* bp[4];
+  uint32_t* po[4];
+  uint32_t* bo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pp[i] = i < ncp ? jc.p[i] : nullptr;
+    bp[i] = i < ncb ? jc.b[i] : nullptr;
+    po[i] = i < ncp && MODE == 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
+    bo[i] = i < ncb && MODE == 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+  }
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * kBalChunk;
     const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
@@ -905,7 +919,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
         if (MODE == 1) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (i < jc.np) pv[i] = r < np ? jc.p[i][r] : 0u;
+            if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
         }
         // kXUnroll rounds of 64 outputs resolved before their loads issue
         for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
@@ -949,7 +963,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
 #pragma unroll
             for (int q = 0; q < kXUnroll; ++q)
 #pragma unroll
-              for (int i = 0; i < 4; ++i) bv[q][i] = (i < jc.nb && f[q]) ? jc.b[i][br[q]] : 0u;
+              for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
 #pragma unroll
             for (int q = 0; q < kXUnroll; ++q) {
               if (q >= nr) continue;
@@ -958,14 +972,14 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
               run += (uint32_t)__popcll(m);
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
-                if (i >= jc.np) break;
+                if (i >= ncp) break;
                 const uint32_t x = lane_get(pv[i], ll[q]);
-                if (f[q]) out[(uint64_t)jc.po[i] * cap + pos] = x;
+                if (f[q]) po[i][pos] = x;
               }
               if (f[q]) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                  if (i < jc.nb) out[(uint64_t)jc.bo[i] * cap + pos] = bv[q][i];
+                  if (i < ncb) bo[i][pos] = bv[q][i];
               }
             }
           }
@@ -2903,6 +2917,36 @@ __global__ void k_bits_set(const uint32_t* __restrict__ key, uint64_t n, uint32_
   }
   if (__ballot(d) && __lane_id() == 0) atomicOr(dup, 1u);
 }
+// Same for a SORTED key column: lanes of a wave whose keys share a bitmap
+// word are contiguous, so a segmented OR scan (duplicates show up as bits
+// already present) leaves one atomic per word segment -- hub keys sit in
+// adjacent ids, and per-key atomics on their few words would serialise.
+__global__ void k_bits_set_sorted(const uint32_t* __restrict__ key, uint64_t n, uint32_t kmin, uint32_t range,
+                                  uint32_t* bits, uint32_t* dup) {
+  const int lane = __lane_id();
+  uint32_t d = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {     // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t k = i < n ? key[i] - kmin : 0xFFFFFFFFu;
+    const bool act = k < range;
+    const uint32_t w = act ? k >> 5 : 0xFFFFFFFFu;
+    uint32_t m = act ? 1u << (k & 31) : 0u;
+#pragma unroll
+    for (int st = 1; st < 64; st <<= 1) {
+      const uint32_t om = (uint32_t)__shfl_up(m, st, 64), ow = (uint32_t)__shfl_up(w, st, 64);
+      if (lane >= st && ow == w && act) {
+        if (om & (1u << (k & 31))) d = 1;              // another lane of the segment holds this key
+        m |= om;
+      }
+    }
+    const uint32_t nw = (uint32_t)__shfl_down(w, 1, 64);
+    const bool tail = act && (lane == 63 || nw != w);
+    if (tail && (atomicOr(&bits[w], m) & m)) d = 1;
+  }
+  if (__ballot(d) && __lane_id() == 0) atomicOr(dup, 1u);
+}
+
 struct BitsPred {
   const uint32_t* key;
   uint32_t kmin, range;
@@ -2982,8 +3026,12 @@ bool key_bits(Ctx& c, const std::vector<const Table*>& Qs, int32_t var, uint64_t
     fill_dev(bits, 0, 4 * (words + 1), c.s);
     {
       ProfScope ps(c, "join_build", 4.0 * Qs[i]->nrows + 4.0 * words);
-      hipLaunchKernelGGL(k_bits_set, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0), Qs[i]->nrows,
-                         (uint32_t)lo, (uint32_t)range, bits, bits + words);
+      if (Qs[i]->sorted_col == 0)
+        hipLaunchKernelGGL(k_bits_set_sorted, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, bits + words);
+      else
+        hipLaunchKernelGGL(k_bits_set, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, bits + words);
       DAS_HIP(hipGetLastError());
     }
     if (read_u32(bits + words, c.s)) return false;          // duplicate keys: counts matter
@@ -3088,9 +3136,15 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     // + the probe columns, the flags, the kept outputs' build rows and their columns out
     ProfScope ps(c, "k_dj_filt<1>",
                  (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
-    hipLaunchKernelGGL(k_dj_filt<1>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
-                       (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,
-                       (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap);
+#define FILT_W(NPV, NBV)                                                                                     \
+  hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV>), dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
+                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,        \
+                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap)
+    if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1);
+    else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1);
+    else if (jc.np == 1 && jc.nb == 2) FILT_W(1, 2);
+    else FILT_W(-1, -1);
+#undef FILT_W
     DAS_HIP(hipGetLastError());
   }
   out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;

@@ -70,8 +70,10 @@ def test_gpu_composite_kernel_matches_hashlib(k):
 
 # ------------------------------------------------------------ index build
 
+@pytest.mark.parametrize("degree", ["1", "0"])
 @pytest.mark.parametrize("fixture", KB_FIXTURES)
-def test_gpu_index_reproduces_reference_atoms(golden, fixture):
+def test_gpu_index_reproduces_reference_atoms(golden, fixture, degree, monkeypatch):
+    monkeypatch.setenv("DAS_DEGREE_ORDER", degree)
     d, db = _fixture_db(golden, fixture)
     assert list(db.count_atoms()) == d["count_atoms"]
     dig, cat, ar, ty, nl = db._host_mirror()
@@ -80,9 +82,17 @@ def test_gpu_index_reproduces_reference_atoms(golden, fixture):
     assert len(set(hexes)) == len(hexes)
     named = [int(ty[i]) if cat[i] in (1, 2) else 1 << 32 for i in range(len(hexes))]
     assert named == sorted(named)                                  # ids clustered by named type
-    for t in set(named):                                           # handle order inside a type
+    # inside a type: atoms referenced more often first (power-of-two bucket of
+    # the link-target references, exact below 2^22 of them), then handle order;
+    # DAS_DEGREE_ORDER=0: handle order only
+    refs = {}
+    for l in d["links"]:
+        for t in l[2]:
+            refs[t] = refs.get(t, 0) + 1
+    bucket = lambda h: -int(np.floor(np.log2(refs.get(h, 0) + 1))) if degree == "1" else 0  # noqa: E731
+    for t in set(named):
         grp = [h for h, k in zip(hexes, named) if k == t]
-        assert grp == sorted(grp)
+        assert grp == sorted(grp, key=lambda h: (bucket(h), h))
     assert db.ids_of(hexes).tolist() == list(range(len(hexes)))
     nodes = sorted([h, db.arrays.type_names[int(ty[i])], db.arrays.node_name(int(nl[i]))]
                    for i, h in enumerate(hexes) if cat[i] == 1)
