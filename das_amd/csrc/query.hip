@@ -3123,7 +3123,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
-    ProfScope ps(c, "k_dj_filt<0>", 12.0 * A.nrows + 5.0 * total);
+    ProfScope ps(c, "k_dj_filt<0,-1,-1>", 12.0 * A.nrows + 5.0 * total);
     hipLaunchKernelGGL(k_dj_filt<0>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
                        (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p,
                        (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
@@ -3134,7 +3134,10 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   out->nrows = m;
   if (m) {
     // + the probe columns, the flags, the kept outputs' build rows and their columns out
-    ProfScope ps(c, "k_dj_filt<1>",
+    // (named as rocprof names the instantiation launched below)
+    const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
+    ProfScope ps(c, spec ? "k_dj_filt<1," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ">"
+                         : std::string("k_dj_filt<1,-1,-1>"),
                  (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
 #define FILT_W(NPV, NBV)                                                                                     \
   hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV>), dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
