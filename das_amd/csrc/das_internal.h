@@ -115,9 +115,10 @@ struct Table {
   uint64_t nrows = 0, cap = 0;
   uint32_t* data = nullptr;   // ncols columns of `cap` u32 each
   hipStream_t s = nullptr;
+  bool view = false;          // data points into an index table (not owned; plan-internal only)
   uint32_t* col(int c) const { return data + (uint64_t)c * cap; }
   ~Table() {
-    if (data) cache_free(data);
+    if (data && !view) cache_free(data);
   }
 };
 
@@ -135,6 +136,10 @@ struct PendingEv {
 
 struct Ctx {
   bool prof = false;
+  // while a plan evaluates (das_plan_execute): a predicate-free scan whose
+  // columns are consecutive index columns returns a view of them instead of
+  // a copy; views are materialised before a table leaves the plan
+  int scan_views = 0;
   std::string prof_only;             // non-empty: only scopes of this name record events
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;   // recycled timing events (creation is not cheap on ROCm)

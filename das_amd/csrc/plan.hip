@@ -433,13 +433,34 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   Exec ex{c, nodes, n, no_overload};
   DAS_CHECK(ex.next(0) == n, DAS_E_INVALID, "plan: node array is not one expression tree");
   trace_mark("plan");
-  Res r = ex.eval(0);
+  struct Views {                       // scans may return index views while the plan runs
+    Ctx& c;
+    explicit Views(Ctx& cc) : c(cc) {
+      const char* f = std::getenv("DAS_SCAN_VIEWS");       // 0: scans copy (A/B, tests)
+      c.scan_views = !(f && f[0] == '0');
+    }
+    ~Views() { c.scan_views = 0; }
+  };
+  Res r;
+  {
+    Views v(c);
+    r = ex.eval(0);
+  }
   trace_mark("done");
   trace_dump("das_plan_execute");
   PlanOutput out;
   out.matched = r.matched;
   out.negation = r.neg;
-  for (auto& t : r.rel.t) out.tables.push_back(std::move(t));
+  for (auto& t : r.rel.t) {
+    if (t->view) {
+      // a view must not outlive the index: the caller gets a copy
+      auto m = new_table_like(c, *t, t->nrows);
+      m->nrows = t->nrows;
+      for (int k = 0; k < t->ncols; ++k) copy_dev(m->col(k), t->col(k), 4 * t->nrows, c.s);
+      t = std::move(m);
+    }
+    out.tables.push_back(std::move(t));
+  }
   return out;
 }
 

@@ -1273,6 +1273,29 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
   const uint64_t chunks = (n + kChunk - 1) / kChunk;
   DAS_CHECK(chunks < (1ull << 31), DAS_E_UNSUPPORTED, "scan range too large");
   if (sp.all_keep) {
+    if (!sp.unordered && c.scan_views && sp.nout > 0 && (int)sp.nout == ncols) {
+      // consecutive source columns (stride = the index table's column
+      // stride): the scan is a view of rows [begin, end) -- no copy
+      const uint32_t* c0 = sp.col[1 + sp.outpos[0]];
+      const int64_t st = sp.nout > 1 ? sp.col[1 + sp.outpos[1]] - c0 : (int64_t)n;
+      bool ok = st >= (int64_t)n;
+      for (uint32_t k = 1; k < sp.nout && ok; ++k) ok = sp.col[1 + sp.outpos[k]] == c0 + k * st;
+      if (ok) {
+        auto t = new_table(c, kind, 0, vars, 0);
+        t->ncols = ncols;
+        for (int i = 0; i < ncols; ++i) {
+          t->vars[i] = vars[i];
+          t->member[i] = -1;
+          t->lo[i] = 0;
+          t->hi[i] = kNone;
+        }
+        t->view = true;
+        t->data = const_cast<uint32_t*>(c0) + begin;
+        t->cap = (uint64_t)st;
+        t->nrows = n;
+        return t;
+      }
+    }
     auto t = new_table(c, kind, ncols, vars, n);
     t->nrows = n;
     if (!sp.unordered) {   // pure projection
