@@ -702,3 +702,21 @@ def test_gpu_no_overload_matches_oracle(gen):
             assert same(got, want), (q, got.get("n"), want.get("n"))
     finally:
         pm.CONFIG["no_overload"] = O.CONFIG["no_overload"] = False
+
+
+@pytest.mark.parametrize("gen", ["bio", "powerlaw"])
+def test_gpu_scan_views_match_oracle(gen, monkeypatch):
+    """DAS_SCAN_VIEWS=1: predicate-free scans inside a plan are views of the
+    index rows (no copy); the answers, including single-Link ones whose view
+    leaves the plan as a copy, equal the oracle's."""
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_SCAN_VIEWS", "1")
+    arrays = synthetic.bio_kb(300, 60, 4000, 200) if gen == "bio" else \
+        synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    rng = np.random.default_rng(3)
+    for q in _random_queries(rng, arrays, 30):
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
