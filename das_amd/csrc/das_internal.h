@@ -136,10 +136,10 @@ struct PendingEv {
 
 struct Ctx {
   bool prof = false;
-  // while a plan evaluates (das_plan_execute) with DAS_SCAN_VIEWS=1: a
-  // predicate-free scan whose columns are consecutive index columns returns a
-  // view of them instead of a copy; views are materialised before a table
-  // leaves the plan
+  // while a plan evaluates (das_plan_execute): a predicate-free scan whose
+  // columns are consecutive index columns returns a view of them instead of
+  // a copy (2: scans up to kViewRows rows, 1: all, 0: none); views are
+  // materialised before a table leaves the plan
   int scan_views = 0;
   std::string prof_only;             // non-empty: only scopes of this name record events
   std::vector<PendingEv> pending;

@@ -436,10 +436,12 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   struct Views {                       // scans may return index views while the plan runs
     Ctx& c;
     explicit Views(Ctx& cc) : c(cc) {
-      // opt-in (DAS_SCAN_VIEWS=1): ~1-6 % less bio step time, but the And
-      // join then reads its probe side cold from HBM (profiles/r2_ab_views.json)
+      // default (2): views of scans up to kViewRows rows -- a small anchored
+      // range's copy is mostly launch and allocation; a large probe side is
+      // copied, which leaves it MALL-warm for the join that reads it next
+      // (profiles/r2_ab_views.json).  1: always views, 0: never.
       const char* f = std::getenv("DAS_SCAN_VIEWS");
-      c.scan_views = f && f[0] == '1';
+      c.scan_views = f && f[0] == '1' ? 1 : f && f[0] == '0' ? 0 : 2;
     }
     ~Views() { c.scan_views = 0; }
   };

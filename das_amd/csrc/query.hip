@@ -1266,6 +1266,8 @@ std::unique_ptr<Table> run_scan(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t e
   return t;
 }
 
+constexpr uint64_t kViewRows = 1ull << 20;   // scans views by default up to this size (Ctx::scan_views)
+
 std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint64_t end, int kind, int ncols,
                                      const int32_t* vars) {
   const uint64_t n = end > begin ? end - begin : 0;
@@ -1273,7 +1275,8 @@ std::unique_ptr<Table> run_scan_rows(Ctx& c, ScanSpec& sp, uint64_t begin, uint6
   const uint64_t chunks = (n + kChunk - 1) / kChunk;
   DAS_CHECK(chunks < (1ull << 31), DAS_E_UNSUPPORTED, "scan range too large");
   if (sp.all_keep) {
-    if (!sp.unordered && c.scan_views && sp.nout > 0 && (int)sp.nout == ncols) {
+    if (!sp.unordered && c.scan_views && (c.scan_views == 1 || n <= kViewRows) && sp.nout > 0 &&
+        (int)sp.nout == ncols) {
       // consecutive source columns (stride = the index table's column
       // stride): the scan is a view of rows [begin, end) -- no copy
       const uint32_t* c0 = sp.col[1 + sp.outpos[0]];
