@@ -95,6 +95,10 @@ _SIGS = {
     "das_hash_fixed_dev": (C.c_int, [P, P, C.c_uint32, C.c_uint64, P]),
     "das_build_index": (C.c_int, [P, C.POINTER(das_atoms_t)]),
     "das_build_index_ex": (C.c_int, [P, C.POINTER(das_atoms_t), C.c_uint32]),
+    "das_build_index_sharded": (C.c_int, [P, C.POINTER(das_atoms_t), C.c_uint32, C.c_uint32, C.c_uint32]),
+    "das_hash_owners": (C.c_int, [P, C.POINTER(das_atoms_t), C.c_uint32, C.c_uint32, P]),
+    "das_partition_rows": (C.c_int, [P, P, C.c_uint64, C.c_uint32, P, C.c_uint32, P, P]),
+    "das_numbered_strings": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint64, P, P]),
     "das_synth_powerlaw_links": (C.c_int, [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, C.c_uint64, C.c_double, C.c_uint64]),
     "das_index_stats": (C.c_int, [P, C.POINTER(das_index_stats_t)]),
@@ -226,6 +230,18 @@ def parse_canonical(texts, threads=0):
         lib().das_parsed_free(h)
 
 
+def numbered_strings(prefix, n, first=0):
+    """(bytes u8 array, n+1 u64 offsets) of prefix + str(first + i), i < n
+    (das_numbered_strings: multi-threaded host C++)."""
+    pre = prefix.encode()
+    last = first + max(n - 1, 0)
+    cap = n * (len(pre) + len(str(last)))
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    off = np.empty(n + 1, dtype=np.uint64)
+    check(lib().das_numbered_strings(pre, len(pre), first, n, ptr(out), ptr(off)))
+    return out[:int(off[-1])], off
+
+
 # ---------------------------------------------------------------------------
 # host hashing helpers (query planning); bulk hashing happens on the GPU
 # ---------------------------------------------------------------------------
@@ -343,10 +359,10 @@ class Context:
         check(fn(self.h, *args, C.byref(out)), self.h)
         return Table(self, out)
 
-    def build_index(self, arrays):
-        """Host arrays (das_build_index), or a KB whose expression arrays are
-        device tensors (`arrays.expr_on_device`, das_build_index_ex)."""
-        a = arrays
+    @staticmethod
+    def _atoms(a):
+        """(das_atoms_t, build flags, buffers to keep alive) of host AtomArrays
+        or of a KB whose expression arrays are device tensors (`expr_on_device`)."""
         dev = bool(getattr(a, "expr_on_device", False))
         eptr = (lambda t: C.c_void_p(t.data_ptr())) if dev else ptr
         keep = [a.leaf_bytes, a.leaf_off, a.leaf_kind, a.leaf_ctype, a.leaf_type_id, a.expr_off,
@@ -357,11 +373,36 @@ class Context:
             expr_off=eptr(a.expr_off), expr_child=eptr(a.expr_child), expr_kind=eptr(a.expr_kind),
             expr_ctype_leaf=eptr(a.expr_ctype_leaf), n_levels=len(a.level_off) - 1, level_off=ptr(a.level_off),
             n_types=len(a.type_names))
-        if dev:
-            check(lib().das_build_index_ex(self.h, C.byref(s), DAS_BUILD_EXPR_ON_DEVICE), self.h)
+        return s, (DAS_BUILD_EXPR_ON_DEVICE if dev else 0), keep
+
+    def build_index(self, arrays, shard=None):
+        """Host arrays (das_build_index), or a KB whose expression arrays are
+        device tensors (`arrays.expr_on_device`, das_build_index_ex).
+        shard=(rank, world): links hash-partitioned by handle, this context
+        indexing the links whose handles `rank` owns (das_build_index_sharded)."""
+        s, flags, keep = self._atoms(arrays)
+        if shard is not None and shard[1] > 1:
+            check(lib().das_build_index_sharded(self.h, C.byref(s), flags, int(shard[0]), int(shard[1])), self.h)
+        elif flags:
+            check(lib().das_build_index_ex(self.h, C.byref(s), flags), self.h)
         else:
             check(lib().das_build_index(self.h, C.byref(s)), self.h)
         del keep
+
+    def hash_owners(self, arrays, world, d_owner):
+        """Owner shard of every expression's handle into device u8 tensor d_owner."""
+        s, flags, keep = self._atoms(arrays)
+        check(lib().das_hash_owners(self.h, C.byref(s), flags, int(world), C.c_void_p(d_owner.data_ptr())), self.h)
+        del keep
+
+    def partition_rows(self, rows, n, k, owner, world, out):
+        """n rows of k u32 (device tensor) regrouped by device u8 `owner` into
+        `out`; returns the per-owner row counts."""
+        counts = np.zeros(world, dtype=np.uint64)
+        check(lib().das_partition_rows(self.h, C.c_void_p(rows.data_ptr()), int(n), int(k),
+                                       C.c_void_p(owner.data_ptr()), int(world), C.c_void_p(out.data_ptr()),
+                                       ptr(counts)), self.h)
+        return counts
 
     def synth_powerlaw_links(self, d_child, first, n, k, n_link_types, type_leaf0, node_leaf0, n_nodes,
                              s=1.1, seed=0):
@@ -439,12 +480,17 @@ class Context:
         """das_plan_execute over n_nodes das_plan_node_t records given as a
         u32 array (51 words each) -> (matched, negation, [Table])."""
         cap = 64
-        out = (P * cap)()
-        n_out, matched, neg = C.c_uint32(), C.c_int32(), C.c_int32()
         nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
-        check(lib().das_plan_execute(self.h, nodes, n_nodes, 1 if no_overload else 0, out, cap, C.byref(n_out),
-                                     C.byref(matched), C.byref(neg)), self.h)
-        return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
+        while True:
+            out = (P * cap)()
+            n_out, matched, neg = C.c_uint32(), C.c_int32(), C.c_int32()
+            rc = lib().das_plan_execute(self.h, nodes, n_nodes, 1 if no_overload else 0, out, cap, C.byref(n_out),
+                                        C.byref(matched), C.byref(neg))
+            if rc == ERR_INVALID and n_out.value > cap:
+                cap = n_out.value          # more answer schemas than slots: run again with room for all
+                continue
+            check(rc, self.h)
+            return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
 
     @staticmethod
     def link_scan_struct(q, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False,

@@ -4,7 +4,7 @@
 #include <string>
 #include <vector>
 
-#include "common.h"
+#include "status.h"
 
 namespace das {
 

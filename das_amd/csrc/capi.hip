@@ -326,6 +326,34 @@ int das_build_index_ex(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags)
   });
 }
 
+int das_build_index_sharded(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags, uint32_t rank,
+                            uint32_t world) {
+  if (!ctx || !atoms) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  if (flags & ~DAS_BUILD_EXPR_ON_DEVICE) return fail(ctx, DAS_ERR_INVALID, "unknown build flags");
+  return guarded(ctx, [&] {
+    BuildHold hold;
+    das::build_index(ctx->c, *atoms, flags, rank, world);
+  });
+}
+
+int das_hash_owners(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags, uint32_t world, uint8_t* d_owner) {
+  if (!ctx || !atoms || (atoms->n_expr && !d_owner)) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  if (flags & ~DAS_BUILD_EXPR_ON_DEVICE) return fail(ctx, DAS_ERR_INVALID, "unknown build flags");
+  return guarded(ctx, [&] { das::hash_owners(ctx->c, *atoms, flags, world, d_owner); });
+}
+
+int das_partition_rows(das_ctx_t* ctx, const uint32_t* d_rows, uint64_t n, uint32_t K, const uint8_t* d_owner,
+                       uint32_t world, uint32_t* d_out, uint64_t* counts) {
+  if (!ctx || !counts || (n && (!d_rows || !d_owner || !d_out))) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] { das::partition_rows(ctx->c, d_rows, n, K, d_owner, world, d_out, counts); });
+}
+
+int das_numbered_strings(const char* prefix, uint64_t plen, uint64_t first, uint64_t n, uint8_t* out,
+                         uint64_t* off) {
+  if ((plen && !prefix) || !off || (n && !out)) return fail(nullptr, DAS_ERR_INVALID, "null argument");
+  return guarded(nullptr, [&] { das::numbered_strings(prefix, plen, first, n, out, off); });
+}
+
 int das_synth_powerlaw_links(das_ctx_t* ctx, uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K,
                              uint32_t n_link_types, uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes,
                              double s, uint64_t seed) {
@@ -620,6 +648,7 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
                      das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation) {
   return guarded(ctx, [&] {
     auto r = das::plan_execute(ctx->c, nodes, n, (int)no_overload);
+    *n_out = (uint32_t)r.tables.size();     // on overflow: the capacity the caller needs
     DAS_CHECK(r.tables.size() <= cap, das::DAS_E_INVALID, "plan: more answer tables than `cap`");
     for (size_t i = 0; i < r.tables.size(); ++i) out[i] = wrap(std::move(r.tables[i]));
     *n_out = (uint32_t)r.tables.size();

@@ -7,39 +7,19 @@
 #include <string>
 #include <vector>
 
+#include "status.h"
+
 namespace das {
 
 constexpr int kWave = 64;          // CDNA wavefront width
-constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-struct Error : std::runtime_error {
-  int code;
-  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-enum Status : int {
-  DAS_S_OK = 0,
-  DAS_E_INVALID = -1,     // bad argument / misuse          -> ValueError
-  DAS_E_HIP = -2,         // HIP runtime failure            -> RuntimeError
-  DAS_E_NOT_BUILT = -3,   // index not built                -> RuntimeError
-  DAS_E_UNSUPPORTED = -4, // shape outside this build       -> NotImplementedError
-  DAS_E_INTERNAL = -5,
-  DAS_E_ATTRIBUTE = -6,   // the reference raises AttributeError here -> AttributeError
-  DAS_E_SYNTAX = -7,      // malformed input where the reference asserts -> AssertionError
-};
-
-#define DAS_HIP(expr)                                                              \
+#define DAS_HIP(expr)                                                            \
   do {                                                                             \
     hipError_t _e = (expr);                                                        \
     if (_e != hipSuccess)                                                          \
       throw ::das::Error(::das::DAS_E_HIP, std::string(#expr) + ": " +             \
                                                hipGetErrorString(_e) + " at " +    \
                                                __FILE__ + ":" + std::to_string(__LINE__)); \
-  } while (0)
-
-#define DAS_CHECK(cond, code, msg)                 \
-  do {                                             \
-    if (!(cond)) throw ::das::Error((code), (msg)); \
   } while (0)
 
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 8u) {
@@ -121,5 +101,14 @@ struct Digest {
     return ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
   }
 };
+
+// Shard that owns a handle when links are hash-partitioned by handle across
+// `world` GPUs: the handle's first 8 hex characters as a
+// number (int(handle[:8], 16), the digest's first four bytes big-endian), mod
+// world.  Every copy of one expression has one digest, so exactly one shard
+// indexes it.
+__host__ __device__ inline uint32_t handle_owner(const Digest& d, uint32_t world) {
+  return world > 1 ? __builtin_bswap32(d.w[0]) % world : 0u;
+}
 
 }  // namespace das

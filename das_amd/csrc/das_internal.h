@@ -208,7 +208,17 @@ void hash_group(Digest* table, Digest* ctab, const uint32_t* child, const uint64
 void hash_fixed(const Digest* elems, uint32_t k, uint64_t n, Digest* out, hipStream_t s);
 
 // index.hip
-void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags);
+// shard_rank / shard_world > 1: a link (expr kind 1 or 3) gets pattern-index
+// rows iff handle_owner(its digest, world) == rank, else it is directory-only
+// (links hash-partitioned by handle); world 1: kinds as given.
+void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_rank = 0, uint32_t shard_world = 1);
+// Owning shard of every expression's handle (hashes leaves and expressions as
+// the build does, step 1); d_owner: n_expr device bytes.
+void hash_owners(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t world, uint8_t* d_owner);
+// Rows (K u32 each) regrouped by owner, stable inside an owner; counts[world].
+void partition_rows(Ctx& c, const uint32_t* d_rows, uint64_t n, uint32_t K, const uint8_t* d_owner, uint32_t world,
+                    uint32_t* d_out, uint64_t* counts);
+void numbered_strings(const char* prefix, uint64_t plen, uint64_t first, uint64_t n, uint8_t* out, uint64_t* off);
 void synth_powerlaw_links(uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K, uint32_t n_link_types,
                           uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes, double s, uint64_t seed,
                           hipStream_t st);

@@ -206,23 +206,75 @@ __global__ void k_leaf_ctype(const Digest* dig, const uint32_t* leaf_ctype, Dige
 }
 
 // flag/catl over unified indices: nodes, links, and anything a link targets.
-__global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, uint64_t n_leaf, uint64_t n_expr,
-                           uint8_t* catl, uint32_t* flag) {
+// world > 1: a link's category comes from its handle's owner (indexed here iff
+// handle_owner == rank), so every copy of one handle agrees on every shard.
+__global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, const Digest* dig, uint64_t n_leaf,
+                           uint64_t n_expr, uint32_t rank, uint32_t world, uint8_t* catl, uint32_t* flag) {
   const uint64_t n = n_leaf + n_expr;
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x) {
     uint8_t c = PRIO_OTHER;
     uint32_t f = 0;
     if (u < n_leaf) {
       if (leaf_kind[u] == 1) { c = PRIO_NODE; f = 1; }
-    } else if (expr_kind[u - n_leaf] == 1) {
-      c = PRIO_LINK;
-      f = 1;
-    } else if (expr_kind[u - n_leaf] == 3) {
-      c = PRIO_REMOTE;
-      f = 1;
+    } else {
+      const uint8_t k = expr_kind[u - n_leaf];
+      if (k == 1 || k == 3) {
+        const bool own = world > 1 ? handle_owner(dig[u], world) == rank : k == 1;
+        c = own ? PRIO_LINK : PRIO_REMOTE;
+        f = 1;
+      }
     }
     catl[u] = c;
     flag[u] = f;
+  }
+}
+
+__global__ void k_expr_owner(const Digest* dig, uint64_t n_leaf, uint64_t n_expr, uint32_t world, uint8_t* owner) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_expr; j += (uint64_t)gridDim.x * blockDim.x)
+    owner[j] = (uint8_t)handle_owner(dig[n_leaf + j], world);
+}
+
+// partition_rows: per-block owner histograms (block-major), then a stable
+// scatter.  One wave's rows go out in lane order per owner (ballot prefix),
+// waves of a block in order through an LDS running count.
+constexpr int kPartMaxWorld = 64;
+__global__ void __launch_bounds__(256) k_owner_hist(const uint8_t* owner, uint64_t n, uint32_t world, uint64_t per_block,
+                                                    uint32_t* hist) {
+  __shared__ uint32_t h[kPartMaxWorld];
+  for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) h[w] = 0;
+  __syncthreads();
+  const uint64_t b = blockIdx.x * per_block, e = b + per_block < n ? b + per_block : n;
+  for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) atomicAdd(&h[owner[i]], 1u);
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) hist[(uint64_t)w * gridDim.x + blockIdx.x] = h[w];
+}
+
+__global__ void __launch_bounds__(256) k_owner_scatter(const uint32_t* rows, const uint8_t* owner, uint64_t n,
+                                                       uint32_t K, uint32_t world, uint64_t per_block,
+                                                       const uint32_t* off, uint32_t* out) {
+  __shared__ uint32_t base[kPartMaxWorld];
+  for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) base[w] = off[(uint64_t)w * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint64_t b = blockIdx.x * per_block, e = b + per_block < n ? b + per_block : n;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t t = b; t < e; t += blockDim.x) {
+    const uint64_t i = t + threadIdx.x;
+    const uint32_t o = i < e ? owner[i] : 0xFFu;
+    // waves of the block take their turn so rows stay in input order
+    for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) {
+      if (wv == wave) {
+        for (uint32_t w = 0; w < world; ++w) {
+          const uint64_t m = __ballot(o == w);
+          if (!m) continue;
+          if (o == w) {
+            const uint64_t dst = (uint64_t)base[w] + __popcll(m & ((1ull << lane) - 1));
+            for (uint32_t k = 0; k < K; ++k) out[dst * K + k] = rows[i * K + k];
+          }
+          if (lane == 0) base[w] += (uint32_t)__popcll(m);
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -990,9 +1042,101 @@ bool keys_sorted(const uint32_t* key, uint64_t n, hipStream_t s) {
   DAS_HIP(hipGetLastError());
   return read_u32(bad.p, s) == 0;
 }
+// Step 1 of the build: md5 of every leaf string, composite_hash of every
+// expression level by level (children first), and the composite types.
+void hash_all(Ctx& c, const das_atoms_t& a, bool dev_expr, const uint8_t* d_bytes, const uint64_t* d_loff,
+              const uint32_t* d_lct, const uint32_t* p_child, const uint64_t* p_eoff, const int32_t* p_ectl,
+              Digest* dig, Digest* ct) {
+  hipStream_t s = c.s;
+  const uint64_t nl = a.n_leaf;
+  {
+    ProfScope ps(c, "k_hash_strings", (double)a.leaf_off[nl] + 8.0 * nl + 16.0 * nl);
+    hash_strings(d_bytes, d_loff, nl, dig, s);
+  }
+  if (nl) {
+    KScope ks("k_leaf_ctype", 36.0 * nl);
+    hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig, d_lct, ct, nl);
+  }
+  for (uint32_t g = 0; g < a.n_levels; ++g) {
+    const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
+    if (e <= b) continue;
+    uint32_t K;
+    if (dev_expr) {
+      uint64_t o[2];
+      read_u64x2(a.expr_off + b, s, o);
+      K = (uint32_t)(o[1] - o[0]);
+    } else {
+      K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
+    }
+    // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
+    ProfScope ps(c, K <= 9 ? "k_hash_group<" + std::to_string(K) + ">" : std::string("k_hash_group_dyn"),
+                 (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
+    hash_group(dig, ct, p_child, p_eoff, p_ectl, nl, b, e - b, K, s);
+  }
+}
 }  // namespace
 
-void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
+void hash_owners(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t world, uint8_t* d_owner) {
+  DAS_CHECK(world >= 1 && world <= 256, DAS_E_INVALID, "bad world size");
+  const bool dev_expr = (flags & DAS_BUILD_EXPR_ON_DEVICE) != 0;
+  hipStream_t s = c.s;
+  const uint64_t nl = a.n_leaf, ne = a.n_expr, nu = nl + ne;
+  DAS_CHECK(nu > 0 && nu < 0xFFFFFFF0ull, DAS_E_INVALID, "atom count out of range");
+  if (!ne) return;
+  const uint64_t n_child = dev_expr ? read_u64(a.expr_off + ne, s) : a.expr_off[ne];
+  auto d_bytes = upload(a.leaf_bytes, a.leaf_off[nl], s);
+  auto d_loff = upload(a.leaf_off, nl + 1, s);
+  auto d_lct = upload(a.leaf_ctype, nl, s);
+  DBuf<uint64_t> d_eoff;
+  DBuf<uint32_t> d_child;
+  DBuf<int32_t> d_ectl;
+  if (!dev_expr) {
+    d_eoff = upload(a.expr_off, ne + 1, s);
+    d_child = upload(a.expr_child, n_child, s);
+    d_ectl = upload(a.expr_ctype_leaf, ne, s);
+  }
+  ProfScope whole(c, "hash_owners", 0.0);
+  DBuf<Digest> dig(nu, s), ct(nu, s);
+  hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, dev_expr ? a.expr_child : d_child.p,
+           dev_expr ? a.expr_off : d_eoff.p, dev_expr ? a.expr_ctype_leaf : d_ectl.p, dig.p, ct.p);
+  KScope ks("k_expr_owner", 17.0 * ne);
+  hipLaunchKernelGGL(k_expr_owner, G(ne), dim3(B), 0, s, (const Digest*)dig.p, nl, ne, world, d_owner);
+  DAS_HIP(hipGetLastError());
+}
+
+void partition_rows(Ctx& c, const uint32_t* d_rows, uint64_t n, uint32_t K, const uint8_t* d_owner, uint32_t world,
+                    uint32_t* d_out, uint64_t* counts) {
+  DAS_CHECK(world >= 1 && world <= (uint32_t)kPartMaxWorld && K >= 1, DAS_E_INVALID, "partition_rows: bad sizes");
+  hipStream_t s = c.s;
+  for (uint32_t w = 0; w < world; ++w) counts[w] = 0;
+  if (!n) return;
+  ProfScope whole(c, "partition_rows", 0.0);
+  const uint64_t per_block = 4096;
+  const uint64_t nb = (n + per_block - 1) / per_block;
+  DAS_CHECK(nb * world < (1ull << 31) && n < (1ull << 32), DAS_E_UNSUPPORTED, "partition_rows: too many rows");
+  DBuf<uint32_t> hist(nb * world, s), off(nb * world, s);
+  {
+    KScope ks("k_owner_hist", 1.0 * n + 4.0 * nb * world);
+    hipLaunchKernelGGL(k_owner_hist, dim3((unsigned)nb), dim3(256), 0, s, d_owner, n, world, per_block, hist.p);
+  }
+  exclusive_scan<uint32_t>(hist.p, nb * world, off.p, s);
+  {
+    KScope ks("k_owner_scatter", 1.0 * n + 8.0 * K * n);
+    hipLaunchKernelGGL(k_owner_scatter, dim3((unsigned)nb), dim3(256), 0, s, d_rows, d_owner, n, K, world, per_block,
+                       (const uint32_t*)off.p, d_out);
+  }
+  DAS_HIP(hipGetLastError());
+  std::vector<uint32_t> starts(world + 1);
+  for (uint32_t w = 0; w < world; ++w) starts[w] = read_u32(off.p + (uint64_t)w * nb, s);
+  starts[world] = (uint32_t)n;
+  for (uint32_t w = 0; w < world; ++w) counts[w] = starts[w + 1] - starts[w];
+}
+
+namespace {
+}  // namespace
+
+void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_rank, uint32_t shard_world) {
+  DAS_CHECK(shard_world >= 1 && shard_rank < shard_world && shard_world <= 256, DAS_E_INVALID, "bad shard rank/world");
   // DAS_BUILD_EXPR_ON_DEVICE: expr_off / expr_child / expr_kind /
   // expr_ctype_leaf are device pointers (resident input, nothing uploaded)
   const bool dev_expr = (flags & DAS_BUILD_EXPR_ON_DEVICE) != 0;
@@ -1047,38 +1191,15 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags) {
 
   // 1. digests + composite types of every unified index
   DBuf<Digest> dig(nu, s), ct(nu, s);
-  {
-    ProfScope ps(c, "k_hash_strings", (double)n_bytes + 8.0 * nl + 16.0 * nl);
-    hash_strings(d_bytes.p, d_loff.p, nl, dig.p, s);
-  }
-  if (nl) {
-    KScope ks("k_leaf_ctype", 36.0 * nl);
-    hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig.p, (const uint32_t*)d_lct.p, ct.p, nl);
-  }
-  for (uint32_t g = 0; g < a.n_levels; ++g) {
-    const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
-    if (e <= b) continue;
-    uint32_t K;
-    if (dev_expr) {
-      uint64_t o[2];
-      read_u64x2(a.expr_off + b, s, o);
-      K = (uint32_t)(o[1] - o[0]);
-    } else {
-      K = (uint32_t)(a.expr_off[b + 1] - a.expr_off[b]);
-    }
-    // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
-    ProfScope ps(c, K <= 9 ? "k_hash_group<" + std::to_string(K) + ">" : std::string("k_hash_group_dyn"),
-                 (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
-    hash_group(dig.p, ct.p, p_child, p_eoff, p_ectl, nl, b, e - b, K, s);
-  }
+  hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig.p, ct.p);
 
   // 2. which unified indices are atoms (nodes, links, link targets)
   DBuf<uint8_t> catl(nu, s);
   DBuf<uint32_t> flag(nu, s);
   {
     KScope ks("k_init_cat", 1.0 * nu + 5.0 * nu);
-    hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind, nl, ne,
-                       catl.p, flag.p);
+    hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind,
+                       (const Digest*)dig.p, nl, ne, shard_rank, shard_world, catl.p, flag.p);
   }
   if (ne) {
     KScope ks("k_mark_targets", 9.0 * ne + 8.0 * n_child);

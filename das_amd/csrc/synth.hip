@@ -7,6 +7,10 @@
 // Link i (global index) draws every field from a counter-based hash of
 // (seed, i, field), so the KB is the same whatever range a rank generates:
 // the union of the N per-rank ranges is the one-GPU KB.
+#include <cstring>
+#include <thread>
+#include <vector>
+
 #include "das_internal.h"
 
 namespace das {
@@ -67,6 +71,50 @@ void synth_powerlaw_links(uint32_t* d_child, uint64_t first, uint64_t n, uint32_
     default: throw Error(DAS_E_UNSUPPORTED, "synth: arity 2 or 3 only");
   }
   DAS_HIP(hipGetLastError());
+}
+
+// Host: the n strings prefix + decimal(first + i) packed back to back, with
+// n + 1 offsets (the node leaves "Concept n<i>" of configs 4-5; 2^27 of them
+// are ~2.4 GB, written by up to 16 host threads at memory speed).
+void numbered_strings(const char* prefix, uint64_t plen, uint64_t first, uint64_t n, uint8_t* out, uint64_t* off) {
+  auto digits = [](uint64_t v) {
+    int d = 1;
+    while (v >= 10) { v /= 10; ++d; }
+    return d;
+  };
+  // offsets: closed form per digit-length run
+  auto offset_of = [&](uint64_t i) {     // bytes before string i
+    uint64_t total = i * plen, v = first, end = first + i, p = 10;
+    int d = 1;
+    while (v < end) {
+      while (v >= p) { p *= 10; ++d; }
+      const uint64_t run_end = end < p ? end : p;
+      total += (run_end - v) * (uint64_t)d;
+      v = run_end;
+    }
+    return total;
+  };
+  const unsigned T = n < (1u << 16) ? 1u : 16u;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      const uint64_t b = n * t / T, e = n * (t + 1) / T;
+      uint64_t o = offset_of(b);
+      char tmp[24];
+      for (uint64_t i = b; i < e; ++i) {
+        off[i] = o;
+        std::memcpy(out + o, prefix, plen);
+        o += plen;
+        uint64_t v = first + i;
+        const int d = digits(v);
+        for (int k = d - 1; k >= 0; --k) { tmp[k] = (char)('0' + v % 10); v /= 10; }
+        std::memcpy(out + o, tmp, d);
+        o += d;
+      }
+      if (t == T - 1) off[n] = o;
+    });
+  for (auto& x : th) x.join();
+  if (!n) off[0] = 0;
 }
 
 }  // namespace das

@@ -11,6 +11,7 @@ Two extra, non-reference entry points feed the pattern matcher without
 materialising Python tuples: `match_link` and `match_template` return device
 binding tables (`Relation`).
 """
+import itertools
 import os
 import re
 from typing import Any, List, Tuple
@@ -21,6 +22,10 @@ from .. import _lib
 from .. import loader as _loader
 from ..expression_hasher import ExpressionHasher
 from .db_interface import UNORDERED_LINK_TYPES, WILDCARD, DBInterface
+
+# one token per index load of any HipDB in the process: a lowered plan cached on
+# an expression names the load it was lowered against (ids are per load)
+_LOADS = itertools.count(1)
 
 
 class Relation:
@@ -104,6 +109,7 @@ class HipDB(RelationalDB):
         self._node_handles = {}
         self._plan_records = {}
         self.generation = 0
+        self.shard = None
         self._mirror = None
         self.pattern_black_list = []
 
@@ -111,12 +117,16 @@ class HipDB(RelationalDB):
         return "<HipDB>"
 
     # ------------------------------------------------------------------ load
-    def load_arrays(self, arrays: "_loader.AtomArrays"):
+    def load_arrays(self, arrays: "_loader.AtomArrays", shard=None):
         """Hash + intern + index every atom on the GPU (replaces the Mongo
-        insert / key-value files / Redis SADD of canonical_parser.py:111-240)."""
-        self.generation = getattr(self, "generation", 0) + 1      # invalidates lowered query plans
+        insert / key-value files / Redis SADD of canonical_parser.py:111-240).
+        shard=(rank, world) (default: `arrays.shard`, set by
+        parallel.shard_arrays): the whole KB is this rank's atom directory, and
+        only the links whose handle `rank` owns get pattern-index rows."""
+        self.generation = next(_LOADS)      # invalidates lowered query plans (unique across HipDBs)
         self._plan_records = {}
-        self.ctx.build_index(arrays)
+        self.shard = shard if shard is not None else getattr(arrays, "shard", None)
+        self.ctx.build_index(arrays, self.shard)
         self.arrays = arrays
         self.type_id = dict(arrays.type_id)
         self._hex_cache = {}

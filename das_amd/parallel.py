@@ -25,8 +25,6 @@ The collectives go through torch.distributed ("nccl" = RCCL on ROCm, over
 xGMI; "gloo" in the CPU tests).  `local` is a HipDB (or, in tests, a CPU
 double with the same surface).
 """
-import zlib
-
 import os
 
 import numpy as np
@@ -574,14 +572,36 @@ class ShardedMatcher:
 # the whole KB; index rows only for the links it owns)
 # ---------------------------------------------------------------------------
 
-def owner_of(children, world):
-    """Content hash of a link (its type + targets) -> owning rank."""
-    h = np.zeros(children.shape[0], dtype=np.uint64)
-    for c in range(children.shape[1]):
-        x = children[:, c].astype(np.uint64)
-        h = (h * np.uint64(0x100000001B3)) ^ (x * np.uint64(0x9E3779B97F4A7C15))
-    h ^= h >> np.uint64(29)
-    return (h % np.uint64(world)).astype(np.int64)
+def handle_owner(handle, world):
+    """Shard that owns a handle (links hash-partitioned by handle, SURVEY.md
+    §8e): int(handle[:8], 16) % world -- das_amd/csrc/common.h handle_owner."""
+    return int(handle[:8], 16) % world if world > 1 else 0
+
+
+def host_owners(arrays, world, exprs=None):
+    """Owner shard of expressions' handles, hashed on the host (hashlib md5,
+    expression_hasher.py:9-35): the restatement of das_hash_owners for small
+    KBs and the CPU tests.  exprs: the expression indices wanted (default all;
+    their contained expressions are hashed too)."""
+    import hashlib
+    nl, ne = arrays.n_leaf, arrays.n_expr
+    off = arrays.expr_off.astype(np.int64)
+    child = arrays.expr_child.astype(np.int64)
+    want = np.arange(ne) if exprs is None else np.asarray(exprs, dtype=np.int64)
+    memo = {}
+
+    def h(u):
+        r = memo.get(u)
+        if r is None:
+            if u < nl:
+                r = hashlib.md5(bytes(arrays.leaf_bytes[int(arrays.leaf_off[u]):int(arrays.leaf_off[u + 1])])).hexdigest()
+            else:
+                j = u - nl
+                ch = [h(int(c)) for c in child[off[j]:off[j + 1]]]
+                r = ch[0] if len(ch) == 1 else hashlib.md5(" ".join(ch).encode()).hexdigest()
+            memo[u] = r
+        return r
+    return np.array([handle_owner(h(nl + int(j)), world) for j in want], dtype=np.int64)
 
 
 def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
@@ -601,59 +621,38 @@ def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
     child = rng.integers(1, n_bps, n_inh)
     parent = (rng.random(n_inh) * child).astype(np.int64)
     ich = np.stack([total_genes + child, total_genes + parent], 1)
-    own = owner_of(ich, world)
-    blocks.append(("Inheritance", ich, np.where(own == rank, 1, 3).astype(np.uint8)))
+    blocks.append(("Inheritance", ich, np.ones(n_inh, np.uint8)))
     arrays, _ = synthetic.build_arrays(["Member", "Inheritance"],
                                        [("Gene", "g", total_genes), ("BiologicalProcess", "bp", n_bps)], blocks)
+    if world > 1:
+        # Inheritance links by their handle's owner (every rank computes the
+        # same split); Member links by their gene's rank (partition_spec)
+        inh = np.arange(arrays.n_expr - n_inh, arrays.n_expr)
+        kinds = arrays.expr_kind.copy()
+        kinds[inh[host_owners(arrays, world, inh) != rank]] = 3
+        arrays.expr_kind = kinds
     return arrays, np.arange(rank * n_genes, (rank + 1) * n_genes)
 
 
-def content_owner(arrays, world):
-    """Owning rank of every expression, by content: a repeated expression
-    (same type and targets, stored twice, possibly over distinct copies of a
-    nested child) maps to one canonical id first -- children before parents
-    -- so all copies of one handle land on one rank."""
-    nl, ne = arrays.n_leaf, arrays.n_expr
-    off = arrays.expr_off.astype(np.int64)
-    child = arrays.expr_child.astype(np.int64)
-    canon = np.arange(nl + ne, dtype=np.int64)
-    own = np.zeros(ne, dtype=np.int64)
-    nested = np.zeros(ne, dtype=bool)
-    nested[child[child >= nl] - nl] = True
-    for g in range(len(arrays.level_off) - 1):
-        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
-        if e <= b:
-            continue
-        k = int(off[b + 1] - off[b])
-        ch = canon[child[off[b]:off[e]].reshape(e - b, k)]
-        if nested[b:e].any():          # only a contained expression's id reaches a parent's hash
-            _, first, inv = np.unique(ch, axis=0, return_index=True, return_inverse=True)
-            canon[nl + b:nl + e] = nl + b + first[inv.ravel()]
-        own[b:e] = owner_of(ch, world)
-    return own
-
-
 def shard_arrays(arrays, rank, world):
-    """Generic link sharding for a fixed KB (strong scaling): every rank keeps
-    the whole atom directory; a link's pattern-index rows stay on the rank its
-    content hash (type + targets) selects, elsewhere it becomes a remote link
-    (expr kind 3).  Typedef expressions are never sharded."""
-    if world == 1:
-        return arrays
-    kinds = arrays.expr_kind.copy()
-    kinds[(kinds == 1) & (content_owner(arrays, world) != rank)] = 3
-    arrays.expr_kind = kinds
+    """Query layout of a fixed KB over `world` GPUs (strong scaling): every
+    rank loads the whole KB as its atom directory (ids agree across ranks) and
+    indexes only the links whose handle it owns (handle_owner); the build does
+    the split (das_build_index_sharded), so every copy of one handle --
+    repeated expressions, nested children -- lands on one rank."""
+    arrays.shard = (rank, world) if world > 1 else None
     return arrays
 
 
-def partition_arrays(arrays, rank, world):
-    """Independent shards for the bulk build (config 4 at N GPUs): rank r
-    indexes only the links its content hash selects (nested or not), keeps the
-    expressions those links contain so their handles hash, and every leaf.  A
-    contained link owned by another rank stays directory-only (kind 3): each
-    link is indexed on exactly one rank.  Atom ids are then local to the shard
-    (the reference's sharded Redis keys, not the replicated directory
-    ShardedDB queries need)."""
+def partition_arrays(arrays, rank, world, owners=None):
+    """Independent shards for the bulk build (config 4 at N GPUs, host-side
+    input): rank r indexes only the links whose handle it owns (handle_owner;
+    `owners` = per-expression owner if already known, else hashed on the
+    host), keeps the expressions those links contain so their handles hash,
+    and every leaf.  A contained link owned by another rank stays
+    directory-only (kind 3): each link is indexed on exactly one rank.  Atom
+    ids are then local to the shard (the reference's sharded Redis keys, not
+    the replicated directory ShardedDB queries need)."""
     from .loader import AtomArrays
     if world == 1:
         return arrays
@@ -662,7 +661,7 @@ def partition_arrays(arrays, rank, world):
     child = arrays.expr_child.astype(np.int64)
     keep = np.zeros(ne, dtype=bool)
     groups = [(int(arrays.level_off[g]), int(arrays.level_off[g + 1])) for g in range(len(arrays.level_off) - 1)]
-    own = content_owner(arrays, world) == rank
+    own = (host_owners(arrays, world) if owners is None else np.asarray(owners)) == rank
     for b, e in groups:
         if e <= b:
             continue
@@ -694,3 +693,59 @@ def partition_arrays(arrays, rank, world):
     return AtomArrays(arrays.leaf_bytes, arrays.leaf_off, arrays.leaf_kind, arrays.leaf_ctype, arrays.leaf_type_id,
                       arrays.name_start, expr_off, ch.astype(np.uint32), kinds[keep],
                       arrays.expr_ctype_leaf[keep], np.array(level_off, dtype=np.uint64), arrays.type_names)
+
+
+# ---------------------------------------------------------------------------
+# Config 4 at N GPUs from device-generated ranges: links regrouped on the
+# owners of their handles before the per-shard build
+# ---------------------------------------------------------------------------
+
+def regroup_by_owner(ctx, arrays, world, exchange):
+    """`arrays`: this rank's generated range of a flat two-level KB
+    (synthetic.device_arrays: arity-2 rows then arity-3 rows, node leaves
+    only).  Every link's handle is hashed on the device (das_hash_owners), the
+    rows are grouped by owner (das_partition_rows) and handed to
+    `exchange(rows (n, K) int32 tensor, counts) -> received rows (m, K)`,
+    the all-to-all (rccl_exchange below; tests pass an in-process stand-in).
+    Returns the DeviceAtomArrays of the received rows: all owned here, so a
+    plain build indexes each distinct link on exactly one rank.  Duplicates
+    of one handle generated on several ranks all arrive at its owner and
+    intern to one atom there."""
+    import torch
+    from . import synthetic
+    ne = arrays.n_expr
+    owner = torch.empty(max(ne, 1), dtype=torch.uint8, device=arrays.expr_child.device)
+    ctx.hash_owners(arrays, world, owner)
+    lv = [int(x) for x in arrays.level_off]
+    assert len(lv) == 3, "regroup_by_owner: expected the arity-2 / arity-3 groups of a flat KB"
+    c2, c3 = lv[1], lv[2] - lv[1]
+    out = []
+    for b, n, K, base in ((0, c2, 3, 0), (c2, c3, 4, 3 * c2)):
+        rows = arrays.expr_child[base:base + n * K]
+        grouped = torch.empty_like(rows)
+        counts = ctx.partition_rows(rows, n, K, owner[b:b + n], world, grouped) if n else \
+            np.zeros(world, dtype=np.uint64)
+        out.append(exchange(grouped.reshape(-1, K), counts))
+    leaves = (arrays.leaf_bytes, arrays.leaf_off, arrays.leaf_kind, arrays.leaf_ctype, arrays.leaf_type_id,
+              arrays.name_start)
+    return synthetic.device_arrays(leaves, arrays.type_names, out[0].reshape(-1), out[1].reshape(-1))
+
+
+def rccl_exchange(dist, group=None, cpu_staging=False):
+    """exchange() for regroup_by_owner over torch.distributed: split sizes
+    first, then one all_to_all_single of the rows (RCCL over xGMI with device
+    tensors; gloo with cpu_staging)."""
+    import torch
+
+    def ex(rows, counts):
+        dev = rows.device
+        stage = torch.device("cpu") if cpu_staging else dev
+        sc = torch.from_numpy(counts.astype(np.int64)).to(stage)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        rcl = [int(x) for x in rc.tolist()]
+        recv = torch.empty((sum(rcl), rows.shape[1]), dtype=rows.dtype, device=stage)
+        dist.all_to_all_single(recv, rows.to(stage), output_split_sizes=rcl,
+                               input_split_sizes=[int(x) for x in counts], group=group)
+        return recv.to(dev)
+    return ex

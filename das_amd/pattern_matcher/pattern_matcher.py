@@ -497,7 +497,7 @@ def _try_plan(expr, db, answer):
     if type(db) is not HipDB or answer.negation or os.environ.get("DAS_PLAN") == "0":
         return None
     no_overload = bool(CONFIG['no_overload'])
-    key = (id(db), db.generation, no_overload)
+    key = (db.generation, no_overload)          # generation: unique per load, any HipDB
     cached = getattr(expr, '_plan', None)
     if cached is None or cached[0] != key:
         cached = (key, _lower(expr, db, no_overload))

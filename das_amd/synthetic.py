@@ -415,31 +415,10 @@ def similarity_kb(n_nodes=300, n_inh=1200, n_sim=600, n_set=200, seed=SEED):
 
 
 def numbered_leaves(prefix, n):
-    """Leaf bytes + offsets of the n strings prefix + str(i), i = 0..n-1.
-    The numbers with d digits are one contiguous run of fixed-length strings,
-    written as the columns of a (count, len) view (no per-string objects)."""
-    pre = np.frombuffer(prefix.encode(), dtype=np.uint8)
-    P = len(pre)
-    nd = np.ones(n, dtype=np.uint64)
-    p = 10
-    while p <= max(n - 1, 0):
-        nd[p:] += 1
-        p *= 10
-    off = np.zeros(n + 1, dtype=np.uint64)
-    np.cumsum(nd + np.uint64(P), out=off[1:])
-    buf = np.empty(int(off[-1]), dtype=np.uint8)
-    lo, d = 0, 1
-    while lo < n:
-        hi = min(n, 10 ** d)
-        L = P + d
-        view = buf[int(off[lo]):int(off[hi])].reshape(hi - lo, L)
-        view[:, :P] = pre
-        q = np.arange(lo, hi, dtype=np.uint32)
-        for k in range(d - 1, -1, -1):
-            view[:, P + k] = q % 10 + 48
-            q //= 10
-        lo, d = hi, d + 1
-    return buf, off
+    """Leaf bytes + offsets of the n strings prefix + str(i), i = 0..n-1
+    (native host generator: 2^27 strings in well under a second)."""
+    from ._lib import numbered_strings
+    return numbered_strings(prefix, n)
 
 
 class DeviceAtomArrays(AtomArrays):
@@ -480,22 +459,9 @@ class DeviceAtomArrays(AtomArrays):
                           self.expr_ctype_leaf.cpu().numpy(), self.level_off, self.type_names)
 
 
-def powerlaw_kb_device(ctx, n_nodes, n_links, frac_arity2=0.7, link_types=4, seed=SEED, s=1.1,
-                       first=0, count=None, own=None, device=0):
-    """Configs 4-5 shape generated on the GPU (das_synth_powerlaw_links):
-    global links 0 .. n2-1 have arity 2, n2 .. n_links-1 arity 3 (n2 =
-    frac_arity2 * n_links); link i's type and Zipf(s) targets are a hash of
-    (seed, i).  This call materialises links [first, first+count); with
-    `own=(lo, hi)` only links lo..hi-1 get index rows (kind 1), the rest are
-    directory-only (kind 3, the multi-GPU layout of parallel.shard_arrays).
-    Nodes are the terminals "Concept n<i>"; link types T0..T{link_types-1}."""
-    import torch
-    count = n_links - first if count is None else count
-    end = first + count
-    n2 = int(n_links * frac_arity2)
-    r2 = (min(max(first, 0), n2), min(end, n2))
-    r3 = (max(first, n2), max(end, n2))
-    c2, c3 = r2[1] - r2[0], r3[1] - r3[0]
+def powerlaw_leaves(n_nodes, link_types):
+    """Host leaf arrays of the configs 4-5 KB: type names T0..T{k-1}, Concept,
+    then the node terminals "Concept n<i>"."""
     names = [f"T{i}" for i in range(link_types)] + ["Concept"]
     n_types = len(names)
     nb, noff = numbered_leaves("Concept n", n_nodes)
@@ -508,23 +474,53 @@ def powerlaw_kb_device(ctx, n_nodes, n_links, frac_arity2=0.7, link_types=4, see
     leaf_ctype = np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, n_types - 1, np.uint32)])
     leaf_type_id = np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, NONE, np.uint32)])
     name_start = np.concatenate([np.zeros(n_types, np.uint32), np.full(n_nodes, len("Concept") + 1, np.uint32)])
-    dev = torch.device("cuda", device)
-    child = torch.empty(3 * c2 + 4 * c3, dtype=torch.int32, device=dev)
-    if c2:
-        ctx.synth_powerlaw_links(child[:3 * c2], r2[0], c2, 3, link_types, 0, n_types, n_nodes, s, seed)
-    if c3:
-        ctx.synth_powerlaw_links(child[3 * c2:], r3[0], c3, 4, link_types, 0, n_types, n_nodes, s, seed)
+    return (leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start), names
+
+
+def device_arrays(leaves, names, child2, child3, shard=None):
+    """DeviceAtomArrays over host leaves and device link rows: child2 = flat
+    int32 tensor of arity-2 rows (type leaf + 2 node leaves, 3 words each),
+    child3 of arity-3 rows (4 words each)."""
+    import torch
+    dev = child2.device
+    c2, c3 = child2.numel() // 3, child3.numel() // 4
+    child = torch.cat([child2.reshape(-1), child3.reshape(-1)]) if c3 else child2.reshape(-1)
     ne = c2 + c3
     eoff = torch.empty(ne + 1, dtype=torch.int64, device=dev)
     eoff[:c2 + 1] = torch.arange(c2 + 1, dtype=torch.int64, device=dev) * 3
     if c3:
         eoff[c2 + 1:] = 3 * c2 + torch.arange(1, c3 + 1, dtype=torch.int64, device=dev) * 4
     kind = torch.ones(ne, dtype=torch.uint8, device=dev)
-    if own is not None:
-        gid = torch.cat([torch.arange(r2[0], r2[1], device=dev), torch.arange(r3[0], r3[1], device=dev)])
-        kind[(gid < own[0]) | (gid >= own[1])] = 3
-        del gid
     ctl = torch.full((ne,), -1, dtype=torch.int32, device=dev)
     level_off = np.array([0, c2, ne], dtype=np.uint64)
-    return DeviceAtomArrays(leaf_bytes, leaf_off, leaf_kind, leaf_ctype, leaf_type_id, name_start,
-                            eoff, child, kind, ctl, level_off, names)
+    out = DeviceAtomArrays(*leaves, eoff, child, kind, ctl, level_off, names)
+    out.shard = shard if shard is not None and shard[1] > 1 else None
+    return out
+
+
+def powerlaw_kb_device(ctx, n_nodes, n_links, frac_arity2=0.7, link_types=4, seed=SEED, s=1.1,
+                       first=0, count=None, shard=None, device=0):
+    """Configs 4-5 shape generated on the GPU (das_synth_powerlaw_links):
+    global links 0 .. n2-1 have arity 2, n2 .. n_links-1 arity 3 (n2 =
+    frac_arity2 * n_links); link i's type and Zipf(s) targets are a hash of
+    (seed, i).  This call materialises links [first, first+count).
+    shard=(rank, world): the multi-GPU query layout (parallel.shard_arrays) --
+    the build indexes only the links whose handle `rank` owns.
+    Nodes are the terminals "Concept n<i>"; link types T0..T{link_types-1}."""
+    import torch
+    count = n_links - first if count is None else count
+    end = first + count
+    n2 = int(n_links * frac_arity2)
+    r2 = (min(max(first, 0), n2), min(end, n2))
+    r3 = (max(first, n2), max(end, n2))
+    c2, c3 = r2[1] - r2[0], r3[1] - r3[0]
+    leaves, names = powerlaw_leaves(n_nodes, link_types)
+    n_types = len(names)
+    dev = torch.device("cuda", device)
+    child2 = torch.empty(3 * c2, dtype=torch.int32, device=dev)
+    child3 = torch.empty(4 * c3, dtype=torch.int32, device=dev)
+    if c2:
+        ctx.synth_powerlaw_links(child2, r2[0], c2, 3, link_types, 0, n_types, n_nodes, s, seed)
+    if c3:
+        ctx.synth_powerlaw_links(child3, r3[0], c3, 4, link_types, 0, n_types, n_nodes, s, seed)
+    return device_arrays(leaves, names, child2, child3, shard)

@@ -138,6 +138,26 @@ int das_build_index(das_ctx_t* ctx, const das_atoms_t* atoms);
 int das_build_index_ex(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags);
 int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out);
 
+/* ---- links hash-partitioned by handle across GPUs --------- */
+/* The owning shard of a handle: int(handle[:8], 16) % world (its first four
+ * digest bytes, big-endian).  The build for shard `rank` of `world`
+ * indexes a link (expr kind 1 or 3) iff its handle's owner is `rank`; every
+ * other link keeps its global id and outgoing set (directory only, like kind
+ * 3).  Every copy of one expression has one handle, so each distinct link is
+ * indexed on exactly one shard (canonical_parser.py:132-183 writes one entry
+ * per handle).  world 1 = das_build_index_ex. */
+int das_build_index_sharded(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags, uint32_t rank,
+                            uint32_t world);
+/* Owner shard of every expression's handle (hashes the KB as the build does):
+ * d_owner = n_expr device bytes.  With das_partition_rows and an all-to-all of
+ * the rows, a KB generated in ranges is regrouped on the owners of its
+ * handles before the per-shard build (bench.py --workload build at N GPUs). */
+int das_hash_owners(das_ctx_t* ctx, const das_atoms_t* atoms, uint32_t flags, uint32_t world, uint8_t* d_owner);
+/* n device rows of K u32 regrouped by d_owner (stable inside an owner) into
+ * d_out; counts[world] = rows per owner (host).  world <= 64. */
+int das_partition_rows(das_ctx_t* ctx, const uint32_t* d_rows, uint64_t n, uint32_t K, const uint8_t* d_owner,
+                       uint32_t world, uint32_t* d_out, uint64_t* counts);
+
 /* ---- synthetic input (bench / tests) ---------- */
 /* Writes n links of K-1 targets (K = 3 or 4 u32 per row: type leaf, then node
  * leaves) into device memory d_child, for global link indices first ..
@@ -147,6 +167,11 @@ int das_index_stats(das_ctx_t* ctx, das_index_stats_t* out);
 int das_synth_powerlaw_links(das_ctx_t* ctx, uint32_t* d_child, uint64_t first, uint64_t n, uint32_t K,
                              uint32_t n_link_types, uint32_t type_leaf0, uint32_t node_leaf0, uint64_t n_nodes,
                              double s, uint64_t seed);
+
+/* Host: the n strings prefix + decimal(first + i) back to back into `out`, and
+ * n + 1 byte offsets (the configs 4-5 node leaves "Concept n<i>"). */
+int das_numbered_strings(const char* prefix, uint64_t plen, uint64_t first, uint64_t n, uint8_t* out,
+                         uint64_t* off);
 
 /* digests -> atom ids (-1 if absent); cat: 0 other, 1 node, 2 link. */
 int das_lookup(das_ctx_t* ctx, const uint32_t* digests, uint64_t n, int64_t* ids,
@@ -266,7 +291,8 @@ int das_table_free(das_table_t* t);
  * `index_join` (LINK) allows And to evaluate the term as das_index_join(`ij`)
  * against its running result, as the host path does.
  * The answer's tables (one per schema, rows distinct) go to out[0..*n_out);
- * DAS_ERR_INVALID if more than `cap`. */
+ * DAS_ERR_INVALID if more than `cap`, with *n_out set to the number needed (call
+ * again with that capacity). */
 #define DAS_PLAN_LINK 1
 #define DAS_PLAN_CONST 2
 #define DAS_PLAN_NOT 3

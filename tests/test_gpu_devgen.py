@@ -85,24 +85,108 @@ def test_gpu_device_build_equals_host_build():
         assert _answer_set(db_d, q) == _answer_set(db_h, q)
 
 
-def test_gpu_device_build_remote_links():
-    """own=(lo, hi): links outside the range are directory-only (kind 3):
-    same atoms, pattern rows only for the owned links."""
+def _indexed_links(db):
+    """Handles of the links this shard indexes (pattern rows: T_a by type)."""
+    out = set()
+    for t in db.arrays.type_names:
+        tid = db.type_id.get(t)
+        for tab in db.ctx.scan_type(tid) if tid is not None else []:
+            if tab is not None and tab.nrows:
+                out.update(db.hex_of(tab.fetch()[0]))
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_device_build_handle_sharded(world):
+    """shard=(rank, world) on a Zipf KB dense in duplicate links (hub pairs
+    are generated many times): every rank holds the same directory, each
+    distinct link is indexed on exactly the rank its handle names
+    (int(handle[:8], 16) % world), and the shards' answers union to the
+    single build's (canonical_parser.py:132-183: one index entry per handle)."""
     import torch
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
+    from das_amd.parallel import handle_owner
     from das_amd.pattern_matcher import pattern_matcher as pm
-    n_nodes, n_links = 2000, 20_000
+    n_nodes, n_links = 300, 20_000
     db_all = HipDB(device=0)
-    full = synthetic.powerlaw_kb_device(db_all.ctx, n_nodes, n_links)
-    db_all.load_arrays(full)
-    db_a, db_b = HipDB(device=0), HipDB(device=0)
-    db_a.load_arrays(synthetic.powerlaw_kb_device(db_a.ctx, n_nodes, n_links, own=(0, 9000)))
-    db_b.load_arrays(synthetic.powerlaw_kb_device(db_b.ctx, n_nodes, n_links, own=(9000, n_links)))
+    db_all.load_arrays(synthetic.powerlaw_kb_device(db_all.ctx, n_nodes, n_links))
+    full = _indexed_links(db_all)
+    assert len(full) < n_links - 1000               # many generated duplicates collapse
+    shards = []
+    for r in range(world):
+        db = HipDB(device=0)
+        db.load_arrays(synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links, shard=(r, world)))
+        shards.append(db)
     torch.cuda.synchronize()
-    assert db_a.stats().n_atoms == db_b.stats().n_atoms == db_all.stats().n_atoms
+    seen = {}
+    for r, db in enumerate(shards):
+        assert db.stats().n_atoms == db_all.stats().n_atoms
+        links = _indexed_links(db)
+        assert all(handle_owner(h, world) == r for h in links)
+        for h in links:
+            seen[h] = seen.get(h, 0) + 1
+    assert seen == {h: 1 for h in full}
     V = pm.Variable
     for t in ("T0", "T3"):
-        q = pm.Link(t, [V("V1"), V("V2"), V("V3")], True)
-        a, b, w = _answer_set(db_a, q), _answer_set(db_b, q), _answer_set(db_all, q)
-        assert a | b == w            # an atom both shards generate is indexed by both
+        for q in (pm.Link(t, [V("V1"), V("V2"), V("V3")], True), pm.Link(t, [V("V1"), V("V2")], True)):
+            parts = [_answer_set(db, q) for db in shards]
+            w = _answer_set(db_all, q)
+            assert set().union(*parts) == w
+            assert sum(len(p) for p in parts) == len(w)       # disjoint
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_exchange_build_indexes_each_link_once(world):
+    """Config 4 at N GPUs (bench.py --workload build): each rank generates a
+    range, hashes it (das_hash_owners), groups rows by owner
+    (das_partition_rows) and sends them to the owners (here an in-process
+    all-to-all); each rank builds what it received.  The shards' indexed
+    links are disjoint, owned by handle, and union to the single build."""
+    import torch
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    from das_amd.parallel import handle_owner, regroup_by_owner
+    n_nodes, n_links = 400, 30_000
+    db_all = HipDB(device=0)
+    db_all.load_arrays(synthetic.powerlaw_kb_device(db_all.ctx, n_nodes, n_links))
+    full = _indexed_links(db_all)
+    sent = {}                                        # (src, arity group) -> (rows, counts)
+
+    def make_exchange(src, box):
+        def ex(rows, counts):
+            box.append((rows.clone(), counts.copy()))
+            return rows[:0]                          # filled in after every rank has sent
+        return ex
+    boxes = []
+    for r in range(world):
+        ctx_db = HipDB(device=0)
+        lo, hi = n_links * r // world, n_links * (r + 1) // world
+        part = synthetic.powerlaw_kb_device(ctx_db.ctx, n_nodes, n_links, first=lo, count=hi - lo)
+        box = []
+        regroup_by_owner(ctx_db.ctx, part, world, make_exchange(r, box))
+        boxes.append(box)
+        leaves = (part.leaf_bytes, part.leaf_off, part.leaf_kind, part.leaf_ctype, part.leaf_type_id,
+                  part.name_start)
+        names = part.type_names
+        sent[r] = box
+    seen = {}
+    for dst in range(world):
+        recv = []
+        for g in range(2):
+            chunks = []
+            for src in range(world):
+                rows, counts = boxes[src][g]
+                off = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+                chunks.append(rows[int(off[dst]):int(off[dst + 1])])
+            recv.append(torch.cat(chunks).reshape(-1))
+        db = HipDB(device=0)
+        db.load_arrays(synthetic.device_arrays(leaves, names, recv[0], recv[1]))
+        links = _indexed_links(db)
+        assert all(handle_owner(h, world) == dst for h in links)
+        for h in links:
+            seen[h] = seen.get(h, 0) + 1
+    assert seen == {h: 1 for h in full}
+    # grouping is stable and complete: every sent row's owner is its group
+    rows, counts = boxes[0][0]
+    assert int(counts.sum()) == rows.shape[0]

@@ -265,62 +265,89 @@ def test_gpu_facade_readme_examples():
         [h for h, _ in das.db.get_matched_links("Inheritance", ["*", "bdfe4e7a431f73386f37c6448afe5840"])])
 
 
+def _sharded_kb(kind):
+    """(AtomArrays, queries) of a two-rank sharded GPU test: the bio KB, and
+    the hub / FlyBase shapes of configs 5 / 3 (Zipf KBs dense in duplicates)."""
+    from das_amd import synthetic
+    from tests.golden import make_synthetic as MS
+    from tests.test_parallel_gloo import _fly_queries, _hub_queries, _queries
+    if kind in ("default", "heavy"):
+        return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
+    if kind == "hub":
+        return MS.make_arrays("hub"), _hub_queries()
+    return MS.make_arrays("flybase"), _fly_queries()
+
+
 def _sharded_worker(rank, world, port, out_path, mode):
     import os as _os
     import torch
     import torch.distributed as dist
-    if mode == "heavy":          # exchanged joins with skewed buckets split
+    if mode in ("heavy", "hub"):          # exchanged joins with skewed buckets split
         _os.environ["DAS_JOIN_PLACEMENT"] = "exchange"
         _os.environ["DAS_HEAVY_FRAC"] = "0.05"
     _os.environ["MASTER_ADDR"] = "127.0.0.1"
     _os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
     from das_amd.parallel import HipLocal, ShardedDB, shard_arrays
     from das_amd.pattern_matcher import pattern_matcher as pm
-    from tests.test_parallel_gloo import _queries
-    # links not owned by this rank are remote (kind 3): same directory, split index
-    arrays = shard_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3), rank, world)
+    from tests.test_gpu_devgen import _indexed_links
+    arrays, queries = _sharded_kb(mode)
+    # the whole KB is every rank's directory; links indexed by their handle's owner
     db = HipDB(device=0)
-    db.load_arrays(arrays)
+    db.load_arrays(shard_arrays(arrays, rank, world))
     sdb = ShardedDB(HipLocal(db, cpu_staging=True), dist)
     res = []
-    for q in _queries():
+    for q in queries:
         ans = pm.PatternMatchingAnswer()
-        m = build(q).matched(sdb, ans)
+        try:
+            m = build(q).matched(sdb, ans)
+        except AttributeError as e:
+            res.append({"error": type(e).__name__})
+            continue
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
         res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
                     "local": sdb.rel_local_count(ans._relation())})
+    res.append(sorted(_indexed_links(db)))
     res.append(sdb.plan_stats)
     with open(f"{out_path}.{rank}", "w") as f:
         json.dump(res, f)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["default", "heavy"])
+@pytest.mark.parametrize("mode", ["default", "heavy", "hub", "flybase"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
-    """The multi-GPU path (partition / export / import kernels + exchange) with
-    two ranks sharing cuda:0 over gloo, against the single-process oracle."""
+    """The multi-GPU path (handle-sharded builds, partition / export / import
+    kernels + exchange) with two ranks sharing cuda:0 over gloo, against the
+    single-process oracle: bio, the hub 4-clause And with the heavy-hitter
+    split (config 5) and the FlyBase And / Not / Or shapes (config 3).  Each
+    link is indexed on exactly one rank."""
     import socket
     import tempfile
     import torch.multiprocessing as mp
-    from das_amd import synthetic
-    from tests.test_parallel_gloo import _queries
+    from das_amd.parallel import handle_owner
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    odb = O.RedisMongoSemantics(O.KB.from_arrays(synthetic.bio_kb(60, 25, 600, 80, seed=3)))
+    arrays, queries = _sharded_kb(mode)
+    okb = O.KB.from_arrays(arrays)
+    odb = O.RedisMongoSemantics(okb)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
         mp.spawn(_sharded_worker, args=(2, port, out, mode), nprocs=2, join=True)
         per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
-    if mode == "heavy":
+    if mode in ("heavy", "hub"):
         assert per_rank[0][-1]["heavy"] > 0, per_rank[0][-1]
-    for qi, q in enumerate(_queries()):
+    indexed = [set(per_rank[r][-2]) for r in range(2)]
+    assert not (indexed[0] & indexed[1]) and indexed[0] | indexed[1] == set(okb.links)
+    assert all(handle_owner(h, 2) == r for r in range(2) for h in indexed[r])
+    for qi, q in enumerate(queries):
         want = O.evaluate(q, odb)
+        if "error" in want:
+            assert all(per_rank[r][qi] == {"error": want["error"]} for r in range(2)), q
+            continue
         want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])
         assert sum(per_rank[r][qi]["local"] for r in range(2)) == want["n"], q
         for r in range(2):

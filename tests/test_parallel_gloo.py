@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from das_amd.parallel import handle_owner
 from oracle import das_oracle as O
 
 ORDERED, UNORDERED, COMPOSITE = 0, 1, 2
@@ -126,7 +127,7 @@ class NumpyLocal:
 
         def owner(h, v):
             key = v[1][by_target[v[0]]] if v[0] in by_target else h
-            return int(key[:8], 16) % world
+            return handle_owner(key, world)
         local.links = {h: v for h, v in kb_full.links.items() if owner(h, v) == rank} if local_kb is None \
             else dict(local_kb.links)
         self.odb = O.RedisMongoSemantics(local)
@@ -402,13 +403,8 @@ def _worker(rank, world, port, out_path, kind):
     from das_amd.pattern_matcher import pattern_matcher as pm
     kb, queries = _kb(kind)
     spec = {"Member": 0} if kind == "bio_part" else None
-    local_kb = None
-    if kind == "flybase":
-        # the bench's strong-scaling layout: links sharded by content hash
-        from das_amd.parallel import shard_arrays
-        from tests.golden import make_synthetic as MS
-        local_kb = O.KB.from_arrays(shard_arrays(MS.make_arrays("flybase"), rank, world))
-    sdb = ShardedDB(NumpyLocal(kb, rank, world, by_target=spec, local_kb=local_kb), dist, partition_spec=spec)
+    # links by their handle's owner (the bench's layout, parallel.shard_arrays)
+    sdb = ShardedDB(NumpyLocal(kb, rank, world, by_target=spec), dist, partition_spec=spec)
     res = []
     for q in queries:
         ans = pm.PatternMatchingAnswer()
@@ -474,7 +470,7 @@ def test_partition_arrays_build_union_equals_single_build(world, name):
     The shards' key-value families (outgoing / incoming sets, pattern and
     template keys, names -- canonical_parser.py:119-183) must union to the
     single build's, and every link (nested ones too) is indexed on exactly
-    one rank."""
+    one rank: the one its handle names."""
     from das_amd.parallel import partition_arrays
     from tests.golden import make_synthetic as MS
     full_kb = O.KB.from_arrays(MS.make_arrays(name))
@@ -487,6 +483,7 @@ def test_partition_arrays_build_union_equals_single_build(world, name):
             union[k] |= set(lines)
         for h in kb.links:
             owners[h] = owners.get(h, 0) + 1
+            assert handle_owner(h, world) == r
     for k in full:
         assert union[k] == set(full[k]), k
     assert owners == {h: 1 for h in full_kb.links}

@@ -1,4 +1,4 @@
-"""Link sharding helpers of das_amd.parallel (host code): content-hash
+"""Link sharding helpers of das_amd.parallel (host code): handle-owner
 partitions are disjoint, cover the KB, and keep nested links whole."""
 import numpy as np
 
@@ -32,10 +32,26 @@ def test_partition_arrays_cover_and_disjoint():
                 assert not ((tops[i] & tops[j]) - nested_handles)
 
 
-def test_shard_arrays_marks_remote_links():
+def test_host_owners_are_handle_owners():
+    """parallel.host_owners = int(handle[:8], 16) % world of each expression's
+    reference handle (the device's das_hash_owners, common.h handle_owner)."""
+    for arrays in (synthetic.powerlaw_kb(200, 1000, link_types=2, seed=3), _nested()):
+        kb_hex = _expr_handles(arrays)
+        for world in (2, 3, 8):
+            got = parallel.host_owners(arrays, world)
+            assert got.tolist() == [int(h[:8], 16) % world for h in kb_hex]
+
+
+def _expr_handles(arrays):
+    leaf = [O.md5hex(s) for s in arrays.leaf_strings()]
+    h = leaf + [None] * arrays.n_expr
+    for j in sorted(range(arrays.n_expr), key=lambda j: arrays.expr_level[j]):
+        h[arrays.n_leaf + j] = O.composite_hash([h[c] for c in arrays.children(j)])
+    return h[arrays.n_leaf:]
+
+
+def test_shard_arrays_declares_the_handle_split():
     arrays = synthetic.powerlaw_kb(200, 1000, link_types=2, seed=3)
-    kinds = [parallel.shard_arrays(synthetic.powerlaw_kb(200, 1000, link_types=2, seed=3), r, 2).expr_kind
-             for r in range(2)]
-    local = [(k == 1) for k in kinds]
-    assert not np.any(local[0] & local[1])
-    assert np.all(local[0] | local[1] | (arrays.expr_kind != 1))
+    kinds = arrays.expr_kind.copy()
+    a = parallel.shard_arrays(arrays, 1, 2)
+    assert a.shard == (1, 2) and np.array_equal(a.expr_kind, kinds)     # the build splits by handle
