@@ -1,8 +1,8 @@
 """bench.py — DAS query hot path on MI355X: bindings/s + HBM roofline.
 
-Default workload (BASELINE.json configs[1], the config the metric is quoted on
-that fits one GPU): a seeded synthetic gene-level KB in scripts/benchmark.py's
-shape (Member(Gene, BiologicalProcess) with Zipf(1.1) process popularity,
+Headline (BASELINE.json configs[1], the config the metric is quoted on that
+fits one GPU): a seeded synthetic gene-level KB in scripts/benchmark.py's shape
+(Member(Gene, BiologicalProcess) with Zipf(1.1) process popularity,
 Inheritance(BP, BP)); the real bio_atomspace dump is not available offline.
 One step = one pass of the query batch below through the reference API
 (`expr.matched(db, answer)`), single-Link and 2-clause And queries:
@@ -13,23 +13,25 @@ One step = one pass of the query batch below through the reference API
   Q4 And[Member(V_g, bp_hub), Member(V_g, V_bp)]        hub join
 
 value = distinct bindings produced by all ranks / wall time (answers counted
-on the device, no Python object materialisation).  Multi-GPU: links are
-partitioned across ranks (Member by gene range, Inheritance by content hash)
-and And joins repartition both binding tables by the join key with an RCCL
-all-to-all (das_amd/parallel.py); per-rank KB size is fixed (weak scaling).
+on the device, no Python object materialisation).  Multi-GPU: Member links
+live on their gene's rank, Inheritance links on their handle's owner; And
+joins are placed by cost (co-located / broadcast / all-to-all exchange,
+das_amd/parallel.py); per-rank KB size is fixed (weak scaling).
 
-Other workloads (`--workload`, one JSON line each; not the driver's default):
+The default run (`--workload all`) then measures the other configurations
+one after another in the same process and adds their lines under
+"workloads" (each with its own roofline, kernel table and CPU baseline):
   flybase  config 3: FlyBase-shaped Execution(Schema, key, value) KB, the
-           QueryFlyBase.ipynb And / And+Not / Or query shapes (fixed KB,
-           links content-hash sharded: strong scaling)
-  hub      config 5: power-law KB, 4-clause And on the top-degree hub nodes
+           QueryFlyBase.ipynb And / And+Not / Or query shapes, a fresh gene
+           anchor per step (fixed KB, links sharded by handle: strong scaling)
+  hub      config 5: 10^9-link power-law KB generated in HBM, 4-clause And
+           on the top-degree hub nodes
   build    config 4: bulk ExpressionHasher + interning + pattern / template /
-           incoming CSR index build; value = links indexed per second of
-           device time (host parse and PCIe upload excluded, reported apart)
-  load     canonical MeTTa text (FlyBase-shaped) -> native multi-threaded
-           reader (canonical.cpp) -> device index; value = links per second
-           of the whole load (parse + upload + build), the reference's
-           CanonicalParser path (canonical_parser.py:315-365)
+           incoming CSR build of the 10^9-link KB; value = links indexed per
+           second of device time (at N GPUs: hash-owner regrouping + RCCL
+           all-to-all + per-shard build)
+`--workload X` runs one of them alone (the line is then X's own);
+`--workload load` measures the canonical MeTTa reader -> device index path.
 """
 import argparse
 import json
@@ -48,7 +50,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="bio", choices=["bio", "flybase", "hub", "build", "load"])
+    ap.add_argument("--workload", default="all", choices=["all", "bio", "flybase", "hub", "build", "load"])
+    ap.add_argument("--legs", default="auto",
+                    help="with --workload all: comma list of the extra workloads (auto: flybase,hub,build on one "
+                         "GPU; build at N > 1)")
+    ap.add_argument("--leg-cpu-seconds", type=float, default=8.0,
+                    help="CPU-baseline budget of each extra workload of --workload all")
     ap.add_argument("--events", default="dominant", choices=["dominant", "all"],
                     help="timed-step HIP events: around the dominant kernel only, or around every kernel scope")
     # bio (config 2)
@@ -185,11 +192,10 @@ def make_kb(args, rank, world, db):
                "anchors": "a different gene per step"}
         return arrays, lambda i: flybase_specs(genes[i % n], do_terms[genes[i % n]]), cfg, "strong"
     if args.gen == "device":
-        # every rank holds the whole atom directory; rank r owns (indexes) the
-        # global link range [r L / N, (r+1) L / N)
-        lo, hi = args.hub_links * rank // world, args.hub_links * (rank + 1) // world
+        # every rank generates the whole KB as its atom directory and indexes
+        # the links whose handle it owns (das_build_index_sharded)
         arrays = synthetic.powerlaw_kb_device(db.ctx, args.hub_nodes, args.hub_links, link_types=4,
-                                              own=(lo, hi) if world > 1 else None, device=db.ctx.device)
+                                              shard=(rank, world), device=db.ctx.device)
     else:
         arrays = synthetic.powerlaw_kb(args.hub_nodes, args.hub_links, link_types=4)
         arrays = parallel.shard_arrays(arrays, rank, world)
@@ -358,17 +364,50 @@ def kernels_of(stats):
 # ---------------------------------------------------------------------------
 # config 4: bulk index build
 # ---------------------------------------------------------------------------
-def run_build(args, rank, world, dist, local_rank):
+def _sync_max(dist, values, device):
+    """Element-wise max over ranks of a few floats (rank timings)."""
+    import torch
+    if not dist:
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def _sync_sum(dist, values, device):
+    import torch
+    if not dist:
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return [float(x) for x in t.tolist()]
+
+
+def build_algorithmic_bytes(n_links, frac_arity2=0.7):
+    """SURVEY.md §8d config-4 algorithmic bytes: hash (arity*16 + 16) in + 16
+    out per link, CSR 2*arity*4 + 4 per link."""
+    n2 = int(n_links * frac_arity2)
+    n3 = n_links - n2
+    return n2 * (2 * 16 + 16 + 16 + 2 * 2 * 4 + 4) + n3 * (3 * 16 + 16 + 16 + 2 * 3 * 4 + 4)
+
+
+def run_build(args, rank, world, dist, local_rank, backend="nccl"):
+    """Config 4.  One GPU: the device build of the whole generated KB.  N GPUs:
+    rank r generates the global link range [r L / N, (r+1) L / N) in HBM; the
+    timed region hashes it (das_hash_owners), groups the rows by the owner of
+    their handles (das_partition_rows), sends them to the owners with one RCCL
+    all-to-all per arity and builds the shard it received -- links
+    hash-partitioned by handle, each distinct link indexed on exactly one GPU.
+    Inputs are resident in HBM when the timing starts; the host leaf strings'
+    upload is input hand-over and is not timed (reported as wall_incl_upload_s)."""
     import torch
     from das_amd import parallel, synthetic
     from das_amd.database.hip_db import HipDB
+    dev = torch.device("cuda", local_rank)
     t0 = time.perf_counter()
     db = HipDB(device=local_rank)
     log(f"generating {args.links} links ({args.gen})")
     if args.gen == "device":
-        # generated on the device; rank r materialises
-        # the global link range [r L / N, (r+1) L / N) of the one KB
-        # (independent shards, nodes replicated: strong scaling)
         lo, hi = args.links * rank // world, args.links * (rank + 1) // world
         arrays = synthetic.powerlaw_kb_device(db.ctx, args.nodes, args.links, link_types=4, first=lo,
                                               count=hi - lo, device=local_rank)
@@ -385,22 +424,33 @@ def run_build(args, rank, world, dist, local_rank):
         dist.barrier()
     log("building")
     t1 = time.perf_counter()
+    ex_ms = 0.0
+    if world > 1 and args.gen == "device":
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ex = parallel.rccl_exchange(dist, cpu_staging=(backend != "nccl"))
+
+        def timed_ex(rows, counts):
+            ev[0].record()
+            out = ex(rows, counts)
+            ev[1].record()
+            ev[1].synchronize()
+            nonlocal ex_ms
+            ex_ms += ev[0].elapsed_time(ev[1])
+            return out
+        arrays = parallel.regroup_by_owner(db.ctx, arrays, world, timed_ex)
     db.load_arrays(arrays)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t1
     db.ctx.prof_enable(False)
     stats = db.ctx.prof_stats()
-    dev_ms = stats.get("build_device", {}).get("ms", wall * 1e3)
+    # device time of the timed region: owner hashing + row grouping + the
+    # all-to-all + the build (each measured by events on the stream)
+    dev_ms = stats.get("build_device", {}).get("ms", wall * 1e3) + stats.get("hash_owners", {}).get("ms", 0.0) + \
+        stats.get("partition_rows", {}).get("ms", 0.0) + ex_ms
     st = db.stats()
-    local_links = int((arrays.expr_kind == 1).sum())
-    links = local_links
-    if dist:
-        t = torch.tensor([dev_ms, wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dev_ms, wall = float(t[0]), float(t[1])
-        n = torch.tensor([local_links], dtype=torch.float64, device="cuda")
-        dist.all_reduce(n)
-        links = int(n.item())
+    local_links = int(st.n_links)
+    dev_ms, wall = _sync_max(dist, [dev_ms, wall], dev if backend == "nccl" else "cpu")
+    links = int(_sync_sum(dist, [local_links], dev if backend == "nccl" else "cpu")[0])
     # MD5 blocks hashed: a message of L bytes takes
     # ceil((L + 9) / 64) blocks; a composite message is K 32-hex handles joined
     # by spaces (33 K - 1 bytes), a terminal one its "Type name" string; a
@@ -415,37 +465,47 @@ def run_build(args, rank, world, dist, local_rank):
     else:
         nch = np.diff(arrays.expr_off.astype(np.int64))
         blocks_expr = 2 * int(((33 * nch - 1 + 9 + 63) // 64).sum())
+    out = None
     if rank == 0:
         hash_ks = {k: v for k, v in stats.items() if k.startswith("k_hash_group")}
         hms = sum(v["ms"] for v in hash_ks.values())
         hl = stats.get("k_hash_strings", {"ms": 0, "bytes": 0, "launches": 0})
-        # §8d algorithmic bytes of the whole build: hash (arity*16 + 16) in +
-        # 16 out, CSR 2*arity*4 + 4 per link
-        n2, n3 = int(args.links * 0.7) // world, (args.links - int(args.links * 0.7)) // world
-        algo = n2 * (2 * 16 + 16 + 16 + 2 * 2 * 4 + 4) + n3 * (3 * 16 + 16 + 16 + 2 * 3 * 4 + 4)
+        # §8d algorithmic bytes of the whole build, all links (per GPU: / N)
+        algo = build_algorithmic_bytes(args.links)
+        achieved = algo / (dev_ms * 1e-3) / 1e9
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
             cpu = cpu_baseline_build(args, args.cpu_baseline_seconds)
         out = {"metric": "links indexed/s (bulk ExpressionHasher + intern + pattern/template/incoming CSR build)",
-               "value": links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
+               "value": args.links / (dev_ms * 1e-3), "unit": "links/s", "n_gpus": world, "steps": 1, "warmup": 1,
                "ms_per_step": dev_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                "dtype": "u32",
                "data": "synthetic power-law hypergraph, Zipf(1.1) targets, " + (
                    "generated in HBM (das_synth_powerlaw_links)" if args.gen == "device" else "generated on the host"),
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
-                          "parallelism": f"links partitioned x{world} (independent shards, nodes replicated)"},
-               "roofline": roofline_of(stats, "build"), "cpu_baseline": cpu,
-               "build_8d": {"algorithmic_bytes": algo, "achieved_GBps": round(algo / (dev_ms * 1e-3) / 1e9, 1),
-                            "frac": round(algo / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                            "note": "SURVEY.md §8d bytes of hash + CSR per link over the whole device build"},
+                          "distinct_links_indexed": links,
+                          "parallelism": (f"links hash-partitioned by handle x{world}: generated in ranges, "
+                                          "regrouped on their owners by RCCL all-to-all" if world > 1 else "1 GPU")},
+               # the build's roofline is SURVEY.md §8d's: algorithmic bytes of
+               # hash + CSR over all links / device time of the whole build (sort
+               # passes, scratch and intern traffic count against it)
+               "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS * world,
+                            "unit": "GB/s", "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
+                            "kernel": "whole build (SURVEY.md §8d bytes: hash (arity*16+16) in + 16 out, "
+                                      "CSR 2*arity*4 + 4 per link)",
+                            "algorithmic_bytes": algo},
+               "dominant_kernel": roofline_of(stats, "build"),
+               "cpu_baseline": cpu,
+               "exchange_ms": round(ex_ms, 3) if world > 1 else None,
                "hash": {"ms": round(hms, 3), "md5_blocks_per_s": (blocks_leaf + blocks_expr) / max((hms + hl["ms"]) * 1e-3, 1e-12),
                         "md5_blocks": blocks_leaf + blocks_expr, "terminal_ms": round(hl["ms"], 3),
                         "valu": md5_valu(hash_ks)},
                "kernels": kernels_of(stats), "wall_incl_upload_s": round(wall, 3), "host_generate_s": round(t_gen, 2),
                "atoms": int(st.n_atoms), "device_bytes": int(st.device_bytes)}
-        print(json.dumps(out))
+    del db, arrays
+    return out
 
 
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2   # CUs x SIMDs x clock / 2 cycles per wave64 VALU op (MI355X_MICROARCH.md)
@@ -557,40 +617,36 @@ def run_load(args, rank, world, local_rank):
     print(json.dumps(out))
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+# kernel scopes that are scratch, not algorithmic bytes (sort
+# passes and count -> offset scans count against the fraction)
+_SCRATCH = ("k_radix", "k_scan_tiles", "k_scan_reduce", "k_scan_single", "k_bounds_u32")
+
+
+def step_roofline(stats, ms_per_step, world, steps=1):
+    """Step-level roofline: the algorithmic bytes of every kernel one step
+    launches (each kernel's own inputs read once + outputs written once; sort
+    passes and prefix-scan scratch excluded) over the whole step time --
+    launch gaps, host work and small kernels count against it."""
+    b = sum(v["bytes"] for k, v in stats.items() if k.startswith("k_") and not k.startswith(_SCRATCH)) / steps
+    if ms_per_step <= 0:
+        return None
+    achieved = b / (ms_per_step * 1e-3) / 1e9
+    peak = HBM_PEAK_GBS * world
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(achieved / peak, 4), "algorithmic_bytes_per_step": b,
+            "note": "sum of the step's per-kernel algorithmic bytes (k_* scopes of one profiled step, sort/scan "
+                    "scratch excluded) / ms_per_step"}
+
+
+def run_query(args, workload, rank, world, dist, local_rank, backend):
+    """One query workload (bio / flybase / hub): KB, warmup, K timed steps
+    between barriers, max over ranks.  Returns rank 0's JSON dict."""
     import torch
-    # DAS_BENCH_SAME_DEVICE=1 + DAS_DIST_BACKEND=gloo rehearse N ranks on one GPU
-    if os.environ.get("DAS_BENCH_SAME_DEVICE") == "1":
-        local_rank = 0
-    backend = os.environ.get("DAS_DIST_BACKEND", "nccl")
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
-    if args.workload == "load":
-        run_load(args, rank, world, local_rank)
-        if dist:
-            dist.destroy_process_group()
-        return
-    if args.workload == "build":
-        run_build(args, rank, world, dist, local_rank)
-        if dist:
-            dist.destroy_process_group()
-        return
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
-
-    # ---- knowledge base (per-rank partition for N > 1) ----
+    args = argparse.Namespace(**dict(vars(args), workload=workload))
     t_build = time.perf_counter()
-    log(f"generating {args.workload} KB")
+    log(f"generating {workload} KB")
     # one non-null stream shared by torch (collectives, staging buffers) and
     # the native context: exchanges are then ordered on the stream, with no
     # host synchronisation around each collective (parallel.HipLocal)
@@ -607,10 +663,11 @@ def main():
     # one query set per step: anchored queries change their anchor every step
     n_sets = args.warmup + args.steps + 1
     qsets = [[(name, build_expr(pm, s)) for name, s in specs(i)] for i in range(n_sets)]
+    engine = None
     if world > 1:
         from das_amd import parallel
         # bio_shard places a gene's Member links on the gene's rank
-        spec = {"Member": 0} if args.workload == "bio" else None
+        spec = {"Member": 0} if workload == "bio" else None
         engine = parallel.ShardedMatcher(db, dist, cpu_staging=(backend != "nccl"), partition_spec=spec)
 
         def run(q):
@@ -636,7 +693,7 @@ def main():
         step(i)
     db.ctx.prof_enable(False)
     warm_stats = db.ctx.prof_stats()
-    dominant = roofline_of(warm_stats, args.workload) if args.events == "dominant" else None
+    dominant = roofline_of(warm_stats, workload) if args.events == "dominant" else None
     per_query = {name: run(q) for name, q in qsets[args.warmup]}
     db.ctx.prof_reset()
     db.ctx.prof_only(dominant["kernel"] if dominant else None)
@@ -666,17 +723,15 @@ def main():
         pr.disable()
         with open(args.cprofile, "w") as f:
             pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        b = torch.tensor([bindings], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-        dist.all_reduce(b)
-        bindings = float(b.item())
+    stage = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
+    elapsed = _sync_max(dist, [elapsed], stage)[0]
+    bindings = _sync_sum(dist, [bindings], stage)[0]
     value = bindings / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
     incl = None
     if world == 1 and not args.no_materialise:
         incl = materialised_rate(pm, db, qsets[n_sets - 1], args.materialise_cap)
+    out = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -685,21 +740,93 @@ def main():
         data = {"bio": "synthetic (seeded bio_kb in scripts/benchmark.py shape; bio_atomspace dump unavailable offline)",
                 "flybase": "synthetic FlyBase-shaped KB (flybase2metta Execution layout; the FlyBase dump needs a "
                            "network fetch)",
-                "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[args.workload]
+                "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
         cfg = dict(cfg, bindings_per_step_rank0=per_query, parallelism=f"links sharded x{world}")
         out = {
             "metric": "pattern matches/sec (bindings/s) + % HBM roofline",
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": scaling,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "u32", "data": data, "config": cfg,
-            "roofline": roofline_of(stats, args.workload, dominant["kernel"] if dominant else None),
+            "roofline": roofline_of(stats, workload, dominant["kernel"] if dominant else None),
+            "step_roofline": step_roofline(warm_stats if dominant else stats, ms_per_step, world,
+                                           1 if dominant else args.steps),
             "cpu_baseline": cpu,
             "incl_materialisation": incl,
             "kernels": kernels_of(warm_stats if dominant else stats),
             "kernels_from": "last warmup step (every scope)" if dominant else "timed steps (every scope)",
             "build_s": round(t_build, 2),
         }
-        print(json.dumps(out))
+        if world > 1:
+            out["sharded_plan_stats"] = dict(engine.sdb.plan_stats)
+    del engine, qsets, db
+    return out
+
+
+def _free_device():
+    import gc
+    import torch
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    # DAS_BENCH_SAME_DEVICE=1 + DAS_DIST_BACKEND=gloo rehearse N ranks on one GPU
+    if os.environ.get("DAS_BENCH_SAME_DEVICE") == "1":
+        local_rank = 0
+    backend = os.environ.get("DAS_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    if args.workload == "load":
+        run_load(args, rank, world, local_rank)
+        if dist:
+            dist.destroy_process_group()
+        return
+    if args.workload == "all":
+        head = "bio"
+        legs = args.legs.split(",") if args.legs != "auto" else (["flybase", "hub", "build"] if world == 1
+                                                                 else ["build"])
+        legs = [w for w in legs if w]
+    else:
+        head, legs = args.workload, []
+
+    def run_leg(w, a):
+        if w == "build":
+            return run_build(a, rank, world, dist, local_rank, backend)
+        return run_query(a, w, rank, world, dist, local_rank, backend)
+
+    t_head = time.perf_counter()
+    line = run_leg(head, args)
+    _free_device()
+    extra = {}
+    for w in legs:
+        t_leg = time.perf_counter()
+        a = argparse.Namespace(**dict(vars(args), cpu_baseline_seconds=args.leg_cpu_seconds))
+        try:
+            r = run_leg(w, a)
+        except Exception as e:            # one leg failing must not lose the headline line
+            log(f"workload {w} failed: {type(e).__name__}: {e}")
+            r = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0 and r is not None:
+            r["leg_wall_s"] = round(time.perf_counter() - t_leg, 1)
+            extra[w] = r
+        _free_device()
+    if rank == 0:
+        if extra:
+            line["workloads"] = extra
+            line["headline_wall_s"] = round(time.perf_counter() - t_head, 1)
+        print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
 
