@@ -315,11 +315,13 @@ class Table:
         b = (C.c_uint32 * max(k, 1))(*[int(x) for x in hi])
         check(lib().das_table_set_bounds(self.h, a, b))
 
-    def fetch(self):
-        n, k = self.nrows, len(self.vars)
-        out = np.zeros((k, n), dtype=np.uint32)
+    def fetch(self, row0=0, nrows=None):
+        """Rows [row0, row0 + nrows) (default: all) as a (ncols, n) host array."""
+        n = self.nrows - row0 if nrows is None else min(nrows, self.nrows - row0)
+        n, k = max(n, 0), len(self.vars)
+        out = np.empty((k, n), dtype=np.uint32)
         if n and k:
-            check(lib().das_table_fetch(self.ctx.h, self.h, 0, n, ptr(out)), self.ctx.h)
+            check(lib().das_table_fetch(self.ctx.h, self.h, row0, n, ptr(out)), self.ctx.h)
         return out
 
     def free(self):

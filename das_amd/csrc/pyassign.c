@@ -1,0 +1,311 @@
+/* Answer materialisation for the drop-in API (CPython extension das_amd._assign).
+ *
+ * The reference's answer is a Python set of Assignment objects
+ * (pattern_matcher.py:370-384; DistributedAtomSpace.query prints str(set),
+ * distributed_atom_space.py:298-321).  Building one OrderedAssignment per row
+ * through assign()/freeze() costs microseconds of interpreter time per
+ * binding; this module builds the same objects from a fetched binding table in
+ * C: the instance __dict__ the Python class would hold after freeze()
+ * (pattern_matcher.OrderedAssignment / UnorderedAssignment), with the same
+ * `hash` value -- hash(frozenset(mapping.items())) for ordered rows,
+ * hash((hash(frozenset(symbols.items())), hash(frozenset(values.items()))))
+ * for unordered ones -- computed by the interpreter's own hash functions.
+ * Handle strings are shared: one str per distinct atom id (`strs`, indexed
+ * through `lut`), so a row costs one dict, a few tuples and two frozensets.
+ *
+ * format_set(s) returns str(s) for a set of assignments, taking repr() of an
+ * OrderedAssignment's mapping in C instead of calling its Python __repr__.
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <stdint.h>
+
+static PyObject *s_variables, *s_hash, *s_frozen, *s_mapping, *s_values, *s_symbols;
+
+static int get_u32(PyObject *o, Py_buffer *b, const char *what) {
+  if (PyObject_GetBuffer(o, b, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) < 0) return -1;
+  if (b->itemsize != 4) {
+    PyErr_Format(PyExc_TypeError, "%s: expected a 4-byte integer buffer", what);
+    PyBuffer_Release(b);
+    return -1;
+  }
+  return 0;
+}
+
+static PyObject *new_instance(PyTypeObject *cls, PyObject *empty, PyObject *dict) {
+  PyObject *obj = cls->tp_new(cls, empty, NULL);
+  if (!obj) return NULL;
+  PyObject **dp = _PyObject_GetDictPtr(obj);
+  if (!dp) {
+    Py_DECREF(obj);
+    PyErr_SetString(PyExc_TypeError, "assignment class has no __dict__");
+    return NULL;
+  }
+  Py_XSETREF(*dp, dict);   /* steals dict */
+  return obj;
+}
+
+/* hash(frozenset(d.items())) without building the items and the frozenset:
+ * the interpreter's tuple hash (xxHash lanes) of each (key, value) pair and
+ * its frozenset hash (shuffled XOR over the entries; the empty slots of the
+ * table cancel out, and a set of <= 4 entries has no dummy slots).  Checked
+ * against the interpreter at import (fast_hash_ok); otherwise, and for more
+ * than 4 entries, items_hash below is used. */
+#define XXPRIME_1 11400714785074694791ULL
+#define XXPRIME_2 14029467366897019727ULL
+#define XXPRIME_5 2870177450012600261ULL
+#define XXROTATE(x) ((x << 31) | (x >> 33))
+static int fast_hash_ok = 0;
+
+static Py_uhash_t pair_hash(Py_uhash_t a, Py_uhash_t b) {
+  Py_uhash_t acc = XXPRIME_5;
+  acc += a * XXPRIME_2; acc = XXROTATE(acc); acc *= XXPRIME_1;
+  acc += b * XXPRIME_2; acc = XXROTATE(acc); acc *= XXPRIME_1;
+  acc += 2 ^ (XXPRIME_5 ^ 3527539UL);
+  if (acc == (Py_uhash_t)-1) return 1546275796;
+  return acc;
+}
+static Py_uhash_t shuffle_bits(Py_uhash_t h) { return ((h ^ 89869747UL) ^ (h << 16)) * 3644798167UL; }
+/* frozenset of n <= 4 distinct elements with these hashes (8-slot table, no dummies) */
+static Py_hash_t small_frozenset_hash(const Py_uhash_t *h, Py_ssize_t n) {
+  Py_uhash_t hash = 0;
+  for (Py_ssize_t i = 0; i < n; ++i) hash ^= shuffle_bits(h[i]);   /* empty slots cancel out */
+  hash ^= ((Py_uhash_t)n + 1) * 1927868237UL;
+  hash ^= (hash >> 11) ^ (hash >> 25);
+  hash = hash * 69069U + 907133923UL;
+  if (hash == (Py_uhash_t)-1) hash = 590923713UL;
+  return (Py_hash_t)hash;
+}
+
+/* hash(frozenset(d.items())) */
+static Py_hash_t items_hash(PyObject *d) {
+  PyObject *items = PyDict_Items(d);
+  if (!items) return -1;
+  PyObject *fs = PyFrozenSet_New(items);
+  Py_DECREF(items);
+  if (!fs) return -1;
+  Py_hash_t h = PyObject_Hash(fs);
+  Py_DECREF(fs);
+  return h;
+}
+
+/* row value -> shared handle string */
+static PyObject *value_of(const uint32_t *lut, Py_ssize_t nlut, PyObject *strs, uint32_t id) {
+  if ((Py_ssize_t)id >= nlut) {
+    PyErr_SetString(PyExc_IndexError, "atom id outside the lookup table");
+    return NULL;
+  }
+  const uint32_t k = lut[id];
+  if ((Py_ssize_t)k >= PyList_GET_SIZE(strs)) {
+    PyErr_SetString(PyExc_IndexError, "atom id without a handle string");
+    return NULL;
+  }
+  return PyList_GET_ITEM(strs, k);   /* borrowed */
+}
+
+/* add_rows(out_set, cls, kind, names, cols, lut, strs)
+ *   kind 0 ordered / 1 unordered; names: tuple of k variable names; cols: u32
+ *   buffer (k, n) row-major by column; lut: u32 buffer id -> index in strs. */
+static PyObject *add_rows(PyObject *self, PyObject *args) {
+  PyObject *out, *cls, *names, *colso, *luto, *strs;
+  int kind;
+  if (!PyArg_ParseTuple(args, "O!OiO!OOO!", &PySet_Type, &out, &cls, &kind, &PyTuple_Type, &names, &colso, &luto,
+                        &PyList_Type, &strs))
+    return NULL;
+  if (!PyType_Check(cls)) {
+    PyErr_SetString(PyExc_TypeError, "cls must be a type");
+    return NULL;
+  }
+  Py_buffer cb, lb;
+  if (get_u32(colso, &cb, "cols") < 0) return NULL;
+  if (get_u32(luto, &lb, "lut") < 0) {
+    PyBuffer_Release(&cb);
+    return NULL;
+  }
+  const Py_ssize_t k = PyTuple_GET_SIZE(names);
+  const Py_ssize_t n = k ? (cb.len / 4) / k : 0;
+  const uint32_t *cols = (const uint32_t *)cb.buf, *lut = (const uint32_t *)lb.buf;
+  const Py_ssize_t nlut = lb.len / 4;
+  PyObject *empty = PyTuple_New(0), *vars = PyFrozenSet_New(names);
+  PyObject *result = NULL;
+  if (!empty || !vars) goto done;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject *d = PyDict_New();
+    if (!d) goto done;
+    if (PyDict_SetItem(d, s_variables, vars) < 0 || PyDict_SetItem(d, s_frozen, Py_True) < 0) {
+      Py_DECREF(d);
+      goto done;
+    }
+    Py_hash_t h;
+    if (kind == 0) {
+      PyObject *m = PyDict_New(), *vals = PyTuple_New(k);
+      if (!m || !vals) {
+        Py_XDECREF(m); Py_XDECREF(vals); Py_DECREF(d);
+        goto done;
+      }
+      int bad = 0;
+      for (Py_ssize_t c = 0; c < k && !bad; ++c) {
+        PyObject *v = value_of(lut, nlut, strs, cols[c * n + i]);
+        if (!v || PyDict_SetItem(m, PyTuple_GET_ITEM(names, c), v) < 0) bad = 1;
+        else {
+          Py_INCREF(v);
+          PyTuple_SET_ITEM(vals, c, v);
+        }
+      }
+      PyObject *fv = bad ? NULL : PyFrozenSet_New(vals);
+      Py_DECREF(vals);
+      if (fv && fast_hash_ok && k <= 4) {
+        Py_uhash_t lanes[4];
+        for (Py_ssize_t c = 0; c < k; ++c)
+          lanes[c] = pair_hash((Py_uhash_t)PyObject_Hash(PyTuple_GET_ITEM(names, c)),
+                               (Py_uhash_t)PyObject_Hash(value_of(lut, nlut, strs, cols[c * n + i])));
+        h = small_frozenset_hash(lanes, k);
+      } else {
+        h = fv ? items_hash(m) : -1;
+      }
+      if (h == -1 || PyDict_SetItem(d, s_mapping, m) < 0 || PyDict_SetItem(d, s_values, fv) < 0) {
+        Py_XDECREF(fv); Py_DECREF(m); Py_DECREF(d);
+        goto done;
+      }
+      Py_DECREF(fv);
+      Py_DECREF(m);
+    } else {
+      /* symbols: var -> count, values: value -> count (assign(), :207-214) */
+      PyObject *sym = PyDict_New(), *val = PyDict_New();
+      if (!sym || !val) {
+        Py_XDECREF(sym); Py_XDECREF(val); Py_DECREF(d);
+        goto done;
+      }
+      int bad = 0;
+      for (Py_ssize_t c = 0; c < k && !bad; ++c) {
+        PyObject *var = PyTuple_GET_ITEM(names, c);
+        PyObject *v = value_of(lut, nlut, strs, cols[c * n + i]);
+        if (!v) { bad = 1; break; }
+        PyObject *cs = PyDict_GetItemWithError(sym, var), *cv = PyDict_GetItemWithError(val, v);
+        if (PyErr_Occurred()) { bad = 1; break; }
+        PyObject *ns = PyLong_FromLong(cs ? PyLong_AsLong(cs) + 1 : 1);
+        PyObject *nv = PyLong_FromLong(cv ? PyLong_AsLong(cv) + 1 : 1);
+        if (!ns || !nv || PyDict_SetItem(sym, var, ns) < 0 || PyDict_SetItem(val, v, nv) < 0) bad = 1;
+        Py_XDECREF(ns);
+        Py_XDECREF(nv);
+      }
+      Py_hash_t hs = bad ? -1 : items_hash(sym), hv = hs == -1 ? -1 : items_hash(val);
+      PyObject *pair = hv == -1 ? NULL : Py_BuildValue("(nn)", (Py_ssize_t)hs, (Py_ssize_t)hv);
+      h = pair ? PyObject_Hash(pair) : -1;
+      Py_XDECREF(pair);
+      if (h == -1 || PyDict_SetItem(d, s_symbols, sym) < 0 || PyDict_SetItem(d, s_values, val) < 0) {
+        Py_DECREF(sym); Py_DECREF(val); Py_DECREF(d);
+        goto done;
+      }
+      Py_DECREF(sym);
+      Py_DECREF(val);
+    }
+    PyObject *hh = PyLong_FromSsize_t((Py_ssize_t)h);
+    if (!hh || PyDict_SetItem(d, s_hash, hh) < 0) {
+      Py_XDECREF(hh); Py_DECREF(d);
+      goto done;
+    }
+    Py_DECREF(hh);
+    PyObject *obj = new_instance((PyTypeObject *)cls, empty, d);
+    if (!obj) goto done;
+    int rc = PySet_Add(out, obj);
+    Py_DECREF(obj);
+    if (rc < 0) goto done;
+  }
+  result = Py_None;
+  Py_INCREF(result);
+done:
+  Py_XDECREF(empty);
+  Py_XDECREF(vars);
+  PyBuffer_Release(&cb);
+  PyBuffer_Release(&lb);
+  return result;
+}
+
+/* format_set(s, ordered_cls) == str(s) */
+static PyObject *format_set(PyObject *self, PyObject *args) {
+  PyObject *s, *ocls;
+  if (!PyArg_ParseTuple(args, "OO", &s, &ocls)) return NULL;
+  if (!PyAnySet_Check(s)) return PyObject_Str(s);
+  if (PySet_GET_SIZE(s) == 0) return PyObject_Repr(s);
+  PyObject *parts = PyList_New(0), *it = PyObject_GetIter(s), *x, *res = NULL;
+  if (!parts || !it) goto done;
+  while ((x = PyIter_Next(it))) {
+    PyObject *r;
+    if ((PyObject *)Py_TYPE(x) == ocls) {
+      PyObject **dp = _PyObject_GetDictPtr(x);
+      PyObject *m = dp && *dp ? PyDict_GetItemWithError(*dp, s_mapping) : NULL;
+      r = m ? PyObject_Repr(m) : PyObject_Repr(x);
+    } else {
+      r = PyObject_Repr(x);
+    }
+    Py_DECREF(x);
+    if (!r || PyList_Append(parts, r) < 0) {
+      Py_XDECREF(r);
+      goto done;
+    }
+    Py_DECREF(r);
+  }
+  if (PyErr_Occurred()) goto done;
+  {
+    PyObject *sep = PyUnicode_FromString(", ");
+    PyObject *body = sep ? PyUnicode_Join(sep, parts) : NULL;
+    Py_XDECREF(sep);
+    if (body) res = PyUnicode_FromFormat("{%U}", body);
+    Py_XDECREF(body);
+  }
+done:
+  Py_XDECREF(parts);
+  Py_XDECREF(it);
+  return res;
+}
+
+static PyObject *fast_hash_enabled(PyObject *self, PyObject *noargs);
+
+static PyMethodDef methods[] = {
+    {"add_rows", add_rows, METH_VARARGS, "Add Assignment objects built from a binding table to a set."},
+    {"format_set", format_set, METH_VARARGS, "str() of a set of assignments."},
+    {"fast_hash_enabled", fast_hash_enabled, METH_NOARGS, "True when the C restatement of the hashes is in use."},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_assign", NULL, -1, methods};
+
+/* fast_hash_ok: the restated hashes equal the interpreter's on sample rows */
+static void check_fast_hash(void) {
+  fast_hash_ok = 0;
+  for (int k = 1; k <= 4; ++k)
+    for (int trial = 0; trial < 8; ++trial) {
+      PyObject *d = PyDict_New();
+      Py_uhash_t lanes[4];
+      for (int c = 0; c < k; ++c) {
+        PyObject *key = PyUnicode_FromFormat("$v%d_%d", c, trial);
+        PyObject *val = PyUnicode_FromFormat("%032x", 7919 * (trial + 1) * (c + 3));
+        if (!key || !val || PyDict_SetItem(d, key, val) < 0) {
+          PyErr_Clear();
+          Py_XDECREF(key); Py_XDECREF(val); Py_DECREF(d);
+          return;
+        }
+        lanes[c] = pair_hash((Py_uhash_t)PyObject_Hash(key), (Py_uhash_t)PyObject_Hash(val));
+        Py_DECREF(key);
+        Py_DECREF(val);
+      }
+      const Py_hash_t want = items_hash(d);
+      Py_DECREF(d);
+      if (want == -1) { PyErr_Clear(); return; }
+      if (small_frozenset_hash(lanes, k) != want) return;
+    }
+  fast_hash_ok = 1;
+}
+
+static PyObject *fast_hash_enabled(PyObject *self, PyObject *noargs) { return PyBool_FromLong(fast_hash_ok); }
+
+PyMODINIT_FUNC PyInit__assign(void) {
+  check_fast_hash();
+  s_variables = PyUnicode_InternFromString("variables");
+  s_hash = PyUnicode_InternFromString("hash");
+  s_frozen = PyUnicode_InternFromString("frozen");
+  s_mapping = PyUnicode_InternFromString("mapping");
+  s_values = PyUnicode_InternFromString("values");
+  s_symbols = PyUnicode_InternFromString("symbols");
+  return PyModule_Create(&module);
+}

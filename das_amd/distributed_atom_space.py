@@ -25,6 +25,16 @@ class QueryOutputFormat(int, Enum):
     JSON = auto()
 
 
+def _format_assignments(assignments) -> str:
+    """str(set of assignments) (distributed_atom_space.py:308), with each
+    OrderedAssignment's repr(mapping) taken in C (das_amd._assign.format_set)
+    instead of through its Python __repr__."""
+    from .pattern_matcher import pattern_matcher as _pm
+    if _pm._assign is None:
+        return str(assignments)
+    return _pm._assign.format_set(assignments, _pm.OrderedAssignment)
+
+
 class DistributedAtomSpace:
 
     def __init__(self, **kwargs):
@@ -185,7 +195,7 @@ class DistributedAtomSpace:
             if query_answer.negation:
                 tag_not = "NOT "
             if output_format == QueryOutputFormat.HANDLE:
-                mapping = str(query_answer.assignments)
+                mapping = _format_assignments(query_answer.assignments)
             elif output_format in (QueryOutputFormat.ATOM_INFO, QueryOutputFormat.JSON):
                 # the reference calls .items() on a set here and raises
                 # (distributed_atom_space.py:312-318); kept as-is.

@@ -19,6 +19,7 @@ for unordered (Similarity/Set) operands the reference's Unordered /
 CompositeAssignment algebra (:158-368: containment / coverage /
 compatibility checks, XOR set identity), das_amd/csrc/composite.hip.
 """
+import gc
 import os
 import struct
 from abc import ABC, abstractmethod
@@ -564,12 +565,67 @@ class PatternMatchingAnswer:
         return self._db.rel_count(self._relation())
 
 
-def _materialize(db, rel):
+try:
+    from .. import _assign          # C builder of the answer's Assignment objects (csrc/pyassign.c)
+except ImportError:                 # not built: the same objects through assign() / freeze() below
+    _assign = None
+
+
+def _handle_strings(db, fetched):
+    """One handle string per distinct atom id of the fetched tables: (lut,
+    strs) with strs[lut[id]] = the id's 32-hex handle."""
+    parts = [c.ravel() for _, c in fetched if c.size]
+    if not parts:
+        return np.zeros(1, np.uint32), []
+    hi = int(max(int(p.max()) for p in parts))
+    if hi < (1 << 27):
+        present = np.zeros(hi + 1, dtype=bool)
+        for p in parts:
+            present[p] = True
+        ids = np.flatnonzero(present).astype(np.uint32)
+    else:
+        ids = np.unique(np.concatenate(parts))
+    lut = np.zeros(hi + 1, dtype=np.uint32)
+    lut[ids] = np.arange(ids.size, dtype=np.uint32)
+    return lut, list(db.hex_of(ids))
+
+
+def _materialize(db, rel, limit=None):
+    """answer.assignments: the reference's set of Assignment objects for the
+    device relation (lazy: built when a caller reads it).  `limit`: only the
+    first `limit` rows (bench.py's materialisation rate on large answers)."""
     out = set()
     if rel is None or not rel:
         return out
+    fetched = []
     for t in db.rel_local_tables(rel):
-        cols = t.fetch()
+        if limit is not None:
+            if limit <= 0:
+                break
+            fetched.append((t, t.fetch(0, limit)))
+            limit -= fetched[-1][1].shape[1]
+        else:
+            fetched.append((t, t.fetch()))
+    fast = _assign is not None and all(t.kind != _lib.TABLE_COMPOSITE for t, _ in fetched)
+    if fast:
+        lut, strs = _handle_strings(db, fetched)
+        # the objects hold strings and frozensets only (no reference cycles):
+        # the cyclic collector's passes over millions of young objects would
+        # cost more than building them
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            for t, cols in fetched:
+                if not t.nrows:
+                    continue
+                names = tuple(_var_name(v) for v in t.vars)
+                cls, kind = (OrderedAssignment, 0) if t.kind == _lib.TABLE_ORDERED else (UnorderedAssignment, 1)
+                _assign.add_rows(out, cls, kind, names, np.ascontiguousarray(cols, np.uint32), lut, strs)
+        finally:
+            if gc_on:
+                gc.enable()
+        return out
+    for t, cols in fetched:
         names = [_var_name(v) for v in t.vars]
         hexcols = [db.hex_of(c) for c in cols]
         if t.kind == _lib.TABLE_COMPOSITE:
@@ -578,7 +634,7 @@ def _materialize(db, rel):
             for k, m in enumerate(t.members):
                 if m >= 0:
                     m_cols.setdefault(m, []).append(k)
-        for i in range(t.nrows):
+        for i in range(cols.shape[1] if cols.ndim == 2 else 0):
             if t.kind == _lib.TABLE_ORDERED:
                 a = _ordered(names, hexcols, range(len(names)), i)
             elif t.kind == _lib.TABLE_UNORDERED:
