@@ -573,21 +573,26 @@ except ImportError:                 # not built: the same objects through assign
 
 def _handle_strings(db, fetched):
     """One handle string per distinct atom id of the fetched tables: (lut,
-    strs) with strs[lut[id]] = the id's 32-hex handle."""
+    strs, fetched') with strs[lut[v]] = the 32-hex handle of value v of the
+    (possibly re-coded) columns in fetched'.  Dense id ranges index a lookup
+    table directly; a few values over a wide id range are re-coded to their
+    rank among the distinct ids (no id-sized allocation)."""
     parts = [c.ravel() for _, c in fetched if c.size]
     if not parts:
-        return np.zeros(1, np.uint32), []
+        return np.zeros(1, np.uint32), [], fetched
+    total = sum(p.size for p in parts)
     hi = int(max(int(p.max()) for p in parts))
-    if hi < (1 << 27):
+    if hi < (1 << 27) and 8 * total >= hi:
         present = np.zeros(hi + 1, dtype=bool)
         for p in parts:
             present[p] = True
         ids = np.flatnonzero(present).astype(np.uint32)
-    else:
-        ids = np.unique(np.concatenate(parts))
-    lut = np.zeros(hi + 1, dtype=np.uint32)
-    lut[ids] = np.arange(ids.size, dtype=np.uint32)
-    return lut, list(db.hex_of(ids))
+        lut = np.zeros(hi + 1, dtype=np.uint32)
+        lut[ids] = np.arange(ids.size, dtype=np.uint32)
+        return lut, list(db.hex_of(ids)), fetched
+    ids = np.unique(np.concatenate(parts))
+    recoded = [(t, np.searchsorted(ids, c).astype(np.uint32)) for t, c in fetched]
+    return np.arange(ids.size, dtype=np.uint32), list(db.hex_of(ids)), recoded
 
 
 def _materialize(db, rel, limit=None):
@@ -608,7 +613,7 @@ def _materialize(db, rel, limit=None):
             fetched.append((t, t.fetch()))
     fast = _assign is not None and all(t.kind != _lib.TABLE_COMPOSITE for t, _ in fetched)
     if fast:
-        lut, strs = _handle_strings(db, fetched)
+        lut, strs, fetched = _handle_strings(db, fetched)
         # the objects hold strings and frozensets only (no reference cycles):
         # the cyclic collector's passes over millions of young objects would
         # cost more than building them

@@ -84,3 +84,12 @@ def test_two_tables_one_set_and_limit():
     lim_fast, lim_slow = _both([a, b], limit=420)
     assert lim_fast == lim_slow and len(lim_fast) <= 420
     assert pm._assign.format_set(set(), pm.OrderedAssignment) == "set()"
+
+
+def test_sparse_ids_recoded():
+    """Few values over a wide id range: re-coded, no id-sized lookup table."""
+    cols = np.array([[5, 100_000_000, 7, 3_000_000_000], [9, 9, 200_000_001, 11]], dtype=np.uint32)
+    t = _T(0, [pm._vid("$s1"), pm._vid("$s2")], cols)
+    fast, slow = _both([t])
+    assert fast == slow and len(fast) == 4
+    assert {tuple(sorted(a.mapping.items())) for a in fast} == {tuple(sorted(a.mapping.items())) for a in slow}
