@@ -76,7 +76,9 @@ class das_plan_node_t(C.Structure):
     ]
 
 
-PLAN_LINK, PLAN_CONST, PLAN_NOT, PLAN_AND, PLAN_OR = 1, 2, 3, 4, 5
+PLAN_LINK, PLAN_CONST, PLAN_NOT, PLAN_AND, PLAN_OR, PLAN_INPUT = 1, 2, 3, 4, 5, 6
+PLAN_WORDS = 51                   # u32 words per das_plan_node_t
+PLAN_SCAN = 5                     # word offset of its `scan` (das_link_scan_t)
 
 P = C.c_void_p
 DAS_BUILD_EXPR_ON_DEVICE = 1
@@ -119,6 +121,7 @@ _SIGS = {
     "das_set_minus": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P]),
     "das_table_members": (C.c_int, [P, P]),
     "das_table_set_bounds": (C.c_int, [P, P, P]),
+    "das_table_get_bounds": (C.c_int, [P, P, P]),
     "das_table_info": (C.c_int, [P, P, P, P, P]),
     "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
@@ -135,6 +138,10 @@ _SIGS = {
     "das_parsed_free": (C.c_int, [P]),
     "das_plan_execute": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32,
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "das_plan_execute_sharded": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32, P,
+                                           C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_int32), P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "das_plan_estimates": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, P]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
@@ -315,6 +322,13 @@ class Table:
         b = (C.c_uint32 * max(k, 1))(*[int(x) for x in hi])
         check(lib().das_table_set_bounds(self.h, a, b))
 
+    def bounds(self):
+        """(lo, hi) lists of the inclusive per-column value bounds."""
+        k = len(self.vars)
+        lo, hi = (C.c_uint32 * max(k, 1))(), (C.c_uint32 * max(k, 1))()
+        check(lib().das_table_get_bounds(self.h, lo, hi))
+        return [lo[i] for i in range(k)], [hi[i] for i in range(k)]
+
     def fetch(self, row0=0, nrows=None):
         """Rows [row0, row0 + nrows) (default: all) as a (ncols, n) host array."""
         n = self.nrows - row0 if nrows is None else min(nrows, self.nrows - row0)
@@ -493,6 +507,37 @@ class Context:
                 continue
             check(rc, self.h)
             return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
+
+    def plan_execute_sharded(self, words, n_nodes, inputs, no_overload=False):
+        """das_plan_execute_sharded: (matched, negation, [Table], checks)."""
+        nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
+        ins = (P * max(len(inputs), 1))(*[t.h for t in inputs])
+        cap, ccap = 64, max(64, n_nodes)
+        while True:
+            out = (P * cap)()
+            ck = np.zeros(ccap, dtype=np.uint8)
+            n_out, matched, neg, n_ck = C.c_uint32(), C.c_int32(), C.c_int32(), C.c_uint32()
+            rc = lib().das_plan_execute_sharded(self.h, nodes, n_nodes, 1 if no_overload else 0, ins, len(inputs),
+                                                out, cap, C.byref(n_out), C.byref(matched), C.byref(neg), ptr(ck),
+                                                ccap, C.byref(n_ck))
+            if rc == ERR_INVALID and (n_out.value > cap or n_ck.value > ccap):
+                cap, ccap = max(cap, n_out.value), max(ccap, n_ck.value)
+                continue
+            check(rc, self.h)
+            return (bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)],
+                    ck[:n_ck.value].copy())
+
+    def plan_estimates(self, words, n_nodes):
+        """Index rows each LINK node's scan would read on this GPU (u64 per node)."""
+        out = np.zeros(max(n_nodes, 1), dtype=np.uint64)
+        nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
+        check(lib().das_plan_estimates(self.h, nodes, n_nodes, ptr(out)), self.h)
+        return out[:n_nodes]
+
+    def scan_words(self, words, node):
+        """das_scan_link of plan node `node`'s scan record."""
+        q = C.cast(words.ctypes.data + 4 * (PLAN_WORDS * node + PLAN_SCAN), C.POINTER(das_link_scan_t))
+        return self._table(lib().das_scan_link, q)
 
     @staticmethod
     def link_scan_struct(q, arity, type_id, targets, var, n_vars, ordered, no_overload=False, emit_link=False,

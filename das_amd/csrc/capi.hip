@@ -617,6 +617,15 @@ int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi)
   return DAS_OK;
 }
 
+int das_table_get_bounds(const das_table_t* t, uint32_t* lo, uint32_t* hi) {
+  if (!t || !lo || !hi) return fail(nullptr, DAS_ERR_INVALID, "null argument");
+  for (int c = 0; c < t->t.ncols; ++c) {
+    lo[c] = t->t.lo[c];
+    hi[c] = t->t.hi[c];
+  }
+  return DAS_OK;
+}
+
 int das_table_members(const das_table_t* t, int32_t* member) {
   if (!t) return fail(nullptr, DAS_ERR_INVALID, "null table");
   for (int c = 0; c < t->t.ncols; ++c) member[c] = t->t.kind == DAS_TABLE_COMPOSITE ? t->t.member[c]
@@ -654,6 +663,38 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
     *n_out = (uint32_t)r.tables.size();
     *matched = r.matched ? 1 : 0;
     *negation = r.negation ? 1 : 0;
+  });
+}
+
+int das_plan_execute_sharded(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                             const das_table_t* const* inputs, uint32_t n_inputs, das_table_t** out, uint32_t cap,
+                             uint32_t* n_out, int32_t* matched, int32_t* negation, uint8_t* checks,
+                             uint32_t checks_cap, uint32_t* n_checks) {
+  if (!ctx || !nodes || !n_out || !matched || !negation || !n_checks || (n_inputs && !inputs))
+    return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    std::vector<const das::Table*> in(n_inputs);
+    for (uint32_t i = 0; i < n_inputs; ++i) in[i] = inputs[i] ? &inputs[i]->t : nullptr;
+    std::vector<uint8_t> ck;
+    auto r = das::plan_execute_sharded(ctx->c, nodes, n, (int)no_overload, in, ck);
+    *n_out = (uint32_t)r.tables.size();
+    *n_checks = (uint32_t)ck.size();
+    DAS_CHECK(r.tables.size() <= cap && ck.size() <= checks_cap, das::DAS_E_INVALID,
+              "plan: more answer tables or checks than their capacity");
+    for (size_t i = 0; i < r.tables.size(); ++i) out[i] = wrap(std::move(r.tables[i]));
+    for (size_t i = 0; i < ck.size(); ++i) checks[i] = ck[i];
+    *matched = r.matched ? 1 : 0;
+    *negation = r.negation ? 1 : 0;
+  });
+}
+
+int das_plan_estimates(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint64_t* rows) {
+  if (!ctx || (n && (!nodes || !rows))) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    DAS_CHECK(ctx->c.idx.built, das::DAS_E_NOT_BUILT, "index not built");
+    for (uint32_t i = 0; i < n; ++i)
+      rows[i] = nodes[i].op == DAS_PLAN_LINK || nodes[i].op == DAS_PLAN_INPUT ? das::scan_estimate(ctx->c, nodes[i].scan)
+                                                                               : 0;
   });
 }
 

@@ -285,6 +285,15 @@ struct PlanOutput {
   std::vector<std::unique_ptr<Table>> tables;
 };
 PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload);
+// Sharded evaluation (das_plan_execute_sharded): INPUT leaves are the
+// caller's tables (replicated relations), LINK leaves scan / index-join this
+// shard's index (partial relations, whose emptiness is assumed, not tested);
+// `checks` gets one bit per positive term of the top-level And: the local
+// running result is non-empty after that term.
+PlanOutput plan_execute_sharded(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload,
+                                const std::vector<const Table*>& inputs, std::vector<uint8_t>& checks);
+// Rows a das_scan_link would read (its index ranges; an upper bound of its output).
+uint64_t scan_estimate(Ctx& c, const das_link_scan_t& q);
 // query.hip: an And of ordered Links (terms) and Not(Link) filters (anti)
 // evaluated by one single-workgroup launch when its running result stays
 // small.  0: not taken (the caller evaluates it operator by operator);

@@ -27,6 +27,7 @@ using TablePtr = std::unique_ptr<Table>;
 
 struct Rel {
   std::vector<TablePtr> t;
+  bool partial = false;     // sharded: this shard's part of a relation split across shards
   bool nonempty() const {
     for (auto& x : t)
       if (x->nrows) return true;
@@ -55,11 +56,19 @@ struct Exec {
   const das_plan_node_t* nd;
   uint32_t n;
   int no_overload;
+  // sharded mode (das_plan_execute_sharded): INPUT leaves, partial relations
+  const std::vector<const Table*>* inputs = nullptr;
+  std::vector<uint8_t>* checks = nullptr;
+  bool sharded() const { return inputs != nullptr; }
+  // Emptiness as the fold sees it.  A partial relation is assumed non-empty
+  // (its global emptiness needs every shard); the caller verifies the
+  // assumption afterwards from the `checks` bits of all shards.
+  bool ne(const Rel& r) const { return (sharded() && r.partial) || r.nonempty(); }
 
   uint32_t next(uint32_t i) const {
     DAS_CHECK(i < n, DAS_E_INVALID, "plan: truncated node array");
     const das_plan_node_t& x = nd[i];
-    if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_CONST) return i + 1;
+    if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_CONST || x.op == DAS_PLAN_INPUT) return i + 1;
     if (x.op == DAS_PLAN_NOT) return next(i + 1);
     DAS_CHECK(x.op == DAS_PLAN_AND || x.op == DAS_PLAN_OR, DAS_E_INVALID, "plan: bad node op");
     uint32_t j = i + 1;
@@ -94,6 +103,7 @@ struct Exec {
       }
     }
     Rel out;
+    out.partial = a.partial;
     for (auto& g : groups) {
       if (g.size() == 1) {
         out.push(std::move(g[0]));
@@ -109,6 +119,7 @@ struct Exec {
 
   Rel join_rel(const Rel& a, const Rel& b) {
     Rel out;
+    out.partial = a.partial || b.partial;
     for (auto& ta : a.t)
       for (auto& tb : b.t) out.push(join(c, *ta, *tb, no_overload));
     return out;
@@ -117,6 +128,7 @@ struct Exec {
   Rel antijoin_rel(Rel r, const Rel& f) {
     for (auto& ft : f.t) {
       Rel nx;
+      nx.partial = r.partial;
       for (auto& t : r.t) nx.push(antijoin(c, *t, *ft));
       r = std::move(nx);
     }
@@ -125,6 +137,7 @@ struct Exec {
 
   Rel minus_rel(Rel a, const Rel& b) {
     Rel out;
+    out.partial = a.partial;
     for (auto& t : a.t) {
       TablePtr cur = std::move(t);
       for (auto& f : b.t)
@@ -136,8 +149,8 @@ struct Exec {
 
   Res eval(uint32_t i) {
     const das_plan_node_t& x = nd[i];
-    static const char* const kOp[] = {"?", "LINK", "CONST", "NOT", "AND", "OR"};
-    if (trace_on()) trace_mark("node", x.op <= 5 ? kOp[x.op] : "?");
+    static const char* const kOp[] = {"?", "LINK", "CONST", "NOT", "AND", "OR", "INPUT"};
+    if (trace_on()) trace_mark("node", x.op <= 6 ? kOp[x.op] : "?");
     Res r;
     switch (x.op) {
       case DAS_PLAN_CONST:
@@ -148,6 +161,18 @@ struct Exec {
         TablePtr t = scan_link(c, x.scan);
         if (x.dedup && t->nrows) t = dedup(c, *t);
         r.rel.push(std::move(t));
+        r.rel.partial = sharded();        // this shard's links only
+        r.matched = ne(r.rel);
+        return r;
+      }
+      case DAS_PLAN_INPUT: {
+        // a caller's table (e.g. a term's rows gathered from every shard):
+        // read in place, never freed here
+        DAS_CHECK(sharded() && x.value < inputs->size() && (*inputs)[x.value], DAS_E_INVALID,
+                  "plan: INPUT leaf without a table");
+        auto v = std::make_unique<Table>(*(*inputs)[x.value]);
+        v->view = true;
+        r.rel.push(std::move(v));
         r.matched = r.rel.nonempty();
         return r;
       }
@@ -157,7 +182,7 @@ struct Exec {
         r.matched = true;
         return r;
       case DAS_PLAN_AND:
-        return eval_and(children(i));
+        return eval_and(children(i), i == 0);
       case DAS_PLAN_OR:
         return eval_or(children(i));
       default:
@@ -169,7 +194,10 @@ struct Exec {
   // other target grounded (its scan is one column of distinct keys), or -1.
   int32_t one_var(uint32_t ti) const {
     const das_plan_node_t& x = nd[ti];
-    if (x.op != DAS_PLAN_LINK || !x.scan.ordered || x.scan.emit_link || x.scan.type_id == kNone) return -1;
+    // sharded: only a replicated (INPUT) term is a whole key set to filter by
+    if (x.op != (sharded() ? DAS_PLAN_INPUT : DAS_PLAN_LINK) || !x.scan.ordered || x.scan.emit_link ||
+        x.scan.type_id == kNone)
+      return -1;
     int32_t v = -1;
     for (uint32_t p = 0; p < x.scan.arity && p < 8; ++p) {
       if (x.scan.target[p] != kNone) continue;
@@ -202,11 +230,12 @@ struct Exec {
   // term fails the And (:712-713).
   bool step(uint32_t ti, Rel& acc, bool& have, std::vector<Rel>& forbidden) {
     const das_plan_node_t& x = nd[ti];
-    if (have && x.op == DAS_PLAN_LINK && x.index_join && acc.nonempty()) {
+    if (have && x.op == DAS_PLAN_LINK && x.index_join && ne(acc)) {
       // the term's rows looked up from the running result's keys; an empty
       // result takes the scan path, which tells a failing term (And ->
       // False) from an empty join (reset-on-empty)
       Rel r;
+      r.partial = sharded();              // looked up in this shard's index
       bool ok = true;
       for (auto& t : acc.t) {
         auto j = index_join(c, *t, x.ij);
@@ -216,19 +245,19 @@ struct Exec {
         }
         r.push(std::move(j));
       }
-      if (ok && r.nonempty()) {
+      if (ok && ne(r)) {
         acc = std::move(r);
         return true;
       }
     }
     Res s = eval(ti);
     if (!s.matched) return false;
-    if (!s.rel.nonempty()) return true;
+    if (!ne(s.rel)) return true;
     if (s.neg) {
       forbidden.push_back(std::move(s.rel));
       return true;
     }
-    if (!have || !acc.nonempty()) {
+    if (!have || !ne(acc)) {
       acc = std::move(s.rel);
       have = true;
     } else {
@@ -257,7 +286,7 @@ struct Exec {
     return e;
   }
 
-  Res eval_and(const std::vector<uint32_t>& terms) {
+  Res eval_and(const std::vector<uint32_t>& terms, bool root = false) {
     Res out;
     if (terms.empty()) return out;
     Rel acc;
@@ -265,7 +294,12 @@ struct Exec {
     std::vector<Rel> forbidden;
     std::vector<uint32_t> anti;        // Not(Link) terms applied as anti index joins
     uint32_t skip = 0;                 // positive terms the fused chain already folded into acc
-    {
+    const bool top = checks && root;
+    auto log = [&](size_t n_terms) {   // sharded: acc's local emptiness after each positive term
+      if (top)
+        for (size_t j = 0; j < n_terms; ++j) checks->push_back(acc.nonempty() ? 1 : 0);
+    };
+    if (!sharded()) {
       // the leading Link terms of the And (and its Not(Link) filters): one
       // fused launch while the running result stays small
       std::vector<const das_plan_node_t*> pos, neg;
@@ -294,15 +328,20 @@ struct Exec {
     for (size_t k = 0; k < terms.size(); ++k) {
       const uint32_t ti = terms[k];
       const das_plan_node_t& x = nd[ti];
-      if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) {
+      if (!sharded() && x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) {
         // Not.matched is always True and its rows only ever filter the final
         // result (:720-724, :741-746): instead of scanning the term, each
         // result row's link is looked up in the index at the end
         anti.push_back(ti + 1);
         continue;
       }
+      if (x.op == DAS_PLAN_NOT) {
+        // a negated term: its rows join `forbidden` (no fold of acc)
+        if (!step(ti, acc, have, forbidden)) return Res{};
+        continue;
+      }
       if (seen++ < skip) continue;
-      if (have && acc.nonempty()) {
+      if (have && ne(acc)) {
         const size_t e = semi_run(terms, k, acc);
         if (e >= k + 2) {
           // consecutive one-variable terms on one variable of a large running
@@ -317,16 +356,19 @@ struct Exec {
           std::vector<const Table*> qs;
           for (auto& r : rs) qs.push_back(r.t[0].get());
           TablePtr f = semi_join_multi(c, *acc.t[0], qs);
-          if (f && f->nrows) {
+          const bool part = acc.partial;
+          if (f && (f->nrows || (sharded() && part))) {
             // non-empty: every prefix of the term-by-term fold is non-empty
             // too (the fold's rows project onto each prefix), so no
             // reset-on-empty step was skipped and the rows are the same
             acc = Rel{};
+            acc.partial = part;
             acc.push(std::move(f));
           } else {
-            for (auto& r : rs) acc = acc.nonempty() ? join_rel(acc, r) : std::move(r);
+            for (auto& r : rs) acc = ne(acc) ? join_rel(acc, r) : std::move(r);
           }
           seen += (uint32_t)(e - k - 1);
+          log(e - k);
           k = e - 1;
           continue;
         }
@@ -348,21 +390,24 @@ struct Exec {
           std::vector<const Table*> qs;
           for (auto& r : rs) qs.push_back(r.t[0].get());
           TablePtr f = index_join_filtered(c, *acc.t[0], x.ij, v, qs);
-          if (f && f->nrows) {
+          if (f && (f->nrows || sharded())) {
             // non-empty: no prefix of the term-by-term fold was empty (see
             // semi_join_multi above), so the rows are the fold's
             acc = Rel{};
+            acc.partial = sharded();      // expanded through this shard's index
             acc.push(std::move(f));
           } else {
             if (!step(ti, acc, have, forbidden)) return Res{};
-            for (auto& r : rs) acc = acc.nonempty() ? join_rel(acc, r) : std::move(r);
+            for (auto& r : rs) acc = ne(acc) ? join_rel(acc, r) : std::move(r);
           }
           seen += (uint32_t)(e - k - 1);
+          log(e - k);
           k = e - 1;
           continue;
         }
       }
       if (!step(ti, acc, have, forbidden)) return Res{};
+      log(1);
     }
     for (auto& f : forbidden)
       if (acc.nonempty()) acc = antijoin_rel(std::move(acc), f);
@@ -385,7 +430,7 @@ struct Exec {
   Res eval_or(const std::vector<uint32_t>& terms) {
     Res out;
     if (terms.empty()) return out;
-    {
+    if (!sharded()) {
       // an Or of Links of one schema: scans and union in one launch
       std::vector<const das_plan_node_t*> links;
       for (uint32_t ti : terms) links.push_back(&nd[ti]);
@@ -426,6 +471,34 @@ struct Exec {
 };
 
 }  // namespace
+
+PlanOutput plan_execute_sharded(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload,
+                                const std::vector<const Table*>& inputs, std::vector<uint8_t>& checks) {
+  DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
+  DAS_CHECK(n > 0, DAS_E_INVALID, "plan: no nodes");
+  Exec ex{c, nodes, n, no_overload};
+  ex.inputs = &inputs;
+  ex.checks = &checks;
+  DAS_CHECK(ex.next(0) == n, DAS_E_INVALID, "plan: node array is not one expression tree");
+  trace_mark("plan (sharded)");
+  Res r = ex.eval(0);
+  trace_mark("done");
+  trace_dump("das_plan_execute_sharded");
+  PlanOutput out;
+  out.matched = r.matched;
+  out.negation = r.neg;
+  for (auto& t : r.rel.t) {
+    if (t->view) {
+      // an INPUT table is the caller's: the answer gets its own copy
+      auto m = new_table_like(c, *t, t->nrows);
+      m->nrows = t->nrows;
+      for (int k = 0; k < t->ncols; ++k) copy_dev(m->col(k), t->col(k), 4 * t->nrows, c.s);
+      t = std::move(m);
+    }
+    out.tables.push_back(std::move(t));
+  }
+  return out;
+}
 
 PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload) {
   DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");

@@ -1540,6 +1540,15 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
 }
 }  // namespace
 
+uint64_t scan_estimate(Ctx& c, const das_link_scan_t& q) {
+  ScanPrep P;
+  scan_prepare(c, q, P);
+  if (P.empty) return 0;
+  uint64_t n = 0;
+  for (auto& r : P.ranges) n += r.second - r.first;
+  return n;
+}
+
 std::unique_ptr<Table> scan_link(Ctx& c, const das_link_scan_t& q) {
   ScanPrep P;
   scan_prepare(c, q, P);

@@ -102,7 +102,10 @@ class ShardedDB(RelationalDB):
         self.rank = dist.get_rank(group)
         self.tuple_targets = local.tuple_targets
         self.spec = dict(partition_spec or {})
-        self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0, "heavy": 0}   # join placements taken
+        # join placements taken; native = expressions evaluated by one sharded
+        # native plan (fallback: its check failed), collectives issued
+        self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0, "heavy": 0, "native": 0,
+                           "native_fallback": 0, "collectives": 0}
         # DAS_JOIN_PLACEMENT=exchange|broadcast forces one placement (tests)
         self.force = os.environ.get("DAS_JOIN_PLACEMENT", "")
         # a key bucket is heavy when its rows (both sides) exceed this fraction
@@ -113,7 +116,16 @@ class ShardedDB(RelationalDB):
     def _allreduce_sum(self, values):
         t = self.local.xfer_tensor(np.asarray(values, dtype=np.int64))
         self.dist.all_reduce(t, group=self.group)
+        self.plan_stats["collectives"] += 1
         return self.local.xfer_numpy(t)
+
+    def _allgather_i64(self, values):
+        """[world, len(values)] int64 of every rank's `values` (one collective)."""
+        t = self.local.xfer_tensor(np.asarray(values, dtype=np.int64))
+        out = self.local.xfer_tensor(np.zeros(self.world * t.numel(), dtype=np.int64))
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        self.plan_stats["collectives"] += 1
+        return self.local.xfer_numpy(out).reshape(self.world, -1)
 
     def _exchange(self, table, key_vars):
         """Repartition `table` by hash(key_vars) (every column if empty)."""
@@ -129,6 +141,7 @@ class ShardedDB(RelationalDB):
         send_counts = self.local.xfer_tensor(counts.astype(np.int64))
         recv_counts = self.local.xfer_tensor(np.zeros(self.world, dtype=np.int64))
         self.dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        self.plan_stats["collectives"] += 2
         rc = self.local.xfer_numpy(recv_counts).tolist()
         ncols = len(table.vars)
         send = self.local.rows_out(part)
@@ -148,6 +161,7 @@ class ShardedDB(RelationalDB):
         padded = self.local.rows_pad(send, width, ncols)
         outs = [self.local.rows_buffer(width, ncols) for _ in range(self.world)]
         self.dist.all_gather(outs, padded, group=self.group)
+        self.plan_stats["collectives"] += 1
         return self.local.rows_in_many(table.kind, table.vars, outs, [int(x) for x in n], _members(table))
 
     def _rank_slice(self, table):
@@ -162,6 +176,7 @@ class ShardedDB(RelationalDB):
         t = self.local.xfer_tensor(np.array([n], dtype=np.int64))
         outs = [self.local.xfer_tensor(np.zeros(1, dtype=np.int64)) for _ in range(self.world)]
         self.dist.all_gather(outs, t, group=self.group)
+        self.plan_stats["collectives"] += 1
         return np.array([int(self.local.xfer_numpy(o)[0]) for o in outs], dtype=np.int64)
 
     # ----------------------------------------------------- DBInterface (global)
@@ -250,6 +265,211 @@ class ShardedDB(RelationalDB):
         if not ordered or len(set(var_ids)) != len(var_ids):
             t = self.local.dedup(self._exchange(t, []))
         return DRel([t])
+
+    # ------------------------------------------------- sharded native plans
+    # A term whose rows over all shards exceed SMALL (DAS_SHARD_SMALL) stays
+    # split (read from each shard's index); smaller terms are gathered to
+    # every shard.
+    SMALL = 1 << 22
+    GATHER_LIMIT = 1 << 26              # rows gathered per query at most (else the per-operator path)
+
+    def plan_sharded(self, expr, answer):
+        """Evaluates `expr` as ONE das_plan_execute_sharded call per GPU, or
+        returns None (the caller then folds it operator by operator).
+
+        Shapes: a single Link, an And of Links / grounded terms / Not(Link),
+        an Or of Links (each Link ordered, its rows distinct).  Every Link's
+        index rows are estimated on each shard and all-gathered (collective
+        1); an And keeps its one large term -- or several, when
+        partition_spec places them all by the same variable -- split across
+        shards, read through each shard's index (scan, index join, filtered
+        expansion), and gathers every other term to every shard in one
+        all-gather (collective 2).  The fold assumes the split running result
+        non-empty where it tests it; the final all-reduce of the result rows
+        and of those tests' outcomes (collective 3) confirms it, or the
+        expression falls back (pattern_matcher.py:705-748 semantics either way)."""
+        from .pattern_matcher import pattern_matcher as pm
+        from . import _lib as L
+        db = getattr(self.local, "db", None)
+        if db is None or not hasattr(db, "ctx") or os.environ.get("DAS_SHARDED_PLAN") == "0" or answer.negation:
+            return None
+        no_overload = bool(pm.CONFIG['no_overload'])
+        key = (db.generation, no_overload)
+        cached = getattr(expr, '_plan', None)
+        if cached is None or cached[0] != key:
+            cached = (key, pm._lower(expr, db, no_overload))
+            expr._plan = cached
+        nodes = cached[1]
+        if nodes is None:
+            return None
+        W = L.PLAN_WORDS
+        n = len(nodes) // W
+        rec = nodes.reshape(n, W)
+        op = rec[:, 0]
+        # shape: the root's children are leaves (LINK / CONST / NOT LINK)
+        if op[0] == L.PLAN_LINK:
+            leaves, pos, neg = [0], [0], []
+        elif op[0] in (L.PLAN_AND, L.PLAN_OR):
+            leaves, pos, neg = [], [], []
+            i = 1
+            for _ in range(int(rec[0, 1])):
+                if op[i] == L.PLAN_NOT and i + 1 < n and op[i + 1] == L.PLAN_LINK and op[0] == L.PLAN_AND:
+                    leaves.append(i + 1)
+                    neg.append(i + 1)
+                    i += 2
+                elif op[i] in (L.PLAN_LINK, L.PLAN_CONST):
+                    if op[i] == L.PLAN_LINK:
+                        leaves.append(i)
+                    pos.append(i)
+                    i += 1
+                else:
+                    return None
+            if i != n:
+                return None
+        else:
+            return None
+        if any(rec[i, 3] for i in leaves):              # dedup leaves: rows may repeat across shards
+            return None
+        ctx = db.ctx
+        single = op[0] == L.PLAN_LINK
+        if single:
+            local, gathered = [0], []
+        else:
+            est = self._allgather_i64(ctx.plan_estimates(nodes, n)[leaves])        # collective 1
+            G = dict(zip(leaves, est.sum(axis=0).tolist()))
+            M = dict(zip(leaves, est.max(axis=0).tolist()))
+            local = []
+            if op[0] == L.PLAN_AND:
+                small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
+                big = [i for i in leaves if i not in neg and G[i] > small]
+                if len(big) == 1:
+                    local = big
+                elif len(big) > 1:
+                    pv = {self._placement_var(db, rec[i]) for i in big}
+                    if len(pv) != 1 or None in pv:
+                        return None
+                    local = big
+            gathered = [i for i in leaves if i not in local]
+            if sum(G[i] for i in gathered) > self.GATHER_LIMIT:
+                return None
+        # gathered terms: this shard's rows, all-gathered into every shard (collective 2)
+        tables = [ctx.scan_words(nodes, i) for i in gathered]
+        inputs = self._gather_many(tables, [M[i] for i in gathered]) if gathered else []
+        words = nodes.copy().reshape(n, W)
+        for slot, i in enumerate(gathered):
+            words[i, 0] = L.PLAN_INPUT
+            words[i, 2] = slot
+        words = words.reshape(-1)
+        matched, negation, out, checks = ctx.plan_execute_sharded(words, n, inputs, no_overload)
+        del inputs, tables
+        if not local:
+            # every shard holds the whole answer: shard 0 keeps it
+            total = sum(t.nrows for t in out)
+            if self.rank != 0:
+                out = [self.local.empty_table(t.kind, list(t.vars), t.members) for t in out]
+            rel = DRel(out)
+            rel._global = total
+        else:
+            # the tested running results must hold rows on some shard: after
+            # each positive term from the first split one up to (not
+            # including) the last, whose emptiness is just the answer's
+            first = min(pos.index(i) for i in local) if not single else 0
+            need = list(range(first, len(checks) - 1)) if not single else []
+            # one ordered table per shard, the And's schema (sorted variable
+            # ids of its positive terms), even where this shard has no rows:
+            # later collectives over the relation pair tables up by position
+            s0 = L.PLAN_SCAN
+            vars_ = sorted({int(np.int32(rec[i, s0 + 10 + p])) for i in (pos if not single else [0])
+                            if op[i] == L.PLAN_LINK for p in range(int(rec[i, s0]))
+                            if int(np.int32(rec[i, s0 + 10 + p])) >= 0})
+            out = [t for t in out if t.nrows]
+            bad = int(len(out) > 1 or any(t.kind != L.TABLE_ORDERED or list(t.vars) != vars_ for t in out))
+            if not out:
+                out = [self.local.empty_table(L.TABLE_ORDERED, vars_)]
+            got = self._allreduce_sum([sum(t.nrows for t in out), bad] +
+                                      [int(checks[j]) for j in need])                               # collective 3
+            if int(got[1]) or any(int(x) == 0 for x in got[2:]):
+                self.plan_stats["native_fallback"] += 1
+                return None
+            rel = DRel(out)
+            rel._global = int(got[0])
+            if matched:
+                matched = rel._global > 0
+        self.plan_stats["native"] += 1
+        answer._set(self, rel)
+        answer.negation = negation
+        return matched
+
+    def _placement_var(self, db, words):
+        """The variable that places this Link term's rows (partition_spec:
+        links of its type live on the owner of the atom at a position), or None."""
+        from . import _lib as L
+        s0 = L.PLAN_SCAN
+        tid = int(words[s0 + 1])
+        name = next((t for t, i in db.type_id.items() if i == tid), None)
+        p = self.spec.get(name)
+        if p is None or p >= int(words[s0]):
+            return None
+        v = int(np.int32(words[s0 + 10 + p]))
+        return v if v >= 0 else None
+
+    def _gather_many(self, tables, caps):
+        """Every shard's rows of each table, to every shard, in ONE
+        all-gather: per shard a header (row count and column bounds per
+        table) and each table's rows (row-major) in a slot of `caps[j]` rows
+        (caps: the largest estimate any shard reported, an upper bound)."""
+        import torch
+        lo_hi = [t.bounds() for t in tables]
+        ncols = [max(len(t.vars), 1) for t in tables]
+        H = sum(1 + 2 * len(t.vars) for t in tables)
+        offs, off = [], H
+        for c, k in zip(caps, ncols):
+            offs.append(off)
+            off += int(c) * k
+        width = off
+        hdr = []
+        for t, (lo, hi) in zip(tables, lo_hi):
+            hdr += [t.nrows] + list(lo) + list(hi)
+        loc = self.local
+        gpu = loc.gpu
+        buf = torch.zeros(width, dtype=torch.int32, device=gpu)
+        buf[:H] = torch.from_numpy(np.array(hdr, dtype=np.uint32).view(np.int32)).to(gpu)
+        if not loc.stream_ordered:
+            torch.cuda.current_stream().synchronize()
+        for t, o in zip(tables, offs):
+            if t.nrows:
+                assert t.nrows * len(t.vars) <= (width - o), "gather: estimate below the rows"
+                loc.db.ctx.export_rows(t, buf.data_ptr() + 4 * o)
+        if not loc.stream_ordered:
+            loc.db.ctx.sync()
+        stage = buf if loc.dev == gpu else buf.cpu()
+        out = torch.empty(self.world * width, dtype=torch.int32, device=stage.device)
+        self.dist.all_gather_into_tensor(out, stage, group=self.group)
+        self.plan_stats["collectives"] += 1
+        out_dev = out.to(gpu)
+        heads = out.view(self.world, width)[:, :H].cpu().numpy().view(np.uint32)
+        if not loc.stream_ordered:
+            torch.cuda.current_stream().synchronize()
+        result = []
+        h = 0
+        for j, (t, o) in enumerate(zip(tables, offs)):
+            k = len(t.vars)
+            cnt = heads[:, h].astype(np.int64)
+            lo = heads[:, h + 1:h + 1 + k]
+            hi = heads[:, h + 1 + k:h + 1 + 2 * k]
+            h += 1 + 2 * k
+            parts = [loc.db.ctx.import_rows(t.kind, list(t.vars), out_dev.data_ptr() + 4 * (r * width + o), int(cnt[r]),
+                                            t.members) for r in range(self.world) if cnt[r]]
+            g = parts[0] if len(parts) == 1 else (loc.db.ctx.concat(parts) if parts else
+                                                  loc.db.ctx.import_rows(t.kind, list(t.vars), None, 0, t.members))
+            has = cnt > 0
+            if has.any() and k:
+                g.set_bounds(lo[has].min(axis=0), hi[has].max(axis=0))
+            result.append(g)
+        if not loc.stream_ordered:
+            loc.db.ctx.sync()
+        del out_dev
+        return result
 
     # ------------------------------------------------------- relation algebra
     def rel_empty(self):

@@ -495,8 +495,12 @@ def _lower(expr, db, no_overload):
 def _try_plan(expr, db, answer):
     """Evaluates `expr` with one das_plan_execute call when it can; returns
     its matched() result, or None for the per-operator path."""
-    if type(db) is not HipDB or answer.negation or os.environ.get("DAS_PLAN") == "0":
+    if os.environ.get("DAS_PLAN") == "0" or answer.negation:
         return None
+    if type(db) is not HipDB:
+        # a sharded DB (das_amd.parallel.ShardedDB) plans across its GPUs
+        sharded = getattr(db, "plan_sharded", None)
+        return sharded(expr, answer) if sharded is not None else None
     no_overload = bool(CONFIG['no_overload'])
     key = (db.generation, no_overload)          # generation: unique per load, any HipDB
     cached = getattr(expr, '_plan', None)

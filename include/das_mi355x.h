@@ -269,6 +269,8 @@ int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
  * it (values outside are dropped by the build).  Scan and join results carry
  * bounds derived from the index, so callers only set them on imported tables. */
 int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi);
+/* The declared / derived inclusive bounds per column ([0, DAS_NONE] = unknown). */
+int das_table_get_bounds(const das_table_t* t, uint32_t* lo, uint32_t* hi);
 /* Member id per column: -1 ordered, m = unordered member m (DAS_TABLE_COMPOSITE;
  * an UNORDERED table is member 0 throughout). */
 int das_table_members(const das_table_t* t, int32_t* member);
@@ -309,6 +311,27 @@ typedef struct {
 } das_plan_node_t;
 int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
                      das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation);
+
+/* ---- sharded plans (links hash-partitioned by handle across GPUs) ---------- */
+/* One GPU's part of a plan over a KB sharded across GPUs (das_amd.parallel
+ * ShardedDB): an INPUT leaf (`value` = index into `inputs`, `scan` = the term
+ * it stands for) is a relation every shard holds whole -- e.g. a term's rows
+ * gathered from all shards -- and is read in place; a LINK leaf scans or
+ * index-joins this shard's index, giving this shard's part of the term.  The
+ * And fold assumes that such partial relations are non-empty where it tests
+ * them; checks[j] = 1 if the running result of the top-level And holds rows
+ * on this shard after its j-th positive term.  The caller verifies the
+ * assumption (for every j after the first LINK leaf, some shard has rows) and
+ * otherwise evaluates the expression another way.  No fused chain, no anti
+ * index join (a negated link's owner may be another shard), no fused Or. */
+#define DAS_PLAN_INPUT 6
+int das_plan_execute_sharded(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                             const das_table_t* const* inputs, uint32_t n_inputs, das_table_t** out, uint32_t cap,
+                             uint32_t* n_out, int32_t* matched, int32_t* negation, uint8_t* checks,
+                             uint32_t checks_cap, uint32_t* n_checks);
+/* rows[i] = the index rows node i's scan would read (LINK / INPUT nodes; an
+ * upper bound of its output on this shard), 0 for other nodes. */
+int das_plan_estimates(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint64_t* rows);
 
 /* ---- multi-GPU exchange (RCCL all-to-all of binding rows) ----- */
 /* Rows of `t` regrouped by destination = mix(key columns) % nparts (stable

@@ -271,20 +271,27 @@ def _sharded_kb(kind):
     from das_amd import synthetic
     from tests.golden import make_synthetic as MS
     from tests.test_parallel_gloo import _fly_queries, _hub_queries, _queries
-    if kind in ("default", "heavy"):
+    if kind in ("default", "heavy", "small"):
         return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
-    if kind == "hub":
+    if kind in ("hub", "hub_small"):
         return MS.make_arrays("hub"), _hub_queries()
     return MS.make_arrays("flybase"), _fly_queries()
+
+
+# mode -> environment of the two ranks: "heavy" folds operator by operator
+# with the heavy-hitter split (no sharded native plan); "*small" lowers the
+# gathered-term threshold so terms stay split on the shards (index joins
+# through each shard's index, the fold's emptiness checks, fallbacks)
+_SHARD_ENV = {"heavy": {"DAS_SHARDED_PLAN": "0", "DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
+              "hub": {"DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
+              "small": {"DAS_SHARD_SMALL": "40"}, "hub_small": {"DAS_SHARD_SMALL": "30"}}
 
 
 def _sharded_worker(rank, world, port, out_path, mode):
     import os as _os
     import torch
     import torch.distributed as dist
-    if mode in ("heavy", "hub"):          # exchanged joins with skewed buckets split
-        _os.environ["DAS_JOIN_PLACEMENT"] = "exchange"
-        _os.environ["DAS_HEAVY_FRAC"] = "0.05"
+    _os.environ.update(_SHARD_ENV.get(mode, {}))
     _os.environ["MASTER_ADDR"] = "127.0.0.1"
     _os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -301,14 +308,18 @@ def _sharded_worker(rank, world, port, out_path, mode):
     res = []
     for q in queries:
         ans = pm.PatternMatchingAnswer()
+        st0 = dict(sdb.plan_stats)
         try:
             m = build(q).matched(sdb, ans)
         except AttributeError as e:
             res.append({"error": type(e).__name__})
             continue
+        st1 = dict(sdb.plan_stats)
+        n = ans.count()
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
-        res.append({"matched": bool(m), "negation": ans.negation, "n": ans.count(), "rows": rows,
-                    "local": sdb.rel_local_count(ans._relation())})
+        res.append({"matched": bool(m), "negation": ans.negation, "n": n, "rows": rows,
+                    "local": sdb.rel_local_count(ans._relation()),
+                    "native": st1["native"] - st0["native"], "collectives": st1["collectives"] - st0["collectives"]})
     res.append(sorted(_indexed_links(db)))
     res.append(sdb.plan_stats)
     with open(f"{out_path}.{rank}", "w") as f:
@@ -316,13 +327,15 @@ def _sharded_worker(rank, world, port, out_path, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["default", "heavy", "hub", "flybase"])
+@pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "flybase"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
-    """The multi-GPU path (handle-sharded builds, partition / export / import
-    kernels + exchange) with two ranks sharing cuda:0 over gloo, against the
-    single-process oracle: bio, the hub 4-clause And with the heavy-hitter
-    split (config 5) and the FlyBase And / Not / Or shapes (config 3).  Each
-    link is indexed on exactly one rank."""
+    """The multi-GPU path with two ranks sharing cuda:0 over gloo, against the
+    single-process oracle: handle-sharded builds (each link indexed on exactly
+    one rank), sharded native plans (gathered terms + one split term read
+    through each shard's index, das_plan_execute_sharded) and the
+    operator-by-operator fold with exchanges and the heavy-hitter split;
+    bio, the hub 4-clause And (config 5) and the FlyBase And / Not / Or
+    shapes (config 3).  FlyBase queries take <= 3 collectives each."""
     import socket
     import tempfile
     import torch.multiprocessing as mp
@@ -338,8 +351,14 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
         out = os.path.join(d, "res")
         mp.spawn(_sharded_worker, args=(2, port, out, mode), nprocs=2, join=True)
         per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
-    if mode in ("heavy", "hub"):
-        assert per_rank[0][-1]["heavy"] > 0, per_rank[0][-1]
+    stats = per_rank[0][-1]
+    if mode == "heavy":
+        assert stats["heavy"] > 0 and stats["native"] == 0, stats
+    else:
+        assert stats["native"] > 0, stats
+    if mode in ("small", "hub_small"):
+        # some queries keep terms split across the shards and still verify
+        assert any(r.get("native") and r.get("collectives") == 3 for r in per_rank[0][:-2]), per_rank[0][:-2]
     indexed = [set(per_rank[r][-2]) for r in range(2)]
     assert not (indexed[0] & indexed[1]) and indexed[0] | indexed[1] == set(okb.links)
     assert all(handle_owner(h, 2) == r for r in range(2) for h in indexed[r])
@@ -354,6 +373,9 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
             got = per_rank[r][qi]
             assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
             assert got["rows"] == want_rows, q
+        if mode == "flybase":
+            got = per_rank[0][qi]
+            assert got["native"] == 1 and got["collectives"] <= 3, (q, got["native"], got["collectives"])
 
 
 def _composite_queries(rng, arrays, n):
