@@ -76,7 +76,7 @@ class das_plan_node_t(C.Structure):
     ]
 
 
-PLAN_LINK, PLAN_CONST, PLAN_NOT, PLAN_AND, PLAN_OR, PLAN_INPUT = 1, 2, 3, 4, 5, 6
+PLAN_LINK, PLAN_CONST, PLAN_NOT, PLAN_AND, PLAN_OR, PLAN_INPUT, PLAN_TEMPLATE, PLAN_TVM = 1, 2, 3, 4, 5, 6, 7, 8
 PLAN_WORDS = 51                   # u32 words per das_plan_node_t
 PLAN_SCAN = 5                     # word offset of its `scan` (das_link_scan_t)
 
@@ -535,8 +535,14 @@ class Context:
         return out[:n_nodes]
 
     def scan_words(self, words, node):
-        """das_scan_link of plan node `node`'s scan record."""
-        q = C.cast(words.ctypes.data + 4 * (PLAN_WORDS * node + PLAN_SCAN), C.POINTER(das_link_scan_t))
+        """The rows of plan leaf `node` on this GPU: das_scan_link of a LINK
+        record's scan, das_scan_template of a TEMPLATE record's."""
+        base = PLAN_WORDS * node
+        if int(words[base]) == PLAN_TEMPLATE:
+            w = words[base + PLAN_SCAN:base + PLAN_SCAN + 23]
+            return self.scan_template(int(w[1]), int(w[0]), [int(np.int32(v)) for v in w[10:10 + int(w[0])]],
+                                      bool(w[19]), bool(w[20]))
+        q = C.cast(words.ctypes.data + 4 * (base + PLAN_SCAN), C.POINTER(das_link_scan_t))
         return self._table(lib().das_scan_link, q)
 
     @staticmethod

@@ -692,9 +692,16 @@ int das_plan_estimates(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n,
   if (!ctx || (n && (!nodes || !rows))) return fail(ctx, DAS_ERR_INVALID, "null argument");
   return guarded(ctx, [&] {
     DAS_CHECK(ctx->c.idx.built, das::DAS_E_NOT_BUILT, "index not built");
-    for (uint32_t i = 0; i < n; ++i)
-      rows[i] = nodes[i].op == DAS_PLAN_LINK || nodes[i].op == DAS_PLAN_INPUT ? das::scan_estimate(ctx->c, nodes[i].scan)
-                                                                               : 0;
+    const das::Index& idx = ctx->c.idx;
+    for (uint32_t i = 0; i < n; ++i) {
+      const das_plan_node_t& x = nodes[i];
+      if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_INPUT)
+        rows[i] = das::scan_estimate(ctx->c, x.scan);
+      else if (x.op == DAS_PLAN_TEMPLATE && x.scan.type_id < idx.ctype_range.size())
+        rows[i] = idx.ctype_range[x.scan.type_id].end - idx.ctype_range[x.scan.type_id].begin;
+      else
+        rows[i] = 0;
+    }
   });
 }
 

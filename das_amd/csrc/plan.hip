@@ -68,9 +68,11 @@ struct Exec {
   uint32_t next(uint32_t i) const {
     DAS_CHECK(i < n, DAS_E_INVALID, "plan: truncated node array");
     const das_plan_node_t& x = nd[i];
-    if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_CONST || x.op == DAS_PLAN_INPUT) return i + 1;
+    if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_CONST || x.op == DAS_PLAN_INPUT || x.op == DAS_PLAN_TEMPLATE)
+      return i + 1;
     if (x.op == DAS_PLAN_NOT) return next(i + 1);
-    DAS_CHECK(x.op == DAS_PLAN_AND || x.op == DAS_PLAN_OR, DAS_E_INVALID, "plan: bad node op");
+    DAS_CHECK(x.op == DAS_PLAN_AND || x.op == DAS_PLAN_OR || x.op == DAS_PLAN_TVM, DAS_E_INVALID,
+              "plan: bad node op");
     uint32_t j = i + 1;
     for (uint32_t k = 0; k < x.nchild; ++k) j = next(j);
     return j;
@@ -149,8 +151,8 @@ struct Exec {
 
   Res eval(uint32_t i) {
     const das_plan_node_t& x = nd[i];
-    static const char* const kOp[] = {"?", "LINK", "CONST", "NOT", "AND", "OR", "INPUT"};
-    if (trace_on()) trace_mark("node", x.op <= 6 ? kOp[x.op] : "?");
+    static const char* const kOp[] = {"?", "LINK", "CONST", "NOT", "AND", "OR", "INPUT", "TEMPLATE", "TVM"};
+    if (trace_on()) trace_mark("node", x.op <= 8 ? kOp[x.op] : "?");
     Res r;
     switch (x.op) {
       case DAS_PLAN_CONST:
@@ -174,6 +176,39 @@ struct Exec {
         v->view = true;
         r.rel.push(std::move(v));
         r.matched = r.rel.nonempty();
+        return r;
+      }
+      case DAS_PLAN_TEMPLATE: {
+        // LinkTemplate.matched (:603-614): the links of one composite type,
+        // every target a typed variable (scan_template)
+        DAS_CHECK(!sharded(), DAS_E_UNSUPPORTED, "plan: LinkTemplate terms are not sharded");
+        das_template_scan_t q{};
+        q.ctype_id = x.scan.type_id;
+        q.arity = x.scan.arity;
+        for (int p = 0; p < 8; ++p) q.var[p] = x.scan.var[p];
+        q.ordered = x.scan.ordered;
+        q.no_overload = x.scan.no_overload;
+        TablePtr t = scan_template(c, q);
+        if (x.dedup && t->nrows) t = dedup(c, *t);
+        r.rel.push(std::move(t));
+        r.matched = r.rel.nonempty();
+        return r;
+      }
+      case DAS_PLAN_TVM: {
+        // Link._typed_variable_matched (:491-500): every target matched in
+        // order on the same answer (all() stops at the first failure); the
+        // answer is the last one a target wrote (a template, a nested Link)
+        uint32_t j = i + 1;
+        Rel last;
+        for (uint32_t k = 0; k < x.nchild; ++k) {
+          Res s = eval(j);
+          if (!s.matched) return Res{};
+          const int32_t o = nd[j].op;
+          if (o == DAS_PLAN_TEMPLATE || o == DAS_PLAN_TVM || o == DAS_PLAN_LINK) last = std::move(s.rel);
+          j = next(j);
+        }
+        r.rel = std::move(last);
+        r.matched = true;
         return r;
       }
       case DAS_PLAN_NOT:

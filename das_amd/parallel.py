@@ -306,42 +306,44 @@ class ShardedDB(RelationalDB):
         n = len(nodes) // W
         rec = nodes.reshape(n, W)
         op = rec[:, 0]
-        # shape: the root's children are leaves (LINK / CONST / NOT LINK)
+        leaves = [i for i in range(n) if op[i] in (L.PLAN_LINK, L.PLAN_TEMPLATE)]
+        # A tree whose leaves are all gathered evaluates identically on every
+        # shard (any shape).  Terms can stay split only under a root And (or
+        # Link) whose children are leaves: LINK / CONST / TEMPLATE / NOT LINK.
+        pos, neg = [], []
+        flat = op[0] == L.PLAN_LINK
         if op[0] == L.PLAN_LINK:
-            leaves, pos, neg = [0], [0], []
-        elif op[0] in (L.PLAN_AND, L.PLAN_OR):
-            leaves, pos, neg = [], [], []
-            i = 1
+            pos = [0]
+        elif op[0] == L.PLAN_AND:
+            i, flat = 1, True
             for _ in range(int(rec[0, 1])):
-                if op[i] == L.PLAN_NOT and i + 1 < n and op[i + 1] == L.PLAN_LINK and op[0] == L.PLAN_AND:
-                    leaves.append(i + 1)
+                if op[i] == L.PLAN_NOT and i + 1 < n and op[i + 1] in (L.PLAN_LINK, L.PLAN_TEMPLATE):
                     neg.append(i + 1)
                     i += 2
-                elif op[i] in (L.PLAN_LINK, L.PLAN_CONST):
-                    if op[i] == L.PLAN_LINK:
-                        leaves.append(i)
+                elif op[i] in (L.PLAN_LINK, L.PLAN_CONST, L.PLAN_TEMPLATE):
                     pos.append(i)
                     i += 1
                 else:
-                    return None
-            if i != n:
-                return None
-        else:
-            return None
-        if any(rec[i, 3] for i in leaves):              # dedup leaves: rows may repeat across shards
-            return None
+                    flat = False
+                    break
+            flat = flat and i == n
         ctx = db.ctx
-        single = op[0] == L.PLAN_LINK
+        single = op[0] == L.PLAN_LINK and not rec[0, 3]
         if single:
             local, gathered = [0], []
+        elif op[0] == L.PLAN_LINK:
+            return None                                  # one '*'-type / repeated-variable Link: host fold
+        elif not leaves:
+            local, gathered = [], []                     # settled on the host: the same on every shard
         else:
             est = self._allgather_i64(ctx.plan_estimates(nodes, n)[leaves])        # collective 1
             G = dict(zip(leaves, est.sum(axis=0).tolist()))
             M = dict(zip(leaves, est.max(axis=0).tolist()))
             local = []
-            if op[0] == L.PLAN_AND:
+            if flat:
                 small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
-                big = [i for i in leaves if i not in neg and G[i] > small]
+                # split candidates: Links whose rows are distinct across shards
+                big = [i for i in pos if op[i] == L.PLAN_LINK and not rec[i, 3] and G[i] > small]
                 if len(big) == 1:
                     local = big
                 elif len(big) > 1:
@@ -352,9 +354,11 @@ class ShardedDB(RelationalDB):
             gathered = [i for i in leaves if i not in local]
             if sum(G[i] for i in gathered) > self.GATHER_LIMIT:
                 return None
-        # gathered terms: this shard's rows, all-gathered into every shard (collective 2)
+        # gathered terms: this shard's rows, all-gathered into every shard (collective 2);
+        # a term whose rows may repeat ('*' type, repeated variable) is deduplicated after
         tables = [ctx.scan_words(nodes, i) for i in gathered]
         inputs = self._gather_many(tables, [M[i] for i in gathered]) if gathered else []
+        inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(gathered, inputs)]
         words = nodes.copy().reshape(n, W)
         for slot, i in enumerate(gathered):
             words[i, 0] = L.PLAN_INPUT

@@ -429,7 +429,22 @@ def _link_record(link, db, no_overload):
     return _node_record(_lib.PLAN_LINK, 0, 0, spec, ij)
 
 
-def _walk(expr, out, links):
+def _template_record(tmpl, db, no_overload):
+    """LinkTemplate.matched (pattern_matcher.py:603-614 over
+    get_matched_type_template, redis_mongo_db.py:269-275) as one TEMPLATE
+    record: the composite type's links, every target a typed variable."""
+    ct, named = db._template_ctype([tmpl.link_type, *[v.type for v in tmpl.targets]])
+    if named is not None:
+        raise _Unsupported()                  # a template without targets (match_template's assertion case)
+    if ct < 0:
+        return _header(_lib.PLAN_CONST, 0, 0)
+    var_ids = [_vid(v.name) for v in tmpl.targets]
+    words = [_lib.PLAN_TEMPLATE, 0, 0, 1 if len(set(var_ids)) != len(var_ids) else 0, 0] + [0] * 46
+    words[5:28] = _scan_words(len(var_ids), ct, [], var_ids, 0, True, no_overload)
+    return _RECORD.pack(*[w & 0xFFFFFFFF for w in words])
+
+
+def _walk(expr, out, links, root=True):
     """Prefix-order skeleton of `expr`: header records and Link slots."""
     k = expr._k
     if k == 'a' or k == 'o':
@@ -441,14 +456,31 @@ def _walk(expr, out, links):
             expr._planned = True
         out.append(_header(_lib.PLAN_AND if k == 'a' else _lib.PLAN_OR, len(expr.terms)))
         for t in expr.terms:
-            _walk(t, out, links)
+            _walk(t, out, links, False)
     elif k == 'x':
         out.append(_header(_lib.PLAN_NOT, 1))
-        _walk(expr.term, out, links)
+        _walk(expr.term, out, links, False)
     elif k == 'l':
+        if any(t._k == 't' for t in expr.targets):
+            # Link._typed_variable_matched (:491-500); at the root its answer
+            # after a failing target is observable: the host path keeps that
+            if root:
+                raise _Unsupported()
+            if any(t._k in ('v', 'tv') for t in expr.targets):
+                out.append(_header(_lib.PLAN_CONST, 0, 0))
+                return
+            out.append(_header(_lib.PLAN_TVM, len(expr.targets)))
+            for t in expr.targets:
+                _walk(t, out, links, False)
+            return
         if not expr.ordered:
             raise _Unsupported()
         links.append((len(out), expr, _link_signature(expr)))
+        out.append(None)
+    elif k == 't':
+        if not expr.ordered or root:
+            raise _Unsupported()
+        links.append((len(out), expr, ('t', expr.link_type, tuple((v.name, v.type) for v in expr.targets))))
         out.append(None)
     elif k == 'n' or k == 'v':
         links.append((len(out), expr, None))
@@ -479,7 +511,18 @@ def _lower(expr, db, no_overload):
                 continue
         todo.append((pos, e, sig))
     if todo:
-        nodes = [t for _, e, _ in todo for t in (e.targets if e._k == 'l' else [e]) if t._k == 'n']
+        try:
+            _resolve(todo, out, cache, db, no_overload)
+        except _Unsupported:
+            return None
+    return np.frombuffer(b"".join(out), dtype=np.uint32)
+
+
+def _resolve(todo, out, cache, db, no_overload):
+    """Records of the leaves _lower found no cached record for."""
+    if todo:
+        nodes = [t for _, e, _ in todo for t in (e.targets if e._k == 'l' else [e] if e._k == 'n' else [])
+                 if t._k == 'n']
         if nodes:
             db.prefetch_handles([n.get_handle(db) for n in nodes])
         for pos, e, sig in todo:
@@ -487,9 +530,10 @@ def _lower(expr, db, no_overload):
                 out[pos] = _header(_lib.PLAN_CONST, 0, 1 if e.matched(db, None) else 0)
             elif e._k == 'v':
                 out[pos] = _header(_lib.PLAN_CONST, 0, 1)
+            elif e._k == 't':
+                out[pos] = cache[(no_overload, sig)] = _template_record(e, db, no_overload)
             else:
                 out[pos] = cache[(no_overload, sig)] = _link_record(e, db, no_overload)
-    return np.frombuffer(b"".join(out), dtype=np.uint32)
 
 
 def _try_plan(expr, db, answer):

@@ -300,6 +300,15 @@ int das_table_free(das_table_t* t);
 #define DAS_PLAN_NOT 3
 #define DAS_PLAN_AND 4
 #define DAS_PLAN_OR 5
+/* TEMPLATE leaf: LinkTemplate.matched (:603-614), the scan_template of
+ * composite type `scan.type_id` (arity, var, ordered, no_overload as in
+ * das_template_scan_t); `dedup` when a variable repeats.
+ * TVM node: a Link with LinkTemplate targets (Link._typed_variable_matched
+ * :491-500), followed by its `nchild` targets (CONST node checks, TEMPLATE,
+ * LINK, nested TVM): matched iff every target matches, in order; its
+ * assignments are the last template / link target's. */
+#define DAS_PLAN_TEMPLATE 7
+#define DAS_PLAN_TVM 8
 typedef struct {
   int32_t op;
   uint32_t nchild;

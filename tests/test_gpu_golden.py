@@ -76,3 +76,30 @@ def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
         if not same(got, q):
             bad.append((q["query"], q.get("no_overload"), got.get("n", got), q.get("n", q.get("error"))))
     assert not bad, bad
+    if plan[0] == "1":
+        # scripts/benchmark.py QUERY_2 / QUERY_3 (ordered LinkTemplate terms,
+        # Links with template targets inside And / Or) take the native plan
+        from tests.util import build
+        tq = [q["query"] for q in d["queries"] if _has_ordered_templates_below_root(q["query"])]
+        assert tq or name != "bio_full"
+        for spec in tq:
+            e = build(spec)
+            e.matched(db, pm.PatternMatchingAnswer())
+            assert getattr(e, "_plan", (None, None))[1] is not None, spec
+
+
+def _has_ordered_templates_below_root(spec):
+    def templates(s):
+        if not isinstance(s, list) or not s:
+            return []
+        if s[0] == "Template":
+            return [s]
+        if s[0] == "Link":
+            return [t for x in s[3] for t in templates(x)]
+        if s[0] == "Not":
+            return templates(s[1])
+        if s[0] in ("And", "Or"):
+            return [t for x in s[1] for t in templates(x)]
+        return []
+    ts = templates(spec)
+    return spec[0] in ("And", "Or") and bool(ts) and all(t[2] for t in ts)
