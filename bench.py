@@ -98,20 +98,54 @@ def _L(t, *targets):
     return ["Link", t, True, list(targets)]
 
 
+def _TV(n, t):
+    return ["TVar", n, t]
+
+
+def _T(t, *targets):
+    return ["Template", t, True, list(targets)]
+
+
+def reference_benchmark_specs(ga, gb):
+    """scripts/benchmark.py:89-128 QUERY_1-3 on one gene pair (Q3, Q5, Q6)."""
+    g = lambda i: ["Node", "Gene", f"g{i}"]  # noqa: E731
+    member = lambda a, b: _L("Member", a, b)  # noqa: E731
+    same_bp = ["And", [member(g(ga), _V("V_BiologicalProcess")), member(g(gb), _V("V_BiologicalProcess"))]]
+    bpt = lambda n: _TV(n, "BiologicalProcess")  # noqa: E731
+    same_or_inherited = ["And", [
+        member(g(ga), _V("V1_BiologicalProcess")),
+        ["Or", [["And", [member(g(gb), _V("V2_BiologicalProcess")),
+                         _T("Inheritance", bpt("V2_BiologicalProcess"), bpt("V3_BiologicalProcess")),
+                         _T("Inheritance", bpt("V1_BiologicalProcess"), bpt("V3_BiologicalProcess"))]],
+                member(g(gb), _V("V1_BiologicalProcess"))]]]]
+    up, r = _TV("V_Uniprot", "Uniprot"), _TV("V_Reactome", "Reactome")
+    evaluation = lambda p, a, b: _L("Evaluation", ["Node", "Predicate", p], _T("List", a, b))  # noqa: E731
+    reactome = ["And", [
+        same_bp,
+        _T("Member", up, _TV("V_BiologicalProcess", "BiologicalProcess")),
+        evaluation("has_name", up, _TV("V_UniprotName", "Concept")),
+        _L("Context", _T("Member", up, r), evaluation("has_location", up, _TV("V_Location", "Concept"))),
+        evaluation("has_name", r, _TV("V_ReactomeName", "Concept"))]]
+    return same_bp, same_or_inherited, reactome
+
+
 def bio_specs(rank_genes, seed=17, anchor=0):
-    """Q1-Q4; `anchor` picks Q3's gene pair (each timed step uses its own,
-    so no step replays an anchored lookup of an earlier one)."""
+    """Q1-Q6; `anchor` picks the gene pair of the reference's own queries
+    (each timed step uses its own, so no step replays an anchored lookup of
+    an earlier one)."""
     import numpy as np
     rng = np.random.default_rng(seed + 7919 * anchor)
     ga, gb = (int(x) for x in rng.choice(rank_genes, 2, replace=False))
-    g = lambda i: ["Node", "Gene", f"g{i}"]  # noqa: E731
     bp = lambda i: ["Node", "BiologicalProcess", f"bp{i}"]  # noqa: E731
+    q1, q2, q3 = reference_benchmark_specs(ga, gb)
     return [
         ("Q1 Member(Vg,Vbp)", _L("Member", _V("V_g"), _V("V_bp"))),
         ("Q2 Member*Inheritance", ["And", [_L("Member", _V("V_g"), _V("V_bp")),
                                            _L("Inheritance", _V("V_bp"), _V("V_p"))]]),
-        ("Q3 same_biological_process", ["And", [_L("Member", g(ga), _V("V_bp")), _L("Member", g(gb), _V("V_bp"))]]),
+        ("Q3 same_biological_process (QUERY_1)", q1),
         ("Q4 hub join", ["And", [_L("Member", _V("V_g"), bp(0)), _L("Member", _V("V_g"), _V("V_bp"))]]),
+        ("Q5 same_or_inherited_biological_process (QUERY_2)", q2),
+        ("Q6 linked_reactome_uniprot (QUERY_3)", q3),
     ]
 
 
@@ -157,6 +191,10 @@ def build_expr(pm, spec):
         return pm.Node(spec[1], spec[2])
     if k == "Var":
         return pm.Variable(spec[1])
+    if k == "TVar":
+        return pm.TypedVariable(spec[1], spec[2])
+    if k == "Template":
+        return pm.LinkTemplate(spec[1], [build_expr(pm, t) for t in spec[3]], spec[2])
     if k == "Link":
         return pm.Link(spec[1], [build_expr(pm, t) for t in spec[3]], spec[2])
     if k == "Not":
@@ -171,11 +209,12 @@ def make_kb(args, rank, world, db):
     from das_amd import parallel, synthetic
     if args.workload == "bio":
         if world == 1:
-            arrays = synthetic.bio_kb(args.genes, args.bps, args.members, args.inheritance)
+            arrays = synthetic.bio_full_kb(args.genes, args.bps, args.members, args.inheritance)
             rank_genes = np.arange(args.genes)
         else:
             arrays, rank_genes = parallel.bio_shard(args.genes, args.bps, args.members, args.inheritance, rank, world)
-        cfg = {"workload": "config2 bio gene-level KB: single-Link + 2-clause And (Q1-Q4)",
+        cfg = {"workload": "config2 bio gene-level KB (+ annotation layouts): single-Link + 2-clause And (Q1-Q4) "
+                           "+ scripts/benchmark.py QUERY_1-3 (Q3, Q5, Q6)",
                "genes_per_rank": int(len(rank_genes)), "bps": args.bps, "member_links_per_rank": args.members,
                "inheritance_links": args.inheritance}
         return arrays, lambda i: bio_specs(rank_genes, anchor=i), cfg, "weak"
@@ -223,9 +262,11 @@ def _cpu_sample(workload, args_d):
         scale = 1000
         genes, bps = max(a.genes // scale, 50), max(a.bps // scale, 20)
         members, inh = max(a.members // scale, 500), max(a.inheritance // scale, 40)
-        arrays = synthetic.bio_kb(genes, bps, members, inh)
+        arrays = synthetic.bio_full_kb(genes, bps, members, inh, n_uniprot=max(5000 // scale, 20),
+                                       n_up_member=max(50_000 // scale, 100), n_reactome=max(1000 // scale, 10),
+                                       n_context=max(20_000 // scale, 40))
         specs = [s for k in range(8) for _, s in bio_specs(range(1, genes), anchor=k)]
-        what = f"bio_kb(genes={genes}, bps={bps}, members={members}, inheritance={inh}) = 1/{scale} of the GPU workload"
+        what = f"bio_full_kb(genes={genes}, bps={bps}, members={members}, inheritance={inh}) = 1/{scale} of the GPU workload"
     elif workload == "flybase":
         scale = 1000
         arrays = synthetic.flybase_kb(max(a.fb_genes // scale, 100), max(a.fb_schema // 10, 4),

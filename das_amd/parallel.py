@@ -829,32 +829,36 @@ def host_owners(arrays, world, exprs=None):
 
 
 def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
-    """Weak scaling: rank r owns the Member links of its own n_genes genes
-    (gene range r*n_genes..), the Inheritance links are shared and owned by
-    content hash.  Returns (AtomArrays for this rank, this rank's gene ids)."""
+    """Weak scaling of the gene-level KB (synthetic.bio_full_kb's layouts):
+    rank r owns the Member links of its own n_genes genes (gene range
+    r*n_genes.., placed by gene: partition_spec {"Member": 0}); Inheritance
+    and the annotation layouts (Uniprot / Reactome Member, List, Evaluation,
+    Context) are the same on every rank and indexed by their handle's owner.
+    Returns (AtomArrays for this rank, this rank's gene ids)."""
     from . import synthetic
-    blocks = []
     total_genes = n_genes * world
+    nodes, off = synthetic.bio_nodes(total_genes, n_bps)
+    blocks = []
     for r in range(world):
         rng = np.random.default_rng(seed + 1000 * (r + 1))
         genes = r * n_genes + rng.integers(0, n_genes, n_members)
         bps = synthetic.zipf_indices(rng, n_bps, n_members)
-        ch = np.stack([genes, total_genes + bps], 1)
-        blocks.append(("Member", ch, np.full(n_members, 1 if r == rank else 3, np.uint8)))
+        blocks.append(("Member", np.stack([off["g"] + genes, off["bp"] + bps], 1),
+                       np.full(n_members, 1 if r == rank or world == 1 else 3, np.uint8)))
     rng = np.random.default_rng(seed)
     child = rng.integers(1, n_bps, n_inh)
     parent = (rng.random(n_inh) * child).astype(np.int64)
-    ich = np.stack([total_genes + child, total_genes + parent], 1)
-    blocks.append(("Inheritance", ich, np.ones(n_inh, np.uint8)))
-    arrays, _ = synthetic.build_arrays(["Member", "Inheritance"],
-                                       [("Gene", "g", total_genes), ("BiologicalProcess", "bp", n_bps)], blocks)
+    BY_HANDLE = 4                        # placeholder kind: owner decided from the handle below
+    rest = [("Inheritance", np.stack([off["bp"] + child, off["bp"] + parent], 1))]
+    rest += synthetic.bio_annotation_blocks(rng, off, n_bps, base=len(blocks) + 1)
+    blocks += [(t, ch, np.full(len(ch), BY_HANDLE, np.uint8)) for t, ch in rest]
+    arrays = synthetic.build_nested(synthetic.BIO_TYPES, nodes, blocks)
+    kinds = arrays.expr_kind.copy()
+    idx = np.nonzero(kinds == BY_HANDLE)[0]
+    kinds[idx] = 1
     if world > 1:
-        # Inheritance links by their handle's owner (every rank computes the
-        # same split); Member links by their gene's rank (partition_spec)
-        inh = np.arange(arrays.n_expr - n_inh, arrays.n_expr)
-        kinds = arrays.expr_kind.copy()
-        kinds[inh[host_owners(arrays, world, inh) != rank]] = 3
-        arrays.expr_kind = kinds
+        kinds[idx[host_owners(arrays, world, idx) != rank]] = 3
+    arrays.expr_kind = kinds
     return arrays, np.arange(rank * n_genes, (rank + 1) * n_genes)
 
 

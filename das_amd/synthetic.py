@@ -147,7 +147,8 @@ def expr_ref(block, rows):
 def build_nested(type_names, node_blocks, link_blocks):
     """build_arrays for nested expressions: link block children are global
     node indices (>= 0) or expr_ref(b, row) references to rows of an earlier
-    block b; a node block (type, [names], n) names its nodes explicitly.
+    block b; a node block (type, [names], n) names its nodes explicitly; a
+    link block (type, children[, expr kinds]).
     Expressions are grouped by (nesting level, arity) as the
     AtomArrays layout requires, each block keeping its row order."""
     types = list(type_names)
@@ -169,8 +170,8 @@ def build_nested(type_names, node_blocks, link_blocks):
     n_leaf = n_types + n_nodes
     # nesting level and arity of every block
     level, chs = [], []
-    for t, ch in link_blocks:
-        ch = np.asarray(ch, dtype=np.int64)
+    for blk in link_blocks:
+        ch = np.asarray(blk[1], dtype=np.int64)
         refs = -(ch[ch < 0] + 1) >> np.int64(32)
         level.append(1 + max([level[int(b)] for b in np.unique(refs)], default=0))
         chs.append(ch)
@@ -180,8 +181,11 @@ def build_nested(type_names, node_blocks, link_blocks):
         start[b] = total
         total += chs[b].shape[0]
     childs, nchs, groups, prev = [], [], [0], None
+    kinds = []
     run = 0
     for b in key:
+        blk = link_blocks[b]
+        kinds.append(np.asarray(blk[2], np.uint8) if len(blk) > 2 else np.ones(chs[b].shape[0], np.uint8))
         ch = chs[b]
         neg = ch < 0
         r = -(ch[neg] + 1)
@@ -208,8 +212,55 @@ def build_nested(type_names, node_blocks, link_blocks):
                       np.concatenate([np.arange(n_types, dtype=np.uint32)] + node_ctype),
                       np.concatenate([np.arange(n_types, dtype=np.uint32), np.full(n_nodes, NONE, np.uint32)]),
                       np.concatenate([np.zeros(n_types, np.uint32)] + name_start),
-                      expr_off, np.concatenate(childs), np.ones(total, np.uint8), np.full(total, -1, np.int32),
+                      expr_off, np.concatenate(childs), np.concatenate(kinds), np.full(total, -1, np.int32),
                       np.array(groups, np.uint64), types)
+
+
+BIO_TYPES = ["Member", "Inheritance", "List", "Evaluation", "Context"]
+
+
+def bio_nodes(n_genes, n_bps, n_uniprot=5000, n_reactome=1000, n_loc=40):
+    """Node blocks of the gene-level KB and each block's first node index."""
+    nodes = [("Gene", "g", n_genes), ("BiologicalProcess", "bp", n_bps), ("Uniprot", "up", n_uniprot),
+             ("Reactome", "r", n_reactome), ("Concept", "upname", n_uniprot), ("Concept", "rname", n_reactome),
+             ("Concept", "loc", n_loc), ("Predicate", ["has_name"], 1), ("Predicate", ["has_location"], 1)]
+    off, o = {}, 0
+    for t, p, c in nodes:
+        off[p if isinstance(p, str) else p[0]] = o
+        o += c
+    return nodes, off
+
+
+def bio_annotation_blocks(rng, off, n_bps, n_uniprot=5000, n_up_member=50_000, n_reactome=1000, n_context=20_000,
+                          n_loc=40, base=0):
+    """The annotation-service layouts (data/annotation_service/*.metta) around
+    the gene-level core, as link blocks; `base` = index of the first of them
+    in the caller's block list (nested children reference blocks by index):
+      Member(Uniprot, BiologicalProcess)                      Zipf(1.1)
+      Evaluation(has_name, List(Uniprot, Concept name))       one per protein
+      Evaluation(has_name, List(Reactome, Concept name))      one per pathway
+      Context(Member(Uniprot, Reactome),
+              Evaluation(has_location, List(Uniprot, Concept location)))"""
+    up_m = rng.integers(0, n_uniprot, n_up_member)
+    up_bp = zipf_indices(rng, n_bps, n_up_member)
+    ctx_up = rng.integers(0, n_uniprot, n_context)
+    ctx_r = zipf_indices(rng, n_reactome, n_context)
+    ctx_loc = zipf_indices(rng, n_loc, n_context)
+    ups, rs = np.arange(n_uniprot), np.arange(n_reactome)
+    name_pred = lambda n: np.full(n, off["has_name"], np.int64)  # noqa: E731
+    B = lambda k: base + k  # noqa: E731
+    return [
+        ("Member", np.stack([off["up"] + up_m, off["bp"] + up_bp], 1)),                  # 0
+        ("List", np.stack([off["up"] + ups, off["upname"] + ups], 1)),                   # 1
+        ("List", np.stack([off["r"] + rs, off["rname"] + rs], 1)),                       # 2
+        ("Member", np.stack([off["up"] + ctx_up, off["r"] + ctx_r], 1)),                 # 3
+        ("List", np.stack([off["up"] + ctx_up, off["loc"] + ctx_loc], 1)),               # 4
+        ("Evaluation", np.stack([name_pred(n_uniprot), expr_ref(B(1), ups)], 1)),        # 5
+        ("Evaluation", np.stack([name_pred(n_reactome), expr_ref(B(2), rs)], 1)),        # 6
+        ("Evaluation", np.stack([np.full(n_context, off["has_location"], np.int64),
+                                 expr_ref(B(4), np.arange(n_context))], 1)),             # 7
+        ("Context", np.stack([expr_ref(B(3), np.arange(n_context)), expr_ref(B(7), np.arange(n_context))], 1)),
+    ]
 
 
 def bio_full_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, n_uniprot=5000,
@@ -219,48 +270,22 @@ def bio_full_kb(n_genes=20000, n_bps=10000, n_member=1_000_000, n_inh=None, n_un
     (data/annotation_service/*.metta):
       Member(Gene, BiologicalProcess)           Zipf(1.1) process popularity
       Inheritance(BP, BP)                       parents have lower index
-      Member(Uniprot, BiologicalProcess)        Zipf(1.1)
-      Evaluation(has_name, List(Uniprot, Concept name))     one per protein
-      Evaluation(has_name, List(Reactome, Concept name))    one per pathway
-      Context(Member(Uniprot, Reactome),
-              Evaluation(has_location, List(Uniprot, Concept location)))
+      + bio_annotation_blocks (Uniprot / Reactome Member, List, Evaluation, Context)
     Nodes: g<i>, bp<i>, up<i>, r<i>, upname<i>, rname<i>, loc<i>, and the
-    predicates has_name / has_location."""
+    predicates has_name / has_location.  The Member(Gene) and Inheritance
+    links are bio_kb's with the same arguments."""
     rng = np.random.default_rng(seed)
     n_inh = n_inh if n_inh is not None else 2 * n_bps
-    nodes = [("Gene", "g", n_genes), ("BiologicalProcess", "bp", n_bps), ("Uniprot", "up", n_uniprot),
-             ("Reactome", "r", n_reactome), ("Concept", "upname", n_uniprot), ("Concept", "rname", n_reactome),
-             ("Concept", "loc", n_loc), ("Predicate", ["has_name"], 1), ("Predicate", ["has_location"], 1)]
-    off, o = {}, 0
-    for t, p, c in nodes:
-        off[p if isinstance(p, str) else p[0]] = o
-        o += c
+    nodes, off = bio_nodes(n_genes, n_bps, n_uniprot, n_reactome, n_loc)
     genes = rng.integers(0, n_genes, n_member)
     bps = zipf_indices(rng, n_bps, n_member)
     child = rng.integers(1, n_bps, n_inh)
     parent = (rng.random(n_inh) * child).astype(np.int64)
-    up_m = rng.integers(0, n_uniprot, n_up_member)
-    up_bp = zipf_indices(rng, n_bps, n_up_member)
-    ctx_up = rng.integers(0, n_uniprot, n_context)
-    ctx_r = zipf_indices(rng, n_reactome, n_context)
-    ctx_loc = zipf_indices(rng, n_loc, n_context)
-    ups, rs = np.arange(n_uniprot), np.arange(n_reactome)
-    name_pred = lambda n: np.full(n, off["has_name"], np.int64)  # noqa: E731
     blocks = [
-        ("Member", np.stack([off["g"] + genes, off["bp"] + bps], 1)),                    # 0
-        ("Inheritance", np.stack([off["bp"] + child, off["bp"] + parent], 1)),           # 1
-        ("Member", np.stack([off["up"] + up_m, off["bp"] + up_bp], 1)),                  # 2
-        ("List", np.stack([off["up"] + ups, off["upname"] + ups], 1)),                   # 3
-        ("List", np.stack([off["r"] + rs, off["rname"] + rs], 1)),                       # 4
-        ("Member", np.stack([off["up"] + ctx_up, off["r"] + ctx_r], 1)),                 # 5
-        ("List", np.stack([off["up"] + ctx_up, off["loc"] + ctx_loc], 1)),               # 6
-        ("Evaluation", np.stack([name_pred(n_uniprot), expr_ref(3, ups)], 1)),           # 7
-        ("Evaluation", np.stack([name_pred(n_reactome), expr_ref(4, rs)], 1)),           # 8
-        ("Evaluation", np.stack([np.full(n_context, off["has_location"], np.int64),
-                                 expr_ref(6, np.arange(n_context))], 1)),                # 9
-        ("Context", np.stack([expr_ref(5, np.arange(n_context)), expr_ref(9, np.arange(n_context))], 1)),
-    ]
-    return build_nested(["Member", "Inheritance", "List", "Evaluation", "Context"], nodes, blocks)
+        ("Member", np.stack([off["g"] + genes, off["bp"] + bps], 1)),
+        ("Inheritance", np.stack([off["bp"] + child, off["bp"] + parent], 1)),
+    ] + bio_annotation_blocks(rng, off, n_bps, n_uniprot, n_up_member, n_reactome, n_context, n_loc, base=2)
+    return build_nested(BIO_TYPES, nodes, blocks)
 
 
 def flybase_kb(n_genes=200_000, n_schema=60, rows_per_schema=400_000, n_loc=5_000, n_do=2_000,
