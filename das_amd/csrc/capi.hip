@@ -790,6 +790,14 @@ void trace_dump(const char* title) {
 }
 KScope::~KScope() { delete static_cast<ProfScope*>(impl); }
 
+void prof_add_bytes(Ctx& c, const std::string& name, double bytes) {
+  for (auto it = c.pending.rbegin(); it != c.pending.rend(); ++it)
+    if (it->name == name) {
+      it->bytes += bytes;
+      return;
+    }
+}
+
 void prof_collect(Ctx& c) {
   if (c.pending.empty()) return;
   DAS_HIP(hipStreamSynchronize(c.s));

@@ -197,6 +197,9 @@ struct ProfScope {
   }
 };
 void prof_collect(Ctx& c);
+// Adds algorithmic bytes to the latest recorded launch of scope `name` (bytes
+// known only after the kernel: e.g. the outputs a filter kept).
+void prof_add_bytes(Ctx& c, const std::string& name, double bytes);
 // The context whose C-ABI call runs on this thread (KScope's target).
 Ctx*& active_ctx();
 

@@ -990,6 +990,159 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   }
 }
 
+// Single pass of the filtered expansion: each wave takes 1024-output chunks;
+// pass A over the chunk tests every output's build value against the key
+// bitmap (flag bytes in LDS, kept count), one atomic reserves the chunk's
+// kept outputs at the end of the output, pass B re-walks the chunk (its probe
+// rows, owner prefixes and build rows are L1/L2-resident now) and writes the
+// kept outputs in chunk order.  Chunks land in completion order, so the
+// output is not sorted; no flag array goes through HBM and the virtual
+// outputs are walked from HBM once (k_dj_filt<0> + k_dj_filt<1> walk them twice).
+template <int NPC = -1, int NBC = -1>
+__global__ void __launch_bounds__(B) k_dj_filt_fused(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                                     uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                                     const uint64_t* __restrict__ unit_off, uint64_t total,
+                                                     FiltKey fk, JoinCols jc, uint32_t* __restrict__ out,
+                                                     uint64_t cap, unsigned long long* __restrict__ kept) {
+  __shared__ uint8_t sflag[B / 64][kBalChunk];
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t lt = __lanemask_lt();
+  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
+  const uint32_t* pp[4];
+  const uint32_t* bp[4];
+  uint32_t* po[4];
+  uint32_t* bo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pp[i] = i < ncp ? jc.p[i] : nullptr;
+    bp[i] = i < ncb ? jc.b[i] : nullptr;
+    po[i] = i < ncp ? out + (uint64_t)jc.po[i] * cap : nullptr;
+    bo[i] = i < ncb ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+  }
+  uint8_t* fl = sflag[wv];
+  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + wv; w < chunks; w += waves) {
+    const uint64_t ob = w * kBalChunk;
+    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+    uint64_t ulo = 0, uhi = units;                     // last unit with unit_off[u] <= ob
+    while (uhi - ulo > 1) {
+      const uint64_t step = (uhi - ulo + 63) / 64;
+      const uint64_t idx = ulo + (uint64_t)lane * step;
+      const bool ok = idx < uhi && unit_off[idx] <= ob;
+      const uint64_t m = __ballot(ok);
+      const uint64_t nlo = ulo + (uint64_t)(63 - __clzll((long long)m)) * step;
+      uhi = nlo + step < uhi ? nlo + step : uhi;
+      ulo = nlo;
+    }
+    uint32_t run = 0;
+    uint64_t obase = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) {
+        // reserve the chunk's kept outputs (one atomic per 1024 outputs)
+        unsigned long long b0 = 0;
+        if (lane == 0 && run) b0 = atomicAdd(kept, (unsigned long long)run);
+        obase = (uint64_t)__shfl((long long)b0, 0, 64);
+        if (!run) break;
+        run = 0;
+      }
+      for (uint64_t u = ulo; u < units; ++u) {
+        uint64_t base = unit_off[u];
+        if (base >= oe) break;
+        const uint64_t r0 = u * kXRows;
+        uint2 e[kXGroups];
+#pragma unroll
+        for (int g = 0; g < kXGroups; ++g) {
+          const uint64_t r = r0 + g * 64 + lane;
+          const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+          e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int g = 0; g < kXGroups; ++g) {
+          const uint32_t c = e[g].y;
+          const uint32_t inc = wave_inclusive_scan(c);
+          const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+          const uint32_t pre = inc - c;
+          const uint64_t gb = base, ge = base + tot;
+          base = ge;
+          if (ge <= ob || gb >= oe) continue;
+          const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
+          const uint64_t r = r0 + g * 64 + lane;
+          uint32_t pv[4] = {0u, 0u, 0u, 0u};
+          if (pass == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
+          }
+          for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+            const int nr = (re - o0) >= 64u * kXUnroll ? kXUnroll : (int)((re - o0 + 63) / 64);
+            uint32_t o[kXUnroll], br[kXUnroll];
+            int ll[kXUnroll];
+#pragma unroll
+            for (int q = 0; q < kXUnroll; ++q) {
+              o[q] = o0 + (uint32_t)(q * 64 + lane);
+              ll[q] = 0;
+              br[q] = 0;
+              if (q >= nr) continue;
+              int l = 0;                               // owner: max lane with pre <= o
+#pragma unroll
+              for (int st = 32; st >= 1; st >>= 1) {
+                const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
+                if (l + st < 64 && pl <= o[q]) l += st;
+              }
+              ll[q] = l;
+              br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+            }
+            if (pass == 0) {
+              uint32_t v[kXUnroll];
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+              uint32_t wd[kXUnroll];
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q) {
+                if (q >= nr) continue;
+                const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
+                if (o[q] < re) fl[gb + o[q] - ob] = f ? 1 : 0;
+                run += (uint32_t)__popcll(__ballot(f));
+              }
+            } else {
+              bool f[kXUnroll];
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q] - ob] != 0;
+              uint32_t bv[kXUnroll][4];
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
+#pragma unroll
+              for (int q = 0; q < kXUnroll; ++q) {
+                if (q >= nr) continue;
+                const uint64_t m = __ballot(f[q]);
+                const uint64_t pos = obase + run + __popcll(m & lt);
+                run += (uint32_t)__popcll(m);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  if (i >= ncp) break;
+                  const uint32_t x = lane_get(pv[i], ll[q]);
+                  if (f[q]) po[i][pos] = x;
+                }
+                if (f[q]) {
+#pragma unroll
+                  for (int i = 0; i < 4; ++i)
+                    if (i < ncb) bo[i][pos] = bv[q][i];
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 ColSet cols_of(const Table& t) {
@@ -3153,6 +3306,45 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
   const unsigned fgrid = grid_for(chunks, B / 64, 65535u * 4u);
   const FiltKey fk{jc.b[fb], (uint32_t)lo, (uint32_t)(hi - lo + 1), (const uint32_t*)bits.p};
+  // one pass, unsorted output (DAS_FILT_FUSED=0: the two ordered passes),
+  // while the worst case (every virtual output kept) fits the output buffer
+  const char* ff = std::getenv("DAS_FILT_FUSED");
+  if (!(ff && ff[0] == '0') && (uint64_t)nu * total * 4 <= (16ull << 30)) {
+    auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
+    DBuf<unsigned long long> kept(1, c.s);
+    fill_dev(kept.p, 0, 8, c.s);
+    const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
+    {
+      // per probe row its row id, (first, count) and probe columns; per
+      // output its build value and (kept) its build columns; kept outputs out
+      ProfScope ps(c, spec ? "k_dj_filt_fused<" + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ">"
+                           : std::string("k_dj_filt_fused<-1,-1>"),
+                   (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
+#define FILT_F(NPV, NBV)                                                                                          \
+  hipLaunchKernelGGL((k_dj_filt_fused<NPV, NBV>), dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
+                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, jc, out->data,  \
+                     out->cap, kept.p)
+      if (jc.np == 1 && jc.nb == 1) FILT_F(1, 1);
+      else if (jc.np == 2 && jc.nb == 1) FILT_F(2, 1);
+      else if (jc.np == 1 && jc.nb == 2) FILT_F(1, 2);
+      else FILT_F(-1, -1);
+#undef FILT_F
+      DAS_HIP(hipGetLastError());
+    }
+    out->nrows = read_u64(reinterpret_cast<const uint64_t*>(kept.p), c.s);
+    // the kept outputs' columns written (bytes known only now: charged to the scope's launch below)
+    prof_add_bytes(c, spec ? "k_dj_filt_fused<" + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ">"
+                           : std::string("k_dj_filt_fused<-1,-1>"),
+                   (4.0 * nu) * out->nrows);
+    out->sorted_col = -1;                          // chunks land in completion order
+    for (int k = 0; k < nu; ++k) {
+      out->lo[k] = pl.lo[k];
+      out->hi[k] = pl.hi[k];
+    }
+    out->lo[fo] = (uint32_t)lo;
+    out->hi[fo] = (uint32_t)hi;
+    return out;
+  }
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(chunks, c.s), coff(chunks + 1, c.s);
   {
