@@ -756,6 +756,17 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     warm_stats = db.ctx.prof_stats()
     dominant = roofline_of(warm_stats, workload) if args.events == "dominant" else None
     per_query = {name: run(q) for name, q in qsets[args.warmup]}
+    # per-query wall time (the warm query set of the first timed step, 5 runs each)
+    per_query_ms = {}
+    for name, q in qsets[args.warmup]:
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_q = time.perf_counter()
+        for _ in range(5):
+            run(q)
+        torch.cuda.synchronize()
+        per_query_ms[name] = round((time.perf_counter() - t_q) * 1e3 / 5, 4)
     db.ctx.prof_reset()
     db.ctx.prof_only(dominant["kernel"] if dominant else None)
     db.ctx.prof_enable(True)
@@ -803,6 +814,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                            "network fetch)",
                 "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
         cfg = dict(cfg, bindings_per_step_rank0=per_query, parallelism=f"links sharded x{world}")
+        cfg["query_ms_rank0"] = per_query_ms
         out = {
             "metric": "pattern matches/sec (bindings/s) + % HBM roofline",
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

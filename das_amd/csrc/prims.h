@@ -576,11 +576,214 @@ __global__ void __launch_bounds__(kSortBlock) k_radix_scatter_lds(const K* kin, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Onesweep passes (large sorts): the digit histograms of EVERY pass come from
+// one read of the keys up front (k_radix_ghist); each pass is then a single
+// kernel -- a block takes the next tile in launch order (atomic ticket),
+// counts its digits in LDS, publishes the counts, and derives its tile offset
+// per digit by looking back over the earlier tiles' published counts
+// (decoupled look-back: a tile's inclusive prefix once known, else its own
+// count and the look-back continues).  No per-pass histogram kernel, no
+// tiles x 256 scan.  Earlier tiles were ticketed by blocks already running,
+// so every wait ends; a wait longer than kLookbackSpin rounds sets an error
+// flag instead of spinning on (the caller raises).
+// ---------------------------------------------------------------------------
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbMask = (1ull << 62) - 1;
+constexpr uint32_t kLookbackSpin = 1u << 24;
+
+template <typename K>
+__global__ void __launch_bounds__(kSortBlock) k_radix_ghist(const K* keys, uint64_t n, int shift0, int npass,
+                                                           uint32_t* ghist) {
+  __shared__ uint32_t h[8][256];
+  for (int p = 0; p < npass; ++p) h[p][threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kSortBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kSortBlock) {
+    const K k = keys[i];
+    for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(k >> (shift0 + 8 * p)) & 255u], 1u);
+  }
+  __syncthreads();
+  for (int p = 0; p < npass; ++p)
+    if (h[p][threadIdx.x]) atomicAdd(&ghist[p * 256 + threadIdx.x], h[p][threadIdx.x]);
+}
+
+template <typename K, bool kHasVals>
+__global__ void __launch_bounds__(kSortBlock) k_radix_onesweep(const K* kin, const uint32_t* vin, K* kout,
+                                                              uint32_t* vout, uint64_t n, int shift,
+                                                              const uint32_t* ghist, uint64_t* status,
+                                                              uint32_t* ticket, uint32_t* err) {
+  __shared__ K s_key[kSortTile];
+  __shared__ uint32_t s_gbase[256], s_loff[256], s_run[256], s_hist[256];
+  __shared__ uint32_t s_cnt[kSortBlock / 64][256];
+  __shared__ uint32_t s_wsum[kSortBlock / 64];
+  __shared__ uint32_t s_tile;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  s_hist[tid] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t base = (uint64_t)tile * kSortTile;
+  K kr[kSortItems];
+  uint32_t vr[kHasVals ? kSortItems : 1];
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
+    kr[r] = i < n ? kin[i] : (K)0;
+    if (kHasVals) vr[r] = i < n ? vin[i] : 0u;
+    if (i < n) atomicAdd(&s_hist[(uint32_t)(kr[r] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  {
+    // publish this tile's count of digit `tid`, then look back for the
+    // earlier tiles' total (thread = digit)
+    const uint32_t c = s_hist[tid];
+    uint64_t* st = status + (uint64_t)tile * 256 + tid;
+    __hip_atomic_store(st, (tile == 0 ? kLbInc : kLbAgg) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t pre = 0;
+    for (int64_t j = (int64_t)tile - 1; j >= 0;) {
+      const uint64_t v = __hip_atomic_load(status + (uint64_t)j * 256 + tid, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (v & kLbInc) { pre += v & kLbMask; break; }
+      if (v & kLbAgg) { pre += v & kLbMask; --j; continue; }
+      uint32_t spins = 0;                              // tile j not published yet
+      while (!(__hip_atomic_load(status + (uint64_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+               (kLbInc | kLbAgg))) {
+        if (++spins > kLookbackSpin) { atomicOr(err, 1u); j = -1; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    if (tile) __hip_atomic_store(st, kLbInc | (pre + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // global base of digit `tid` = all smaller digits + earlier tiles' count of it
+    uint32_t g = ghist[tid];
+    const uint32_t ginc = wave_incl_sum_u32(g);
+    if (__lane_id() == 63) s_wsum[wave] = ginc;
+    const uint32_t linc = wave_incl_sum_u32(c);
+    __syncthreads();
+    uint32_t gpre = ginc - g, lpre = linc - c;
+    for (int w = 0; w < wave; ++w) gpre += s_wsum[w];
+    __syncthreads();
+    if (__lane_id() == 63) s_wsum[wave] = linc;
+    __syncthreads();
+    for (int w = 0; w < wave; ++w) lpre += s_wsum[w];
+    s_gbase[tid] = gpre + (uint32_t)pre;
+    s_loff[tid] = lpre;
+    s_run[tid] = 0;
+#pragma unroll
+    for (int w = 0; w < kSortBlock / 64; ++w) s_cnt[w][tid] = 0;
+    __syncthreads();
+  }
+  const uint64_t lt = __lanemask_lt();
+  uint32_t lpos[kHasVals ? kSortItems : 1];
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortBlock + tid;
+    const bool valid = i < n;
+    const uint32_t d = (uint32_t)(kr[r] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = __popcll(peers & lt);
+    if (valid && rank == 0) s_cnt[wave][d] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = s_loff[d] + s_run[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += s_cnt[w][d];
+      s_key[pos] = kr[r];
+      if (kHasVals) lpos[r] = pos;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < kSortBlock / 64; ++w) {
+      add += s_cnt[w][tid];
+      s_cnt[w][tid] = 0;
+    }
+    s_run[tid] += add;
+    __syncthreads();
+  }
+  const uint32_t valid_n = (uint32_t)(n - base < (uint64_t)kSortTile ? n - base : (uint64_t)kSortTile);
+  uint32_t gpos[kHasVals ? kSortItems : 1];
+#pragma unroll
+  for (int k = 0; k < kSortItems; ++k) {
+    const uint32_t j = (uint32_t)tid + (uint32_t)k * kSortBlock;
+    if (j < valid_n) {
+      const K key = s_key[j];
+      const uint32_t d = (uint32_t)(key >> shift) & 255u;
+      const uint32_t g = s_gbase[d] + (j - s_loff[d]);
+      kout[g] = key;
+      if (kHasVals) gpos[k] = g;
+    }
+  }
+  if (kHasVals) {
+    uint32_t* s_val = reinterpret_cast<uint32_t*>(s_key);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r)
+      if (base + (uint64_t)r * kSortBlock + tid < n) s_val[lpos[r]] = vr[r];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)k * kSortBlock;
+      if (j < valid_n) vout[gpos[k]] = s_val[j];
+    }
+  }
+}
+
+uint32_t read_u32(const uint32_t* d, hipStream_t s);
+inline void fill_dev(void* dst, int byte, uint64_t bytes, hipStream_t s);
+
 // Sorts keys[0..n) (and vals alongside, if given) by bits [begin_bit, end_bit).
 // Result lands back in keys/vals.
 template <typename K>
 void radix_sort_pairs(K* keys, uint32_t* vals, uint64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || end_bit <= begin_bit) return;
+  const char* os_env = std::getenv("DAS_ONESWEEP");            // tests: 0 = per-pass histograms
+  const bool onesweep = !(os_env && os_env[0] == '0');
+  if (onesweep && n >= (1ull << 20)) {
+    DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "radix sort: more than 2^32 keys");
+    const uint32_t tiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    const int npass = (end_bit - begin_bit + 7) / 8;
+    DBuf<K> k2(n, s);
+    DBuf<uint32_t> v2(vals ? n : 0, s);
+    DBuf<uint32_t> ghist(256 * (uint64_t)npass, s), ctl(2 * (uint64_t)npass + 1, s);
+    DBuf<uint64_t> status((uint64_t)tiles * 256, s);
+    fill_dev(ghist.p, 0, 4 * 256 * (uint64_t)npass, s);
+    fill_dev(ctl.p, 0, 4 * (2 * (uint64_t)npass + 1), s);
+    const std::string tag = key_tag<K>();
+    {
+      KScope ks(("k_radix_ghist<" + tag + ">").c_str(), (double)n * sizeof(K));
+      hipLaunchKernelGGL((k_radix_ghist<K>), dim3(grid_for(n, kSortBlock, 2048)), dim3(kSortBlock), 0, s,
+                         (const K*)keys, n, begin_bit, npass, ghist.p);
+      DAS_HIP(hipGetLastError());
+    }
+    const double kv = (double)n * (sizeof(K) + (vals ? 4.0 : 0.0));
+    K* ka = keys; K* kb = k2.p;
+    uint32_t* va = vals; uint32_t* vb = v2.p;
+    for (int p = 0; p < npass; ++p) {
+      fill_dev(status.p, 0, 8 * (uint64_t)tiles * 256, s);
+      KScope ks(("k_radix_onesweep<" + tag + (vals ? ",true>" : ",false>")).c_str(), 2.0 * kv);
+      if (vals)
+        hipLaunchKernelGGL((k_radix_onesweep<K, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                           (const uint32_t*)va, kb, vb, n, begin_bit + 8 * p, (const uint32_t*)ghist.p + 256 * p,
+                           status.p, ctl.p + p, ctl.p + 2 * npass);
+      else
+        hipLaunchKernelGGL((k_radix_onesweep<K, false>), dim3(tiles), dim3(kSortBlock), 0, s, (const K*)ka,
+                           (const uint32_t*)nullptr, kb, (uint32_t*)nullptr, n, begin_bit + 8 * p,
+                           (const uint32_t*)ghist.p + 256 * p, status.p, ctl.p + p, ctl.p + 2 * npass);
+      DAS_HIP(hipGetLastError());
+      std::swap(ka, kb);
+      std::swap(va, vb);
+    }
+    if (npass & 1) {
+      copy_dev(keys, ka, sizeof(K) * n, s);
+      if (vals) copy_dev(vals, va, sizeof(uint32_t) * n, s);
+    }
+    DAS_CHECK(read_u32(ctl.p + 2 * npass, s) == 0, DAS_E_INTERNAL, "radix sort: look-back wait exceeded its bound");
+    return;
+  }
   DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "radix sort: more than 2^32 keys");
   const uint32_t tiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
   DBuf<K> k2(n, s);
