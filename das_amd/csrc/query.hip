@@ -631,8 +631,12 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, con
   }
 }
 
+// warm0 / warm1 (nullable): probe payload columns the expansion reads next;
+// touched here so they arrive from the MALL, not cold HBM, when the probe is
+// a view of index rows (no projection copy left them warm)
 __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
-                                                const uint2* lc, uint64_t units, uint64_t* unit_tot) {
+                                                const uint2* lc, uint64_t units, uint64_t* unit_tot,
+                                                const uint32_t* warm0, const uint32_t* warm1) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   for (uint64_t u = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); u < units; u += waves) {
@@ -642,6 +646,14 @@ __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t n
     for (int g = 0; g < kXGroups; ++g) {
       const uint64_t r = r0 + g * 64 + lane;
       d[g] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;       // wraps for keys below kmin
+      if (warm0 && r < np) {
+        const uint32_t w0 = warm0[r];
+        asm volatile("" ::"v"(w0));
+      }
+      if (warm1 && r < np) {
+        const uint32_t w1 = warm1[r];
+        asm volatile("" ::"v"(w1));
+      }
     }
     uint64_t acc = 0;
 #pragma unroll
@@ -1784,9 +1796,16 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
   const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
   DBuf<uint64_t> tot(units, c.s), toff(units + 1, c.s);
   {
+    // a view's payload columns are read cold by the expansion: warm them here
+    const uint32_t* w[2] = {nullptr, nullptr};
+    int nw = 0;
+    const char* wf = std::getenv("DAS_DJ_WARM");           // A/B: 0 = no warming
+    if (P.view && !(wf && wf[0] == '0'))
+      for (int i = 0; i < jc.np && nw < 2; ++i)
+        if (jc.p[i] != pkey) w[nw++] = jc.p[i];
     ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
     hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
-                       lc, units, tot.p);
+                       lc, units, tot.p, w[0], w[1]);
     DAS_HIP(hipGetLastError());
   }
   uint64_t tm[2];
@@ -3297,7 +3316,8 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   {
     ProfScope ps(c, "k_dj_count", 4.0 * A.nrows);
     hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
-                       (uint32_t)A.nrows, (const uint2*)lc.p, units, tot.p);
+                       (uint32_t)A.nrows, (const uint2*)lc.p, units, tot.p, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr);
     DAS_HIP(hipGetLastError());
   }
   const uint64_t total = scan_total<uint64_t>(SpanIn<uint64_t>{tot.p}, units, toff.p, c.s);

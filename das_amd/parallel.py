@@ -344,12 +344,13 @@ class ShardedDB(RelationalDB):
                 small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
                 # split candidates: Links whose rows are distinct across shards
                 big = [i for i in pos if op[i] == L.PLAN_LINK and not rec[i, 3] and G[i] > small]
-                if len(big) == 1:
-                    local = big
-                elif len(big) > 1:
+                if len(big) > 1:
+                    # several large terms: all stay split when partition_spec
+                    # places them by one variable (co-located joins), else the
+                    # largest does and the others are gathered
                     pv = {self._placement_var(db, rec[i]) for i in big}
-                    if len(pv) != 1 or None in pv:
-                        return None
+                    local = big if len(pv) == 1 and None not in pv else [max(big, key=lambda i: G[i])]
+                else:
                     local = big
             gathered = [i for i in leaves if i not in local]
             if sum(G[i] for i in gathered) > self.GATHER_LIMIT:
