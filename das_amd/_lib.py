@@ -129,6 +129,7 @@ _SIGS = {
     "das_table_free": (C.c_int, [P]),
     "das_partition": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P), P]),
     "das_table_gather": (C.c_int, [P, P, P, C.c_uint64, C.POINTER(P)]),
+    "das_table_gather_ranges": (C.c_int, [P, P, P, P, C.c_uint32, C.POINTER(P)]),
     "das_table_export_rows": (C.c_int, [P, P, P]),
     "das_table_import_rows": (C.c_int, [P, C.c_int32, C.c_int32, P, P, P, C.c_uint64, C.POINTER(P)]),
     "das_parse_canonical": (C.c_int, [P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
@@ -653,6 +654,12 @@ class Context:
         """Rows idx (host indices) of table t as a new table."""
         idx = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
         return self._table(lib().das_table_gather, t.h, ptr(idx), idx.shape[0])
+
+    def gather_ranges(self, t, begin, end):
+        """Rows [begin[i], end[i]) of table t, in range order, as a new table."""
+        b = np.ascontiguousarray(np.asarray(begin, dtype=np.uint64))
+        e = np.ascontiguousarray(np.asarray(end, dtype=np.uint64))
+        return self._table(lib().das_table_gather_ranges, t.h, ptr(b), ptr(e), b.shape[0])
 
     def export_rows(self, t, dptr):
         check(lib().das_table_export_rows(self.h, t.h, dptr), self.h)

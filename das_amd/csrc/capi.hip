@@ -596,6 +596,12 @@ int das_table_gather(das_ctx_t* ctx, const das_table_t* t, const uint32_t* idx, 
   });
 }
 
+int das_table_gather_ranges(das_ctx_t* ctx, const das_table_t* t, const uint64_t* begin, const uint64_t* end,
+                            uint32_t n_ranges, das_table_t** out) {
+  if (!ctx || !t || !out || (n_ranges && (!begin || !end))) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] { *out = wrap(das::gather_ranges(ctx->c, t->t, begin, end, n_ranges)); });
+}
+
 int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst) {
   return guarded(ctx, [&] { das::export_rows(ctx->c, t->t, d_dst); });
 }

@@ -243,6 +243,9 @@ ColSet cols_of(const Table& t);
 void sort_perm(const ColSet& cs, uint64_t n, uint32_t* perm, int bits, hipStream_t s);
 int id_bits(const Ctx& c);
 std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx, uint64_t m);
+// rows [begin[i], end[i]) of `a` for every range i, in range order (host arrays)
+std::unique_ptr<Table> gather_ranges(Ctx& c, const Table& a, const uint64_t* begin, const uint64_t* end,
+                                     uint32_t n_ranges);
 std::unique_ptr<Table> compact_table(Ctx& c, const Table& a, const uint32_t* keep);
 // lo/cnt per probe row: the equal range of its key in the sorted build keys
 void join_ranges(Ctx& c, const ColSet& probe, uint64_t np, const ColSet& build_sorted, uint64_t nb, uint32_t* lo,

@@ -1178,6 +1178,49 @@ void sort_perm(const ColSet& cs, uint64_t n, uint32_t* perm, int bits, hipStream
 int id_bits(const Ctx& c) { return bits_for(c.idx.n_atoms ? c.idx.n_atoms - 1 : 0); }
 
 // Gathers rows idx[0..m) of table `a` into a new table (same schema).
+namespace {
+// output row o -> the source row of the range holding it (prefix = exclusive
+// range-length sums, n_ranges + 1 entries)
+__global__ void k_gather_ranges(ColSet src, const uint64_t* prefix, const uint64_t* begin, uint32_t n_ranges,
+                                uint64_t m, uint32_t* dst, uint64_t cap) {
+  for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < m; o += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = n_ranges;                  // last range with prefix[r] <= o
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (prefix[mid] <= o) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t r = begin[lo] + (o - prefix[lo]);
+    for (int k = 0; k < src.n; ++k) dst[(uint64_t)k * cap + o] = src.c[k][r];
+  }
+}
+}  // namespace
+
+std::unique_ptr<Table> gather_ranges(Ctx& c, const Table& a, const uint64_t* begin, const uint64_t* end,
+                                     uint32_t n_ranges) {
+  std::vector<uint64_t> h(2 * (uint64_t)n_ranges + 1, 0);
+  uint64_t m = 0;
+  for (uint32_t i = 0; i < n_ranges; ++i) {
+    DAS_CHECK(begin[i] <= end[i] && end[i] <= a.nrows, DAS_E_INVALID, "gather range outside the table");
+    h[i] = m;                                        // prefix
+    h[n_ranges + 1 + i] = begin[i];
+    m += end[i] - begin[i];
+  }
+  h[n_ranges] = m;
+  auto t = new_table_like(c, a, m);
+  t->nrows = m;
+  if (m && a.ncols) {
+    DBuf<uint64_t> d(h.size(), c.s);
+    uint8_t* st = pinned_stage(8 * h.size());
+    std::memcpy(st, h.data(), 8 * h.size());
+    DAS_HIP(hipMemcpyAsync(d.p, st, 8 * h.size(), hipMemcpyHostToDevice, c.s));
+    hipLaunchKernelGGL(k_gather_ranges, G(m), dim3(B), 0, c.s, cols_of(a), (const uint64_t*)d.p,
+                       (const uint64_t*)d.p + n_ranges + 1, n_ranges, m, t->data, t->cap);
+    DAS_HIP(hipGetLastError());
+  }
+  return t;
+}
+
 std::unique_ptr<Table> gather_table(Ctx& c, const Table& a, const uint32_t* idx, uint64_t m) {
   auto t = new_table_like(c, a, m);
   t->nrows = m;

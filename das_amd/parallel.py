@@ -604,20 +604,21 @@ class ShardedDB(RelationalDB):
         offa = np.concatenate([[0], np.cumsum(ca.astype(np.int64))])
         offb = np.concatenate([[0], np.cumsum(cb.astype(np.int64))])
 
-        def rows(off, mask):
-            idx = [np.arange(off[k], off[k + 1]) for k in np.nonzero(mask)[0]]
-            return np.concatenate(idx).astype(np.uint32) if idx else np.zeros(0, np.uint32)
+        def rows(t, off, mask):
+            # the rows of the selected buckets (runs of the partitioned
+            # table), gathered on the device from their row ranges
+            ks = np.nonzero(mask)[0]
+            keep = off[ks + 1] > off[ks]
+            return self.local.gather_ranges(t, off[ks][keep], off[ks + 1][keep])
         light = ~heavy
-        a_light, b_light = self.local.gather_rows(pa, rows(offa, light)), self.local.gather_rows(pb, rows(offb, light))
+        a_light, b_light = rows(pa, offa, light), rows(pb, offb, light)
         out = [self.local.join(self._exchange(a_light, shared), self._exchange(b_light, shared), no_overload),
-               self.local.join(self.local.gather_rows(pa, rows(offa, a_stays)),
-                               self._gather_all(self.local.gather_rows(pb, rows(offb, a_stays))), no_overload),
-               self.local.join(self._gather_all(self.local.gather_rows(pa, rows(offa, b_stays))),
-                               self.local.gather_rows(pb, rows(offb, b_stays)), no_overload)]
+               self.local.join(rows(pa, offa, a_stays), self._gather_all(rows(pb, offb, a_stays)), no_overload),
+               self.local.join(self._gather_all(rows(pa, offa, b_stays)), rows(pb, offb, b_stays), no_overload)]
         out = [t for t in out if t.nrows]
         if not out:
-            return self.local.join(self.local.gather_rows(pa, np.zeros(0, np.uint32)),
-                                   self.local.gather_rows(pb, np.zeros(0, np.uint32)), no_overload)
+            none = np.zeros(nb, dtype=bool)
+            return self.local.join(rows(pa, offa, none), rows(pb, offb, none), no_overload)
         return _with_part(out[0] if len(out) == 1 else self.local.concat(out), None)
 
     def rel_antijoin(self, rel, forbidden):
@@ -721,10 +722,13 @@ class HipLocal:
         return self.db.ctx.set_minus(a, b)
 
     def slice(self, t, lo, hi):
-        return self.db.ctx.gather(t, np.arange(lo, hi, dtype=np.uint32))
+        return self.db.ctx.gather_ranges(t, [lo], [hi])
 
     def gather_rows(self, t, idx):
         return self.db.ctx.gather(t, idx)
+
+    def gather_ranges(self, t, begin, end):
+        return self.db.ctx.gather_ranges(t, begin, end)
 
     def xfer_tensor(self, arr):
         return self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.dev)

@@ -351,6 +351,11 @@ int das_partition(das_ctx_t* ctx, const das_table_t* t, const int32_t* key_vars,
 /* Rows idx[0..n) of `t` (host indices) as a new table, same schema: the
  * heavy / light split of a skewed join's buckets. */
 int das_table_gather(das_ctx_t* ctx, const das_table_t* t, const uint32_t* idx, uint64_t n, das_table_t** out);
+/* Rows [begin[i], end[i]) of `t` for every range i, in range order (host range
+ * arrays; the rows never pass through the host): the heavy / light buckets of
+ * a partitioned table (das_partition groups rows by bucket). */
+int das_table_gather_ranges(das_ctx_t* ctx, const das_table_t* t, const uint64_t* begin, const uint64_t* end,
+                            uint32_t n_ranges, das_table_t** out);
 /* Row-major (n x ncols u32) device copies for the collective buffers. */
 int das_table_export_rows(das_ctx_t* ctx, const das_table_t* t, uint32_t* d_dst);
 int das_table_import_rows(das_ctx_t* ctx, int32_t kind, int32_t ncols, const int32_t* vars,

@@ -248,6 +248,10 @@ class NumpyLocal:
     def gather_rows(self, t, idx):
         return NTable(t.kind, t.vars, t.rows[np.asarray(idx, dtype=np.int64)], t.members)
 
+    def gather_ranges(self, t, begin, end):
+        idx = [np.arange(int(b), int(e)) for b, e in zip(begin, end)]
+        return self.gather_rows(t, np.concatenate(idx) if idx else np.zeros(0, np.int64))
+
     def join(self, a, b, no_overload=False):
         if a.kind != ORDERED or b.kind != ORDERED:
             vars_, members = _join_schema(a, b)
