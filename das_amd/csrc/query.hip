@@ -363,10 +363,34 @@ __global__ void k_join_expand(const uint64_t* offs, uint64_t np, const uint32_t*
   }
 }
 
-__global__ void k_cartesian(OutMap om, uint64_t nb, uint64_t total, uint32_t* out, uint64_t cap) {
-  for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < total; o += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t i = o / nb, j = o - i * nb;
-    for (int c = 0; c < om.n; ++c) out[(uint64_t)c * cap + o] = om.side[c] ? om.col[c][j] : om.col[c][i];
+// Output o = (probe row o / nb, build row o % nb).  One division per thread:
+// the grid stride S advances (i, j) by (S / nb, S % nb) with a carry, so the
+// kernel is a pure column-store stream (NC: output columns, specialised up to 6).
+template <int NC>
+__global__ void __launch_bounds__(B) k_cartesian(OutMap om, uint64_t nb, uint64_t total, uint64_t sq, uint64_t sr,
+                                                 uint32_t* out, uint64_t cap) {
+  const int nc = NC > 0 ? NC : om.n;
+  uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  uint64_t i = o / nb, j = o - i * nb;
+  const uint32_t* col[kMaxCols];
+  bool side[kMaxCols];
+#pragma unroll
+  for (int c = 0; c < (NC > 0 ? NC : kMaxCols); ++c) {
+    if (c >= nc) break;
+    col[c] = om.col[c];
+    side[c] = om.side[c] != 0;
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (; o < total; o += stride) {
+#pragma unroll
+    for (int c = 0; c < (NC > 0 ? NC : kMaxCols); ++c) {
+      if (c >= nc) break;
+      out[(uint64_t)c * cap + o] = side[c] ? col[c][j] : col[c][i];
+    }
+    i += sq;
+    j += sr;
+    if (j >= nb) { j -= nb; ++i; }
   }
 }
 
@@ -1002,26 +1026,29 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   }
 }
 
-// Single pass of the filtered expansion: each wave takes 1024-output chunks;
-// pass A over the chunk tests every output's build value against the key
-// bitmap (flag bytes in LDS, kept count), one atomic reserves the chunk's
-// kept outputs at the end of the output, pass B re-walks the chunk (its probe
-// rows, owner prefixes and build rows are L1/L2-resident now) and writes the
-// kept outputs in chunk order.  Chunks land in completion order, so the
-// output is not sorted; no flag array goes through HBM and the virtual
-// outputs are walked from HBM once (k_dj_filt<0> + k_dj_filt<1> walk them twice).
+// Single pass of the filtered expansion.  A block takes kFuseChunks 1024-output
+// chunks per wave; pass A tests every output's build value against the key
+// bitmap (flag bytes in LDS, kept count per chunk), ONE atomic per block
+// reserves the block's kept outputs at the end of the output, pass B re-walks
+// the chunks (probe rows, owner prefixes and build rows are cache-resident now)
+// and writes the kept outputs in chunk order.  Blocks land in completion
+// order, so the output is not sorted; no flag array goes through HBM and the
+// virtual outputs are walked from HBM once.
+constexpr int kFuseChunks = 4;
 template <int NPC = -1, int NBC = -1>
 __global__ void __launch_bounds__(B) k_dj_filt_fused(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                      uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                      const uint64_t* __restrict__ unit_off, uint64_t total,
                                                      FiltKey fk, JoinCols jc, uint32_t* __restrict__ out,
                                                      uint64_t cap, unsigned long long* __restrict__ kept) {
-  __shared__ uint8_t sflag[B / 64][kBalChunk];
-  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  __shared__ uint8_t sflag[B / 64][kFuseChunks][kBalChunk];
+  __shared__ uint32_t s_cnt[B / 64];
+  __shared__ unsigned long long s_base;
   const int lane = __lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t lt = __lanemask_lt();
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const uint64_t per_block = (uint64_t)(B / 64) * kFuseChunks;
   const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
   const uint32_t* pp[4];
   const uint32_t* bp[4];
@@ -1034,124 +1061,146 @@ __global__ void __launch_bounds__(B) k_dj_filt_fused(const uint32_t* __restrict_
     po[i] = i < ncp ? out + (uint64_t)jc.po[i] * cap : nullptr;
     bo[i] = i < ncb ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
-  uint8_t* fl = sflag[wv];
-  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + wv; w < chunks; w += waves) {
-    const uint64_t ob = w * kBalChunk;
-    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
-    uint64_t ulo = 0, uhi = units;                     // last unit with unit_off[u] <= ob
-    while (uhi - ulo > 1) {
-      const uint64_t step = (uhi - ulo + 63) / 64;
-      const uint64_t idx = ulo + (uint64_t)lane * step;
-      const bool ok = idx < uhi && unit_off[idx] <= ob;
-      const uint64_t m = __ballot(ok);
-      const uint64_t nlo = ulo + (uint64_t)(63 - __clzll((long long)m)) * step;
-      uhi = nlo + step < uhi ? nlo + step : uhi;
-      ulo = nlo;
-    }
-    uint32_t run = 0;
-    uint64_t obase = 0;
+  // block-uniform trip count: every wave reaches the barriers
+  for (uint64_t it = blockIdx.x; it * per_block < chunks; it += gridDim.x) {
+    uint32_t cnt[kFuseChunks];
+    uint64_t cbase[kFuseChunks];
     for (int pass = 0; pass < 2; ++pass) {
       if (pass == 1) {
-        // reserve the chunk's kept outputs (one atomic per 1024 outputs)
-        unsigned long long b0 = 0;
-        if (lane == 0 && run) b0 = atomicAdd(kept, (unsigned long long)run);
-        obase = (uint64_t)__shfl((long long)b0, 0, 64);
-        if (!run) break;
-        run = 0;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < kFuseChunks; ++k) tot += cnt[k];
+        if (lane == 0) s_cnt[wv] = tot;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          uint32_t all = 0;
+          for (int w = 0; w < B / 64; ++w) all += s_cnt[w];
+          s_base = all ? atomicAdd(kept, (unsigned long long)all) : 0ull;
+        }
+        __syncthreads();
+        uint64_t o0 = s_base;
+        for (int w = 0; w < wv; ++w) o0 += s_cnt[w];
+#pragma unroll
+        for (int k = 0; k < kFuseChunks; ++k) {
+          cbase[k] = o0;
+          o0 += cnt[k];
+        }
       }
-      for (uint64_t u = ulo; u < units; ++u) {
-        uint64_t base = unit_off[u];
-        if (base >= oe) break;
-        const uint64_t r0 = u * kXRows;
-        uint2 e[kXGroups];
 #pragma unroll
-        for (int g = 0; g < kXGroups; ++g) {
-          const uint64_t r = r0 + g * 64 + lane;
-          const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
-          e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+      for (int k = 0; k < kFuseChunks; ++k) {
+        const uint64_t w = it * per_block + (uint64_t)wv * kFuseChunks + k;
+        if (pass == 0) cnt[k] = 0;
+        if (w >= chunks || (pass == 1 && !cnt[k])) continue;
+        uint8_t* fl = sflag[wv][k];
+        const uint64_t ob = w * kBalChunk;
+        const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+        uint64_t ulo = 0, uhi = units;                 // last unit with unit_off[u] <= ob
+        while (uhi - ulo > 1) {
+          const uint64_t step = (uhi - ulo + 63) / 64;
+          const uint64_t idx = ulo + (uint64_t)lane * step;
+          const bool ok = idx < uhi && unit_off[idx] <= ob;
+          const uint64_t m = __ballot(ok);
+          const uint64_t nlo = ulo + (uint64_t)(63 - __clzll((long long)m)) * step;
+          uhi = nlo + step < uhi ? nlo + step : uhi;
+          ulo = nlo;
         }
+        uint32_t run = 0;
+        for (uint64_t u = ulo; u < units; ++u) {
+          uint64_t base = unit_off[u];
+          if (base >= oe) break;
+          const uint64_t r0 = u * kXRows;
+          uint2 e[kXGroups];
 #pragma unroll
-        for (int g = 0; g < kXGroups; ++g) {
-          const uint32_t c = e[g].y;
-          const uint32_t inc = wave_inclusive_scan(c);
-          const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
-          const uint32_t pre = inc - c;
-          const uint64_t gb = base, ge = base + tot;
-          base = ge;
-          if (ge <= ob || gb >= oe) continue;
-          const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
-          const uint64_t r = r0 + g * 64 + lane;
-          uint32_t pv[4] = {0u, 0u, 0u, 0u};
-          if (pass == 1) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
+          for (int g = 0; g < kXGroups; ++g) {
+            const uint64_t r = r0 + g * 64 + lane;
+            const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+            e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
           }
-          for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
-            const int nr = (re - o0) >= 64u * kXUnroll ? kXUnroll : (int)((re - o0 + 63) / 64);
-            uint32_t o[kXUnroll], br[kXUnroll];
-            int ll[kXUnroll];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) {
-              o[q] = o0 + (uint32_t)(q * 64 + lane);
-              ll[q] = 0;
-              br[q] = 0;
-              if (q >= nr) continue;
-              int l = 0;                               // owner: max lane with pre <= o
+          for (int g = 0; g < kXGroups; ++g) {
+            const uint32_t c = e[g].y;
+            const uint32_t inc = wave_inclusive_scan(c);
+            const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+            const uint32_t pre = inc - c;
+            const uint64_t gb = base, ge = base + tot;
+            base = ge;
+            if (ge <= ob || gb >= oe) continue;
+            const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
+            const uint64_t r = r0 + g * 64 + lane;
+            uint32_t pv[4] = {0u, 0u, 0u, 0u};
+            if (pass == 1) {
 #pragma unroll
-              for (int st = 32; st >= 1; st >>= 1) {
-                const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
-                if (l + st < 64 && pl <= o[q]) l += st;
-              }
-              ll[q] = l;
-              br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+              for (int i = 0; i < 4; ++i)
+                if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
             }
-            if (pass == 0) {
-              uint32_t v[kXUnroll];
-#pragma unroll
-              for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
-              uint32_t wd[kXUnroll];
-#pragma unroll
-              for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+            for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+              const int nr = (re - o0) >= 64u * kXUnroll ? kXUnroll : (int)((re - o0 + 63) / 64);
+              uint32_t o[kXUnroll], br[kXUnroll];
+              int ll[kXUnroll];
 #pragma unroll
               for (int q = 0; q < kXUnroll; ++q) {
+                o[q] = o0 + (uint32_t)(q * 64 + lane);
+                ll[q] = 0;
+                br[q] = 0;
                 if (q >= nr) continue;
-                const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
-                if (o[q] < re) fl[gb + o[q] - ob] = f ? 1 : 0;
-                run += (uint32_t)__popcll(__ballot(f));
-              }
-            } else {
-              bool f[kXUnroll];
+                int l = 0;                             // owner: max lane with pre <= o
 #pragma unroll
-              for (int q = 0; q < kXUnroll; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q] - ob] != 0;
-              uint32_t bv[kXUnroll][4];
-#pragma unroll
-              for (int q = 0; q < kXUnroll; ++q)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
-#pragma unroll
-              for (int q = 0; q < kXUnroll; ++q) {
-                if (q >= nr) continue;
-                const uint64_t m = __ballot(f[q]);
-                const uint64_t pos = obase + run + __popcll(m & lt);
-                run += (uint32_t)__popcll(m);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  if (i >= ncp) break;
-                  const uint32_t x = lane_get(pv[i], ll[q]);
-                  if (f[q]) po[i][pos] = x;
+                for (int st = 32; st >= 1; st >>= 1) {
+                  const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
+                  if (l + st < 64 && pl <= o[q]) l += st;
                 }
-                if (f[q]) {
+                ll[q] = l;
+                br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+              }
+              if (pass == 0) {
+                uint32_t v[kXUnroll];
 #pragma unroll
-                  for (int i = 0; i < 4; ++i)
-                    if (i < ncb) bo[i][pos] = bv[q][i];
+                for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+                uint32_t wd[kXUnroll];
+#pragma unroll
+                for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+#pragma unroll
+                for (int q = 0; q < kXUnroll; ++q) {
+                  if (q >= nr) continue;
+                  const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
+                  if (o[q] < re) fl[gb + o[q] - ob] = f ? 1 : 0;
+                  run += (uint32_t)__popcll(__ballot(f));
+                }
+              } else {
+                bool f[kXUnroll];
+#pragma unroll
+                for (int q = 0; q < kXUnroll; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q] - ob] != 0;
+                uint32_t bv[kXUnroll][4];
+#pragma unroll
+                for (int q = 0; q < kXUnroll; ++q)
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
+#pragma unroll
+                for (int q = 0; q < kXUnroll; ++q) {
+                  if (q >= nr) continue;
+                  const uint64_t m = __ballot(f[q]);
+                  const uint64_t pos = cbase[k] + run + __popcll(m & lt);
+                  run += (uint32_t)__popcll(m);
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) {
+                    if (i >= ncp) break;
+                    const uint32_t x = lane_get(pv[i], ll[q]);
+                    if (f[q]) po[i][pos] = x;
+                  }
+                  if (f[q]) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                      if (i < ncb) bo[i][pos] = bv[q][i];
+                  }
                 }
               }
             }
           }
         }
+        if (pass == 0) cnt[k] = run;
       }
     }
+    __syncthreads();                                   // LDS flags and counts reused next iteration
   }
 }
 
@@ -3373,6 +3422,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   // while the worst case (every virtual output kept) fits the output buffer
   const char* ff = std::getenv("DAS_FILT_FUSED");
   if (!(ff && ff[0] == '0') && (uint64_t)nu * total * 4 <= (16ull << 30)) {
+    const unsigned ugrid = grid_for((chunks + (B / 64) * kFuseChunks - 1) / ((B / 64) * kFuseChunks), 1, 65535u * 4u);
     auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
     DBuf<unsigned long long> kept(1, c.s);
     fill_dev(kept.p, 0, 8, c.s);
@@ -3384,7 +3434,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
                            : std::string("k_dj_filt_fused<-1,-1>"),
                    (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
 #define FILT_F(NPV, NBV)                                                                                          \
-  hipLaunchKernelGGL((k_dj_filt_fused<NPV, NBV>), dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
+  hipLaunchKernelGGL((k_dj_filt_fused<NPV, NBV>), dim3(ugrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
                      (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, jc, out->data,  \
                      out->cap, kept.p)
       if (jc.np == 1 && jc.nb == 1) FILT_F(1, 1);
@@ -3480,7 +3530,16 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       else { om.col[k] = Q.col(colof(Q, uni[k])); om.side[k] = 1; }
     }
     ProfScope ps(c, "k_cartesian", 4.0 * nu * total);
-    hipLaunchKernelGGL(k_cartesian, G(total), dim3(B), 0, c.s, om, Q.nrows, total, out->data, out->cap);
+    const unsigned cg = grid_for(total, B);
+    const uint64_t S = (uint64_t)cg * B, sq = S / Q.nrows, sr = S % Q.nrows;
+    switch (nu) {
+      case 2: hipLaunchKernelGGL(k_cartesian<2>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 3: hipLaunchKernelGGL(k_cartesian<3>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 4: hipLaunchKernelGGL(k_cartesian<4>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 5: hipLaunchKernelGGL(k_cartesian<5>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 6: hipLaunchKernelGGL(k_cartesian<6>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      default: hipLaunchKernelGGL(k_cartesian<0>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+    }
     DAS_HIP(hipGetLastError());
   } else if (shared.size() == 1 && Q.ncols == 1 && (out = semi_join(c, P, Q))) {
     // key-set filter taken (the build side adds no columns)
