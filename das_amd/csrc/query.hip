@@ -363,16 +363,22 @@ __global__ void k_join_expand(const uint64_t* offs, uint64_t np, const uint32_t*
   }
 }
 
-// Output o = (probe row o / nb, build row o % nb).  One division per thread:
-// the grid stride S advances (i, j) by (S / nb, S % nb) with a carry, so the
-// kernel is a pure column-store stream (NC: output columns, specialised up to 6).
+// Output o = (probe row o / nb, build row o % nb).  A thread writes four
+// consecutive outputs per column as one 16-byte nontemporal store (columns
+// are 64-row aligned, so a partial last quad stays inside the capacity); one
+// division per thread: the grid stride S quads advances (i, j) by
+// (4S / nb, 4S % nb) with a carry.  A pure write stream at ~6 TB/s on MI355X
+// (4-byte stores: ~3.4 TB/s; tools/ubench/cart_bw.hip, profiles/r3_cart_bw.txt).
+// NC: output columns, specialised up to 6.
 template <int NC>
-__global__ void __launch_bounds__(B) k_cartesian(OutMap om, uint64_t nb, uint64_t total, uint64_t sq, uint64_t sr,
-                                                 uint32_t* out, uint64_t cap) {
+__global__ void __launch_bounds__(B) k_cartesian(OutMap om, uint64_t np, uint64_t nb, uint64_t total, uint64_t sq,
+                                                 uint64_t sr, uint32_t* out, uint64_t cap) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const int nc = NC > 0 ? NC : om.n;
-  uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (o >= total) return;
-  uint64_t i = o / nb, j = o - i * nb;
+  const uint64_t nq = (total + 3) >> 2;
+  uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  uint64_t i = (q << 2) / nb, j = (q << 2) - i * nb;
   const uint32_t* col[kMaxCols];
   bool side[kMaxCols];
 #pragma unroll
@@ -382,11 +388,23 @@ __global__ void __launch_bounds__(B) k_cartesian(OutMap om, uint64_t nb, uint64_
     side[c] = om.side[c] != 0;
   }
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (; o < total; o += stride) {
+  for (; q < nq; q += stride) {
+    uint64_t ii[4], jj[4];
+    ii[0] = i;
+    jj[0] = j;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      ii[k] = ii[k - 1];
+      jj[k] = jj[k - 1] + 1;
+      if (jj[k] == nb) { jj[k] = 0; ++ii[k]; }
+    }
 #pragma unroll
     for (int c = 0; c < (NC > 0 ? NC : kMaxCols); ++c) {
       if (c >= nc) break;
-      out[(uint64_t)c * cap + o] = side[c] ? col[c][j] : col[c][i];
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ii[k] < np ? (side[c] ? col[c][jj[k]] : col[c][ii[k]]) : 0u;
+      __builtin_nontemporal_store(v4u{v[0], v[1], v[2], v[3]}, reinterpret_cast<v4u*>(out + (uint64_t)c * cap) + q);
     }
     i += sq;
     j += sr;
@@ -3418,10 +3436,12 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
   const unsigned fgrid = grid_for(chunks, B / 64, 65535u * 4u);
   const FiltKey fk{jc.b[fb], (uint32_t)lo, (uint32_t)(hi - lo + 1), (const uint32_t*)bits.p};
-  // one pass, unsorted output (DAS_FILT_FUSED=0: the two ordered passes),
-  // while the worst case (every virtual output kept) fits the output buffer
+  // DAS_FILT_FUSED=1: one pass, unsorted output, while the worst case (every
+  // virtual output kept) fits the output buffer.  Off by default: at config 5
+  // it ran 924 us against 337 + 296 us for the two ordered passes (round 3,
+  // profiles/r3_hub_filt_ab.json) -- the LDS flag tiles cut its occupancy
   const char* ff = std::getenv("DAS_FILT_FUSED");
-  if (!(ff && ff[0] == '0') && (uint64_t)nu * total * 4 <= (16ull << 30)) {
+  if (ff && ff[0] == '1' && (uint64_t)nu * total * 4 <= (16ull << 30)) {
     const unsigned ugrid = grid_for((chunks + (B / 64) * kFuseChunks - 1) / ((B / 64) * kFuseChunks), 1, 65535u * 4u);
     auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
     DBuf<unsigned long long> kept(1, c.s);
@@ -3530,15 +3550,17 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       else { om.col[k] = Q.col(colof(Q, uni[k])); om.side[k] = 1; }
     }
     ProfScope ps(c, "k_cartesian", 4.0 * nu * total);
-    const unsigned cg = grid_for(total, B);
-    const uint64_t S = (uint64_t)cg * B, sq = S / Q.nrows, sr = S % Q.nrows;
+    const unsigned cg = grid_for((total + 3) / 4, B);
+    const uint64_t S = 4ull * cg * B, sq = S / Q.nrows, sr = S % Q.nrows;
+    DAS_CHECK(out->cap % 4 == 0 && (reinterpret_cast<uintptr_t>(out->data) & 15) == 0, DAS_E_INTERNAL,
+              "cartesian: output columns not 16-byte aligned");
     switch (nu) {
-      case 2: hipLaunchKernelGGL(k_cartesian<2>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
-      case 3: hipLaunchKernelGGL(k_cartesian<3>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
-      case 4: hipLaunchKernelGGL(k_cartesian<4>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
-      case 5: hipLaunchKernelGGL(k_cartesian<5>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
-      case 6: hipLaunchKernelGGL(k_cartesian<6>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
-      default: hipLaunchKernelGGL(k_cartesian<0>, dim3(cg), dim3(B), 0, c.s, om, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 2: hipLaunchKernelGGL(k_cartesian<2>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 3: hipLaunchKernelGGL(k_cartesian<3>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 4: hipLaunchKernelGGL(k_cartesian<4>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 5: hipLaunchKernelGGL(k_cartesian<5>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      case 6: hipLaunchKernelGGL(k_cartesian<6>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
+      default: hipLaunchKernelGGL(k_cartesian<0>, dim3(cg), dim3(B), 0, c.s, om, P.nrows, Q.nrows, total, sq, sr, out->data, out->cap); break;
     }
     DAS_HIP(hipGetLastError());
   } else if (shared.size() == 1 && Q.ncols == 1 && (out = semi_join(c, P, Q))) {

@@ -548,7 +548,7 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     import bench
     from das_amd import synthetic
     monkeypatch.setenv("DAS_SEMI_MULTI", multi[0])
-    # the filtered expansion in one pass (default) or the two ordered passes
+    # the filtered expansion in two ordered passes (default) or one pass
     monkeypatch.setenv("DAS_FILT_FUSED", "0" if multi == "1-twopass" else "1")
     arrays = synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
     db = _hipdb(arrays)
