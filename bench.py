@@ -756,6 +756,10 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     warm_stats = db.ctx.prof_stats()
     dominant = roofline_of(warm_stats, workload) if args.events == "dominant" else None
     per_query = {name: run(q) for name, q in qsets[args.warmup]}
+    if world > 1:
+        # the answer's size: each rank counts the bindings it holds
+        stage = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
+        per_query = dict(zip(per_query, (int(x) for x in _sync_sum(dist, list(per_query.values()), stage))))
     # per-query wall time (the warm query set of the first timed step, 5 runs each)
     per_query_ms = {}
     for name, q in qsets[args.warmup]:
@@ -847,7 +851,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                 "flybase": "synthetic FlyBase-shaped KB (flybase2metta Execution layout; the FlyBase dump needs a "
                            "network fetch)",
                 "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
-        cfg = dict(cfg, bindings_per_step_rank0=per_query, parallelism=f"links sharded x{world}")
+        cfg = dict(cfg, bindings_per_step=per_query, parallelism=f"links sharded x{world}")
         cfg["query_ms_rank0"] = per_query_ms
         out = {
             "metric": "pattern matches/sec (bindings/s) + % HBM roofline",

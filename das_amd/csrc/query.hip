@@ -834,6 +834,7 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
                      uint64_t cap, uint64_t total, bool balanced, double bytes) {
   const bool wide = total >= (1ull << 32) - (1ull << 16);
   static const int fixed = std::getenv("DAS_DJ_FIXED") && std::getenv("DAS_DJ_FIXED")[0] == '1';
+  // scope names = rocprof's names of the instantiation launched below
   KScope ks((std::string(balanced ? "k_dj_write_bal<" : "k_dj_write<") + std::to_string(NP) + "," +
              std::to_string(NB) + (wide ? ",u64" : ",u32") +
              (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
@@ -908,14 +909,8 @@ struct FiltKey {
 };
 
 // NPC / NBC: the probe / build output column counts when specialised (the
-// pointers then live in registers), -1 = read from jc at run time.
-// OPT (MODE 0): bit 0 -- the streamed build values are loaded and the flag
-// bytes stored nontemporally, so the random bitmap probes keep L2 to
-// themselves; bit 1 -- the first kFiltHotWords words of the bitmap (the
-// degree order puts the most-referenced ids first) are staged in LDS once per
-// block and probed there.
-constexpr uint32_t kFiltHotWords = 8192;           // 32 KB: ids [lo, lo + 2^18)
-template <int MODE, int NPC = -1, int NBC = -1, int OPT = 0>
+// pointers then live in registers), -1 = read from jc at run time
+template <int MODE, int NPC = -1, int NBC = -1>
 __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
@@ -927,14 +922,6 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   const uint64_t lt = __lanemask_lt();
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
   const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
-  constexpr bool kNT = MODE == 0 && (OPT & 1);
-  constexpr bool kHot = MODE == 0 && (OPT & 2);
-  __shared__ uint32_t s_hot[kHot ? kFiltHotWords : 1];
-  const uint32_t nhot = kHot ? ((fk.range + 31) / 32 < kFiltHotWords ? (fk.range + 31) / 32 : kFiltHotWords) : 0u;
-  if (kHot) {
-    for (uint32_t t = threadIdx.x; t < nhot; t += B) s_hot[t] = fk.bits[t];
-    __syncthreads();
-  }
   const uint32_t* pp[4];
   const uint32_t* bp[4];
   uint32_t* po[4];
@@ -1012,23 +999,15 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
           if (MODE == 0) {
             uint32_t v[kXUnroll];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q)
-              v[q] = (q < nr && o[q] < re) ? (kNT ? __builtin_nontemporal_load(&fk.col[br[q]]) : fk.col[br[q]]) - fk.lo
-                                           : 0xFFFFFFFFu;
+            for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
             uint32_t wd[kXUnroll];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) {
-              const uint32_t wi = v[q] >> 5;
-              wd[q] = v[q] < fk.range ? (kHot && wi < nhot ? s_hot[wi] : fk.bits[wi]) : 0u;
-            }
+            for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
 #pragma unroll
             for (int q = 0; q < kXUnroll; ++q) {
               if (q >= nr) continue;
               const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
-              if (o[q] < re) {
-                if (kNT) __builtin_nontemporal_store((uint8_t)(f ? 1 : 0), &fl[gb + o[q]]);
-                else fl[gb + o[q]] = f ? 1 : 0;
-              }
+              if (o[q] < re) fl[gb + o[q]] = f ? 1 : 0;
               run += (uint32_t)__popcll(__ballot(f));
             }
           } else {
@@ -3505,26 +3484,10 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
-    // DAS_FILT_OPT: the flag pass's OPT bits (A/B; default below)
-    static const int opt = [] {
-      const char* e = std::getenv("DAS_FILT_OPT");
-      return e ? std::atoi(e) & 3 : 0;
-    }();
-    // an LDS-staged bitmap prefix is loaded once per block: a grid of a few
-    // blocks per CU keeps those loads small
-    const unsigned g0 = (opt & 2) ? std::min(fgrid, 1024u) : fgrid;
     ProfScope ps(c, "k_dj_filt<0,-1,-1>", 12.0 * A.nrows + 5.0 * total);
-#define FILT_F0(OPTV)                                                                                              \
-  hipLaunchKernelGGL((k_dj_filt<0, -1, -1, OPTV>), dim3(g0), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
-                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
-                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull)
-    switch (opt) {
-      case 1: FILT_F0(1); break;
-      case 2: FILT_F0(2); break;
-      case 3: FILT_F0(3); break;
-      default: FILT_F0(0); break;
-    }
-#undef FILT_F0
+    hipLaunchKernelGGL(k_dj_filt<0>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
+                       (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p,
+                       (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
     DAS_HIP(hipGetLastError());
   }
   const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, chunks, coff.p, c.s);
@@ -3587,7 +3550,7 @@ std::unique_ptr<Table> join(Ctx& c, const Table& A, const Table& Bt, int no_over
       if (ip >= 0) { om.col[k] = P.col(ip); om.side[k] = 0; }
       else { om.col[k] = Q.col(colof(Q, uni[k])); om.side[k] = 1; }
     }
-    ProfScope ps(c, "k_cartesian", 4.0 * nu * total);
+    ProfScope ps(c, "k_cartesian<" + std::to_string(nu >= 2 && nu <= 6 ? nu : 0) + ">", 4.0 * nu * total);
     const unsigned cg = grid_for((total + 3) / 4, B);
     const uint64_t S = 4ull * cg * B, sq = S / Q.nrows, sr = S % Q.nrows;
     DAS_CHECK(out->cap % 4 == 0 && (reinterpret_cast<uintptr_t>(out->data) & 15) == 0, DAS_E_INTERNAL,

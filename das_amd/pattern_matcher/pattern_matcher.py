@@ -32,7 +32,7 @@ from typing import Dict, FrozenSet, List, Optional, Set, Union
 import numpy as np
 
 from .. import _lib
-from ..database.db_interface import WILDCARD, DBInterface
+from ..database.db_interface import UNORDERED_LINK_TYPES, WILDCARD, DBInterface
 from ..database.hip_db import HipDB, Relation, RelationalDB
 
 DEBUG_AND = False
@@ -361,6 +361,7 @@ class _Unsupported(Exception):
 
 
 _RECORD = struct.Struct("<51I")
+_WORDS = 51
 
 
 def _node_record(op, nchild=0, value=0, spec=None, ij=None):
@@ -489,11 +490,75 @@ def _walk(expr, out, links, root=True):
         raise _Unsupported()
 
 
+class _NoShape(Exception):
+    pass
+
+
+def _shape(expr, nodes):
+    """Structure key of `expr` with its nodes' names left out (the nodes are
+    appended to `nodes` in walk order).  Raises _NoShape for what a
+    parameterised plan cannot carry: a Link whose targets are all grounded
+    (its record is link_exists of those very handles) and the unordered link
+    types (their scan keys are sorted by handle)."""
+    k = expr._k
+    if k == 'n':
+        nodes.append(expr)
+        return expr.atom_type
+    if k == 'v':
+        return ('v', expr.name)
+    if k == 'tv':
+        return ('tv', expr.name, expr.type)
+    if k == 'l':
+        if expr.atom_type in UNORDERED_LINK_TYPES or all(t._k == 'n' for t in expr.targets):
+            raise _NoShape()
+        return ('l', expr.atom_type, expr.ordered, tuple([_shape(t, nodes) for t in expr.targets]))
+    if k == 't':
+        return ('t', expr.link_type, expr.ordered, tuple([(v.name, v.type) for v in expr.targets]))
+    if k == 'x':
+        return ('x', _shape(expr.term, nodes))
+    if k == 'a' or k == 'o':
+        return (k, tuple([_shape(t, nodes) for t in expr.terms]))
+    raise _NoShape()
+
+
+def _node_ids(db, nodes):
+    """Atom ids of `nodes` (one batched lookup), or None if one is not a node
+    of the KB (its term's record would then be a constant)."""
+    hs = [n.get_handle(db) for n in nodes]
+    out = []
+    for aid, cat, _ in db._resolve(hs):
+        if aid < 0 or cat != 1:
+            return None
+        out.append(aid)
+    return out
+
+
 def _lower(expr, db, no_overload):
     """The das_plan_node_t array (51 u32 words per node) of `expr`, or None.
-    Link records are cached per (index, signature), so a repeated query
-    shape re-lowers only the links whose anchors changed; their handles are
-    resolved in one batched lookup."""
+
+    A query shape seen before (the same tree with other node names, e.g. a
+    fresh gene anchor) is answered from the shape cache: its words with each
+    node's atom id patched into the scan / index-join target slots it
+    occupies -- one batched handle lookup, no re-lowering.  Otherwise Link
+    records are cached per (index, signature), so a repeated query re-lowers
+    only the links whose anchors changed; their handles are resolved in one
+    batched lookup."""
+    nodes = []
+    try:
+        skey = (no_overload, _shape(expr, nodes))
+    except _NoShape:
+        skey = None
+    shapes = db.__dict__.setdefault('_plan_shapes', {})
+    if skey is not None:
+        hit = shapes.get(skey)
+        if hit is not None:
+            ids = _node_ids(db, nodes) if nodes else []
+            if ids is not None:
+                words, patches = hit
+                w = words.copy()
+                for wi, k in patches:
+                    w[wi] = ids[k]
+                return w
     out, links = [], []
     try:
         _walk(expr, out, links)
@@ -515,7 +580,28 @@ def _lower(expr, db, no_overload):
             _resolve(todo, out, cache, db, no_overload)
         except _Unsupported:
             return None
-    return np.frombuffer(b"".join(out), dtype=np.uint32)
+    words = np.frombuffer(b"".join(out), dtype=np.uint32)
+    if skey is not None and (not nodes or _node_ids(db, nodes) is not None):
+        # every node exists: each Link record's grounded targets are these
+        # nodes' ids at fixed word offsets (scan targets at 7 + p, the index
+        # join's at 30 + p; include/das_mi355x.h das_plan_node_t)
+        ordinal = {id(n): i for i, n in enumerate(nodes)}
+        patches = []
+        for pos, e, _ in links:
+            if e._k != 'l':
+                continue
+            base = _WORDS * pos
+            if int(words[base]) != _lib.PLAN_LINK:
+                continue
+            for p, t in enumerate(e.targets):
+                if t._k == 'n':
+                    patches.append((base + 7 + p, ordinal[id(t)]))
+                    if int(words[base + 4]):
+                        patches.append((base + 30 + p, ordinal[id(t)]))
+        if len(shapes) > (1 << 12):
+            shapes.clear()
+        shapes[skey] = (words, patches)
+    return words
 
 
 def _resolve(todo, out, cache, db, no_overload):

@@ -62,3 +62,30 @@ def test_gpu_plan_more_answer_schemas_than_first_capacity():
     got = record(spec, db)
     assert same(got, want), (got, want.get("n"))
     assert want["n"] > 64
+
+
+def test_gpu_shape_cache_patches_anchor_ids():
+    """A query shape lowered once is reused for other anchors (the same tree
+    with other node names): its words with the new nodes' ids patched in must
+    equal a from-scratch lowering of the new expression, and the answers the
+    oracle's -- including anchors that are no node of the KB (the constant
+    records of the full lowering) and a Not term sharing the anchor node."""
+    import bench
+    from das_amd import synthetic
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    arrays = synthetic.flybase_kb(400, 8, 1500, n_loc=30, n_do=20, seed=3)
+    db = _db(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    genes = [7, 11, 7, 250, 399, 3, 10**6]          # 10**6: FBgn id absent from the KB
+    for g in genes:
+        for name, spec in bench.flybase_specs(g, synthetic.flybase_do_terms(arrays, gene=g) if g < 400 else ()):
+            e1, e2 = build(spec), build(spec)
+            hit = pm._lower(e1, db, False)            # the shape cache, after the first gene
+            db.__dict__.pop('_plan_shapes', None)
+            db.__dict__.pop('_plan_records', None)
+            full = pm._lower(e2, db, False)           # from scratch
+            assert (hit is None) == (full is None), name
+            if full is not None:
+                assert hit.tobytes() == full.tobytes(), (name, g)
+            want = O.evaluate(spec, odb)
+            assert same(record(spec, db), want), (name, g)
