@@ -910,7 +910,7 @@ struct FiltKey {
 
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
-template <int MODE, int NPC = -1, int NBC = -1>
+template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk>
 __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
-  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const uint64_t chunks = (total + CH - 1) / CH;
   const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
   const uint32_t* pp[4];
   const uint32_t* bp[4];
@@ -934,8 +934,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
     bo[i] = i < ncb && MODE == 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
-    const uint64_t ob = w * kBalChunk;
-    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+    const uint64_t ob = w * CH;
+    const uint64_t oe = ob + CH < total ? ob + CH : total;
     uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
     while (hi - lo > 1) {
       const uint64_t step = (hi - lo + 63) / 64;
@@ -2302,6 +2302,60 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
   if (threadIdx.x == 0) publish_u32(slot, seq, total);
 }
 
+// Multi-workgroup index join of a mid-size probe (kIjSmall < rows <= kIjMid)
+// in ONE launch and one read-back: a wave looks up its 64 probe rows, scans
+// their match counts, reserves its outputs with one atomic and expands them
+// (owner lane by a search over the lanes' prefixes), so waves land in
+// completion order -- the output is unsorted.  The last block to finish
+// publishes the total; outputs past the speculative capacity are not
+// written (the host then takes the multi-launch path).
+constexpr uint32_t kIjMid = 32768;
+
+__global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, uint32_t n, IjKeys kx, IjGround g,
+                                              JoinCols jc, uint32_t* __restrict__ out, uint64_t cap,
+                                              uint32_t* __restrict__ ctr, uint32_t* slot, uint32_t seq) {
+  const int lane = __lane_id();
+  const uint32_t r = blockIdx.x * B + threadIdx.x;
+  const uint2 e = r < n ? ij_lookup(key[r], kx, g, r) : make_uint2(0u, 0u);
+  const uint32_t inc = wave_incl_sum_u32(e.y);
+  const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+  const uint32_t pre = inc - e.y;
+  uint32_t base = 0;
+  if (lane == 0 && tot) base = atomicAdd(&ctr[0], tot);
+  base = (uint32_t)__shfl(base, 0, 64);
+  if (tot && (uint64_t)base + tot <= cap) {
+    uint32_t pv[kMaxCols];
+#pragma unroll
+    for (int i = 0; i < kMaxCols; ++i) pv[i] = i < jc.np && r < n ? jc.p[i][r] : 0u;
+    for (uint32_t o0 = 0; o0 < tot; o0 += 64) {
+      const uint32_t o = o0 + lane;
+      int ll = 0;                                    // owner: max lane with pre <= o
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t pl = (uint32_t)__shfl(pre, ll + step, 64);
+        if (ll + step < 64 && pl <= o) ll += step;
+      }
+      const uint32_t br = lane_get(e.x, ll) + (o - (uint32_t)__shfl(pre, ll, 64));
+#pragma unroll
+      for (int i = 0; i < kMaxCols; ++i) {
+        if (i >= jc.np) break;
+        const uint32_t v = lane_get(pv[i], ll);
+        if (o < tot) out[(uint64_t)jc.po[i] * cap + base + o] = v;
+      }
+      if (o < tot)
+        for (int i = 0; i < jc.nb; ++i) out[(uint64_t)jc.bo[i] * cap + base + o] = jc.b[i][br];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
+      __threadfence();
+      publish_u32(slot, seq, atomicAdd(&ctr[0], 0u));
+    }
+  }
+}
+
 // Anti index join: keep row r of A when the link whose targets are the
 // grounded targets and A's values of the term's variables does NOT exist --
 // And's negation filter (pattern_matcher.py:741-746) for a Not(Link) term
@@ -2561,6 +2615,7 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
   if (!ij_prepare(c, A, q, A.nrows, pl)) return nullptr;
   const int nu = (int)pl.uni.size();
   std::unique_ptr<Table> out;
+  bool unsorted = false;                         // k_ij_mid: waves land in completion order
   if (pl.empty) {
     out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), 0);
   } else {
@@ -2581,6 +2636,29 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
         out = std::move(t);
       }
     }
+    if (!out && A.nrows > kIjSmall && A.nrows <= kIjMid) {
+      const char* f = std::getenv("DAS_IJ_MID");                // A/B, tests: 0 never
+      if (!(f && f[0] == '0')) {
+        // one launch when the output fits a speculative table of 2 rows per probe row
+        auto t = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), std::max<uint64_t>(65536, 2 * A.nrows));
+        DBuf<uint32_t> ctr(2, c.s);
+        fill_dev(ctr.p, 0, 8, c.s);
+        const PubSlot ps = pub_reserve();
+        {
+          ProfScope pf(c, "k_ij_mid", 16.0 * A.nrows + 4.0 * A.nrows * A.ncols);
+          hipLaunchKernelGGL(k_ij_mid, dim3((unsigned)((A.nrows + B - 1) / B)), dim3(B), 0, c.s, pl.akey,
+                             (uint32_t)A.nrows, pl.kx, pl.g, pl.jc, t->data, t->cap, ctr.p, ps.p, ps.seq);
+          DAS_HIP(hipGetLastError());
+        }
+        uint32_t total = 0;
+        pub_wait(ps, c.s, &total, 1);
+        if (total <= t->cap) {
+          t->nrows = total;
+          out = std::move(t);
+          unsorted = true;
+        }
+      }
+    }
     if (!out) {
       DBuf<uint2> lc(A.nrows, c.s);
       DBuf<uint32_t> rowid(A.nrows, c.s);
@@ -2594,7 +2672,7 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
       out = dj_expand(c, A, rowid.p, 0u, A.nrows, lc.p, pl.jc, nu, pl.uni.data(), -4.0 * pl.jc.nb);
     }
   }
-  out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
+  out->sorted_col = A.sorted_col >= 0 && !unsorted ? colof_t(*out, A.vars[A.sorted_col]) : -1;
   for (int k = 0; k < nu; ++k) {
     out->lo[k] = pl.lo[k];
     out->hi[k] = pl.hi[k];
@@ -3479,35 +3557,54 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     out->hi[fo] = (uint32_t)hi;
     return out;
   }
+  // outputs per wave chunk of the two passes (DAS_FILT_CHUNK: 1024 / 2048 / 4096, A/B)
+  static const int ch = [] {
+    const char* e = std::getenv("DAS_FILT_CHUNK");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 2048 || v == 4096 ? v : 1024;
+  }();
+  const uint64_t fchunks = (total + ch - 1) / ch;
+  const unsigned fgrid2 = grid_for(fchunks, B / 64, 65535u * 4u);
+  const std::string chs = "," + std::to_string(ch) + ">";
   DBuf<uint8_t> fl(total, c.s);
-  DBuf<uint32_t> ccnt(chunks, c.s), coff(chunks + 1, c.s);
+  DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
-    ProfScope ps(c, "k_dj_filt<0,-1,-1>", 12.0 * A.nrows + 5.0 * total);
-    hipLaunchKernelGGL(k_dj_filt<0>, dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u,
-                       (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p,
-                       (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
+    ProfScope ps(c, "k_dj_filt<0,-1,-1" + chs, 12.0 * A.nrows + 5.0 * total);
+#define FILT_0(CHV)                                                                                                \
+  hipLaunchKernelGGL((k_dj_filt<0, -1, -1, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows,   \
+                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
+                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull)
+    if (ch == 2048) FILT_0(2048);
+    else if (ch == 4096) FILT_0(4096);
+    else FILT_0(1024);
+#undef FILT_0
     DAS_HIP(hipGetLastError());
   }
-  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, chunks, coff.p, c.s);
+  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);
   auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
   out->nrows = m;
   if (m) {
     // + the probe columns, the flags, the kept outputs' build rows and their columns out
     // (named as rocprof names the instantiation launched below)
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-    ProfScope ps(c, spec ? "k_dj_filt<1," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ">"
-                         : std::string("k_dj_filt<1,-1,-1>"),
+    ProfScope ps(c, spec ? "k_dj_filt<1," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + chs
+                         : "k_dj_filt<1,-1,-1" + chs,
                  (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
-#define FILT_W(NPV, NBV)                                                                                     \
-  hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV>), dim3(fgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
-                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,        \
+#define FILT_W(NPV, NBV, CHV)                                                                                  \
+  hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
+                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,      \
                      (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap)
-    if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1);
-    else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1);
-    else if (jc.np == 1 && jc.nb == 2) FILT_W(1, 2);
-    else FILT_W(-1, -1);
+#define FILT_WC(CHV)                                    \
+  if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1, CHV);      \
+  else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1, CHV); \
+  else if (jc.np == 1 && jc.nb == 2) FILT_W(1, 2, CHV); \
+  else FILT_W(-1, -1, CHV);
+    if (ch == 2048) { FILT_WC(2048) }
+    else if (ch == 4096) { FILT_WC(4096) }
+    else { FILT_WC(1024) }
+#undef FILT_WC
 #undef FILT_W
     DAS_HIP(hipGetLastError());
   }

@@ -782,3 +782,38 @@ def test_gpu_scan_views_match_oracle(gen, monkeypatch):
         want = O.evaluate(q, odb)
         got = record(q, db)
         assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+def test_gpu_ij_mid_matches_multi_launch(monkeypatch):
+    """Index joins of mid-size probes (kIjSmall < rows <= kIjMid) in one
+    multi-workgroup launch writing the waves' outputs in completion order
+    (k_ij_mid) give the same answer sets as the multi-launch ordered path
+    (DAS_IJ_MID=0, checked against the oracle by the tests above; the
+    oracle's nested-loop And is too slow at these sizes): the Member scan
+    (~8000 rows) joined through Inheritance's pattern index, and FlyBase
+    chains whose middle result outgrows the fused chain.  The oracle itself
+    covers k_ij_mid at 3000-row probes in test_gpu_index_join_forced_*[bio]."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_INDEX_JOIN", "1")
+    V, L = bench._V, bench._L
+    cases = []
+    arrays = synthetic.bio_kb(600, 200, 8000, 400, seed=12)
+    cases.append((arrays, [
+        ["And", [L("Member", V("G"), V("B")), L("Inheritance", V("B"), V("P"))]],
+        ["And", [L("Member", V("G"), V("B")), L("Inheritance", V("P"), V("B"))]],
+        ["And", [L("Member", V("G"), V("B")), L("Member", V("G2"), V("B")), L("Inheritance", V("B"), V("P"))]]]))
+    arrays = synthetic.flybase_kb(6000, 6, 6000, n_loc=3, n_do=15, seed=5)
+    qs = []
+    for gene in (0, 7):
+        qs += [q for name, q in bench.flybase_specs(gene, synthetic.flybase_do_terms(arrays, gene))
+               if name[:2] in ("F5", "F6", "F7")]
+    cases.append((arrays, qs))
+    for arrays, qs in cases:
+        db = _hipdb(arrays)
+        for q in qs:
+            monkeypatch.setenv("DAS_IJ_MID", "1")
+            got = record(q, db)
+            monkeypatch.setenv("DAS_IJ_MID", "0")
+            want = record(q, db)
+            assert same(got, want), (q, got.get("n"), want.get("n"))

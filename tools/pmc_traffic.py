@@ -36,7 +36,7 @@ def short(name):
 
 
 # kernels whose reads are dominated by isolated random loads (x1)
-RANDOM = {"k_tile_count<BitsPred>", "k_dj_filt<0,-1,-1>", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
+RANDOM = {"k_tile_count<BitsPred>", "k_dj_filt<0,-1,-1,1024>", "k_dj_filt<0,-1,-1,2048>", "k_dj_filt<0,-1,-1,4096>", "k_ij_mid", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
           "k_hset_first", "k_hset_anti", "k_lookup", "k_lookup_pub"}
 
 
