@@ -213,6 +213,53 @@ __device__ __forceinline__ void publish_u32(uint32_t* slot, uint32_t seq, uint32
   __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Or of predicate-free one-column scans (FlyBase's DO-term Or): the union's
+// distinct values in ONE launch.  Each scanned row tests and sets its value's
+// bit in a bitmap over the column's host-known id range; the row that set it
+// writes the value, at a position its wave reserves with one atomic (output
+// unsorted, one row per distinct value -- Python set semantics).  ctr[0]:
+// rows written, ctr[1]: blocks done, ctr[2]: values outside [lo, lo + range)
+// (the host then takes the general path); the last block publishes ctr[0]
+// and ctr[2].
+__global__ void __launch_bounds__(B) k_union_first(MultiScan ms, uint32_t lo, uint32_t range,
+                                                   uint32_t* __restrict__ bits, uint32_t* __restrict__ out,
+                                                   uint32_t* __restrict__ ctr, uint32_t* slot, uint32_t seq) {
+  const MultiScan::Seg& sg = seg_of(ms, blockIdx.x);
+  const uint64_t cb = sg.begin + (uint64_t)(blockIdx.x - sg.chunk0) * kChunk;
+  const uint32_t* src = sg.sp.col[1 + sg.sp.outpos[0]];
+  uint32_t bad = 0;
+  for (int it = 0; it < kChunkIters; ++it) {
+    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
+    bool first = false;
+    uint32_t v = 0;
+    if (r < sg.end) {
+      v = src[r];
+      const uint32_t d = v - lo;
+      if (d < range) {
+        const uint32_t m = 1u << (d & 31);
+        first = (atomicOr(&bits[d >> 5], m) & m) == 0;
+      } else {
+        bad = 1;
+      }
+    }
+    const uint64_t bal = __ballot(first);
+    uint32_t base = 0;
+    if (__lane_id() == 0 && bal) base = atomicAdd(&ctr[0], (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl(base, 0, 64);
+    if (first) out[base + __popcll(bal & __lanemask_lt())] = v;
+  }
+  if (__ballot(bad) && __lane_id() == 0) atomicOr(&ctr[2], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
+      __threadfence();
+      publish_u32(slot, seq, atomicAdd(&ctr[2], 0u) ? 0xFFFFFFFFu : atomicAdd(&ctr[0], 0u));
+    }
+  }
+}
+
+
 __global__ void __launch_bounds__(kSmallBlock) k_scan_small(ScanSpec sp, uint64_t begin, uint64_t end, uint32_t* out,
                                                             uint64_t cap, uint32_t* slot, uint32_t seq) {
   constexpr int W = kSmallBlock / 64;
@@ -3194,6 +3241,58 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
     if (!ms.nseg || chunks >= (1ull << 31)) return 0;
     uint64_t scanned = 0;
     for (uint32_t i = 0; i < ms.nseg; ++i) scanned += ms.seg[i].end - ms.seg[i].begin;
+    // the union's column bounds: the union of the terms' bounds
+    uint32_t ulo[kMaxCols], uhi[kMaxCols];
+    for (int k = 0; k < preps[0].ncols; ++k) {
+      ulo[k] = kNone;
+      uhi[k] = 0;
+    }
+    for (size_t i = 0; i < terms.size(); ++i) {
+      if (preps[i].empty) continue;
+      Table tb;
+      tb.ncols = preps[i].ncols;
+      scan_bounds(idx, preps[i].sp, terms[i]->scan.type_id, tb);
+      for (int k = 0; k < preps[0].ncols; ++k) {
+        ulo[k] = std::min(ulo[k], tb.lo[k]);
+        uhi[k] = std::max(uhi[k], tb.hi[k]);
+      }
+    }
+    {
+      // one column, every row kept: bitmap union in one launch (k_union_first)
+      bool proj = preps[0].ncols == 1 && uhi[0] != kNone && ulo[0] <= uhi[0] && uhi[0] - ulo[0] < (1u << 27) &&
+                  scanned < 0xFFFFFFF0ull;
+      for (uint32_t i = 0; i < ms.nseg && proj; ++i)
+        proj = ms.seg[i].sp.all_keep && !ms.seg[i].sp.unordered && ms.seg[i].sp.nout == 1;
+      const char* fb = std::getenv("DAS_UNION_BITS");                // A/B, tests: 0 never
+      if (proj && !(fb && fb[0] == '0')) {
+        const uint32_t range = uhi[0] - ulo[0] + 1;
+        auto res = new_table(c, DAS_TABLE_ORDERED, 1, preps[0].vars, scanned);
+        DBuf<uint32_t> bits((range + 31) / 32, c.s), ctr(3, c.s);
+        fill_dev(bits.p, 0, 4ull * ((range + 31) / 32), c.s);
+        fill_dev(ctr.p, 0, 12, c.s);
+        const PubSlot ps = pub_reserve();
+        {
+          ProfScope pf(c, "k_union_first", 8.0 * scanned);
+          hipLaunchKernelGGL(k_union_first, dim3((unsigned)chunks), dim3(B), 0, c.s, ms, ulo[0], range, bits.p,
+                             res->data, ctr.p, ps.p, ps.seq);
+          DAS_HIP(hipGetLastError());
+        }
+        uint32_t n = 0;
+        pub_wait(ps, c.s, &n, 1);
+        if (n != 0xFFFFFFFFu) {
+          out.reset();
+          matched = n > 0;
+          if (matched) {
+            res->nrows = n;
+            res->lo[0] = ulo[0];
+            res->hi[0] = uhi[0];
+            res->sorted_col = -1;
+            out = std::move(res);
+          }
+          return 1;
+        }
+      }
+    }
     DBuf<uint32_t> cnt(chunks, c.s), off(chunks + 1, c.s);
     {
       ProfScope pf(c, "k_scan_count_multi", 4.0 * scanned * terms[0]->scan.arity);
@@ -3213,18 +3312,8 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
       DAS_HIP(hipGetLastError());
     }
     for (int k = 0; k < cat->ncols; ++k) {
-      cat->lo[k] = kNone;
-      cat->hi[k] = 0;
-    }
-    for (size_t i = 0; i < terms.size(); ++i) {
-      if (preps[i].empty) continue;
-      Table tb;
-      tb.ncols = preps[i].ncols;
-      scan_bounds(idx, preps[i].sp, terms[i]->scan.type_id, tb);
-      for (int k = 0; k < cat->ncols; ++k) {
-        cat->lo[k] = std::min(cat->lo[k], tb.lo[k]);
-        cat->hi[k] = std::max(cat->hi[k], tb.hi[k]);
-      }
+      cat->lo[k] = ulo[k];
+      cat->hi[k] = uhi[k];
     }
     out = dedup(c, *cat);
     matched = out->nrows > 0;

@@ -817,3 +817,25 @@ def test_gpu_ij_mid_matches_multi_launch(monkeypatch):
             monkeypatch.setenv("DAS_IJ_MID", "0")
             want = record(q, db)
             assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+@pytest.mark.parametrize("bits", ["1", "0"])
+def test_gpu_union_of_scans_matches_oracle(bits, monkeypatch):
+    """Or of anchored one-column scans above the fused chain's size (FlyBase
+    cell 9's DO-term Or over hot terms: thousands of rows, genes repeated
+    across terms): the one-launch bitmap union (k_union_first, unsorted) and
+    the count / write / hash-dedup path (DAS_UNION_BITS=0) against the oracle."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_UNION_BITS", bits)
+    arrays = synthetic.flybase_kb(3000, 5, 500, n_loc=10, n_do=4, seed=9)
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    E, V = (lambda *t: bench._L("Execution", *t)), bench._V
+    do = ["Node", "Schema", "Schema:disease_model_annotations_DO_term"]
+    qs = [["Or", [E(do, V("v1"), ["Node", "Verbatim", f"DOID:{d}"]) for d in ds]]
+          for ds in ((0, 1), (0, 1, 2, 3), (3, 2), (0, 0))]
+    qs.append(["Or", [E(do, V("v1"), ["Node", "Verbatim", "DOID:0"]), E(do, V("v1"), ["Node", "Verbatim", "nope"])]])
+    for q, want in zip(qs, _wants(("union_bits",), odb, qs)):
+        got = record(q, db)
+        assert same(got, want), (q, got.get("n"), want.get("n"))
