@@ -217,7 +217,24 @@ def make_kb(args, rank, world, db):
                            "+ scripts/benchmark.py QUERY_1-3 (Q3, Q5, Q6)",
                "genes_per_rank": int(len(rank_genes)), "bps": args.bps, "member_links_per_rank": args.members,
                "inheritance_links": args.inheritance}
-        return arrays, lambda i: bio_specs(rank_genes, anchor=i), cfg, "weak"
+        if world == 1:
+            return arrays, lambda i: bio_specs(rank_genes, anchor=i), cfg, "weak"
+
+        def specs(i):
+            # the same expressions on every rank (each is one collective plan):
+            # Q1 / Q2 / Q4 over every rank's Member links, and one instance of
+            # the anchored QUERY_1-3 per rank, on a gene pair of that rank's
+            # range (bio_shard: the same Member rows as the 1-GPU KB's genes, so
+            # each instance answers as at 1 GPU; gathered plans are evaluated
+            # by one rank each, round robin)
+            out = [q for q in bio_specs(np.arange(args.genes), anchor=i) if q[0][:2] in ("Q1", "Q2", "Q4")]
+            for r in range(world):
+                out += [(f"{name} @rank{r}", q)
+                        for name, q in bio_specs(np.arange(r * args.genes, (r + 1) * args.genes), anchor=i)
+                        if name[:2] in ("Q3", "Q5", "Q6")]
+            return out
+        cfg["anchored_instances"] = "QUERY_1-3 (Q3, Q5, Q6) once per rank per step, each on its rank's genes"
+        return arrays, specs, cfg, "weak"
     if args.workload == "flybase":
         arrays = synthetic.flybase_kb(args.fb_genes, args.fb_schema, args.fb_rows)
         # one gene anchor per step; each gene's DO terms (cell 9 builds its Or

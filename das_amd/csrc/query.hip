@@ -963,7 +963,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
                                                uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                                const uint32_t* __restrict__ coff, JoinCols jc,
-                                               uint32_t* __restrict__ out, uint64_t cap) {
+                                               uint32_t* __restrict__ out, uint64_t cap,
+                                               const uint32_t* __restrict__ cu) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -983,7 +984,9 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * CH;
     const uint64_t oe = ob + CH < total ? ob + CH : total;
-    uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
+    // last unit with unit_off[u] <= ob: precomputed per chunk (k_chunk_unit),
+    // else a 64-ary search over the unit offsets
+    uint64_t lo = cu ? cu[w] : 0, hi = cu ? lo + 1 : units;
     while (hi - lo > 1) {
       const uint64_t step = (hi - lo + 63) / 64;
       const uint64_t idx = lo + (uint64_t)lane * step;
@@ -1089,6 +1092,18 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       }
     }
     if (MODE == 0 && lane == 0) ccnt[w] = run;
+  }
+}
+
+// First unit of every CH-output chunk: the unit whose outputs
+// [unit_off[u], unit_off[u + 1]) hold the chunk's first output (one thread per
+// unit writes the chunks starting inside it).  Replaces each wave's 64-ary
+// search over the unit offsets -- three dependent loads per chunk.
+__global__ void k_chunk_unit(const uint64_t* __restrict__ unit_off, uint64_t units, uint64_t ch,
+                             uint32_t* __restrict__ cu) {
+  for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < units; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = unit_off[u], e = unit_off[u + 1];
+    for (uint64_t w = (b + ch - 1) / ch; w * ch < e; ++w) cu[w] = (uint32_t)u;
   }
 }
 
@@ -2355,8 +2370,12 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
 // (owner lane by a search over the lanes' prefixes), so waves land in
 // completion order -- the output is unsorted.  The last block to finish
 // publishes the total; outputs past the speculative capacity are not
-// written (the host then takes the multi-launch path).
-constexpr uint32_t kIjMid = 32768;
+// written (the host then takes the multi-launch path), nor are a wave's
+// outputs past kIjMidWave (a hub key's expansion by one wave would
+// serialise: ctr[2] is set and the total published as ~0, the host then
+// takes the output-balanced path).
+constexpr uint32_t kIjMid = 1u << 19;
+constexpr uint32_t kIjMidWave = 16384;
 
 __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, uint32_t n, IjKeys kx, IjGround g,
                                               JoinCols jc, uint32_t* __restrict__ out, uint64_t cap,
@@ -2367,10 +2386,13 @@ __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, 
   const uint32_t inc = wave_incl_sum_u32(e.y);
   const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
   const uint32_t pre = inc - e.y;
+  if (tot > kIjMidWave) {
+    if (lane == 0) atomicOr(&ctr[2], 1u);
+  }
   uint32_t base = 0;
-  if (lane == 0 && tot) base = atomicAdd(&ctr[0], tot);
+  if (lane == 0 && tot && tot <= kIjMidWave) base = atomicAdd(&ctr[0], tot);
   base = (uint32_t)__shfl(base, 0, 64);
-  if (tot && (uint64_t)base + tot <= cap) {
+  if (tot && tot <= kIjMidWave && (uint64_t)base + tot <= cap) {
     uint32_t pv[kMaxCols];
 #pragma unroll
     for (int i = 0; i < kMaxCols; ++i) pv[i] = i < jc.np && r < n ? jc.p[i][r] : 0u;
@@ -2398,7 +2420,7 @@ __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, 
     __threadfence();
     if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
       __threadfence();
-      publish_u32(slot, seq, atomicAdd(&ctr[0], 0u));
+      publish_u32(slot, seq, atomicAdd(&ctr[2], 0u) ? 0xFFFFFFFFu : atomicAdd(&ctr[0], 0u));
     }
   }
 }
@@ -2686,10 +2708,10 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
     if (!out && A.nrows > kIjSmall && A.nrows <= kIjMid) {
       const char* f = std::getenv("DAS_IJ_MID");                // A/B, tests: 0 never
       if (!(f && f[0] == '0')) {
-        // one launch when the output fits a speculative table of 2 rows per probe row
-        auto t = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), std::max<uint64_t>(65536, 2 * A.nrows));
-        DBuf<uint32_t> ctr(2, c.s);
-        fill_dev(ctr.p, 0, 8, c.s);
+        // one launch when the output fits a speculative table of 4 rows per probe row
+        auto t = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), std::max<uint64_t>(65536, 4 * A.nrows));
+        DBuf<uint32_t> ctr(3, c.s);
+        fill_dev(ctr.p, 0, 12, c.s);
         const PubSlot ps = pub_reserve();
         {
           ProfScope pf(c, "k_ij_mid", 16.0 * A.nrows + 4.0 * A.nrows * A.ncols);
@@ -2699,7 +2721,7 @@ std::unique_ptr<Table> index_join(Ctx& c, const Table& A, const das_link_scan_t&
         }
         uint32_t total = 0;
         pub_wait(ps, c.s, &total, 1);
-        if (total <= t->cap) {
+        if (total != 0xFFFFFFFFu && total <= t->cap) {
           t->nrows = total;
           out = std::move(t);
           unsorted = true;
@@ -3657,6 +3679,17 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   const std::string chs = "," + std::to_string(ch) + ">";
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
+  // each chunk's first unit (DAS_CHUNK_UNIT=0: every wave searches, A/B)
+  DBuf<uint32_t> cu;
+  {
+    const char* e = std::getenv("DAS_CHUNK_UNIT");
+    if (!(e && e[0] == '0') && units < 0xFFFFFFFFull) {
+      cu.alloc(fchunks, c.s);
+      KScope ks("k_chunk_unit", 8.0 * units + 4.0 * fchunks);
+      hipLaunchKernelGGL(k_chunk_unit, G(units), dim3(B), 0, c.s, (const uint64_t*)toff.p, units, (uint64_t)ch, cu.p);
+      DAS_HIP(hipGetLastError());
+    }
+  }
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
@@ -3664,7 +3697,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_0(CHV)                                                                                                \
   hipLaunchKernelGGL((k_dj_filt<0, -1, -1, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows,   \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
-                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull)
+                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, (const uint32_t*)cu.p)
     if (ch == 2048) FILT_0(2048);
     else if (ch == 4096) FILT_0(4096);
     else FILT_0(1024);
@@ -3684,7 +3717,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_W(NPV, NBV, CHV)                                                                                  \
   hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,      \
-                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap)
+                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap, (const uint32_t*)cu.p)
 #define FILT_WC(CHV)                                    \
   if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1, CHV);      \
   else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1, CHV); \

@@ -32,6 +32,8 @@ import numpy as np
 from .database.db_interface import UNORDERED_LINK_TYPES, WILDCARD
 from .database.hip_db import RelationalDB
 
+L_MAXCOLS = 16                              # columns of a binding table (das_internal.h kMaxCols)
+
 ORDERED, UNORDERED, COMPOSITE = 0, 1, 2
 
 
@@ -108,6 +110,10 @@ class ShardedDB(RelationalDB):
                            "native_fallback": 0, "collectives": 0}
         # DAS_JOIN_PLACEMENT=exchange|broadcast forces one placement (tests)
         self.force = os.environ.get("DAS_JOIN_PLACEMENT", "")
+        # the top-level expression of the current ShardedMatcher call, and the
+        # round-robin owner of the next wholly gathered top-level plan
+        self._top = None
+        self._gather_seq = 0
         # a key bucket is heavy when its rows (both sides) exceed this fraction
         # of one rank's fair share of the join's rows (DAS_HEAVY_FRAC, tests)
         self.heavy_frac = float(os.environ.get("DAS_HEAVY_FRAC", "1.0"))
@@ -365,6 +371,12 @@ class ShardedDB(RelationalDB):
             words[i, 0] = L.PLAN_INPUT
             words[i, 2] = slot
         words = words.reshape(-1)
+        if not local and expr is self._top and self.world > 1 and os.environ.get("DAS_GATHERED_OWNER") != "0":
+            # a wholly gathered top-level expression is evaluated by ONE shard
+            # (round robin over such plans, the same on every shard): the
+            # others skip the native call and take the answer's size, flags
+            # and table schemas from one all-reduce (collective 3)
+            return self._owner_plan(ctx, words, n, inputs, no_overload, answer)
         matched, negation, out, checks = ctx.plan_execute_sharded(words, n, inputs, no_overload)
         del inputs, tables
         if not local:
@@ -404,6 +416,57 @@ class ShardedDB(RelationalDB):
         answer._set(self, rel)
         answer.negation = negation
         return matched
+
+    OWNER_TABLES = 16                       # answer tables an owner-evaluated plan describes
+
+    def _owner_plan(self, ctx, words, n, inputs, no_overload, answer):
+        from . import _lib as L
+        """A wholly gathered top-level plan (every leaf's rows all-gathered,
+        the same on every shard) evaluated by one owner shard only: shards
+        take turns (round robin over such plans), so N independent gathered
+        queries -- bench.py's per-rank QUERY_1-3 instances -- run on N GPUs at
+        once instead of each on all of them.  The owner keeps the answer; one
+        all-reduce hands every shard its size, matched / negation and the
+        answer tables' schemas (kind, variables, composite members), so the
+        others hold empty tables of the same schemas (later collectives over
+        the relation pair tables up by position)."""
+        owner = self._gather_seq % self.world
+        self._gather_seq += 1
+        K, W = self.OWNER_TABLES, 2 + 2 * L_MAXCOLS
+        vec = np.zeros(4 + K * W, dtype=np.int64)
+        out = []
+        matched = negation = False
+        if self.rank == owner:
+            matched, negation, out, _ = ctx.plan_execute_sharded(words, n, inputs, no_overload)
+            vec[0] = sum(t.nrows for t in out)
+            vec[1], vec[2], vec[3] = int(matched), int(negation), len(out)
+            for i, t in enumerate(out[:K]):
+                v = vec[4 + i * W:4 + (i + 1) * W]
+                v[0], v[1] = int(t.kind), len(t.vars)
+                v[2:2 + len(t.vars)] = [int(x) + 1 for x in t.vars]          # +1: 0 = unused
+                mem = list(t.members) if t.members is not None else []
+                v[2 + L_MAXCOLS:2 + L_MAXCOLS + len(mem)] = [int(x) + 2 for x in mem]
+        got = self._allreduce_sum(vec)                                           # collective 3
+        nt = int(got[3])
+        if self.rank != owner:
+            if nt > K:
+                # more schemas than the vector describes: evaluate here too
+                # for the schemas (same inputs, same answer), keep no rows
+                _, _, res, _ = ctx.plan_execute_sharded(words, n, inputs, no_overload)
+                out = [self.local.empty_table(t.kind, list(t.vars), t.members) for t in res]
+                del res
+            for i in range(nt if nt <= K else 0):
+                v = got[4 + i * W:4 + (i + 1) * W]
+                kind, nv = int(v[0]), int(v[1])
+                vars_ = [int(x) - 1 for x in v[2:2 + nv]]
+                mem = [int(x) - 2 for x in v[2 + L_MAXCOLS:2 + L_MAXCOLS + nv]] if kind == L.TABLE_COMPOSITE else None
+                out.append(self.local.empty_table(kind, vars_, mem))
+        rel = DRel(out)
+        rel._global = int(got[0])
+        self.plan_stats["native"] += 1
+        answer._set(self, rel)
+        answer.negation = bool(got[2])
+        return bool(got[1])
 
     def _placement_var(self, db, words):
         """The variable that places this Link term's rows (partition_spec:
@@ -792,7 +855,11 @@ class ShardedMatcher:
     def count(self, expr):
         from .pattern_matcher.pattern_matcher import PatternMatchingAnswer
         ans = PatternMatchingAnswer()
-        expr.matched(self.sdb, ans)
+        self.sdb._top = expr
+        try:
+            expr.matched(self.sdb, ans)
+        finally:
+            self.sdb._top = None
         return self.sdb.rel_local_count(ans._relation()) if ans._rel is not None else 0
 
 
@@ -839,18 +906,26 @@ def bio_shard(n_genes, n_bps, n_members, n_inh, rank, world, seed=20250209):
     r*n_genes.., placed by gene: partition_spec {"Member": 0}); Inheritance
     and the annotation layouts (Uniprot / Reactome Member, List, Evaluation,
     Context) are the same on every rank and indexed by their handle's owner.
+    Every rank's Member block is drawn from the same random stream as
+    bio_full_kb's (shifted by r*n_genes), so at world 1 the KB IS
+    bio_full_kb(n_genes, n_bps, n_members, n_inh) and rank r's genes answer
+    the anchored queries exactly as the 1-GPU KB's genes do (bench.py's
+    per-rank QUERY_1-3 instances: equal work per rank).
     Returns (AtomArrays for this rank, this rank's gene ids)."""
     from . import synthetic
     total_genes = n_genes * world
     nodes, off = synthetic.bio_nodes(total_genes, n_bps)
     blocks = []
+    rest_rng = None
     for r in range(world):
-        rng = np.random.default_rng(seed + 1000 * (r + 1))
+        rng = np.random.default_rng(seed)
         genes = r * n_genes + rng.integers(0, n_genes, n_members)
         bps = synthetic.zipf_indices(rng, n_bps, n_members)
+        if rest_rng is None:
+            rest_rng = rng                    # bio_full_kb's stream continues with Inheritance
         blocks.append(("Member", np.stack([off["g"] + genes, off["bp"] + bps], 1),
                        np.full(n_members, 1 if r == rank or world == 1 else 3, np.uint8)))
-    rng = np.random.default_rng(seed)
+    rng = rest_rng
     child = rng.integers(1, n_bps, n_inh)
     parent = (rng.random(n_inh) * child).astype(np.int64)
     BY_HANDLE = 4                        # placeholder kind: owner decided from the handle below

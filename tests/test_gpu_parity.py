@@ -271,7 +271,7 @@ def _sharded_kb(kind):
     from das_amd import synthetic
     from tests.golden import make_synthetic as MS
     from tests.test_parallel_gloo import _fly_queries, _hub_queries, _queries
-    if kind in ("default", "heavy", "small"):
+    if kind in ("default", "heavy", "small", "default_owner"):
         return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
     if kind in ("hub", "hub_small"):
         return MS.make_arrays("hub"), _hub_queries()
@@ -309,11 +309,15 @@ def _sharded_worker(rank, world, port, out_path, mode):
     for q in queries:
         ans = pm.PatternMatchingAnswer()
         st0 = dict(sdb.plan_stats)
+        e = build(q)
+        if mode.endswith("_owner"):
+            sdb._top = e                      # as ShardedMatcher.count: gathered plans evaluated by one owner
         try:
-            m = build(q).matched(sdb, ans)
+            m = e.matched(sdb, ans)
         except AttributeError as e:
             res.append({"error": type(e).__name__})
             continue
+        sdb._top = None
         st1 = dict(sdb.plan_stats)
         n = ans.count()
         rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
@@ -327,7 +331,8 @@ def _sharded_worker(rank, world, port, out_path, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "flybase"])
+@pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "flybase", "flybase_owner",
+                                  "default_owner"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
     """The multi-GPU path with two ranks sharing cuda:0 over gloo, against the
     single-process oracle: handle-sharded builds (each link indexed on exactly
@@ -373,9 +378,13 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
             got = per_rank[r][qi]
             assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
             assert got["rows"] == want_rows, q
-        if mode == "flybase":
+        if mode.startswith("flybase"):
             got = per_rank[0][qi]
             assert got["native"] == 1 and got["collectives"] <= 3, (q, got["native"], got["collectives"])
+    if mode.endswith("_owner"):
+        # wholly gathered top-level plans were evaluated by one rank each, in turn
+        owners = [[r for r in range(2) if per_rank[r][qi].get("local")] for qi in range(len(queries))]
+        assert any(o == [1] for o in owners) and any(o == [0] for o in owners), owners
 
 
 def _composite_queries(rng, arrays, n):
@@ -809,6 +818,10 @@ def test_gpu_ij_mid_matches_multi_launch(monkeypatch):
         qs += [q for name, q in bench.flybase_specs(gene, synthetic.flybase_do_terms(arrays, gene))
                if name[:2] in ("F5", "F6", "F7")]
     cases.append((arrays, qs))
+    # hub keys: a wave owning more than kIjMidWave outputs, or more outputs
+    # than the speculative table, sends the join down the balanced path
+    arrays = synthetic.powerlaw_kb(3000, 300000, link_types=4, seed=21)
+    cases.append((arrays, [q for _, q in bench.hub_specs()]))
     for arrays, qs in cases:
         db = _hipdb(arrays)
         for q in qs:

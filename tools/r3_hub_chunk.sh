@@ -8,3 +8,5 @@ for ch in 1024 2048 4096; do
     DAS_FILT_CHUNK=$ch timeout -k 10 200 python bench.py --workload hub $NB > gpurun_out/s3/hub_ch$ch.json \
         2> gpurun_out/s3/hub_ch$ch.err || exit 14
 done
+DAS_CHUNK_UNIT=0 timeout -k 10 200 python bench.py --workload hub $NB > gpurun_out/s3/hub_cu0.json \
+    2> gpurun_out/s3/hub_cu0.err || exit 15
