@@ -204,7 +204,9 @@ struct Exec {
           Res s = eval(j);
           if (!s.matched) return Res{};
           const int32_t o = nd[j].op;
-          if (o == DAS_PLAN_TEMPLATE || o == DAS_PLAN_TVM || o == DAS_PLAN_LINK) last = std::move(s.rel);
+          // (sharded: a gathered template / Link leaf arrives as an INPUT leaf)
+          if (o == DAS_PLAN_TEMPLATE || o == DAS_PLAN_TVM || o == DAS_PLAN_LINK || o == DAS_PLAN_INPUT)
+            last = std::move(s.rel);
           j = next(j);
         }
         r.rel = std::move(last);

@@ -957,14 +957,13 @@ struct FiltKey {
 
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
-template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk>
+template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk, int XU = kXUnroll>
 __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
                                                uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                                const uint32_t* __restrict__ coff, JoinCols jc,
-                                               uint32_t* __restrict__ out, uint64_t cap,
-                                               const uint32_t* __restrict__ cu) {
+                                               uint32_t* __restrict__ out, uint64_t cap) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -984,9 +983,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * CH;
     const uint64_t oe = ob + CH < total ? ob + CH : total;
-    // last unit with unit_off[u] <= ob: precomputed per chunk (k_chunk_unit),
-    // else a 64-ary search over the unit offsets
-    uint64_t lo = cu ? cu[w] : 0, hi = cu ? lo + 1 : units;
+    uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
     while (hi - lo > 1) {
       const uint64_t step = (hi - lo + 63) / 64;
       const uint64_t idx = lo + (uint64_t)lane * step;
@@ -1026,13 +1023,13 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
           for (int i = 0; i < 4; ++i)
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
         }
-        // kXUnroll rounds of 64 outputs resolved before their loads issue
-        for (uint32_t o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
-          const int nr = (re - o0) >= 64u * kXUnroll ? kXUnroll : (int)((re - o0 + 63) / 64);
-          uint32_t o[kXUnroll], br[kXUnroll];
-          int ll[kXUnroll];
+        // XU rounds of 64 outputs resolved before their loads issue
+        for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
+          const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
+          uint32_t o[XU], br[XU];
+          int ll[XU];
 #pragma unroll
-          for (int q = 0; q < kXUnroll; ++q) {
+          for (int q = 0; q < XU; ++q) {
             o[q] = o0 + (uint32_t)(q * 64 + lane);
             ll[q] = 0;
             br[q] = 0;
@@ -1047,30 +1044,30 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
           }
           if (MODE == 0) {
-            uint32_t v[kXUnroll];
+            uint32_t v[XU];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
-            uint32_t wd[kXUnroll];
+            for (int q = 0; q < XU; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+            uint32_t wd[XU];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+            for (int q = 0; q < XU; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) {
+            for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
               const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
               if (o[q] < re) fl[gb + o[q]] = f ? 1 : 0;
               run += (uint32_t)__popcll(__ballot(f));
             }
           } else {
-            bool f[kXUnroll];
+            bool f[XU];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
-            uint32_t bv[kXUnroll][4];
+            for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
+            uint32_t bv[XU][4];
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q)
+            for (int q = 0; q < XU; ++q)
 #pragma unroll
               for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
 #pragma unroll
-            for (int q = 0; q < kXUnroll; ++q) {
+            for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
               const uint64_t m = __ballot(f[q]);
               const uint64_t pos = (uint64_t)obase + run + __popcll(m & lt);
@@ -1092,18 +1089,6 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       }
     }
     if (MODE == 0 && lane == 0) ccnt[w] = run;
-  }
-}
-
-// First unit of every CH-output chunk: the unit whose outputs
-// [unit_off[u], unit_off[u + 1]) hold the chunk's first output (one thread per
-// unit writes the chunks starting inside it).  Replaces each wave's 64-ary
-// search over the unit offsets -- three dependent loads per chunk.
-__global__ void k_chunk_unit(const uint64_t* __restrict__ unit_off, uint64_t units, uint64_t ch,
-                             uint32_t* __restrict__ cu) {
-  for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < units; u += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t b = unit_off[u], e = unit_off[u + 1];
-    for (uint64_t w = (b + ch - 1) / ch; w * ch < e; ++w) cu[w] = (uint32_t)u;
   }
 }
 
@@ -2374,8 +2359,8 @@ __global__ void __launch_bounds__(kSmallBlock) k_ij_small(const uint32_t* __rest
 // outputs past kIjMidWave (a hub key's expansion by one wave would
 // serialise: ctr[2] is set and the total published as ~0, the host then
 // takes the output-balanced path).
-constexpr uint32_t kIjMid = 1u << 19;
-constexpr uint32_t kIjMidWave = 16384;
+constexpr uint32_t kIjMid = 32768;
+constexpr uint32_t kIjMidWave = 4096;
 
 __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, uint32_t n, IjKeys kx, IjGround g,
                                               JoinCols jc, uint32_t* __restrict__ out, uint64_t cap,
@@ -2389,9 +2374,20 @@ __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, 
   if (tot > kIjMidWave) {
     if (lane == 0) atomicOr(&ctr[2], 1u);
   }
-  uint32_t base = 0;
-  if (lane == 0 && tot && tot <= kIjMidWave) base = atomicAdd(&ctr[0], tot);
-  base = (uint32_t)__shfl(base, 0, 64);
+  // one reservation per block (same-address atomics serialise): the block's
+  // waves take consecutive slices in wave order
+  __shared__ uint32_t s_tot[B / 64], s_base;
+  const int wv = threadIdx.x >> 6;
+  if (lane == 0) s_tot[wv] = tot <= kIjMidWave ? tot : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t all = 0;
+    for (int w = 0; w < B / 64; ++w) all += s_tot[w];
+    s_base = all ? atomicAdd(&ctr[0], all) : 0u;
+  }
+  __syncthreads();
+  uint32_t base = s_base;
+  for (int w = 0; w < wv; ++w) base += s_tot[w];
   if (tot && tot <= kIjMidWave && (uint64_t)base + tot <= cap) {
     uint32_t pv[kMaxCols];
 #pragma unroll
@@ -3676,30 +3672,40 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   }();
   const uint64_t fchunks = (total + ch - 1) / ch;
   const unsigned fgrid2 = grid_for(fchunks, B / 64, 65535u * 4u);
-  const std::string chs = "," + std::to_string(ch) + ">";
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
-  // each chunk's first unit (DAS_CHUNK_UNIT=0: every wave searches, A/B)
-  DBuf<uint32_t> cu;
-  {
-    const char* e = std::getenv("DAS_CHUNK_UNIT");
-    if (!(e && e[0] == '0') && units < 0xFFFFFFFFull) {
-      cu.alloc(fchunks, c.s);
-      KScope ks("k_chunk_unit", 8.0 * units + 4.0 * fchunks);
-      hipLaunchKernelGGL(k_chunk_unit, G(units), dim3(B), 0, c.s, (const uint64_t*)toff.p, units, (uint64_t)ch, cu.p);
-      DAS_HIP(hipGetLastError());
-    }
-  }
   {
     // per probe row its row id and (first, count); per output its build
     // value (a P row) and its flag byte
-    ProfScope ps(c, "k_dj_filt<0,-1,-1" + chs, 12.0 * A.nrows + 5.0 * total);
+    // (xu: see DAS_FILT_UNROLL below; the scope names rocprof's instantiation)
+    static const int xu0 = [] {
+      const char* e = std::getenv("DAS_FILT_UNROLL");
+      const int v = e ? std::atoi(e) : 0;
+      return v == 8 || v == 16 ? v : 4;
+    }();
+    ProfScope ps(c, "k_dj_filt<0,-1,-1," + std::to_string(ch) + "," + std::to_string(ch == 1024 ? xu0 : 4) + ">",
+                 12.0 * A.nrows + 5.0 * total);
 #define FILT_0(CHV)                                                                                                \
   hipLaunchKernelGGL((k_dj_filt<0, -1, -1, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows,   \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
-                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, (const uint32_t*)cu.p)
+                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull)
+    // DAS_FILT_UNROLL (8 / 16): rounds of 64 outputs whose build values and
+    // bitmap words are loaded together in the flag pass (A/B; default 4)
+    static const int xu = [] {
+      const char* e = std::getenv("DAS_FILT_UNROLL");
+      const int v = e ? std::atoi(e) : 0;
+      return v == 8 || v == 16 ? v : 4;
+    }();
     if (ch == 2048) FILT_0(2048);
     else if (ch == 4096) FILT_0(4096);
+    else if (xu == 8)
+      hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 8>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
+                         A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
+    else if (xu == 16)
+      hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 16>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
+                         A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
     else FILT_0(1024);
 #undef FILT_0
     DAS_HIP(hipGetLastError());
@@ -3711,13 +3717,14 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     // + the probe columns, the flags, the kept outputs' build rows and their columns out
     // (named as rocprof names the instantiation launched below)
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-    ProfScope ps(c, spec ? "k_dj_filt<1," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + chs
-                         : "k_dj_filt<1,-1,-1" + chs,
+    const std::string chs4 = "," + std::to_string(ch) + ",4>";
+    ProfScope ps(c, spec ? "k_dj_filt<1," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + chs4
+                         : "k_dj_filt<1,-1,-1" + chs4,
                  (12.0 + 4.0 * jc.np) * A.nrows + 1.0 * total + 4.0 * jc.nb * m + 4.0 * nu * m);
 #define FILT_W(NPV, NBV, CHV)                                                                                  \
   hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,      \
-                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap, (const uint32_t*)cu.p)
+                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap)
 #define FILT_WC(CHV)                                    \
   if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1, CHV);      \
   else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1, CHV); \

@@ -275,6 +275,14 @@ def _sharded_kb(kind):
         return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
     if kind in ("hub", "hub_small"):
         return MS.make_arrays("hub"), _hub_queries()
+    if kind.startswith("bio_full"):
+        # scripts/benchmark.py QUERY_1-3 (LinkTemplate leaves, template-target
+        # Links, the nested Context link, the unconstrained last term's cross join)
+        arrays = MS.make_arrays("bio_full")
+        qs = []
+        for genes in (["g3", "g5"], ["g1", "g2"]):
+            qs += MS.benchmark_queries(genes)
+        return arrays, qs
     return MS.make_arrays("flybase"), _fly_queries()
 
 
@@ -332,7 +340,7 @@ def _sharded_worker(rank, world, port, out_path, mode):
 
 
 @pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "flybase", "flybase_owner",
-                                  "default_owner"])
+                                  "default_owner", "bio_full", "bio_full_owner"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
     """The multi-GPU path with two ranks sharing cuda:0 over gloo, against the
     single-process oracle: handle-sharded builds (each link indexed on exactly

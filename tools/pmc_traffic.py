@@ -36,12 +36,13 @@ def short(name):
 
 
 # kernels whose reads are dominated by isolated random loads (x1)
-RANDOM = {"k_tile_count<BitsPred>", "k_dj_filt<0,-1,-1,1024>", "k_dj_filt<0,-1,-1,2048>", "k_dj_filt<0,-1,-1,4096>", "k_ij_mid", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
+RANDOM = {"k_tile_count<BitsPred>", "k_ij_mid", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
           "k_hset_first", "k_hset_anti", "k_lookup", "k_lookup_pub"}
 
 
 def fetch_factor(kernel):
-    return 1.0 if kernel in RANDOM else 2.0
+    # the filtered expansion's flag pass: one random bitmap probe per output
+    return 1.0 if kernel in RANDOM or kernel.startswith("k_dj_filt<0,") else 2.0
 
 
 def _last_counts():
