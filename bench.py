@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-materialise", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="no per-query timings and no join-probe variants after the timed steps (profiling runs: "
+                         "the timed steps' launches are then the process's last ones)")
     ap.add_argument("--materialise-cap", type=int, default=2_000_000,
                     help="largest answer whose Python objects the materialisation-inclusive figure builds")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
@@ -407,7 +410,7 @@ def roofline_of(stats, workload="bio", name=None):
             traffic = json.load(f).get(name, {}).get("bytes_per_launch")
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
-            "avg_launch_us": round(st["ms"] * 1e3 / max(st["launches"], 1), 2),
+            "avg_launch_us": round(st["ms"] * 1e3 / max(st["launches"], 1), 2), "launches": st["launches"],
             "algorithmic_bytes_per_launch": st["bytes"] / max(st["launches"], 1)}
 
 
@@ -779,7 +782,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         per_query = dict(zip(per_query, (int(x) for x in _sync_sum(dist, list(per_query.values()), stage))))
     # per-query wall time (the warm query set of the first timed step, 5 runs each)
     per_query_ms = {}
-    for name, q in qsets[args.warmup]:
+    for name, q in ([] if args.no_extras else qsets[args.warmup]):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
@@ -818,7 +821,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
     variants = None
     join_k = "k_dj_write<2,1,u32,1>"
-    if workload == "bio" and world == 1 and join_k in warm_stats:
+    if workload == "bio" and world == 1 and join_k in warm_stats and not args.no_extras:
         # the And join with the probe read straight from the index (scan
         # views for every size): HBM-cold, and with the count pass warming the
         # probe's payload columns -- beside the default (large probes copied

@@ -7,8 +7,9 @@
 #   3. HBM traffic PMC passes, FETCH_SIZE and WRITE_SIZE in separate runs
 #      (MI355X_MICROARCH.md "HBM": one TCC counter group per pass)
 #   4. tools/pmc_traffic.py -> per-kernel bytes per launch (gfx950 FETCH_SIZE
-#      correction), tools/roofline_check.py -> the bench's roofline recomputed
-#      from the rocprof CSV
+#      correction), tools/roofline_check.py -> the roofline of the bench line
+#      printed UNDER rocprof (same process, --no-extras: the timed steps are
+#      the last launches) recomputed from the rocprof trace of those launches
 # WORKLOAD selects bench.py --workload (default bio); BENCH_ARGS adds flags;
 # TAG names the outputs gpurun_out/<TAG>_<workload>*.  Copy what is worth
 # keeping into profiles/ afterwards.
@@ -19,7 +20,7 @@ D=gpurun_out/prof_${T}_$W
 mkdir -p $D
 export TMPDIR=/tmp
 ARGS="--workload $W --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-}"
-PARGS="$ARGS --no-cpu-baseline --no-materialise"
+PARGS="$ARGS --no-cpu-baseline --no-materialise --no-extras"
 timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
 timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS > $D/kt.log 2>&1 &&
 cp "$(find $D/kt -name 'run_kernel_stats.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_stats.csv &&
@@ -28,5 +29,6 @@ timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/f
 timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $PARGS > $D/write.log 2>&1 &&
 if [ "$W" = build ]; then export LAST_FROM=gpurun_out/${T}_bench_$W.json; fi &&
 python tools/pmc_traffic.py $D/fetch $D/write > gpurun_out/${T}_pmc_traffic_$W.json &&
-python tools/roofline_check.py gpurun_out/${T}_bench_$W.json gpurun_out/${T}_${W}_kernel_stats.csv \
-    gpurun_out/${T}_pmc_traffic_$W.json > gpurun_out/${T}_roofline_check_$W.json
+cp $D/kt.log gpurun_out/${T}_bench_${W}_under_rocprof.log &&
+python tools/roofline_check.py $D/kt.log gpurun_out/${T}_${W}_kernel_stats.csv \
+    gpurun_out/${T}_pmc_traffic_$W.json gpurun_out/${T}_${W}_kernel_trace.csv > gpurun_out/${T}_roofline_check_$W.json

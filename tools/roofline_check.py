@@ -40,7 +40,11 @@ def main():
     if len(sys.argv) > 4:
         trace = sys.argv[4]
     k_bench = bench.get("kernels", {}).get(name, {}).get("launches")
-    if bench.get("unit") == "links/s" and k_bench:
+    if bench.get("unit") != "links/s" and rf.get("launches"):
+        # query workloads profiled with --no-extras: the timed steps' launches
+        # of the kernel are the process's last `launches` dispatches of it
+        k_bench = rf["launches"]
+    if k_bench:
         try:
             with open(trace) as f:
                 d = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -48,7 +52,7 @@ def main():
             last = [x[1] for x in d[-k_bench:]]
             if last:
                 calls, tot = len(last), float(sum(last))
-                out["rocprof_launches"] = f"last {calls} dispatches (the timed build) of {len(d)} in {trace}"
+                out["rocprof_launches"] = f"last {calls} dispatches (the timed region) of {len(d)} in {trace}"
         except OSError:
             pass
     if calls:
