@@ -957,19 +957,13 @@ struct FiltKey {
 
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
-// MODE 2 (DAS_FILT_ONEPASS=1): both passes in one launch -- a wave counts its
-// chunk's kept outputs (phase 0), reserves them with one atomic on *kept and
-// walks the chunk again (phase 1, the chunk's P rows and bitmap words now
-// cache-resident), retesting each output and writing the kept ones; chunks
-// land in completion order (unsorted), no flag bytes go through HBM.
 template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk, int XU = kXUnroll>
 __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
                                                uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                                const uint32_t* __restrict__ coff, JoinCols jc,
-                                               uint32_t* __restrict__ out, uint64_t cap,
-                                               unsigned long long* __restrict__ kept = nullptr) {
+                                               uint32_t* __restrict__ out, uint64_t cap) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -983,8 +977,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   for (int i = 0; i < 4; ++i) {
     pp[i] = i < ncp ? jc.p[i] : nullptr;
     bp[i] = i < ncb ? jc.b[i] : nullptr;
-    po[i] = i < ncp && MODE >= 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
-    bo[i] = i < ncb && MODE >= 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+    po[i] = i < ncp && MODE == 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
+    bo[i] = i < ncb && MODE == 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * CH;
@@ -999,117 +993,102 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       hi = nlo + step < hi ? nlo + step : hi;
       lo = nlo;
     }
-    uint64_t obase = MODE == 1 ? coff[w] : 0u;
-    // phase 0: test and count (MODE 0 also stores flags); phase 1: write
-    for (int ph = MODE == 2 ? 0 : MODE; ph <= (MODE == 2 ? 1 : MODE); ++ph) {
-      uint32_t run = 0;                                // kept outputs of this chunk so far
-      for (uint64_t u = lo; u < units; ++u) {
-        uint64_t base = unit_off[u];
-        if (base >= oe) break;
-        const uint64_t r0 = u * kXRows;
-        uint2 e[kXGroups];
+    uint32_t run = 0;                                  // kept outputs of this chunk so far
+    const uint32_t obase = MODE == 1 ? coff[w] : 0u;
+    for (uint64_t u = lo; u < units; ++u) {
+      uint64_t base = unit_off[u];
+      if (base >= oe) break;
+      const uint64_t r0 = u * kXRows;
+      uint2 e[kXGroups];
 #pragma unroll
-        for (int g = 0; g < kXGroups; ++g) {
-          const uint64_t r = r0 + g * 64 + lane;
-          const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
-          e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+      for (int g = 0; g < kXGroups; ++g) {
+        const uint64_t r = r0 + g * 64 + lane;
+        const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+        e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int g = 0; g < kXGroups; ++g) {
+        const uint32_t c = e[g].y;
+        const uint32_t inc = wave_inclusive_scan(c);
+        const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+        const uint32_t pre = inc - c;
+        const uint64_t gb = base, ge = base + tot;
+        base = ge;
+        if (ge <= ob || gb >= oe) continue;
+        const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
+        const uint64_t r = r0 + g * 64 + lane;
+        uint32_t pv[4] = {0u, 0u, 0u, 0u};
+        if (MODE == 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
         }
+        // XU rounds of 64 outputs resolved before their loads issue
+        for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
+          const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
+          uint32_t o[XU], br[XU];
+          int ll[XU];
 #pragma unroll
-        for (int g = 0; g < kXGroups; ++g) {
-          const uint32_t c = e[g].y;
-          const uint32_t inc = wave_inclusive_scan(c);
-          const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
-          const uint32_t pre = inc - c;
-          const uint64_t gb = base, ge = base + tot;
-          base = ge;
-          if (ge <= ob || gb >= oe) continue;
-          const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
-          const uint64_t r = r0 + g * 64 + lane;
-          uint32_t pv[4] = {0u, 0u, 0u, 0u};
-          if (ph == 1) {
+          for (int q = 0; q < XU; ++q) {
+            o[q] = o0 + (uint32_t)(q * 64 + lane);
+            ll[q] = 0;
+            br[q] = 0;
+            if (q >= nr) continue;
+            int l = 0;                                 // owner: max lane with pre <= o
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
+            for (int st = 32; st >= 1; st >>= 1) {
+              const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
+              if (l + st < 64 && pl <= o[q]) l += st;
+            }
+            ll[q] = l;
+            br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
           }
-          // XU rounds of 64 outputs resolved before their loads issue
-          for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
-            const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
-            uint32_t o[XU], br[XU];
-            int ll[XU];
+          if (MODE == 0) {
+            uint32_t v[XU];
+#pragma unroll
+            for (int q = 0; q < XU; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+            uint32_t wd[XU];
+#pragma unroll
+            for (int q = 0; q < XU; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
 #pragma unroll
             for (int q = 0; q < XU; ++q) {
-              o[q] = o0 + (uint32_t)(q * 64 + lane);
-              ll[q] = 0;
-              br[q] = 0;
               if (q >= nr) continue;
-              int l = 0;                               // owner: max lane with pre <= o
-#pragma unroll
-              for (int st = 32; st >= 1; st >>= 1) {
-                const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
-                if (l + st < 64 && pl <= o[q]) l += st;
-              }
-              ll[q] = l;
-              br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+              const bool f = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
+              if (o[q] < re) fl[gb + o[q]] = f ? 1 : 0;
+              run += (uint32_t)__popcll(__ballot(f));
             }
+          } else {
             bool f[XU];
-            if (ph == 0 || MODE == 2) {
-              uint32_t v[XU];
 #pragma unroll
-              for (int q = 0; q < XU; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
-              uint32_t wd[XU];
+            for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
+            uint32_t bv[XU][4];
 #pragma unroll
-              for (int q = 0; q < XU; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+            for (int q = 0; q < XU; ++q)
 #pragma unroll
-              for (int q = 0; q < XU; ++q) f[q] = q < nr && v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
-            } else {
+              for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
 #pragma unroll
-              for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
-            }
-            if (ph == 0) {
+            for (int q = 0; q < XU; ++q) {
+              if (q >= nr) continue;
+              const uint64_t m = __ballot(f[q]);
+              const uint64_t pos = (uint64_t)obase + run + __popcll(m & lt);
+              run += (uint32_t)__popcll(m);
 #pragma unroll
-              for (int q = 0; q < XU; ++q) {
-                if (q >= nr) continue;
-                if (MODE == 0 && o[q] < re) fl[gb + o[q]] = f[q] ? 1 : 0;
-                run += (uint32_t)__popcll(__ballot(f[q]));
+              for (int i = 0; i < 4; ++i) {
+                if (i >= ncp) break;
+                const uint32_t x = lane_get(pv[i], ll[q]);
+                if (f[q]) po[i][pos] = x;
               }
-            } else {
-              uint32_t bv[XU][4];
+              if (f[q]) {
 #pragma unroll
-              for (int q = 0; q < XU; ++q)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
-#pragma unroll
-              for (int q = 0; q < XU; ++q) {
-                if (q >= nr) continue;
-                const uint64_t m = __ballot(f[q]);
-                const uint64_t pos = obase + run + __popcll(m & lt);
-                run += (uint32_t)__popcll(m);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  if (i >= ncp) break;
-                  const uint32_t x = lane_get(pv[i], ll[q]);
-                  if (f[q]) po[i][pos] = x;
-                }
-                if (f[q]) {
-#pragma unroll
-                  for (int i = 0; i < 4; ++i)
-                    if (i < ncb) bo[i][pos] = bv[q][i];
-                }
+                for (int i = 0; i < 4; ++i)
+                  if (i < ncb) bo[i][pos] = bv[q][i];
               }
             }
           }
-        }
-      }
-      if (ph == 0) {
-        if (MODE == 0 && lane == 0) ccnt[w] = run;
-        if (MODE == 2) {
-          unsigned long long b0 = 0;
-          if (lane == 0 && run) b0 = atomicAdd(kept, (unsigned long long)run);
-          obase = (uint64_t)__shfl((long long)b0, 0, 64);
-          if (!run) break;                             // nothing kept: no write phase
         }
       }
     }
+    if (MODE == 0 && lane == 0) ccnt[w] = run;
   }
 }
 
@@ -3693,43 +3672,6 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   }();
   const uint64_t fchunks = (total + ch - 1) / ch;
   const unsigned fgrid2 = grid_for(fchunks, B / 64, 65535u * 4u);
-  {
-    // DAS_FILT_ONEPASS=1: count and write in one launch (MODE 2), unsorted
-    const char* e1 = std::getenv("DAS_FILT_ONEPASS");
-    if (e1 && e1[0] == '1' && (uint64_t)nu * total * 4 <= (16ull << 30) && ch == 1024) {
-      auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
-      DBuf<unsigned long long> kept(1, c.s);
-      fill_dev(kept.p, 0, 8, c.s);
-      const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-      {
-        ProfScope ps(c, spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
-                             : std::string("k_dj_filt<2,-1,-1,1024,4>"),
-                     (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
-#define FILT_1P(NPV, NBV)                                                                                       \
-  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
-                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
-                     (uint8_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, jc, out->data, out->cap, kept.p)
-        if (jc.np == 1 && jc.nb == 1) FILT_1P(1, 1);
-        else if (jc.np == 2 && jc.nb == 1) FILT_1P(2, 1);
-        else if (jc.np == 1 && jc.nb == 2) FILT_1P(1, 2);
-        else FILT_1P(-1, -1);
-#undef FILT_1P
-        DAS_HIP(hipGetLastError());
-      }
-      out->nrows = read_u64(reinterpret_cast<const uint64_t*>(kept.p), c.s);
-      prof_add_bytes(c, spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
-                             : std::string("k_dj_filt<2,-1,-1,1024,4>"),
-                     (4.0 * jc.nb + 4.0 * nu) * out->nrows);
-      out->sorted_col = -1;
-      for (int k = 0; k < nu; ++k) {
-        out->lo[k] = pl.lo[k];
-        out->hi[k] = pl.hi[k];
-      }
-      out->lo[fo] = (uint32_t)lo;
-      out->hi[fo] = (uint32_t)hi;
-      return out;
-    }
-  }
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
   {

@@ -13,5 +13,3 @@ for u in 8 16; do
     DAS_FILT_UNROLL=$u timeout -k 10 200 python bench.py --workload hub $NB > gpurun_out/s3/hub_u$u.json \
         2> gpurun_out/s3/hub_u$u.err || exit 15
 done
-DAS_FILT_ONEPASS=1 timeout -k 10 200 python bench.py --workload hub $NB > gpurun_out/s3/hub_onepass.json \
-    2> gpurun_out/s3/hub_onepass.err || exit 16
