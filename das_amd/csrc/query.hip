@@ -213,9 +213,10 @@ __device__ __forceinline__ void publish_u32(uint32_t* slot, uint32_t seq, uint32
   __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Or of predicate-free one-column scans (FlyBase's DO-term Or): the union's
-// distinct values in ONE launch.  Each scanned row tests and sets its value's
-// bit in a bitmap over the column's host-known id range; the row that set it
+// Or of one-column scans (FlyBase's DO-term Or): the union's distinct values
+// in ONE launch.  Each scanned row that passes its scan's predicate (the
+// grounded targets outside the key range) tests and sets its value's bit in
+// a bitmap over the column's host-known id range; the row that set it
 // writes the value, at a position its wave reserves with one atomic (output
 // unsorted, one row per distinct value -- Python set semantics).  ctr[0]:
 // rows written, ctr[1]: blocks done, ctr[2]: values outside [lo, lo + range)
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(B) k_union_first(MultiScan ms, uint32_t lo, ui
     const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
     bool first = false;
     uint32_t v = 0;
-    if (r < sg.end) {
+    if (r < sg.end && scan_keep(sg.sp, r)) {
       v = src[r];
       const uint32_t d = v - lo;
       if (d < range) {
@@ -3276,11 +3277,11 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
       }
     }
     {
-      // one column, every row kept: bitmap union in one launch (k_union_first)
+      // one output column: bitmap union in one launch (k_union_first)
       bool proj = preps[0].ncols == 1 && uhi[0] != kNone && ulo[0] <= uhi[0] && uhi[0] - ulo[0] < (1u << 27) &&
                   scanned < 0xFFFFFFF0ull;
       for (uint32_t i = 0; i < ms.nseg && proj; ++i)
-        proj = ms.seg[i].sp.all_keep && !ms.seg[i].sp.unordered && ms.seg[i].sp.nout == 1;
+        proj = !ms.seg[i].sp.unordered && !ms.seg[i].sp.emit_link && ms.seg[i].sp.nout == 1;
       const char* fb = std::getenv("DAS_UNION_BITS");                // A/B, tests: 0 never
       if (proj && !(fb && fb[0] == '0')) {
         const uint32_t range = uhi[0] - ulo[0] + 1;

@@ -24,4 +24,4 @@ show(d, "headline")
 for k, v in (d.get("workloads") or {}).items():
     show(v, k)
 for k, v in (d.get("join_probe_variants") or {}).items():
-    print("  join variant", k, v.get("ms_per_step"), (v.get("roofline") or {}).get("frac"))
+    print("  join variant", k, v.get("ms_per_step") or v.get("ms_per_query"), (v.get("roofline") or {}).get("frac"))
