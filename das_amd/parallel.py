@@ -144,6 +144,11 @@ class ShardedDB(RelationalDB):
 
     def _exchange_rows(self, table, key_vars):
         part, counts = self.local.partition(table, list(key_vars), self.world)
+        return self._send_grouped(table, part, counts)
+
+    def _send_grouped(self, table, part, counts):
+        """All-to-all of `part` (the rows of `table` grouped by destination
+        rank, counts[d] rows for rank d): sizes first, then the rows."""
         send_counts = self.local.xfer_tensor(counts.astype(np.int64))
         recv_counts = self.local.xfer_tensor(np.zeros(self.world, dtype=np.int64))
         self.dist.all_to_all_single(recv_counts, send_counts, group=self.group)
@@ -659,13 +664,28 @@ class ShardedDB(RelationalDB):
         load = ga + gb
         fair = max(load.sum() / self.world, 1)
         heavy = (load > self.heavy_frac * fair) & (ga > 0) & (gb > 0)
+        offa = np.concatenate([[0], np.cumsum(ca.astype(np.int64))])
+        offb = np.concatenate([[0], np.cumsum(cb.astype(np.int64))])
         if not heavy.any():
-            return None
+            if nb % self.world:
+                return None
+            # no heavy bucket: the usual exchange, from these bucket runs (the
+            # partition hash is the exchange's: bucket b goes to rank b % world)
+            # instead of partitioning both sides again
+            key = tuple(shared)
+
+            def grouped(t, p, c, off):
+                ks = [np.arange(d, nb, self.world) for d in range(self.world)]
+                counts = np.array([int(c[k].astype(np.int64).sum()) for k in ks], dtype=np.int64)
+                order = np.concatenate(ks)
+                keep = off[order + 1] > off[order]
+                rows = self.local.gather_ranges(p, off[order][keep], off[order + 1][keep])
+                return _with_part(self._send_grouped(t, rows, counts), ("hash", key))
+            return _with_part(self.local.join(grouped(ta, pa, ca, offa), grouped(tb, pb, cb, offb), no_overload),
+                              ("hash", key))
         self.plan_stats["heavy"] += 1
         a_stays = heavy & (ga >= gb)                      # a split in place, b gathered
         b_stays = heavy & ~a_stays
-        offa = np.concatenate([[0], np.cumsum(ca.astype(np.int64))])
-        offb = np.concatenate([[0], np.cumsum(cb.astype(np.int64))])
 
         def rows(t, off, mask):
             # the rows of the selected buckets (runs of the partitioned
