@@ -546,12 +546,14 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   struct Views {                       // scans may return index views while the plan runs
     Ctx& c;
     explicit Views(Ctx& cc) : c(cc) {
-      // default (2): views of scans up to kViewRows rows -- a small anchored
-      // range's copy is mostly launch and allocation; a large probe side is
-      // copied, which leaves it MALL-warm for the join that reads it next
-      // (profiles/r2_ab_views.json).  1: always views, 0: never.
+      // default (1): every predicate-free scan of consecutive index columns
+      // is a view.  2: views up to kViewRows rows only, larger probe sides
+      // copied (the copy leaves them MALL-warm for the join that reads them
+      // next: the join kernel runs at ~0.50 of the HBM peak instead of ~0.41,
+      // but the bio step is ~4 % slower with the copies, profiles/r3_*).
+      // 0: never.
       const char* f = std::getenv("DAS_SCAN_VIEWS");
-      c.scan_views = f && f[0] == '1' ? 1 : f && f[0] == '0' ? 0 : 2;
+      c.scan_views = f && f[0] == '2' ? 2 : f && f[0] == '0' ? 0 : 1;
     }
     ~Views() { c.scan_views = 0; }
   };

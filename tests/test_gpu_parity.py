@@ -783,13 +783,15 @@ def test_gpu_no_overload_matches_oracle(gen):
         pm.CONFIG["no_overload"] = O.CONFIG["no_overload"] = False
 
 
+@pytest.mark.parametrize("views", ["1", "2"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw"])
-def test_gpu_scan_views_match_oracle(gen, monkeypatch):
-    """DAS_SCAN_VIEWS=1: predicate-free scans inside a plan are views of the
-    index rows (no copy); the answers, including single-Link ones whose view
-    leaves the plan as a copy, equal the oracle's."""
+def test_gpu_scan_views_match_oracle(gen, views, monkeypatch):
+    """DAS_SCAN_VIEWS=1 (default): predicate-free scans inside a plan are views
+    of the index rows (no copy); 2: only scans up to 2^20 rows are.  The
+    answers, including single-Link ones whose view leaves the plan as a copy,
+    equal the oracle's."""
     from das_amd import synthetic
-    monkeypatch.setenv("DAS_SCAN_VIEWS", "1")
+    monkeypatch.setenv("DAS_SCAN_VIEWS", views)
     arrays = synthetic.bio_kb(300, 60, 4000, 200) if gen == "bio" else \
         synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
     db = _hipdb(arrays)
