@@ -47,9 +47,14 @@ struct PosIndex {
   uint64_t* uoff = nullptr;   // nkeys + 1 row offsets
   // Dense key directory per type (index joins): dir[ty][t - dir_lo[ty]] =
   // the index of key (ty, t) in ukey, or kNone; built where the type's t_p
-  // span is at most 2x its key count (else dir[ty] == nullptr: binary search).
+  // span is at most 2x its key count, or 16x up to 2^28 ids.
   std::vector<uint32_t*> dir;
   std::vector<uint32_t> dir_lo, dir_n;
+  // Otherwise a bucket directory: bucket b = (t - dir_lo) >> bshift holds
+  // the keys ukey[bdir[ty][b] .. bdir[ty][b + 1]) (~2 per bucket), searched
+  // in place of the whole type's keys (index joins of sparse key ranges).
+  std::vector<uint32_t*> bdir;
+  std::vector<uint32_t> bshift, bn;
   // host mirror of ukey / uoff (nkeys <= kHostKeyMirror), else empty
   std::vector<uint64_t> h_ukey, h_uoff;
 };

@@ -987,6 +987,18 @@ __global__ void k_dir_scatter(const uint64_t* ukey, uint64_t klo, uint64_t n, ui
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     dir[(uint32_t)ukey[klo + i] - tlo] = (uint32_t)(klo + i);
 }
+// Bucket directory of one type's sorted keys ukey[klo, klo + n): bucket b =
+// (t - tlo) >> shift; bdir[b] = the first key index of bucket >= b, for b in
+// [0, nb] (bdir[nb] = klo + n).  Key i writes the buckets after its
+// predecessor's up to its own: every slot is written exactly once.
+__global__ void k_bdir_fill(const uint64_t* ukey, uint64_t klo, uint64_t n, uint32_t tlo, uint32_t shift,
+                            uint32_t nb, uint32_t* bdir) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b1 = i < n ? ((uint32_t)ukey[klo + i] - tlo) >> shift : nb;
+    const int64_t b0 = i == 0 ? -1 : (int64_t)(((uint32_t)ukey[klo + i - 1] - tlo) >> shift);
+    for (int64_t b = b0 + 1; b <= (int64_t)b1; ++b) bdir[b] = (uint32_t)(klo + i);
+  }
+}
 }  // namespace
 
 void free_index(Index& idx) {
@@ -1000,6 +1012,9 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
   P.dir.assign(nt, nullptr);
   P.dir_lo.assign(nt, 0);
   P.dir_n.assign(nt, 0);
+  P.bdir.assign(nt, nullptr);
+  P.bshift.assign(nt, 0);
+  P.bn.assign(nt, 0);
   if (!P.nkeys || !nt || P.nkeys >= 0xFFFFFFFFull) return;
   DBuf<uint64_t> kb(4ull * nt, s);
   hipLaunchKernelGGL(k_type_key_bounds, dim3((nt + 63) / 64), dim3(64), 0, s, (const uint64_t*)P.ukey, P.nkeys, nt,
@@ -1012,7 +1027,30 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
     const uint64_t klo = hb[4 * ty], khi = hb[4 * ty + 1], tmin = hb[4 * ty + 2], tmax = hb[4 * ty + 3];
     if (khi <= klo) continue;
     const uint64_t span = tmax - tmin + 1;
-    if (span > 2 * (khi - klo) + 4096) continue;
+    // dense key ranges, and sparse ones up to 16 id slots per key (at most
+    // 2^28 slots, 1 GiB): a probe's key is then ONE load instead of a binary
+    // search over the type's keys (~24 dependent loads at 10^7 keys: config
+    // 5's T1 holds ~1.7 10^7 first targets over 1.3 10^8 node ids)
+    // (DAS_KEY_DIR_SPARSE=0: dense ranges only, the round-2/3 rule, for A/B)
+    static const bool sparse = !(std::getenv("DAS_KEY_DIR_SPARSE") && std::getenv("DAS_KEY_DIR_SPARSE")[0] == '0');
+    if (span > 2 * (khi - klo) + 4096 && (!sparse || span > 16 * (khi - klo) || span > (1ull << 28))) {
+      // bucket directory: ~2 keys per bucket (DAS_KEY_BDIR=0: none, A/B)
+      static const bool bd = !(std::getenv("DAS_KEY_BDIR") && std::getenv("DAS_KEY_BDIR")[0] == '0');
+      if (!bd || khi - klo < 64) continue;
+      uint32_t shift = 0;
+      while ((span >> shift) > (khi - klo) / 2) ++shift;
+      const uint32_t nb = (uint32_t)(((span - 1) >> shift) + 1);
+      uint32_t* b = dalloc<uint32_t>(idx, (uint64_t)nb + 1);
+      KScope ks("k_bdir_fill", 8.0 * (khi - klo) + 4.0 * nb);
+      hipLaunchKernelGGL(k_bdir_fill, dim3(grid_for(khi - klo + 1, 256, 8192)), dim3(256), 0, s,
+                         (const uint64_t*)P.ukey, klo, khi - klo, (uint32_t)tmin, shift, nb, b);
+      DAS_HIP(hipGetLastError());
+      P.bdir[ty] = b;
+      P.bshift[ty] = shift;
+      P.bn[ty] = nb;
+      P.dir_lo[ty] = (uint32_t)tmin;
+      continue;
+    }
     uint32_t* d = dalloc<uint32_t>(idx, span);
     fill_dev(d, 0xFF, 4 * span, s);
     KScope ks("k_dir_scatter", 12.0 * (khi - klo));

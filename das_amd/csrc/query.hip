@@ -949,6 +949,12 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
 // build value against the bitmap (one flag byte per output, the chunk's kept
 // count); MODE 1 writes only the kept outputs, in output order, at the
 // chunk's scanned offset.  The unfiltered join is never materialised.
+// MODE 2 (one walk): tests each output and writes the kept ones at the
+// chunk's own slot range [w CH, w CH + kept) of a scratch table (cap = the
+// virtual output count) with the chunk's kept count; k_chunk_compact then
+// moves the chunk runs to their scanned offsets -- the outputs are walked and
+// their build rows gathered once instead of twice, and no flag bytes go
+// through HBM (no atomics: the order is the two-pass order).
 // ---------------------------------------------------------------------------
 struct FiltKey {
   const uint32_t* col;     // build column holding the filtered variable
@@ -978,8 +984,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   for (int i = 0; i < 4; ++i) {
     pp[i] = i < ncp ? jc.p[i] : nullptr;
     bp[i] = i < ncb ? jc.b[i] : nullptr;
-    po[i] = i < ncp && MODE == 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
-    bo[i] = i < ncb && MODE == 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+    po[i] = i < ncp && MODE >= 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
+    bo[i] = i < ncb && MODE >= 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * CH;
@@ -995,7 +1001,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       lo = nlo;
     }
     uint32_t run = 0;                                  // kept outputs of this chunk so far
-    const uint32_t obase = MODE == 1 ? coff[w] : 0u;
+    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? w * CH : 0ull;
     for (uint64_t u = lo; u < units; ++u) {
       uint64_t base = unit_off[u];
       if (base >= oe) break;
@@ -1019,7 +1025,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
         const uint32_t rs = (uint32_t)((ob > gb ? ob : gb) - gb), re = (uint32_t)((oe < ge ? oe : ge) - gb);
         const uint64_t r = r0 + g * 64 + lane;
         uint32_t pv[4] = {0u, 0u, 0u, 0u};
-        if (MODE == 1) {
+        if (MODE >= 1) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
@@ -1060,8 +1066,19 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             }
           } else {
             bool f[XU];
+            if (MODE == 1) {
 #pragma unroll
-            for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
+              for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
+            } else {
+              uint32_t v[XU];
+#pragma unroll
+              for (int q = 0; q < XU; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
+              uint32_t wd[XU];
+#pragma unroll
+              for (int q = 0; q < XU; ++q) wd[q] = v[q] < fk.range ? fk.bits[v[q] >> 5] : 0u;
+#pragma unroll
+              for (int q = 0; q < XU; ++q) f[q] = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
+            }
             uint32_t bv[XU][4];
 #pragma unroll
             for (int q = 0; q < XU; ++q)
@@ -1071,7 +1088,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
               const uint64_t m = __ballot(f[q]);
-              const uint64_t pos = (uint64_t)obase + run + __popcll(m & lt);
+              const uint64_t pos = obase + run + __popcll(m & lt);
               run += (uint32_t)__popcll(m);
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
@@ -1089,7 +1106,38 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
         }
       }
     }
-    if (MODE == 0 && lane == 0) ccnt[w] = run;
+    if (MODE != 1 && lane == 0) ccnt[w] = run;
+  }
+}
+
+// MODE 2's second step: chunk w's kept rows [w CH, w CH + cnt[w]) of the
+// scratch columns move to [off[w], off[w] + cnt[w]) of the output, one wave
+// per chunk, every column (ncols <= kMaxCols).
+template <int CH>
+__global__ void __launch_bounds__(B) k_chunk_compact(const uint32_t* __restrict__ src, uint64_t scap,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const uint32_t* __restrict__ off, uint64_t chunks, int ncols,
+                                                     uint32_t* __restrict__ dst, uint64_t dcap) {
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
+    const uint32_t n = cnt[w];
+    const uint64_t s0 = w * CH, d0 = off[w];
+    for (int k = 0; k < ncols; ++k) {
+      const uint32_t* sc = src + (uint64_t)k * scap + s0;
+      uint32_t* dc = dst + (uint64_t)k * dcap + d0;
+      uint32_t x[CH / 64];
+#pragma unroll
+      for (int j = 0; j < CH / 64; ++j) {
+        const uint32_t i = (uint32_t)(j * 64 + lane);
+        x[j] = i < n ? __builtin_nontemporal_load(sc + i) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < CH / 64; ++j) {
+        const uint32_t i = (uint32_t)(j * 64 + lane);
+        if (i < n) dc[i] = x[j];
+      }
+    }
   }
 }
 
@@ -2109,28 +2157,44 @@ struct IjKeys {
   uint32_t dlo, dn;
   uint32_t flo, fhi;    // ranged mode: rows [flo, fhi)
   int fixed;
+  const uint32_t* bdir; // bucket directory (no dense one): keys of bucket (t - dlo) >> bshift
+  uint32_t bshift, bn;
 };
 
-__device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g, uint64_t row = 0) {
+// Index in ukey of key (type, t) through the dense directory (one load), the
+// bucket directory (two adjacent loads + a search of ~2 keys) or a binary
+// search over every key; false if absent.
+__device__ __forceinline__ bool ij_key_index(uint32_t t, const IjKeys& kx, uint64_t& lo) {
+  if (kx.dir) {
+    const uint32_t d = t - kx.dlo;
+    const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
+    lo = j;
+    return j != 0xFFFFFFFFu;
+  }
   const uint64_t k = kx.thi | t;
+  uint64_t l = 0, h = kx.nkeys;
+  if (kx.bdir) {
+    const uint32_t b = (t - kx.dlo) >> kx.bshift;
+    if (t < kx.dlo || b >= kx.bn) return false;
+    l = kx.bdir[b];
+    h = kx.bdir[b + 1];
+  }
+  while (l < h) {
+    const uint64_t mid = (l + h) >> 1;
+    if (kx.ukey[mid] < k) l = mid + 1; else h = mid;
+  }
+  lo = l;
+  return lo < kx.nkeys && kx.ukey[lo] == k;
+}
+
+__device__ __forceinline__ uint2 ij_lookup(uint32_t t, const IjKeys& kx, const IjGround& g, uint64_t row = 0) {
   uint64_t lo;
   bool hit;
   if (kx.fixed) {
     lo = 0;
     hit = kx.fhi > kx.flo;
-  } else if (kx.dir) {                           // dense directory: one load
-    const uint32_t d = t - kx.dlo;
-    const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
-    lo = j;
-    hit = j != 0xFFFFFFFFu;
-  } else {                                       // lower_bound
-    uint64_t l = 0, h = kx.nkeys;
-    while (l < h) {
-      const uint64_t mid = (l + h) >> 1;
-      if (kx.ukey[mid] < k) l = mid + 1; else h = mid;
-    }
-    lo = l;
-    hit = lo < kx.nkeys && kx.ukey[lo] == k;
+  } else {
+    hit = ij_key_index(t, kx, lo);
   }
   uint2 e = make_uint2(0u, 0u);
   if (hit) {
@@ -2233,21 +2297,7 @@ __device__ __forceinline__ uint2 ij_lookup_group(uint32_t t, const IjKeys& kx, c
   } else {
     uint64_t lo;
     bool hit;
-    if (kx.dir) {
-      const uint32_t d = t - kx.dlo;
-      const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
-      lo = j;
-      hit = j != 0xFFFFFFFFu;
-    } else {
-      const uint64_t k = kx.thi | t;
-      uint64_t l = 0, h = kx.nkeys;
-      while (l < h) {
-        const uint64_t mid = (l + h) >> 1;
-        if (kx.ukey[mid] < k) l = mid + 1; else h = mid;
-      }
-      lo = l;
-      hit = lo < kx.nkeys && kx.ukey[lo] == k;
-    }
+    hit = ij_key_index(t, kx, lo);
     if (hit) {
       b = (uint32_t)kx.uoff[lo];
       end = (uint32_t)kx.uoff[lo + 1];
@@ -2442,9 +2492,12 @@ int colof_t(const Table& t, int32_t v) {
 IjKeys ij_keys(const PosIndex& PI, uint32_t type_id) {
   static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
   const bool use_dir = type_id < PI.dir.size() && PI.dir[type_id] && !no_dir;
+  const bool use_bdir = !use_dir && type_id < PI.bdir.size() && PI.bdir[type_id] && !no_dir;
   return IjKeys{(uint64_t)type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-                use_dir ? PI.dir[type_id] : nullptr, use_dir ? PI.dir_lo[type_id] : 0u,
-                use_dir ? PI.dir_n[type_id] : 0u, 0u, 0u, 0};
+                use_dir ? PI.dir[type_id] : nullptr, use_dir || use_bdir ? PI.dir_lo[type_id] : 0u,
+                use_dir ? PI.dir_n[type_id] : 0u, 0u, 0u, 0,
+                use_bdir ? PI.bdir[type_id] : nullptr, use_bdir ? PI.bshift[type_id] : 0u,
+                use_bdir ? PI.bn[type_id] : 0u};
 }
 
 // Anti index join of A by a Not(Link) term, resolved on the host.
@@ -3673,6 +3726,52 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   }();
   const uint64_t fchunks = (total + ch - 1) / ch;
   const unsigned fgrid2 = grid_for(fchunks, B / 64, 65535u * 4u);
+  // one walk writing kept outputs chunk-locally (k_dj_filt<2>) + a
+  // compaction of the chunk runs: config 5's H4 0.82 -> 0.71 ms against the
+  // flag pass and a second walk (DAS_FILT_LOCAL=0, A/B;
+  // profiles/r3_hub_local_ab.json)
+  const char* fle = std::getenv("DAS_FILT_LOCAL");
+  const bool local = !(fle && fle[0] == '0');
+  if (local && ch == 1024 && (uint64_t)nu * total * 4 <= (16ull << 30)) {
+    DBuf<uint32_t> scr((uint64_t)nu * total, c.s);
+    DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
+    const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
+    const std::string nm = spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
+                                : std::string("k_dj_filt<2,-1,-1,1024,4>");
+    {
+      // per probe row its row id, (first, count) and probe columns; per
+      // output its build value (a P row); kept outputs' columns written
+      ProfScope ps(c, nm, (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
+#define FILT_L(NPV, NBV)                                                                                       \
+  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
+                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
+                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total)
+      if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
+      else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
+      else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
+      else FILT_L(-1, -1);
+#undef FILT_L
+      DAS_HIP(hipGetLastError());
+    }
+    const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);
+    prof_add_bytes(c, nm, 4.0 * nu * m);
+    auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
+    out->nrows = m;
+    if (m) {
+      KScope ks("k_chunk_compact<1024>", 8.0 * nu * m + 8.0 * fchunks);
+      hipLaunchKernelGGL(k_chunk_compact<1024>, dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
+                         (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, fchunks, nu, out->data, out->cap);
+      DAS_HIP(hipGetLastError());
+    }
+    out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
+    for (int k = 0; k < nu; ++k) {
+      out->lo[k] = pl.lo[k];
+      out->hi[k] = pl.hi[k];
+    }
+    out->lo[fo] = (uint32_t)lo;
+    out->hi[fo] = (uint32_t)hi;
+    return out;
+  }
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
   {

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--genes", type=int, default=300_000)
     ap.add_argument("--schema", type=int, default=60)
     ap.add_argument("--rows", type=int, default=450_000)
+    ap.add_argument("--workload", choices=("flybase", "bio"), default="flybase",
+                    help="bio: bench.py's Q1-Q6 on its bio_full KB (20 M Member links), warm and on a fresh gene pair")
     ap.add_argument("--cprofile", default=None, help="also: cProfile of 20 fresh anchors x 5 queries into this file")
     args = ap.parse_args()
     import torch
@@ -25,6 +27,22 @@ def main():
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
+    if args.workload == "bio":
+        arrays = synthetic.bio_full_kb(200_000, 50_000, 20_000_000, 100_000)
+        db = HipDB(device=0)
+        db.load_arrays(arrays)
+        torch.cuda.synchronize()
+        for anchor, tag in ((0, "warm-up"), (0, "warm"), (5, "fresh anchor")):
+            for name, spec in bench.bio_specs(range(1, 200_000), anchor=anchor):
+                q = bench.build_expr(pm, spec)
+                print(f"[trace] === {name} ({tag})", file=sys.stderr, flush=True)
+                t0 = time.perf_counter()
+                a = pm.PatternMatchingAnswer()
+                q.matched(db, a)
+                n = a.count()
+                dt = (time.perf_counter() - t0) * 1e6
+                print(f"[trace] === {name} ({tag}): {dt:.1f} us wall, {n} bindings", file=sys.stderr, flush=True)
+        return
     arrays = synthetic.flybase_kb(args.genes, args.schema, args.rows)
     db = HipDB(device=0)
     db.load_arrays(arrays)
