@@ -765,7 +765,7 @@ Ctx*& active_ctx() {
 KScope::KScope(const char* name, double algorithmic_bytes) {
   Ctx* c = active_ctx();
   if (c && c->prof) impl = new ProfScope(*c, name, algorithmic_bytes);
-  else if (trace_on()) trace_mark("kernel", name);
+  else if (trace_on()) trace_mark("kernel", std::string(name) + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
 }
 
 namespace {

@@ -189,7 +189,7 @@ struct ProfScope {
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
-    if (trace_on()) trace_mark("kernel", name);
+    if (trace_on()) trace_mark("kernel", name + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
     if (!c.prof || (!c.prof_only.empty() && c.prof_only != name)) return;
     a = c.take_event();
     b = c.take_event();

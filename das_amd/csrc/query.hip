@@ -970,11 +970,11 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
                                                const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
                                                uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                                const uint32_t* __restrict__ coff, JoinCols jc,
-                                               uint32_t* __restrict__ out, uint64_t cap) {
+                                               uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo,
+                                               uint64_t whi) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
-  const uint64_t chunks = (total + CH - 1) / CH;
   const int ncp = NPC >= 0 ? NPC : jc.np, ncb = NBC >= 0 ? NBC : jc.nb;
   const uint32_t* pp[4];
   const uint32_t* bp[4];
@@ -987,7 +987,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
     po[i] = i < ncp && MODE >= 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
     bo[i] = i < ncb && MODE >= 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
-  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
+  // chunks [wlo, whi) of the virtual outputs
+  for (uint64_t w = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < whi; w += waves) {
     const uint64_t ob = w * CH;
     const uint64_t oe = ob + CH < total ? ob + CH : total;
     uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
@@ -1001,7 +1002,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       lo = nlo;
     }
     uint32_t run = 0;                                  // kept outputs of this chunk so far
-    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? w * CH : 0ull;
+    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? (w - wlo) * CH : 0ull;
     for (uint64_t u = lo; u < units; ++u) {
       uint64_t base = unit_off[u];
       if (base >= oe) break;
@@ -1110,19 +1111,19 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
   }
 }
 
-// MODE 2's second step: chunk w's kept rows [w CH, w CH + cnt[w]) of the
+// MODE 2's second step: chunk w's kept rows [(w - wlo) CH, + cnt[w]) of the
 // scratch columns move to [off[w], off[w] + cnt[w]) of the output, one wave
-// per chunk, every column (ncols <= kMaxCols).
+// per chunk of [wlo, whi), every column (ncols <= kMaxCols).
 template <int CH>
 __global__ void __launch_bounds__(B) k_chunk_compact(const uint32_t* __restrict__ src, uint64_t scap,
                                                      const uint32_t* __restrict__ cnt,
-                                                     const uint32_t* __restrict__ off, uint64_t chunks, int ncols,
-                                                     uint32_t* __restrict__ dst, uint64_t dcap) {
+                                                     const uint32_t* __restrict__ off, uint64_t wlo, uint64_t whi,
+                                                     int ncols, uint32_t* __restrict__ dst, uint64_t dcap) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
-  for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
+  for (uint64_t w = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < whi; w += waves) {
     const uint32_t n = cnt[w];
-    const uint64_t s0 = w * CH, d0 = off[w];
+    const uint64_t s0 = (w - wlo) * CH, d0 = off[w];
     for (int k = 0; k < ncols; ++k) {
       const uint32_t* sc = src + (uint64_t)k * scap + s0;
       uint32_t* dc = dst + (uint64_t)k * dcap + d0;
@@ -2073,8 +2074,16 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   // the key-slot arrays cost ~20 B per slot of streaming work; the sort-merge
   // alternative costs a log2(|Q|)-step random search per probe row, so a
   // slot range up to a few times either side's rows still pays (10^9-link
-  // KBs: node ranges of 10^8 ids against 10^8-row probes)
-  if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << 26) ||
+  // KBs: node ranges of 10^8 ids against 10^8-row probes).  Small joins over
+  // a wide range (bio QUERY_3: 2*10^4 rows each side keyed by Member link
+  // ids spanning 1.4*10^7 slots, ~100 us of slot arrays) sort instead.
+  // (DAS_DJ_RANGE_FLOOR: log2 of the slots always allowed, A/B; round 3 had 26)
+  static const int floor_bits = [] {
+    const char* e = std::getenv("DAS_DJ_RANGE_FLOOR");
+    const int v = e ? std::atoi(e) : 22;
+    return v >= 10 && v <= 31 ? v : 22;
+  }();
+  if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << floor_bits) ||
       range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
   const uint32_t kmin = h[0];
@@ -3745,7 +3754,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_L(NPV, NBV)                                                                                       \
   hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
-                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total)
+                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks)
       if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
       else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
       else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
@@ -3760,7 +3769,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     if (m) {
       KScope ks("k_chunk_compact<1024>", 8.0 * nu * m + 8.0 * fchunks);
       hipLaunchKernelGGL(k_chunk_compact<1024>, dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
-                         (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, fchunks, nu, out->data, out->cap);
+                         (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, 0ull, fchunks, nu, out->data, out->cap);
       DAS_HIP(hipGetLastError());
     }
     out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
@@ -3788,7 +3797,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_0(CHV)                                                                                                \
   hipLaunchKernelGGL((k_dj_filt<0, -1, -1, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows,   \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
-                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull)
+                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks)
     // DAS_FILT_UNROLL (8 / 16): rounds of 64 outputs whose build values and
     // bitmap words are loaded together in the flag pass (A/B; default 4)
     static const int xu = [] {
@@ -3801,11 +3810,11 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     else if (xu == 8)
       hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 8>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
                          A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
-                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks);
     else if (xu == 16)
       hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 16>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
                          A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
-                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull);
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks);
     else FILT_0(1024);
 #undef FILT_0
     DAS_HIP(hipGetLastError());
@@ -3824,7 +3833,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_W(NPV, NBV, CHV)                                                                                  \
   hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,      \
-                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap)
+                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap, 0ull, fchunks)
 #define FILT_WC(CHV)                                    \
   if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1, CHV);      \
   else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1, CHV); \
