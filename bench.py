@@ -700,7 +700,9 @@ def run_load(args, rank, world, local_rank):
 
 # kernel scopes that are scratch, not algorithmic bytes (sort
 # passes and count -> offset scans count against the fraction)
-_SCRATCH = ("k_radix", "k_scan_tiles", "k_scan_reduce", "k_scan_single", "k_bounds_u32")
+# (k_chunk_compact moves the filtered expansion's chunk runs out of its
+# scratch: the walk already counts those outputs once)
+_SCRATCH = ("k_radix", "k_scan_tiles", "k_scan_reduce", "k_scan_single", "k_bounds_u32", "k_chunk_compact")
 
 
 def step_roofline(stats, ms_per_step, world, steps=1):

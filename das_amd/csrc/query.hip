@@ -960,6 +960,7 @@ struct FiltKey {
   const uint32_t* col;     // build column holding the filtered variable
   uint32_t lo, range;
   const uint32_t* bits;
+  int bcol;                // its index among the join's build output columns
 };
 
 // NPC / NBC: the probe / build output column counts when specialised (the
@@ -1067,11 +1068,11 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             }
           } else {
             bool f[XU];
+            uint32_t v[XU];
             if (MODE == 1) {
 #pragma unroll
               for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
             } else {
-              uint32_t v[XU];
 #pragma unroll
               for (int q = 0; q < XU; ++q) v[q] = (q < nr && o[q] < re) ? fk.col[br[q]] - fk.lo : 0xFFFFFFFFu;
               uint32_t wd[XU];
@@ -1080,11 +1081,14 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
 #pragma unroll
               for (int q = 0; q < XU; ++q) f[q] = v[q] < fk.range && ((wd[q] >> (v[q] & 31)) & 1u);
             }
+            // build columns of the kept outputs (MODE 2: the filtered column
+            // is the value just tested, no second load)
             uint32_t bv[XU][4];
 #pragma unroll
             for (int q = 0; q < XU; ++q)
 #pragma unroll
-              for (int i = 0; i < 4; ++i) bv[q][i] = (i < ncb && f[q]) ? bp[i][br[q]] : 0u;
+              for (int i = 0; i < 4; ++i)
+                bv[q][i] = (i < ncb && f[q]) ? (MODE == 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
 #pragma unroll
             for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
@@ -2074,16 +2078,11 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   // the key-slot arrays cost ~20 B per slot of streaming work; the sort-merge
   // alternative costs a log2(|Q|)-step random search per probe row, so a
   // slot range up to a few times either side's rows still pays (10^9-link
-  // KBs: node ranges of 10^8 ids against 10^8-row probes).  Small joins over
-  // a wide range (bio QUERY_3: 2*10^4 rows each side keyed by Member link
-  // ids spanning 1.4*10^7 slots, ~100 us of slot arrays) sort instead.
-  // (DAS_DJ_RANGE_FLOOR: log2 of the slots always allowed, A/B; round 3 had 26)
-  static const int floor_bits = [] {
-    const char* e = std::getenv("DAS_DJ_RANGE_FLOOR");
-    const int v = e ? std::atoi(e) : 22;
-    return v >= 10 && v <= 31 ? v : 22;
-  }();
-  if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << floor_bits) ||
+  // KBs: node ranges of 10^8 ids against 10^8-row probes).  (Small joins
+  // over a wide range -- bio QUERY_3's 2*10^4-row sides keyed by Member link
+  // ids over 1.4*10^7 slots -- measured no faster sorted: 2^22 instead of
+  // 2^26 below, bio step 1.994 vs 1.964 ms, profiles/r3_bio_range_floor_ab.json)
+  if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << 26) ||
       range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
   const uint32_t kmin = h[0];
@@ -3684,7 +3683,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   if (total >= (1ull << 32) - (1ull << 16)) return nullptr;
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
   const unsigned fgrid = grid_for(chunks, B / 64, 65535u * 4u);
-  const FiltKey fk{jc.b[fb], (uint32_t)lo, (uint32_t)(hi - lo + 1), (const uint32_t*)bits.p};
+  const FiltKey fk{jc.b[fb], (uint32_t)lo, (uint32_t)(hi - lo + 1), (const uint32_t*)bits.p, fb};
   // DAS_FILT_FUSED=1: one pass, unsorted output, while the worst case (every
   // virtual output kept) fits the output buffer.  Off by default: at config 5
   // it ran 924 us against 337 + 296 us for the two ordered passes (round 3,
