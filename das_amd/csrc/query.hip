@@ -1003,7 +1003,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       lo = nlo;
     }
     uint32_t run = 0;                                  // kept outputs of this chunk so far
-    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? (w - wlo) * CH : 0ull;
+    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE >= 2 ? (w - wlo) * CH : 0ull;
     for (uint64_t u = lo; u < units; ++u) {
       uint64_t base = unit_off[u];
       if (base >= oe) break;
@@ -1031,6 +1031,85 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
+        }
+        // owner lane and build row of the XU rounds of 64 outputs from o0
+        auto resolve = [&](uint32_t o0, uint32_t* o, uint32_t* br, int* ll) {
+          const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
+#pragma unroll
+          for (int q = 0; q < XU; ++q) {
+            o[q] = o0 + (uint32_t)(q * 64 + lane);
+            ll[q] = 0;
+            br[q] = 0;
+            if (q >= nr) continue;
+            int l = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1) {
+              const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
+              if (l + st < 64 && pl <= o[q]) l += st;
+            }
+            ll[q] = l;
+            br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
+          }
+          return nr;
+        };
+        if (MODE == 3) {
+          // MODE 2 software-pipelined: the next XU rounds' build values are
+          // loaded before this round's bitmap words, so a chunk's dependent
+          // load chain is ~1 + batches instead of 2 per batch
+          uint32_t oA[XU], brA[XU], vA[XU];
+          int llA[XU];
+          int nrA = resolve(rs, oA, brA, llA);
+#pragma unroll
+          for (int q = 0; q < XU; ++q) vA[q] = (q < nrA && oA[q] < re) ? fk.col[brA[q]] - fk.lo : 0xFFFFFFFFu;
+          for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
+            uint32_t oB[XU], brB[XU], vB[XU];
+            int llB[XU];
+            int nrB = 0;
+            if (o0 + 64 * XU < re) {
+              nrB = resolve(o0 + 64 * XU, oB, brB, llB);
+#pragma unroll
+              for (int q = 0; q < XU; ++q) vB[q] = (q < nrB && oB[q] < re) ? fk.col[brB[q]] - fk.lo : 0xFFFFFFFFu;
+            }
+            uint32_t wd[XU];
+#pragma unroll
+            for (int q = 0; q < XU; ++q) wd[q] = vA[q] < fk.range ? fk.bits[vA[q] >> 5] : 0u;
+            bool f[XU];
+#pragma unroll
+            for (int q = 0; q < XU; ++q) f[q] = vA[q] < fk.range && ((wd[q] >> (vA[q] & 31)) & 1u);
+            uint32_t bv[XU][4];
+#pragma unroll
+            for (int q = 0; q < XU; ++q)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                bv[q][i] = (i < ncb && f[q]) ? (i == fk.bcol ? vA[q] + fk.lo : bp[i][brA[q]]) : 0u;
+#pragma unroll
+            for (int q = 0; q < XU; ++q) {
+              if (q >= nrA) continue;
+              const uint64_t m = __ballot(f[q]);
+              const uint64_t pos = obase + run + __popcll(m & lt);
+              run += (uint32_t)__popcll(m);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (i >= ncp) break;
+                const uint32_t x = lane_get(pv[i], llA[q]);
+                if (f[q]) po[i][pos] = x;
+              }
+              if (f[q]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  if (i < ncb) bo[i][pos] = bv[q][i];
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < XU; ++q) {
+              oA[q] = oB[q];
+              brA[q] = brB[q];
+              vA[q] = vB[q];
+              llA[q] = llB[q];
+            }
+            nrA = nrB;
+          }
+          continue;
         }
         // XU rounds of 64 outputs resolved before their loads issue
         for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
@@ -1088,7 +1167,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             for (int q = 0; q < XU; ++q)
 #pragma unroll
               for (int i = 0; i < 4; ++i)
-                bv[q][i] = (i < ncb && f[q]) ? (MODE == 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
+                bv[q][i] = (i < ncb && f[q]) ? (MODE >= 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
 #pragma unroll
             for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
@@ -3744,20 +3823,31 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     DBuf<uint32_t> scr((uint64_t)nu * total, c.s);
     DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-    const std::string nm = spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
-                                : std::string("k_dj_filt<2,-1,-1,1024,4>");
+    // DAS_FILT_PIPE=1: the software-pipelined walk (MODE 3, A/B)
+    const char* fpe = std::getenv("DAS_FILT_PIPE");
+    const bool pipe = fpe && fpe[0] == '1';
+    const std::string md = pipe ? "3," : "2,";
+    const std::string nm = spec ? "k_dj_filt<" + md + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
+                                : "k_dj_filt<" + md + "-1,-1,1024,4>";
     {
       // per probe row its row id, (first, count) and probe columns; per
       // output its build value (a P row); kept outputs' columns written
       ProfScope ps(c, nm, (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
-#define FILT_L(NPV, NBV)                                                                                       \
-  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
-                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
+#define FILT_L(MD, NPV, NBV)                                                                                    \
+  hipLaunchKernelGGL((k_dj_filt<MD, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
+                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,              \
                      (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks)
-      if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
-      else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
-      else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
-      else FILT_L(-1, -1);
+      if (pipe) {
+        if (jc.np == 1 && jc.nb == 1) FILT_L(3, 1, 1);
+        else if (jc.np == 2 && jc.nb == 1) FILT_L(3, 2, 1);
+        else if (jc.np == 1 && jc.nb == 2) FILT_L(3, 1, 2);
+        else FILT_L(3, -1, -1);
+      } else {
+        if (jc.np == 1 && jc.nb == 1) FILT_L(2, 1, 1);
+        else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 2, 1);
+        else if (jc.np == 1 && jc.nb == 2) FILT_L(2, 1, 2);
+        else FILT_L(2, -1, -1);
+      }
 #undef FILT_L
       DAS_HIP(hipGetLastError());
     }
