@@ -963,21 +963,6 @@ struct FiltKey {
   int bcol;                // its index among the join's build output columns
 };
 
-// MODE 4 (DAS_FILT_LOOKBACK=1): MODE 2's walk, chunks taken in ticket order;
-// a chunk's output offset comes from a decoupled look-back over the earlier
-// chunks' published counts (prims.h's onesweep protocol, bounded wait) and
-// the same wave then moves its kept rows from its scratch slots to the
-// output -- no compaction launch.  A wait past its bound sets lb.err; the
-// caller then compacts from the scratch slots and counts as MODE 2 does.
-struct FiltLb {
-  uint32_t* ticket;
-  uint64_t* status;      // per chunk: kLbAgg / kLbInc | count
-  uint64_t* ctl;         // [0] error flag, [1] total kept (the last chunk)
-  uint32_t* dst;
-  uint64_t dcap;
-  int ncols;
-};
-
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
 template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk, int XU = kXUnroll>
@@ -987,7 +972,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
                                                uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                                const uint32_t* __restrict__ coff, JoinCols jc,
                                                uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo,
-                                               uint64_t whi, FiltLb lb) {
+                                               uint64_t whi) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -1003,19 +988,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
     po[i] = i < ncp && MODE >= 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
     bo[i] = i < ncb && MODE >= 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
   }
-  // chunks [wlo, whi) of the virtual outputs (MODE 4: in ticket order)
-  uint64_t wnext = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6);
-  while (true) {
-    uint64_t w;
-    if (MODE == 4) {
-      uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(lb.ticket, 1u);
-      w = wlo + (uint64_t)(uint32_t)__shfl((int)t, 0, 64);
-    } else {
-      w = wnext;
-      wnext += waves;
-    }
-    if (w >= whi) break;
+  // chunks [wlo, whi) of the virtual outputs
+  for (uint64_t w = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < whi; w += waves) {
     const uint64_t ob = w * CH;
     const uint64_t oe = ob + CH < total ? ob + CH : total;
     uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
@@ -1029,7 +1003,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       lo = nlo;
     }
     uint32_t run = 0;                                  // kept outputs of this chunk so far
-    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE >= 2 ? (w - wlo) * CH : 0ull;
+    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? (w - wlo) * CH : 0ull;
     for (uint64_t u = lo; u < units; ++u) {
       uint64_t base = unit_off[u];
       if (base >= oe) break;
@@ -1057,85 +1031,6 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
-        }
-        // owner lane and build row of the XU rounds of 64 outputs from o0
-        auto resolve = [&](uint32_t o0, uint32_t* o, uint32_t* br, int* ll) {
-          const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
-#pragma unroll
-          for (int q = 0; q < XU; ++q) {
-            o[q] = o0 + (uint32_t)(q * 64 + lane);
-            ll[q] = 0;
-            br[q] = 0;
-            if (q >= nr) continue;
-            int l = 0;
-#pragma unroll
-            for (int st = 32; st >= 1; st >>= 1) {
-              const uint32_t pl = (uint32_t)__shfl(pre, l + st, 64);
-              if (l + st < 64 && pl <= o[q]) l += st;
-            }
-            ll[q] = l;
-            br[q] = lane_get(e[g].x, l) + (o[q] - (uint32_t)__shfl(pre, l, 64));
-          }
-          return nr;
-        };
-        if (MODE == 3) {
-          // MODE 2 software-pipelined: the next XU rounds' build values are
-          // loaded before this round's bitmap words, so a chunk's dependent
-          // load chain is ~1 + batches instead of 2 per batch
-          uint32_t oA[XU], brA[XU], vA[XU];
-          int llA[XU];
-          int nrA = resolve(rs, oA, brA, llA);
-#pragma unroll
-          for (int q = 0; q < XU; ++q) vA[q] = (q < nrA && oA[q] < re) ? fk.col[brA[q]] - fk.lo : 0xFFFFFFFFu;
-          for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
-            uint32_t oB[XU], brB[XU], vB[XU];
-            int llB[XU];
-            int nrB = 0;
-            if (o0 + 64 * XU < re) {
-              nrB = resolve(o0 + 64 * XU, oB, brB, llB);
-#pragma unroll
-              for (int q = 0; q < XU; ++q) vB[q] = (q < nrB && oB[q] < re) ? fk.col[brB[q]] - fk.lo : 0xFFFFFFFFu;
-            }
-            uint32_t wd[XU];
-#pragma unroll
-            for (int q = 0; q < XU; ++q) wd[q] = vA[q] < fk.range ? fk.bits[vA[q] >> 5] : 0u;
-            bool f[XU];
-#pragma unroll
-            for (int q = 0; q < XU; ++q) f[q] = vA[q] < fk.range && ((wd[q] >> (vA[q] & 31)) & 1u);
-            uint32_t bv[XU][4];
-#pragma unroll
-            for (int q = 0; q < XU; ++q)
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                bv[q][i] = (i < ncb && f[q]) ? (i == fk.bcol ? vA[q] + fk.lo : bp[i][brA[q]]) : 0u;
-#pragma unroll
-            for (int q = 0; q < XU; ++q) {
-              if (q >= nrA) continue;
-              const uint64_t m = __ballot(f[q]);
-              const uint64_t pos = obase + run + __popcll(m & lt);
-              run += (uint32_t)__popcll(m);
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                if (i >= ncp) break;
-                const uint32_t x = lane_get(pv[i], llA[q]);
-                if (f[q]) po[i][pos] = x;
-              }
-              if (f[q]) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                  if (i < ncb) bo[i][pos] = bv[q][i];
-              }
-            }
-#pragma unroll
-            for (int q = 0; q < XU; ++q) {
-              oA[q] = oB[q];
-              brA[q] = brB[q];
-              vA[q] = vB[q];
-              llA[q] = llB[q];
-            }
-            nrA = nrB;
-          }
-          continue;
         }
         // XU rounds of 64 outputs resolved before their loads issue
         for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
@@ -1193,7 +1088,7 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
             for (int q = 0; q < XU; ++q)
 #pragma unroll
               for (int i = 0; i < 4; ++i)
-                bv[q][i] = (i < ncb && f[q]) ? (MODE >= 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
+                bv[q][i] = (i < ncb && f[q]) ? (MODE == 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
 #pragma unroll
             for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
@@ -1217,35 +1112,6 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
       }
     }
     if (MODE != 1 && lane == 0) ccnt[w] = run;
-    if (MODE == 4) {
-      uint64_t pre = 0;
-      if (lane == 0) {
-        const uint64_t k = w - wlo;
-        uint64_t* st = lb.status + k;
-        __hip_atomic_store(st, (k == 0 ? kLbInc : kLbAgg) | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int64_t j = (int64_t)k - 1; j >= 0;) {
-          const uint64_t v = __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v & kLbInc) { pre += v & kLbMask; break; }
-          if (v & kLbAgg) { pre += v & kLbMask; --j; continue; }
-          uint32_t spins = 0;                          // chunk j not published yet
-          while (!(__hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (kLbInc | kLbAgg))) {
-            if (++spins > kLookbackSpin) { atomicOr((unsigned long long*)lb.ctl, 1ull); j = -1; break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        if (k) __hip_atomic_store(st, kLbInc | (pre + run), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w + 1 == whi) lb.ctl[1] = pre + run;
-      }
-      pre = (uint64_t)__shfl((long long)pre, 0, 64);
-      // this wave's scratch stores complete, then read back at L2
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const uint64_t s0 = (w - wlo) * CH;
-      for (int k = 0; k < lb.ncols; ++k)
-        for (uint32_t i = (uint32_t)lane; i < run; i += 64)
-          lb.dst[(uint64_t)k * lb.dcap + pre + i] =
-              __hip_atomic_load(out + (uint64_t)k * cap + s0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 
@@ -3878,68 +3744,28 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     DBuf<uint32_t> scr((uint64_t)nu * total, c.s);
     DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-    // DAS_FILT_PIPE=1: the software-pipelined walk (MODE 3, A/B);
-    // DAS_FILT_LOOKBACK=1: offsets by look-back, no compaction (MODE 4, A/B)
-    const char* fpe = std::getenv("DAS_FILT_PIPE");
-    const bool pipe = fpe && fpe[0] == '1';
-    const char* flb = std::getenv("DAS_FILT_LOOKBACK");
-    const bool lbk = !pipe && flb && flb[0] == '1';
-    const std::string md = pipe ? "3," : lbk ? "4," : "2,";
-    std::unique_ptr<Table> lout;
-    DBuf<uint32_t> tk;
-    DBuf<uint64_t> lst, lctl;
-    FiltLb lbarg{};
-    if (lbk) {
-      lout = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
-      tk.alloc(1, c.s);
-      lst.alloc(fchunks, c.s);
-      lctl.alloc(2, c.s);
-      fill_dev(tk.p, 0, 4, c.s);
-      fill_dev(lst.p, 0, 8 * fchunks, c.s);
-      fill_dev(lctl.p, 0, 16, c.s);
-      lbarg = FiltLb{tk.p, lst.p, lctl.p, lout->data, lout->cap, nu};
-    }
-    const std::string nm = spec ? "k_dj_filt<" + md + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
-                                : "k_dj_filt<" + md + "-1,-1,1024,4>";
+    const std::string nm = spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
+                                : std::string("k_dj_filt<2,-1,-1,1024,4>");
     {
       // per probe row its row id, (first, count) and probe columns; per
       // output its build value (a P row); kept outputs' columns written
       ProfScope ps(c, nm, (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
-#define FILT_L(MD, NPV, NBV)                                                                                    \
-  hipLaunchKernelGGL((k_dj_filt<MD, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
-                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,              \
-                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks, lbarg)
-      if (lbk) {
-        if (jc.np == 1 && jc.nb == 1) FILT_L(4, 1, 1);
-        else if (jc.np == 2 && jc.nb == 1) FILT_L(4, 2, 1);
-        else if (jc.np == 1 && jc.nb == 2) FILT_L(4, 1, 2);
-        else FILT_L(4, -1, -1);
-      } else if (pipe) {
-        if (jc.np == 1 && jc.nb == 1) FILT_L(3, 1, 1);
-        else if (jc.np == 2 && jc.nb == 1) FILT_L(3, 2, 1);
-        else if (jc.np == 1 && jc.nb == 2) FILT_L(3, 1, 2);
-        else FILT_L(3, -1, -1);
-      } else {
-        if (jc.np == 1 && jc.nb == 1) FILT_L(2, 1, 1);
-        else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 2, 1);
-        else if (jc.np == 1 && jc.nb == 2) FILT_L(2, 1, 2);
-        else FILT_L(2, -1, -1);
-      }
+#define FILT_L(NPV, NBV)                                                                                       \
+  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
+                     0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
+                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks)
+      if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
+      else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
+      else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
+      else FILT_L(-1, -1);
 #undef FILT_L
       DAS_HIP(hipGetLastError());
     }
-    uint64_t hctl[2] = {1, 0};
-    if (lbk) {
-      DAS_HIP(hipMemcpyAsync(hctl, lctl.p, 16, hipMemcpyDeviceToHost, c.s));
-      DAS_HIP(hipStreamSynchronize(c.s));
-    }
-    // MODE 4 without a look-back timeout: the rows are in place
-    const bool placed = lbk && hctl[0] == 0;
-    const uint64_t m = placed ? hctl[1] : scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);
+    const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);
     prof_add_bytes(c, nm, 4.0 * nu * m);
-    auto out = lbk ? std::move(lout) : new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
+    auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
     out->nrows = m;
-    if (m && !placed) {
+    if (m) {
       KScope ks("k_chunk_compact<1024>", 8.0 * nu * m + 8.0 * fchunks);
       hipLaunchKernelGGL(k_chunk_compact<1024>, dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
                          (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, 0ull, fchunks, nu, out->data, out->cap);
@@ -3970,7 +3796,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_0(CHV)                                                                                                \
   hipLaunchKernelGGL((k_dj_filt<0, -1, -1, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows,   \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p, ccnt.p, \
-                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks, FiltLb{})
+                     (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks)
     // DAS_FILT_UNROLL (8 / 16): rounds of 64 outputs whose build values and
     // bitmap words are loaded together in the flag pass (A/B; default 4)
     static const int xu = [] {
@@ -3983,11 +3809,11 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     else if (xu == 8)
       hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 8>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
                          A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
-                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks, FiltLb{});
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks);
     else if (xu == 16)
       hipLaunchKernelGGL((k_dj_filt<0, -1, -1, 1024, 16>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
                          A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,
-                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks, FiltLb{});
+                         fl.p, ccnt.p, (const uint32_t*)nullptr, jc, (uint32_t*)nullptr, 0ull, 0ull, fchunks);
     else FILT_0(1024);
 #undef FILT_0
     DAS_HIP(hipGetLastError());
@@ -4006,7 +3832,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
 #define FILT_W(NPV, NBV, CHV)                                                                                  \
   hipLaunchKernelGGL((k_dj_filt<1, NPV, NBV, CHV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, fl.p,      \
-                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap, 0ull, fchunks, FiltLb{})
+                     (uint32_t*)nullptr, (const uint32_t*)coff.p, jc, out->data, out->cap, 0ull, fchunks)
 #define FILT_WC(CHV)                                    \
   if (jc.np == 1 && jc.nb == 1) FILT_W(1, 1, CHV);      \
   else if (jc.np == 2 && jc.nb == 1) FILT_W(2, 1, CHV); \

@@ -553,7 +553,7 @@ def test_gpu_hub_four_clause_matches_oracle(semi, monkeypatch):
         assert same(got, want), (name, got.get("n"), want.get("n"))
 
 
-@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "1-pipe", "1-lookback", "0"])
+@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "0"])
 def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     """Runs of one-variable hub clauses on one variable (T2(V2,a), T3(V2,b),
     ...) folded by ONE filter with the intersection of their key sets
@@ -566,11 +566,7 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     from das_amd import synthetic
     monkeypatch.setenv("DAS_SEMI_MULTI", multi[0])
     # the filtered expansion in one pass with LDS flag tiles (unsorted) ...
-    monkeypatch.setenv("DAS_FILT_FUSED", "0" if multi in ("1-twopass", "1-local", "1-pipe", "1-lookback") else "1")
-    # ... with the one walk software-pipelined (k_dj_filt<3>) or placing its
-    # rows by a decoupled look-back (k_dj_filt<4>)
-    monkeypatch.setenv("DAS_FILT_PIPE", "1" if multi == "1-pipe" else "0")
-    monkeypatch.setenv("DAS_FILT_LOOKBACK", "1" if multi == "1-lookback" else "0")
+    monkeypatch.setenv("DAS_FILT_FUSED", "0" if multi in ("1-twopass", "1-local") else "1")
     # ... as one walk writing chunk-locally + a compaction (k_dj_filt<2>,
     # default) or as a flag pass and a second walk
     monkeypatch.setenv("DAS_FILT_LOCAL", "0" if multi == "1-twopass" else "1")
