@@ -1520,11 +1520,23 @@ __global__ void __launch_bounds__(kSmallBlock) k_compact_small(Pred pred, uint64
   if (threadIdx.x == 0) publish_u32(slot, seq, s_run);
 }
 
+// Marks tile 0's count when *guard is set (a condition the host would
+// otherwise read back before the count): the count's read-back then carries it.
+__global__ void k_guard_count(uint32_t* tcnt, const uint32_t* guard) {
+  if (threadIdx.x == 0 && *guard) tcnt[0] |= 0x80000000u;
+}
+
+// guard (optional): a device flag that voids the compaction (nullptr returned),
+// checked with the count's read-back instead of a read-back of its own
 template <typename Pred>
 std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const char* prof = nullptr,
-                                    double pred_bytes = 4.0) {
+                                    double pred_bytes = 4.0, const uint32_t* guard = nullptr) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
+  if (guard && (n <= kSmallScan || n >= (1ull << 31))) {   // one launch / wide counts: read it first
+    if (read_u32(guard, c.s)) return nullptr;
+    guard = nullptr;
+  }
   if (n <= kSmallScan) {
     auto t = new_table_like(c, a, n);
     const PubSlot ps = pub_reserve();
@@ -1546,7 +1558,13 @@ std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const cha
     hipLaunchKernelGGL((k_tile_count<Pred>), dim3((unsigned)tiles), dim3(kScanBlock), 0, c.s, pred, n, tcnt.p, fl.p);
     DAS_HIP(hipGetLastError());
   }
-  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{tcnt.p}, tiles, toff.p, c.s);
+  if (guard) {
+    hipLaunchKernelGGL(k_guard_count, dim3(1), dim3(64), 0, c.s, tcnt.p, guard);
+    DAS_HIP(hipGetLastError());
+  }
+  uint64_t mx = 0;
+  const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{tcnt.p}, tiles, toff.p, c.s, &mx);
+  if (guard && mx >= 0x80000000ull) return nullptr;
   auto t = new_table_like(c, a, m);
   t->nrows = m;
   if (m && a.ncols) {
@@ -3545,10 +3563,10 @@ std::unique_ptr<Table> semi_join(Ctx& c, const Table& P, const Table& Q) {
                        bits.p, bits.p + words);
     DAS_HIP(hipGetLastError());
   }
-  if (read_u32(bits.p + words, c.s)) return nullptr;       // duplicate keys: counts matter
-  // the probe is the compaction's predicate: no flag array
+  // the probe is the compaction's predicate: no flag array; duplicate keys
+  // (counts matter: nullptr, the caller joins) are read back with the count
   return compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), lo, (uint32_t)range, (const uint32_t*)bits.p},
-                      "k_tile_count<BitsPred>", 4.0);
+                      "k_tile_count<BitsPred>", 4.0, (const uint32_t*)bits.p + words);
 }
 
 // Several one-variable build sides on the same variable (consecutive terms of
