@@ -3604,27 +3604,27 @@ bool key_bits(Ctx& c, const std::vector<const Table*>& Qs, int32_t var, uint64_t
   const uint64_t words = (range + 31) / 32;
   acc.alloc(words + 1, c.s);                                // + the duplicate flag
   DBuf<uint32_t> one(Qs.size() > 1 ? words + 1 : 1, c.s);
+  // every term's duplicate-key flag goes to acc[words]: one read-back at the end
   for (size_t i = 0; i < Qs.size(); ++i) {
     uint32_t* bits = i == 0 ? acc.p : one.p;
-    fill_dev(bits, 0, 4 * (words + 1), c.s);
+    fill_dev(bits, 0, 4 * (i == 0 ? words + 1 : words), c.s);
     {
       ProfScope ps(c, "join_build", 4.0 * Qs[i]->nrows + 4.0 * words);
       if (Qs[i]->sorted_col == 0)
         hipLaunchKernelGGL(k_bits_set_sorted, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
-                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, bits + words);
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, acc.p + words);
       else
         hipLaunchKernelGGL(k_bits_set, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
-                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, bits + words);
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, acc.p + words);
       DAS_HIP(hipGetLastError());
     }
-    if (read_u32(bits + words, c.s)) return false;          // duplicate keys: counts matter
     if (i) {
       KScope ks("k_bits_and", 12.0 * words);
       hipLaunchKernelGGL(k_bits_and, G(words), dim3(B), 0, c.s, acc.p, (const uint32_t*)one.p, words);
       DAS_HIP(hipGetLastError());
     }
   }
-  return true;
+  return read_u32(acc.p + words, c.s) == 0;                  // duplicate keys: counts matter
 }
 
 std::unique_ptr<Table> semi_join_multi(Ctx& c, const Table& P, const std::vector<const Table*>& Qs) {
