@@ -646,6 +646,59 @@ __global__ void k_pack_lc(const uint32_t* off, uint32_t range, uint2* lc) {
     lc[d] = make_uint2(off[d], off[d + 1] - off[d]);
 }
 
+// Sparse build keys over a wide slot range (bio QUERY_3: ~2*10^4 rows keyed
+// by Member link ids over 1.4*10^7 slots): the (lo, cnt) descriptors are
+// written straight into a zeroed lc array -- one 8-byte store stream per
+// slot -- instead of a histogram, a scan, a copy and the packing of range+1
+// offsets (~5x the slot bytes).  Counts by wave-aggregated atomics on
+// lc[d].y (each row keeps its rank inside its key); sorted keys take their
+// run start as lo, unsorted ones get a base per key from one atomic per wave
+// (k_lc_base) and are scattered by (base + rank) (k_lc_scatter).
+__global__ void __launch_bounds__(B) k_lc_count(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t range,
+                                                uint2* lc, uint32_t* rank, int sorted) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {   // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t k = i < n ? key[i] : 0u;
+    const uint32_t d = i < n ? k - kmin : range;
+    const bool act = d < range;
+    const uint32_t r = wave_agg_atomic_inc(reinterpret_cast<uint32_t*>(lc) + 1, act ? 2u * d : 0u, act);
+    if (!act) continue;
+    if (sorted) {
+      if (i == 0 || key[i - 1] != k) lc[d].x = (uint32_t)i;
+    } else {
+      rank[i] = r;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(B) k_lc_base(const uint32_t* key, const uint32_t* rank, uint64_t n, uint32_t kmin,
+                                               uint32_t range, uint2* lc, uint32_t* total) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t d = i < n ? key[i] - kmin : range;
+    const uint32_t v = (d < range && rank[i] == 0u) ? lc[d].y : 0u;   // one row per key claims its run
+    const uint32_t inc = wave_incl_sum_u32(v);
+    const uint32_t sum = __shfl(inc, 63, 64);
+    uint32_t base = 0;
+    if (__lane_id() == 63 && sum) base = atomicAdd(total, sum);
+    base = __shfl(base, 63, 64);
+    if (v) lc[d].x = base + inc - v;
+  }
+}
+
+__global__ void __launch_bounds__(B) k_lc_scatter(ColSet src, const uint32_t* key, const uint32_t* rank, uint64_t n,
+                                                  uint32_t kmin, uint32_t range, const uint2* lc, uint32_t* out,
+                                                  uint64_t cap) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = key[i] - kmin;
+    if (d >= range) continue;
+    const uint64_t pos = (uint64_t)lc[d].x + rank[i];
+    for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
+  }
+}
+
 // Probe = wave units of kXRows consecutive probe rows (kXGroups groups of 64,
 // one row per lane).  No LDS arrays and no block barriers: a unit's counts,
 // prefix and expansion live in registers; each output chunk of 64 finds its
@@ -1491,12 +1544,17 @@ struct FlagPred {
 // the kept count published to the pinned slot.
 template <typename Pred>
 __global__ void __launch_bounds__(kSmallBlock) k_compact_small(Pred pred, uint64_t n, ColSet src, uint32_t* out,
-                                                               uint64_t cap, uint32_t* slot, uint32_t seq) {
+                                                               uint64_t cap, uint32_t* slot, uint32_t seq,
+                                                               const uint32_t* guard) {
   constexpr int W = kSmallBlock / 64;
   __shared__ uint32_t s_w[W];
   __shared__ uint32_t s_run;
   const int wave = threadIdx.x >> 6;
   const uint64_t lt = __lanemask_lt();
+  if (guard && *guard) {                      // voided (block-uniform): the count says so
+    if (threadIdx.x == 0) publish_u32(slot, seq, 0xFFFFFFFFu);
+    return;
+  }
   if (threadIdx.x == 0) s_run = 0;
   __syncthreads();
   for (uint64_t r0 = 0; r0 < n; r0 += kSmallBlock) {
@@ -1533,18 +1591,19 @@ std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const cha
                                     double pred_bytes = 4.0, const uint32_t* guard = nullptr) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
-  if (guard && (n <= kSmallScan || n >= (1ull << 31))) {   // one launch / wide counts: read it first
+  if (guard && n >= (1ull << 31)) {             // wide counts: read it first
     if (read_u32(guard, c.s)) return nullptr;
     guard = nullptr;
   }
-  if (n <= kSmallScan) {
+  if (n <= kSmallScan) {                          // one launch; the guard rides on its count
     auto t = new_table_like(c, a, n);
     const PubSlot ps = pub_reserve();
     hipLaunchKernelGGL((k_compact_small<Pred>), dim3(1), dim3(kSmallBlock), 0, c.s, pred, n, cols_of(a), t->data,
-                       t->cap, ps.p, ps.seq);
+                       t->cap, ps.p, ps.seq, guard);
     DAS_HIP(hipGetLastError());
     uint32_t m = 0;
     pub_wait(ps, c.s, &m, 1);
+    if (m == 0xFFFFFFFFu) return nullptr;
     t->nrows = m;
     return t;
   }
@@ -2104,11 +2163,48 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
       range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
   const uint32_t kmin = h[0];
+  std::unique_ptr<Table> Qs;
+  const Table* Qb = &Q;
+  // the (lo, cnt) descriptor of every key slot; one more entry holds the
+  // sparse build's running base
+  DBuf<uint2> lc(range + 1, c.s);
+  auto expand = [&](const Table& Qb, const uint2* lcp) {
+    const int nu = (int)uni.size();
+    JoinCols jc{};
+    for (int k = 0; k < nu; ++k) {
+      const int ip = colof(P, uni[k]);
+      if (ip >= 0) { jc.p[jc.np] = P.col(ip); jc.po[jc.np++] = k; }
+      else { jc.b[jc.nb] = Qb.col(colof(Qb, uni[k])); jc.bo[jc.nb++] = k; }
+    }
+    return dj_expand(c, P, pkey, kmin, range, lcp, jc, nu, uni.data(), 4.0 * Q.nrows * Q.ncols);
+  };
+  const char* bm = std::getenv("DAS_DJ_BUILD");   // A/B, tests: "dense" never, "sparse" whenever it fits
+  const bool sparse = range < (1ull << 31) &&
+      (bm && !std::strcmp(bm, "sparse") ? true
+       : bm && !std::strcmp(bm, "dense") ? false : range > 16 * Q.nrows && range >= (1ull << 20));
+  if (sparse) {
+    // few build rows over a wide slot range: descriptors written in place
+    const bool srt = Q.sorted_col == qk;
+    ProfScope ps(c, "join_build", (srt ? 4.0 : 8.0 + 8.0 * Q.ncols) * Q.nrows + 8.0 * range);
+    fill_dev(lc.p, 0, 8 * (range + 1), c.s);
+    DBuf<uint32_t> rk(srt ? 1 : Q.nrows, c.s);
+    hipLaunchKernelGGL(k_lc_count, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lc.p, rk.p,
+                       srt ? 1 : 0);
+    if (!srt) {
+      hipLaunchKernelGGL(k_lc_base, G(Q.nrows), dim3(B), 0, c.s, qkey, rk.p, Q.nrows, kmin, (uint32_t)range, lc.p,
+                         reinterpret_cast<uint32_t*>(lc.p + range));
+      Qs = new_table_like(c, Q, Q.nrows);
+      Qs->nrows = Q.nrows;
+      hipLaunchKernelGGL(k_lc_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, rk.p, Q.nrows, kmin,
+                         (uint32_t)range, lc.p, Qs->data, Qs->cap);
+      Qb = Qs.get();
+    }
+    DAS_HIP(hipGetLastError());
+    return expand(*Qb, lc.p);
+  }
   // bucket offsets of the build side: already grouped by key when it comes
   // sorted (an order-aware scan), else a counting sort
   DBuf<uint32_t> off(range + 1, c.s);
-  std::unique_ptr<Table> Qs;
-  const Table* Qb = &Q;
   if (Q.sorted_col == qk && range <= 4 * Q.nrows) {
     ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * range);
     hipLaunchKernelGGL(k_bucket_bounds, G(range + 1), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, off.p);
@@ -2136,19 +2232,10 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     DAS_HIP(hipGetLastError());
     Qb = Qs.get();
   }
-  const int nu = (int)uni.size();
-  JoinCols jc{};
-  for (int k = 0; k < nu; ++k) {
-    const int ip = colof(P, uni[k]);
-    if (ip >= 0) { jc.p[jc.np] = P.col(ip); jc.po[jc.np++] = k; }
-    else { jc.b[jc.nb] = Qb->col(colof(*Qb, uni[k])); jc.bo[jc.nb++] = k; }
-  }
-  DBuf<uint2> lc(range, c.s);
   hipLaunchKernelGGL(k_pack_lc, dim3(grid_for(range, B, 2048)), dim3(B), 0, c.s, (const uint32_t*)off.p,
                      (uint32_t)range, lc.p);
   DAS_HIP(hipGetLastError());
-  auto out = dj_expand(c, P, pkey, kmin, range, lc.p, jc, nu, uni.data(), 4.0 * Q.nrows * Q.ncols);
-  return out;
+  return expand(*Qb, lc.p);
 }
 
 // ---------------------------------------------------------------------------
