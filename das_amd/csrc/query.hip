@@ -2166,7 +2166,9 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   std::unique_ptr<Table> Qs;
   const Table* Qb = &Q;
   // the (lo, cnt) descriptor of every key slot; one more entry holds the
-  // sparse build's running base
+  // sparse build's running base.  The sparse build (fewer launches, ~8 B per
+  // slot instead of ~36) takes at most 2^18 build rows: its bases come from
+  // one atomic per wave on one counter
   DBuf<uint2> lc(range + 1, c.s);
   auto expand = [&](const Table& Qb, const uint2* lcp) {
     const int nu = (int)uni.size();
@@ -2181,7 +2183,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   const char* bm = std::getenv("DAS_DJ_BUILD");   // A/B, tests: "dense" never, "sparse" whenever it fits
   const bool sparse = range < (1ull << 31) &&
       (bm && !std::strcmp(bm, "sparse") ? true
-       : bm && !std::strcmp(bm, "dense") ? false : range > 16 * Q.nrows && range >= (1ull << 20));
+       : bm && !std::strcmp(bm, "dense") ? false : range > 16 * Q.nrows && range >= (1ull << 16) && Q.nrows <= (1ull << 18));
   if (sparse) {
     // few build rows over a wide slot range: descriptors written in place
     const bool srt = Q.sorted_col == qk;
