@@ -45,20 +45,14 @@ def _atom_tables(db):
     return nodes, [[h, t, tg, ct(h)] for h, (t, tg) in links.items()]
 
 
-@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "1-sparse", "0"])
+@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "0"])
 @pytest.mark.parametrize("name", FIXTURES)
 def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
     """plan 1: And / Or / Not trees folded natively (das_plan_execute), small
     Ands fused into one launch; 1-unfused: the same without the fused chain;
     1-multi: Ors of Link scans always through the multi-segment scan +
-    dedup; 1-sparse: every direct-address join's build side written
-    straight into its key-slot descriptors (the wide-range path); plan 0:
-    the per-operator host path."""
+    dedup; plan 0: the per-operator host path."""
     monkeypatch.setenv("DAS_PLAN", plan[0])
-    if plan == "1-sparse":
-        monkeypatch.setenv("DAS_DJ_BUILD", "sparse")
-    else:
-        monkeypatch.delenv("DAS_DJ_BUILD", raising=False)
     monkeypatch.setenv("DAS_FUSED", "0" if plan == "1-unfused" else "1")
     monkeypatch.setenv("DAS_UNION_MULTI", "1" if plan == "1-multi" else "0")
     from das_amd.database.hip_db import HipDB

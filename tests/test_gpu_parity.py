@@ -451,19 +451,12 @@ def test_gpu_composite_algebra_matches_oracle(tuple_targets):
         assert same(got, want), (q, got, {k: want.get(k) for k in ("error", "matched", "negation", "n")})
 
 
-@pytest.mark.parametrize("build", ["", "sparse"])
 @pytest.mark.parametrize("force", ["0", "1", ""])
-def test_gpu_hub_join_expansion(force, build, monkeypatch):
+def test_gpu_hub_join_expansion(force, monkeypatch):
     """A hub key whose probe unit owns > 64K outputs (config 5 skew): the
     output-balanced expansion, the per-unit expansion (forced) and the
-    automatic choice all equal the oracle; "sparse": the build side's
-    key-slot descriptors written in place (a 300-row hub key's ranks from
-    the wave-aggregated atomics)."""
+    automatic choice all equal the oracle."""
     from das_amd import synthetic
-    if build:
-        monkeypatch.setenv("DAS_DJ_BUILD", build)
-    else:
-        monkeypatch.delenv("DAS_DJ_BUILD", raising=False)
     if force:
         monkeypatch.setenv("DAS_DJ_BALANCED", force)
     else:
