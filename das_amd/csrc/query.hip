@@ -1591,7 +1591,8 @@ std::unique_ptr<Table> compact_pred(Ctx& c, const Table& a, Pred pred, const cha
                                     double pred_bytes = 4.0, const uint32_t* guard = nullptr) {
   const uint64_t n = a.nrows;
   if (!n) return gather_table(c, a, nullptr, 0);
-  static const bool fused_guard = std::getenv("DAS_SMALL_GUARD") != nullptr;   // opt-in until measured
+  const char* sg = std::getenv("DAS_SMALL_GUARD");        // A/B: 0 = read the guard first
+  const bool fused_guard = !(sg && sg[0] == '0');
   if (guard && (n >= (1ull << 31) || (n <= kSmallScan && !fused_guard))) {   // read it first
     if (read_u32(guard, c.s)) return nullptr;
     guard = nullptr;
@@ -2181,10 +2182,10 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     }
     return dj_expand(c, P, pkey, kmin, range, lcp, jc, nu, uni.data(), 4.0 * Q.nrows * Q.ncols);
   };
-  // opt-in (DAS_DJ_BUILD=sparse) until measured on the GPU; the default
-  // gate to take then: range > 16 * Q.nrows, range >= 2^16, Q.nrows <= 2^18
-  const char* bm = std::getenv("DAS_DJ_BUILD");
-  const bool sparse = range < (1ull << 31) && bm && !std::strcmp(bm, "sparse");
+  const char* bm = std::getenv("DAS_DJ_BUILD");   // A/B, tests: "dense" never, "sparse" whenever it fits
+  const bool sparse = range < (1ull << 31) &&
+      (bm && !std::strcmp(bm, "sparse") ? true
+       : bm && !std::strcmp(bm, "dense") ? false : range > 16 * Q.nrows && range >= (1ull << 16) && Q.nrows <= (1ull << 18));
   if (sparse) {
     // few build rows over a wide slot range: descriptors written in place
     const bool srt = Q.sorted_col == qk;
