@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--materialise-cap", type=int, default=2_000_000,
                     help="largest answer whose Python objects the materialisation-inclusive figure builds")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile of 3 extra steps here")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the full record (kernel tables, join variants, materialisation); the last stdout "
+                         "line is the compact <= 4 KB summary")
     return ap.parse_args()
 
 
@@ -695,7 +698,7 @@ def run_load(args, rank, world, local_rank):
         out["cpu_baseline"] = {"value": n * reps / dt, "unit": "links/s", "cores": 1, "kind": "port",
                                "sample": f"loader.parse_canonical + oracle md5 hashing of a {len(small)} B "
                                          f"FlyBase-shaped text ({n} links), {reps} passes in {dt:.1f} s"}
-    print(json.dumps(out))
+    emit(out, args.detail)
 
 
 # kernel scopes that are scratch, not algorithmic bytes (sort
@@ -910,6 +913,110 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     return out
 
 
+# ---------------------------------------------------------------------------
+# output: one compact JSON line last on stdout (the driver parses it from a
+# bounded stdout tail), the full record in a detail file
+# ---------------------------------------------------------------------------
+LINE_MAX_BYTES = 4096
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data")
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def _compact_roofline(r, full=True):
+    if not r:
+        return None
+    keys = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "avg_launch_us") if full else \
+        ("kernel", "frac", "achieved")
+    out = {k: _r(r.get(k)) for k in keys if k in r}
+    if full and isinstance(out.get("traffic"), float):
+        out["traffic"] = int(out["traffic"])
+    return out
+
+
+def _compact_cpu(c, full=True):
+    if not c:
+        return None
+    if not full:
+        return {"value": _r(c.get("value"), 1)}
+    out = {k: _r(c.get(k), 1) for k in ("value", "unit", "cores", "kind") if k in c}
+    out["sample"] = (c.get("sample") or "")[:240]
+    return out
+
+
+def _compact_leg(d):
+    if "error" in d:
+        return {"error": str(d["error"])[:200]}
+    out = {k: _r(d.get(k)) for k in ("value", "unit", "ms_per_step") if k in d}
+    out["roofline"] = _compact_roofline(d.get("roofline"), full=False)
+    sr = d.get("step_roofline")
+    out["step_roofline"] = {"frac": sr.get("frac")} if sr else None
+    out["cpu_baseline"] = _compact_cpu(d.get("cpu_baseline"), full=False)
+    for k in ("latency", "summary"):          # latency-bound legs: per-query us, launches / read-backs
+        if d.get(k) is not None:
+            out[k] = d[k]
+    return out
+
+
+def compact_line(full):
+    """The ONE JSON line bench.py ends its stdout with: the headline's
+    contract keys, its roofline / step_roofline / cpu_baseline, and per extra
+    workload only value, unit, ms_per_step, roofline {kernel, frac, achieved},
+    step_roofline.frac and cpu_baseline.value (plus a latency leg's compact
+    summary).  Kernel tables, join variants and materialisation detail stay in
+    the detail file.  Guaranteed <= LINE_MAX_BYTES: optional parts are
+    dropped, largest first, if a record ever grows past it."""
+    line = {k: _r(full.get(k)) for k in HEAD_KEYS if k in full}
+    cfg = full.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "parallelism") if k in cfg}
+    line["roofline"] = _compact_roofline(full.get("roofline"))
+    line["step_roofline"] = _compact_roofline(full.get("step_roofline"))
+    line["cpu_baseline"] = _compact_cpu(full.get("cpu_baseline"))
+    for k in ("latency", "summary"):
+        if full.get(k) is not None:
+            line[k] = full[k]
+    if full.get("workloads"):
+        line["workloads"] = {w: _compact_leg(d) for w, d in full["workloads"].items()}
+    line["detail"] = full.get("detail_file")
+    s = json.dumps(line, separators=(",", ":"))
+    # never exceed the bound: shed the optional parts, then shorten the strings
+    for drop in (("workloads", "summary"), ("workloads", "latency"), ("summary",), ("latency",), ("data",)):
+        if len(s.encode()) <= LINE_MAX_BYTES:
+            break
+        if len(drop) == 2:
+            for leg in (line.get("workloads") or {}).values():
+                leg.pop(drop[1], None)
+        else:
+            line.pop(drop[0], None)
+        s = json.dumps(line, separators=(",", ":"))
+    if len(s.encode()) > LINE_MAX_BYTES and line.get("cpu_baseline"):
+        line["cpu_baseline"]["sample"] = line["cpu_baseline"]["sample"][:60]
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def emit(full, detail_path):
+    """Write the full record to `detail_path` (and a one-line-per-leg summary
+    to stderr), then print the compact line as the LAST stdout line."""
+    if detail_path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail_path)), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(full, f)
+            full["detail_file"] = os.path.relpath(os.path.abspath(detail_path), ROOT)
+        except OSError as e:
+            log(f"detail file not written: {e}")
+    for name, d in [("headline", full)] + list((full.get("workloads") or {}).items()):
+        r = d.get("roofline") or {}
+        log(f"{name}: value {d.get('value')} {d.get('unit')} ms/step {d.get('ms_per_step')} "
+            f"roofline {r.get('kernel')} {r.get('frac')}")
+    sys.stdout.flush()
+    print(compact_line(full), flush=True)
+
+
 def _free_device():
     import gc
     import torch
@@ -982,7 +1089,7 @@ def main():
         if extra:
             line["workloads"] = extra
             line["headline_wall_s"] = round(time.perf_counter() - t_head, 1)
-        print(json.dumps(line))
+        emit(line, args.detail)
     if dist:
         dist.destroy_process_group()
 
