@@ -3849,8 +3849,28 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   // profiles/r3_hub_local_ab.json)
   const char* fle = std::getenv("DAS_FILT_LOCAL");
   const bool local = !(fle && fle[0] == '0');
-  if (local && ch == 1024 && (uint64_t)nu * total * 4 <= (16ull << 30)) {
-    DBuf<uint32_t> scr((uint64_t)nu * total, c.s);
+  // its scratch holds every virtual output's columns (4 nu B each, against one
+  // flag byte per output for the two passes): taken while that stays within
+  // 16 GiB and half the device's free memory, and falls back to the two
+  // passes when the allocation fails (DAS_FILT_SCRATCH_MAX caps it, tests)
+  const uint64_t scr_bytes = (uint64_t)nu * total * 4;
+  const char* sme = std::getenv("DAS_FILT_SCRATCH_MAX");
+  const uint64_t scr_cap = sme ? std::strtoull(sme, nullptr, 10) : (16ull << 30);
+  bool fits = local && ch == 1024 && scr_bytes <= scr_cap;
+  if (fits && scr_bytes > (1ull << 30)) {
+    size_t fr = 0, tot = 0;
+    fits = hipMemGetInfo(&fr, &tot) == hipSuccess && scr_bytes <= fr / 2;
+  }
+  DBuf<uint32_t> scr;
+  if (fits) {
+    try {
+      scr.alloc((uint64_t)nu * total, c.s);
+    } catch (const Error&) {
+      (void)hipGetLastError();
+      fits = false;                                   // out of memory: the two passes below
+    }
+  }
+  if (fits) {
     DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
     const std::string nm = spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"

@@ -290,17 +290,41 @@ class HipDB(RelationalDB):
         if link_type != WILDCARD and WILDCARD not in target_handles:
             h = self.get_link_handle(link_type, target_handles)
             return [h] if self._exists(h, len(target_handles)) else []
+        t = self.matched_links_table(link_type, target_handles)
+        return self._pairs(t, len(target_handles)) if t is not None else []
+
+    # the (link, t0 .. t_{a-1}) id rows behind get_matched_links /
+    # get_matched_type_template / get_matched_type, before formatting (a
+    # sharded DB gathers these from every shard, parallel.ShardedDB)
+    def matched_links_table(self, link_type, target_handles):
+        """Rows of the pattern key (link_type, target_handles) with at least
+        one wildcard; None when the key cannot match (unknown type / target)."""
         if link_type in UNORDERED_LINK_TYPES:
             target_handles = sorted(target_handles)
         arity = len(target_handles)
         ttype = self._type_or_empty(link_type)
         if ttype is False:
-            return []
+            return None
         tids = self._target_ids(target_handles)
         if tids is None:
-            return []
-        t = self.ctx.scan_link(arity, ttype, tids, list(range(arity)), 0, True, False, True)
-        return self._pairs(t, arity)
+            return None
+        return self.ctx.scan_link(arity, ttype, tids, list(range(arity)), 0, True, False, True)
+
+    def matched_template_table(self, template):
+        """Rows of templates:<composite type of `template`> (len >= 2); None
+        when no link has that composite type."""
+        ct, _ = self._template_ctype(template)
+        if ct < 0:
+            return None
+        arity = len(template) - 1
+        return self.ctx.scan_template(ct, arity, list(range(arity)), True, False, True)
+
+    def matched_type_tables(self, link_type):
+        """{arity: rows} of templates:<named_type_hash(link_type)>."""
+        tid = self.type_id.get(link_type)
+        if tid is None:
+            return {}
+        return {a: t for a, t in enumerate(self.ctx.scan_type(tid)) if t is not None}
 
     def _pairs(self, t, arity):
         cols = t.fetch()
@@ -333,24 +357,17 @@ class HipDB(RelationalDB):
 
     def get_matched_type_template(self, template: List[Any]) -> List[str]:
         """redis_mongo_db.py:269-275 (templates:<composite_type_hash>)"""
-        ct, named = self._template_ctype(template)
-        if named is not None:
+        if len(template) == 1:
+            self._template_ctype(template)          # the reference's TypeError for a non-str element
             return self.get_matched_type(template[0])
-        if ct < 0:
-            return []
-        arity = len(template) - 1
-        t = self.ctx.scan_template(ct, arity, list(range(arity)), True, False, True)
-        return self._pairs(t, arity)
+        t = self.matched_template_table(template)
+        return self._pairs(t, len(template) - 1) if t is not None else []
 
     def get_matched_type(self, link_type: str) -> List[str]:
         """redis_mongo_db.py:277-279 (templates:<named_type_hash>)"""
-        tid = self.type_id.get(link_type)
-        if tid is None:
-            return []
         out = []
-        for a, t in enumerate(self.ctx.scan_type(tid)):
-            if t is not None:
-                out += self._pairs(t, a)
+        for a, t in self.matched_type_tables(link_type).items():
+            out += self._pairs(t, a)
         return out
 
     def get_node_name(self, node_handle: str) -> str:

@@ -209,17 +209,62 @@ class ShardedDB(RelationalDB):
     def is_ordered(self, handle):
         return self.local.is_ordered(handle)
 
+    # The pattern / template families of a sharded KB: each shard holds the
+    # index rows of the links it owns, so a lookup scans every shard's rows of
+    # the key and gathers them -- the reference reads the same families from
+    # a Redis Cluster whose key slots are spread over nodes
+    # (redis_mongo_db.py:235-279, distributed_atom_space.py:48-61, 259-284).
+    # Every rank calls these together (SPMD) and every rank gets the whole
+    # answer, sorted by link id (the reference returns a Redis set: no order).
+    def _gather_pairs(self, tables):
+        """{arity: local (link, t0..t_{a-1}) table or None} -> [(handle,
+        targets)] of every shard's rows.  The arities present anywhere are
+        agreed first (one all-reduce), then one all-gather per arity present."""
+        have = np.zeros(9, dtype=np.int64)
+        for a, t in tables.items():
+            if t is not None:
+                have[a] = t.nrows
+        got = self._allreduce_sum(have) if self.world > 1 else have
+        out = []
+        fmt = tuple if self.tuple_targets else list
+        for a in range(9):
+            if int(got[a]) == 0:
+                continue
+            t = tables.get(a)
+            if t is None:
+                t = self.local.empty_table(ORDERED, [-1] + list(range(a)))
+            cols = self._gather_all(t).fetch()
+            if cols.shape[1] == 0:
+                continue
+            cols = cols[:, np.argsort(cols[0], kind="stable")]
+            links = self.local.hex_of(cols[0])
+            tg = [self.local.hex_of(cols[1 + k]) for k in range(a)]
+            out += [(links[i], fmt([tg[k][i] for k in range(a)])) for i in range(cols.shape[1])]
+        return out
+
     def get_matched_links(self, link_type, target_handles):
-        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+        """redis_mongo_db.py:235-252 over every shard: a grounded key is a
+        directory lookup (every shard holds the whole atom directory); a key
+        with a wildcard gathers every shard's rows of the pattern key."""
+        if link_type != WILDCARD and WILDCARD not in target_handles:
+            return self.local.get_matched_links(link_type, target_handles)
+        t = self.local.matched_links_table(link_type, list(target_handles))
+        return self._gather_pairs({len(target_handles): t})
 
     def get_all_nodes(self, node_type, names=False):
         return self.local.get_all_nodes(node_type, names)
 
     def get_matched_type_template(self, template):
-        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+        """redis_mongo_db.py:269-275 over every shard (templates:<ctype>)."""
+        if len(template) == 1:
+            return self.get_matched_type(template[0])
+        t = self.local.matched_template_table(list(template))
+        return self._gather_pairs({len(template) - 1: t})
 
-    def get_matched_type(self, link_named_type):
-        raise NotImplementedError("use the pattern matcher on a ShardedDB")
+    def get_matched_type(self, link_type):
+        """redis_mongo_db.py:277-279 over every shard (templates:<type>)."""
+        tables = self.local.matched_type_tables(link_type)
+        return self._gather_pairs({a: tables.get(a) for a in range(9)})
 
     def get_node_name(self, node_handle):
         return self.local.get_node_name(node_handle)
@@ -370,6 +415,8 @@ class ShardedDB(RelationalDB):
         # a term whose rows may repeat ('*' type, repeated variable) is deduplicated after
         tables = [ctx.scan_words(nodes, i) for i in gathered]
         inputs = self._gather_many(tables, [M[i] for i in gathered]) if gathered else []
+        if inputs is None:
+            return None                                  # an estimate below the rows: the operator fold
         inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(gathered, inputs)]
         words = nodes.copy().reshape(n, W)
         for slot, i in enumerate(gathered):
@@ -486,11 +533,26 @@ class ShardedDB(RelationalDB):
         v = int(np.int32(words[s0 + 10 + p]))
         return v if v >= 0 else None
 
+    def get_link_type(self, link_handle):
+        return self.local.get_link_type(link_handle)
+
+    def get_node_type(self, node_handle):
+        return self.local.get_node_type(node_handle)
+
+    def get_atom_as_dict(self, handle, arity=-1):
+        return self.local.get_atom_as_dict(handle, arity)
+
+    def get_atom_as_deep_representation(self, handle, arity=-1):
+        return self.local.get_atom_as_deep_representation(handle, arity)
+
+    OVER = 0xFFFFFFFF                     # _gather_many header: rows over the slot
+
     def _gather_many(self, tables, caps):
         """Every shard's rows of each table, to every shard, in ONE
         all-gather: per shard a header (row count and column bounds per
         table) and each table's rows (row-major) in a slot of `caps[j]` rows
-        (caps: the largest estimate any shard reported, an upper bound)."""
+        (caps: the largest estimate any shard reported, an upper bound).
+        None on every shard when some shard's table exceeds its slot."""
         import torch
         lo_hi = [t.bounds() for t in tables]
         ncols = [max(len(t.vars), 1) for t in tables]
@@ -500,18 +562,21 @@ class ShardedDB(RelationalDB):
             offs.append(off)
             off += int(c) * k
         width = off
+        # a table with more rows than its slot (an estimate below the rows)
+        # is sent as the count OVER with no rows: every shard sees it after the
+        # all-gather and the plan falls back, on every shard alike
+        over = [t.nrows > int(c) for t, c in zip(tables, caps)]
         hdr = []
-        for t, (lo, hi) in zip(tables, lo_hi):
-            hdr += [t.nrows] + list(lo) + list(hi)
+        for t, (lo, hi), ov in zip(tables, lo_hi, over):
+            hdr += [self.OVER if ov else t.nrows] + list(lo) + list(hi)
         loc = self.local
         gpu = loc.gpu
         buf = torch.zeros(width, dtype=torch.int32, device=gpu)
         buf[:H] = torch.from_numpy(np.array(hdr, dtype=np.uint32).view(np.int32)).to(gpu)
         if not loc.stream_ordered:
             torch.cuda.current_stream().synchronize()
-        for t, o in zip(tables, offs):
-            if t.nrows:
-                assert t.nrows * len(t.vars) <= (width - o), "gather: estimate below the rows"
+        for t, o, ov in zip(tables, offs, over):
+            if t.nrows and not ov:
                 loc.db.ctx.export_rows(t, buf.data_ptr() + 4 * o)
         if not loc.stream_ordered:
             loc.db.ctx.sync()
@@ -523,6 +588,10 @@ class ShardedDB(RelationalDB):
         heads = out.view(self.world, width)[:, :H].cpu().numpy().view(np.uint32)
         if not loc.stream_ordered:
             torch.cuda.current_stream().synchronize()
+        cnt_cols = np.cumsum([0] + [1 + 2 * len(t.vars) for t in tables[:-1]])
+        if (heads[:, cnt_cols] == self.OVER).any():
+            self.plan_stats["gather_overflow"] = self.plan_stats.get("gather_overflow", 0) + 1
+            return None
         result = []
         h = 0
         for j, (t, o) in enumerate(zip(tables, offs)):

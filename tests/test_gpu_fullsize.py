@@ -61,15 +61,53 @@ def test_gpu_bio_fullsize_counts(monkeypatch):
         "Q3 same_biological_process (QUERY_1)": len(np.intersect1d(mb[mg == base + ga], mb[mg == base + gb])),
         "Q4 hub join": int(gdeg[mg[mb == bp0]].sum()),
     }
+    want.update(_query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh))
     for name, spec in specs.items():
-        if name in want:
-            assert _count(db, spec) == want[name], name
-    # QUERY_2 / QUERY_3: the native plan (TEMPLATE / TVM nodes) equals the per-operator fold
-    native = {name: _count(db, specs[name]) for name in specs if name not in want}
+        assert _count(db, spec) == want[name], name
+    # QUERY_2 / QUERY_3 through the per-operator fold as well (same counts)
     monkeypatch.setenv("DAS_PLAN", "0")
-    for name, n in native.items():
-        assert _count(db, specs[name]) == n, name
-    assert all(n > 0 for n in native.values()), native
+    for name in ("Q5 same_or_inherited_biological_process (QUERY_2)", "Q6 linked_reactome_uniprot (QUERY_3)"):
+        assert _count(db, specs[name]) == want[name], name
+
+
+def _query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, n_up=5000, n_r=1000, n_loc=40):
+    """Closed forms of scripts/benchmark.py QUERY_2 / QUERY_3 (bench Q5 / Q6)
+    over the generator's distinct link pairs, following the reference fold
+    (pattern_matcher.py:491-500, 644-687, 705-748).  The anchors' intermediate
+    results are asserted non-empty, so reset-on-empty never applies."""
+    from das_amd import synthetic
+    _, off = synthetic.bio_nodes(n_genes, n_bps, n_up, n_r, n_loc)
+    rng_of = lambda k, n: (base + off[k], base + off[k] + n)  # noqa: E731
+    inside = lambda x, r: (x >= r[0]) & (x < r[1])  # noqa: E731
+    G, BP = rng_of("g", n_genes), rng_of("bp", n_bps)
+    UP, R = rng_of("up", n_up), rng_of("r", n_r)
+    concept = [rng_of(k, n) for k, n in (("upname", n_up), ("rname", n_r), ("loc", n_loc))]
+    is_concept = lambda x: np.logical_or.reduce([inside(x, r) for r in concept])  # noqa: E731
+    mg, mb = m >> 32, m & 0xFFFFFFFF
+    A = set(mb[mg == base + ga].tolist())                  # Member(ga, V1)
+    B = set(mb[mg == base + gb].tolist())                  # Member(gb, V2)
+    # QUERY_2 = And[Member(ga,V1), Or[And[Member(gb,V2), InhT(V2,V3), InhT(V1,V3)], Member(gb,V1)]]
+    ic, ip = inh >> 32, inh & 0xFFFFFFFF
+    sel = inside(ic, BP) & inside(ip, BP)                  # template Inheritance(BP, BP)
+    ic, ip = ic[sel], ip[sel]
+    by_parent = {}
+    for c, p in zip(ic.tolist(), ip.tolist()):
+        by_parent.setdefault(p, []).append(c)
+    inner1 = [(c, p) for c, p in zip(ic.tolist(), ip.tolist()) if c in B]         # (V2, V3)
+    assert A and B and inner1
+    inner = {(v1, v2, v3) for v2, v3 in inner1 for v1 in by_parent[v3]}          # (V1, V2, V3)
+    q2 = sum(1 for v1, _, _ in inner if v1 in A) + len(A & B)
+    # QUERY_3: same_bp x MemberT(Up, BP) x ListT(Up, .) x ListT(Up, .) x ListT(Reactome, Concept)
+    S = A & B
+    up = m[inside(mg, UP) & inside(mb, BP)]
+    ups = (up >> 32)[np.isin(up & 0xFFFFFFFF, np.array(sorted(S), dtype=np.int64))]
+    lst = _pairs(arrays, "List")
+    la, lb = lst >> 32, lst & 0xFFFFFFFF
+    nl_up = np.bincount(la[inside(la, UP) & is_concept(lb)], minlength=int(UP[1]))
+    j = int((nl_up[ups] ** 2).sum())
+    lr = int((inside(la, R) & is_concept(lb)).sum())
+    assert S and len(ups) and j and lr
+    return {"Q5 same_or_inherited_biological_process (QUERY_2)": q2, "Q6 linked_reactome_uniprot (QUERY_3)": j * lr}
 
 
 def _dev_pairs(arrays, k):
@@ -83,21 +121,37 @@ def _dev_pairs(arrays, k):
     return torch.unique(key)
 
 
-def test_gpu_hub_fullsize_counts():
+N_NODES, N_LINKS = 1 << 27, 1_000_000_000
+
+
+@pytest.fixture(scope="module")
+def kb1g():
+    """The 10^9-link power-law KB of configs 4 / 5, generated in HBM and
+    indexed ONCE for the module's tests (the generator's arrays are kept for
+    the closed forms)."""
+    import gc
+    import torch
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    db = HipDB(device=0)
+    arrays = synthetic.powerlaw_kb_device(db.ctx, N_NODES, N_LINKS)
+    db.load_arrays(arrays)
+    yield db, arrays
+    del db, arrays
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def test_gpu_hub_fullsize_counts(kb1g):
     """Config 5 at BASELINE size (10^9 links generated in HBM): the bench's
     hub queries against semi-join closed forms over the generator's arrays."""
     import bench
     import torch
-    from das_amd import synthetic
-    from das_amd.database.hip_db import HipDB
-    n_nodes, n_links = 1 << 27, 1_000_000_000
-    db = HipDB(device=0)
-    arrays = synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links)
-    db.load_arrays(arrays)
+    db, arrays = kb1g
+    n_nodes = N_NODES
     base = len(arrays.type_names)
     h0, h1 = base, base + 1
     pairs = {k: _dev_pairs(arrays, k) for k in range(4)}
-    arrays.drop_expr()
     src = {k: (p >> 32) for k, p in pairs.items()}
     dst = {k: (p & 0xFFFFFFFF) for k, p in pairs.items()}
 
@@ -117,19 +171,15 @@ def test_gpu_hub_fullsize_counts():
         assert _count(db, spec) == want[name], name
 
 
-def test_gpu_build_fullsize_incoming_sets():
+def test_gpu_build_fullsize_incoming_sets(kb1g):
     """Config 4 at BASELINE size (10^9 links generated in HBM): the incoming
     CSR (`incomming_set:<target>`, canonical_parser.py:141-143) of nodes
     sampled across the Zipf ranks equals what the generator's arrays imply --
     one entry per (distinct link, position) holding the node -- comes out
     sorted by link id, and every listed link targets the node."""
     import torch
-    from das_amd import synthetic
-    from das_amd.database.hip_db import HipDB
-    n_nodes, n_links = 1 << 27, 1_000_000_000
-    db = HipDB(device=0)
-    arrays = synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links)
-    db.load_arrays(arrays)
+    db, arrays = kb1g
+    n_nodes, n_links = N_NODES, N_LINKS
     base = len(arrays.type_names)
     c2 = int(arrays.level_off[1])
     ch2 = arrays.expr_child[:3 * c2].view(-1, 3)
@@ -165,3 +215,72 @@ def test_gpu_build_fullsize_incoming_sets():
     for r in rng.integers(0, n_nodes, 1000):
         h = md5(f"Concept n{int(r)}")
         assert db.get_node_handle("Concept", f"n{int(r)}") == h and db.node_exists("Concept", f"n{int(r)}")
+
+
+def _exec_rows(arrays):
+    """(schema, key, value) leaf-index rows of the arity-3 Execution links (with repeats)."""
+    off = arrays.expr_off
+    out = []
+    for g in range(len(arrays.level_off) - 1):
+        b, e = int(arrays.level_off[g]), int(arrays.level_off[g + 1])
+        if e <= b or int(off[b + 1] - off[b]) != 4:
+            continue
+        out.append(arrays.expr_child[int(off[b]):int(off[e])].reshape(e - b, 4)[:, 1:].astype(np.int64))
+    return np.concatenate(out)
+
+
+def _flybase_counts(arrays, gene, do_terms):
+    """Closed forms of bench.flybase_specs (QueryFlyBase.ipynb cells 5-9) for
+    one gene anchor, from the generator's distinct Execution rows: And folds
+    as joins (pattern_matcher.py:705-748; every running result is asserted
+    non-empty, so reset-on-empty never applies), Not as the anti-join of
+    check_negation, Or as a union of distinct bindings."""
+    names = {s: i for i, s in enumerate(arrays.leaf_strings())}
+    leaf = lambda t, n: names[f"{t} {n}"]  # noqa: E731
+    rows = _exec_rows(arrays)
+    s = lambda n: leaf("Schema", "Schema:" + n)  # noqa: E731
+    tab = {k: np.unique(rows[rows[:, 0] == s(n)][:, 1:], axis=0) for k, n in (
+        ("uniq", "gene_uniquename"), ("rec", "gene_map_table_recombination_loc"),
+        ("cyto", "gene_map_table_cytogenetic_loc"), ("do", "disease_model_annotations_DO_term"))}
+    fb = leaf("Verbatim", f"FBgn{gene:07d}")
+
+    def by(t, col):
+        d = {}
+        for a, b in tab[t].tolist():
+            d.setdefault((a, b)[col], []).append((a, b)[1 - col])
+        return d
+    rec_by_val, uniq_by_val = by("rec", 1), by("uniq", 1)
+    out = {}
+    for name, t in (("F5 same recombination_loc", "rec"), ("F6 same cytogenetic_loc", "cyto")):
+        r1 = set(tab[t][tab[t][:, 0] == fb][:, 1].tolist())
+        t_by_val = by(t, 1)
+        assert r1
+        out[name] = sum(len(uniq_by_val.get(v2, ())) for v1 in r1 for v2 in t_by_val.get(v1, ()))
+    r1 = set(tab["rec"][tab["rec"][:, 0] == fb][:, 1].tolist())
+    c_fb = set(tab["cyto"][tab["cyto"][:, 0] == fb][:, 1].tolist())
+    cyto = set(map(tuple, tab["cyto"].tolist()))
+    out["F7 same recomb, different cyto"] = sum(
+        len(uniq_by_val.get(v2, ())) * sum(1 for v3 in c_fb if (v2, v3) not in cyto)
+        for v1 in r1 for v2 in rec_by_val.get(v1, ()))
+    terms = [leaf("Verbatim", d) for d in (do_terms or ["DOID:0"]) if f"Verbatim {d}" in names]
+    out["F9 DO-term Or"] = len(set(tab["do"][np.isin(tab["do"][:, 1], terms)][:, 0].tolist()))
+    rec_by_key = by("rec", 0)
+    out["FJ uniquename x recombination_loc"] = sum(len(rec_by_key.get(v2, ())) for _, v2 in tab["uniq"].tolist())
+    return out
+
+
+def test_gpu_flybase_fullsize_counts():
+    """Config 3 at bench size (flybase_kb: 300 k genes, 60 schemas, 26.7 M
+    Execution links): the five FlyBase query shapes at two of the bench's gene
+    anchors against closed forms over the generator's rows."""
+    import bench
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    arrays = synthetic.flybase_kb(300_000, 60, 450_000)
+    db = HipDB(device=0)
+    db.load_arrays(arrays)
+    for gene in (7, 7 + 7919):
+        do_terms = synthetic.flybase_do_terms(arrays, gene=gene)
+        want = _flybase_counts(arrays, gene, do_terms)
+        for name, spec in bench.flybase_specs(gene, do_terms):
+            assert _count(db, spec) == want[name], (gene, name)

@@ -395,6 +395,68 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
         assert any(o == [1] for o in owners) and any(o == [0] for o in owners), owners
 
 
+def _surface_gpu_worker(rank, world, port, out_path):
+    import os as _os
+    import torch
+    import torch.distributed as dist
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    from das_amd.parallel import HipLocal, ShardedDB, shard_arrays
+    from tests.test_parallel_gloo import _call, _canon_pairs, _surface_calls
+    arrays = synthetic.bio_kb(60, 25, 600, 80, seed=3)
+    db = HipDB(device=0)
+    db.load_arrays(shard_arrays(arrays, rank, world))
+    sdb = ShardedDB(HipLocal(db, cpu_staging=True), dist)
+    kb = O.KB.from_arrays(arrays)
+    res = [_canon_pairs(_call(sdb, c)) for c in _surface_calls(kb)]
+    # the facade's get_links over the sharded DB (distributed_atom_space.py:259-284)
+    das = DistributedAtomSpace.__new__(DistributedAtomSpace)
+    das.db = sdb
+    res.append(sorted(das.get_links("Member", None, ["*", "*"])))
+    res.append(sorted(das.get_links("Inheritance", ["BiologicalProcess", "BiologicalProcess"])))
+    res.append(sorted(das.get_links("Inheritance")))
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_gpu_sharded_dbinterface_surface():
+    """ShardedDB's get_matched_links / get_matched_type_template /
+    get_matched_type and the facade's get_links with two ranks sharing
+    cuda:0, each rank indexing only the links its handles own: every rank
+    returns the single-process DB-path answer (oracle) -- the reference's
+    DBInterface over a sharded Redis Cluster (redis_mongo_db.py:235-279)."""
+    import socket
+    import tempfile
+    import torch.multiprocessing as mp
+    from das_amd import synthetic
+    from tests.test_parallel_gloo import _call, _canon_pairs, _surface_calls
+    arrays = synthetic.bio_kb(60, 25, 600, 80, seed=3)
+    kb = O.KB.from_arrays(arrays)
+    odb = O.RedisMongoSemantics(kb)
+    want = [_canon_pairs(_call(odb, c)) for c in _surface_calls(kb)]
+    want += [sorted(h for h, _ in odb.get_matched_links("Member", ["*", "*"])),
+             sorted(h for h, _ in odb.get_matched_type_template(["Inheritance", "BiologicalProcess",
+                                                                 "BiologicalProcess"])),
+             sorted(h for h, _ in odb.get_matched_type("Inheritance"))]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.spawn(_surface_gpu_worker, args=(2, port, out), nprocs=2, join=True)
+        per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    for r in range(2):
+        for i, (g, w) in enumerate(zip(per_rank[r], want)):
+            assert g == w, (r, i, len(g), len(w))
+
+
 def _composite_queries(rng, arrays, n):
     """Similarity / Set (unordered) terms mixed with Inheritance: every
     Assignment.join / check_negation kind pair of pattern_matcher.py:105-362."""
@@ -451,16 +513,20 @@ def test_gpu_composite_algebra_matches_oracle(tuple_targets):
         assert same(got, want), (q, got, {k: want.get(k) for k in ("error", "matched", "negation", "n")})
 
 
-@pytest.mark.parametrize("force", ["0", "1", ""])
+@pytest.mark.parametrize("force", ["0", "1", "", "sparse", "dense"])
 def test_gpu_hub_join_expansion(force, monkeypatch):
     """A hub key whose probe unit owns > 64K outputs (config 5 skew): the
     output-balanced expansion, the per-unit expansion (forced) and the
-    automatic choice all equal the oracle."""
+    automatic choice all equal the oracle; "sparse" / "dense" force the
+    direct join's build side through the in-place (lo, cnt) descriptors
+    (k_lc_count / k_lc_base / k_lc_scatter) or the histogram + scan."""
     from das_amd import synthetic
-    if force:
+    monkeypatch.delenv("DAS_DJ_BALANCED", raising=False)
+    monkeypatch.delenv("DAS_DJ_BUILD", raising=False)
+    if force in ("sparse", "dense"):
+        monkeypatch.setenv("DAS_DJ_BUILD", force)
+    elif force:
         monkeypatch.setenv("DAS_DJ_BALANCED", force)
-    else:
-        monkeypatch.delenv("DAS_DJ_BALANCED", raising=False)
     n = 1200
     rng = np.random.default_rng(4)
     hub = 0
@@ -479,6 +545,44 @@ def test_gpu_hub_join_expansion(force, monkeypatch):
         want = O.evaluate(q, odb)
         got = record(q, db)
         assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+@pytest.mark.parametrize("guard", ["1", "0"])
+@pytest.mark.parametrize("build", ["", "sparse", "dense"])
+@pytest.mark.parametrize("probe_rows", [5000, 40000])
+def test_gpu_key_join_duplicate_build_keys(probe_rows, build, guard, monkeypatch):
+    """das_join of a two-column probe with a one-column build side: distinct
+    build keys take the key-set filter (semi_join, the duplicate-key guard
+    riding on the compaction's count read-back -- DAS_SMALL_GUARD=1, the
+    one-launch compaction below kSmallScan = 16384 rows -- or read first, 0);
+    repeated build keys void the filter and the direct join counts each
+    repeat (dense or sparse build side).  Against a numpy join with
+    multiplicities."""
+    monkeypatch.setenv("DAS_SMALL_GUARD", guard)
+    if build:
+        monkeypatch.setenv("DAS_DJ_BUILD", build)
+    else:
+        monkeypatch.delenv("DAS_DJ_BUILD", raising=False)
+    from das_amd import _lib
+    from das_amd.database.hip_db import HipDB
+    from das_amd import synthetic
+    db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
+    rng = np.random.default_rng(probe_rows)
+    key_lo = 1 << 20 if build == "sparse" else 100
+    pa = rng.integers(0, 1000, probe_rows).astype(np.uint32)
+    pb = (key_lo + rng.integers(0, 70000 if build == "sparse" else 3000, probe_rows)).astype(np.uint32)
+    P = db.ctx.table_from_host(_lib.TABLE_ORDERED, [0, 1], np.stack([pa, pb]))
+    P.set_bounds([0, key_lo], [999, key_lo + 70000])
+    for dup in (False, True):
+        q = np.unique(pb[rng.integers(0, probe_rows, 300)])
+        if dup:
+            q = np.concatenate([q, q[::3]])                    # every third key twice
+        Q = db.ctx.table_from_host(_lib.TABLE_ORDERED, [1], q[None, :].astype(np.uint32))
+        Q.set_bounds([int(q.min())], [int(q.max())])
+        got = db.ctx.join(P, Q).fetch()
+        mult = dict(zip(*np.unique(q, return_counts=True)))
+        want = sorted((int(a), int(b)) for a, b in zip(pa, pb) for _ in range(mult.get(b, 0)))
+        assert sorted(zip(got[0].tolist(), got[1].tolist())) == want, (dup, len(want), got.shape)
 
 
 @pytest.mark.parametrize("fixture", KB_FIXTURES)
@@ -553,7 +657,7 @@ def test_gpu_hub_four_clause_matches_oracle(semi, monkeypatch):
         assert same(got, want), (name, got.get("n"), want.get("n"))
 
 
-@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "0"])
+@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "1-capped", "0"])
 def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     """Runs of one-variable hub clauses on one variable (T2(V2,a), T3(V2,b),
     ...) folded by ONE filter with the intersection of their key sets
@@ -570,6 +674,11 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     # ... as one walk writing chunk-locally + a compaction (k_dj_filt<2>,
     # default) or as a flag pass and a second walk
     monkeypatch.setenv("DAS_FILT_LOCAL", "0" if multi == "1-twopass" else "1")
+    # ... and the one walk's scratch over its budget: the two passes instead
+    if multi == "1-capped":
+        monkeypatch.setenv("DAS_FILT_SCRATCH_MAX", "0")
+    else:
+        monkeypatch.delenv("DAS_FILT_SCRATCH_MAX", raising=False)
     arrays = synthetic.powerlaw_kb(200, 4000, link_types=4, seed=5)
     db = _hipdb(arrays)
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))

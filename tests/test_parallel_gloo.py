@@ -155,6 +155,25 @@ class NumpyLocal:
     def rel_local_tables(self, rel):
         return rel.tables
 
+    # the DBInterface pattern / template families (ShardedDB gathers the
+    # (link, targets) id rows of every rank's own links)
+    def get_matched_links(self, link_type, targets):
+        return self.full.get_matched_links(link_type, targets)
+
+    def _pair_table(self, pairs, arity):
+        rows = [[self.id_of[h]] + [self.id_of[x] for x in tg] for h, tg in pairs if len(tg) == arity]
+        return NTable(ORDERED, [-1] + list(range(arity)), np.array(rows, np.uint32).reshape(-1, arity + 1))
+
+    def matched_links_table(self, link_type, targets):
+        return self._pair_table(self.odb.get_matched_links(link_type, targets), len(targets))
+
+    def matched_template_table(self, template):
+        return self._pair_table(self.odb.get_matched_type_template(template), len(template) - 1)
+
+    def matched_type_tables(self, link_type):
+        pairs = self.odb.get_matched_type(link_type)
+        return {a: self._pair_table(pairs, a) for a in sorted({len(tg) for _, tg in pairs})}
+
     # scans (oracle semantics, local links only)
     def match_link(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         from das_amd.pattern_matcher.pattern_matcher import _var_name
@@ -491,3 +510,59 @@ def test_partition_arrays_build_union_equals_single_build(world, name):
     for k in full:
         assert union[k] == set(full[k]), k
     assert owners == {h: 1 for h in full_kb.links}
+
+
+def _surface_calls(kb):
+    """get_matched_links / get_matched_type_template / get_matched_type calls
+    (DistributedAtomSpace.get_links' three branches, distributed_atom_space.py:259-284)."""
+    node = sorted(kb.nodes)
+    return [("links", "Member", ["*", "*"]), ("links", "Member", ["*", node[3]]), ("links", "*", [node[5], "*"]),
+            ("links", "Inheritance", ["*", "*"]), ("links", "Member", [node[1], node[2]]),
+            ("links", "Nope", ["*", "*"]),
+            ("template", ["Member", "Gene", "BiologicalProcess"]), ("template", ["Inheritance"]),
+            ("template", ["Inheritance", "BiologicalProcess", "BiologicalProcess"]),
+            ("type", "Member"), ("type", "Inheritance"), ("type", "Nope")]
+
+
+def _call(db, c):
+    if c[0] == "links":
+        return db.get_matched_links(c[1], c[2])
+    if c[0] == "template":
+        return db.get_matched_type_template(c[1])
+    return db.get_matched_type(c[1])
+
+
+def _canon_pairs(x):
+    return sorted(json.dumps(p if isinstance(p, str) else [p[0], list(p[1])]) for p in x)
+
+
+def _surface_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from das_amd.parallel import ShardedDB
+    kb, _ = _kb("bio")
+    sdb = ShardedDB(NumpyLocal(kb, rank, world), dist)
+    res = [_canon_pairs(_call(sdb, c)) for c in _surface_calls(kb)]
+    res.append(sdb.plan_stats["collectives"])
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_sharded_dbinterface_surface_equals_single_process():
+    """ShardedDB.get_matched_links / get_matched_type_template /
+    get_matched_type over two ranks, each holding only its own links' index
+    rows: every rank returns the single-process DB-path answer (the reference
+    serves these from a sharded Redis Cluster, redis_mongo_db.py:235-279)."""
+    kb, _ = _kb("bio")
+    odb = O.RedisMongoSemantics(kb)
+    want = [_canon_pairs(_call(odb, c)) for c in _surface_calls(kb)]
+    assert any(len(w) > 10 for w in want)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.spawn(_surface_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    for r in range(2):
+        assert per_rank[r][:-1] == want
+        assert per_rank[r][-1] > 0                      # the rows came through collectives
