@@ -50,10 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="all", choices=["all", "bio", "flybase", "hub", "build", "load"])
+    ap.add_argument("--workload", default="all", choices=["all", "bio", "flybase", "hub", "build", "load",
+                                                          "getlinks"])
     ap.add_argument("--legs", default="auto",
-                    help="with --workload all: comma list of the extra workloads (auto: flybase,hub,build on one "
-                         "GPU; build at N > 1)")
+                    help="with --workload all: comma list of the extra workloads (auto: flybase,hub,build,getlinks "
+                         "on one GPU; build at N > 1)")
     ap.add_argument("--leg-cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline budget of each extra workload of --workload all")
     ap.add_argument("--events", default="dominant", choices=["dominant", "all"],
@@ -67,6 +68,7 @@ def parse():
     ap.add_argument("--fb-genes", type=int, default=300_000)
     ap.add_argument("--fb-schema", type=int, default=60)
     ap.add_argument("--fb-rows", type=int, default=450_000)
+    ap.add_argument("--gl-steps", type=int, default=3, help="getlinks: seed walks timed (at most --steps)")
     # hub (config 5): H4's output grows ~ links^1.6 (Zipf hubs): 3M links -> ~4.3e8 bindings
     ap.add_argument("--hub-links", type=int, default=1_000_000_000)
     ap.add_argument("--hub-nodes", type=int, default=1 << 27)
@@ -189,6 +191,97 @@ def hub_specs():
                   _L("T3", _V("V2"), n(0))]]),
         ("H2 T0(V1,h0) T1(V1,V2)", ["And", [_L("T0", _V("V1"), n(0)), _L("T1", _V("V1"), _V("V2"))]]),
     ]
+
+
+# ---------------------------------------------------------------------------
+# the DBInterface surface behind the reference's only published timings
+# (notebooks/SimplePatternMiner.ipynb): a halo walk of get_links(None, None,
+# template) + get_link_targets around a seed node, then pattern counting
+# len(get_links(type, None, template)) over a sample of the walked links
+# ---------------------------------------------------------------------------
+W_ = "*"
+
+
+def _halo_templates(h):
+    """SimplePatternMiner.ipynb cell 6 (:395-401)."""
+    return [[h, W_], [W_, h], [h, W_, W_], [W_, h, W_], [W_, W_, h]]
+
+
+def _pattern_templates(link_type, targets):
+    """build_patterns' templates per link (cell 5, arity 2 / 3)."""
+    if len(targets) == 2:
+        return [[link_type, W_, targets[1]], [link_type, targets[0], W_]]
+    if len(targets) == 3:
+        t0, t1, t2 = targets
+        return [[link_type, W_, t1, t2], [link_type, t0, W_, t2], [link_type, t0, t1, W_],
+                [link_type, W_, W_, t2], [link_type, W_, t1, W_], [link_type, t0, W_, W_]]
+    return []
+
+
+def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_length=2):
+    """SimplePatternMiner.ipynb cells 6 and 9 through the facade API `api`
+    (get_links / get_link_targets / get_link_type / get_node_type /
+    get_node_name): the halo walk (level by level, every template around
+    every node handle, get_link_targets of every link found) and
+    build_patterns' counts over the level-0 links plus a `link_rate` sample
+    of the deeper ones.  Returns per phase: seconds, calls, links."""
+    node_handles = sorted(set(seeds))
+    levels, halo = [], []
+    for _ in range(halo_length):
+        t0 = time.perf_counter()
+        new_nodes, level_links, n_queries = set(), set(), 0
+        for h in node_handles:
+            for tpl in _halo_templates(h):
+                found = set(api.get_links(None, None, tpl))
+                n_queries += len(found) + 1                       # the notebook's count (:411-413)
+                for link in found:
+                    new_nodes.update(api.get_link_targets(link))
+                level_links |= found
+        halo.append({"s": time.perf_counter() - t0, "queries": n_queries, "links": len(level_links),
+                     "nodes": len(node_handles)})
+        levels.append(level_links)
+        node_handles = sorted(new_nodes)
+    sample = sorted(levels[0])
+    for lv in levels[1:]:
+        sample += [link for link in sorted(lv) if rng.random() < link_rate][:max_pattern_links]
+    t0 = time.perf_counter()
+    calls, counted = 0, 0
+    for link in sample:
+        targets = api.get_link_targets(link)
+        link_type = api.get_link_type(link)
+        for tpl in _pattern_templates(link_type, targets):
+            try:                                                  # build_pattern_from_template
+                for t in tpl[1:]:
+                    if t != W_:
+                        api.get_node_type(t)
+                        api.get_node_name(t)
+            except Exception:
+                continue
+            counted += len(api.get_links(tpl[0], None, tpl[1:]))
+            calls += 1
+    return {"halo": halo, "pattern": {"s": time.perf_counter() - t0, "links": len(sample), "get_links": calls,
+                                      "matched": counted}}
+
+
+class OracleFacade:
+    """The facade calls miner_walk makes, over the oracle's DB-path
+    restatement (distributed_atom_space.py:259-296 over RedisMongoDB)."""
+
+    def __init__(self, odb):
+        self.db = odb
+
+    def get_links(self, link_type, target_types=None, targets=None):
+        link_type = W_ if link_type is None else link_type
+        if target_types is not None and link_type != W_:
+            ans = self.db.get_matched_type_template([link_type, *target_types])
+        elif targets is not None:
+            ans = self.db.get_matched_links(link_type, targets)
+        else:
+            ans = self.db.get_matched_type(link_type)
+        return [a if isinstance(a, str) else a[0] for a in ans]
+
+    def __getattr__(self, name):
+        return getattr(self.db, name)
 
 
 def build_expr(pm, spec):
@@ -701,6 +794,112 @@ def run_load(args, rank, world, local_rank):
     emit(out, args.detail)
 
 
+def _miner_totals(runs):
+    """queries, seconds of the halo walks and pattern counts of miner_walk runs."""
+    hq = sum(h["queries"] for r in runs for h in r["halo"])
+    hs = sum(h["s"] for r in runs for h in r["halo"])
+    pc = sum(r["pattern"]["get_links"] for r in runs)
+    ps = sum(r["pattern"]["s"] for r in runs)
+    pl = sum(r["pattern"]["links"] for r in runs)
+    return {"halo_queries": hq, "halo_s": hs, "halo_ms_per_query": 1e3 * hs / max(hq, 1),
+            "level_ms_per_query": [round(1e3 * sum(r["halo"][k]["s"] for r in runs) /
+                                         max(sum(r["halo"][k]["queries"] for r in runs), 1), 5)
+                                   for k in range(len(runs[0]["halo"]))] if runs else [],
+            "pattern_get_links": pc, "pattern_s": ps, "pattern_ms_per_get_links": 1e3 * ps / max(pc, 1),
+            # the notebook's own formula: elapsed / (8 x links) (SimplePatternMiner.ipynb:283)
+            "pattern_ms_per_notebook_query": 1e3 * ps / max(8 * pl, 1)}
+
+
+def _gl_cpu_worker(job):
+    """CPU baseline of the getlinks leg: miner_walk over the oracle's DB-path
+    restatement (dict-backed pattern / template / outgoing families, the
+    reference's Redis + Mongo minus the network) on a scaled FlyBase KB."""
+    genes, schemas, rows, budget = job
+    import numpy as np
+    from das_amd import synthetic
+    from oracle import das_oracle as O
+    arrays = synthetic.flybase_kb(genes, schemas, rows)
+    api = OracleFacade(O.RedisMongoSemantics(O.KB.from_arrays(arrays)))
+    rng = np.random.default_rng(5)
+    runs, i = [], 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget:
+        runs.append(miner_walk(api, [O.terminal_hash("gene", f"g{(7 + 7919 * i) % genes}")], rng))
+        i += 1
+    return runs
+
+
+def run_getlinks(args, rank, world, local_rank):
+    """The DBInterface query surface on the FlyBase-shaped KB (config 3's
+    generator at the notebook's size, SimplePatternMiner.ipynb:19): per step
+    one seed gene's halo walk (get_links(None, None, template) x 5 templates
+    per node, get_link_targets per link, two levels) and build_patterns'
+    pattern counts over the walked links -- the calls the reference's only
+    published timings measure (2.289 / 0.097-0.131 ms per query, 74-104 ms per
+    pattern count).  Host-driven single lookups: one replica
+    is the measurement at N GPUs."""
+    import numpy as np
+    import torch
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    from das_amd.expression_hasher import ExpressionHasher as EH
+    if world > 1 and rank != 0:
+        return None
+    log("generating the FlyBase-shaped KB (getlinks)")
+    arrays = synthetic.flybase_kb(args.fb_genes, args.fb_schema, args.fb_rows)
+    db = HipDB(device=local_rank)
+    db.load_arrays(arrays)
+    t_pre = time.perf_counter()
+    db.prefetch()                       # host copies of per-atom metadata + outgoing sets (redis_mongo_db.py:89-127)
+    t_pre = time.perf_counter() - t_pre
+    das = DistributedAtomSpace(db=db)
+    steps = max(1, min(args.steps, args.gl_steps))
+    seed = lambda i: EH.terminal_hash("gene", f"g{(7 + 7919 * i) % args.fb_genes}")  # noqa: E731
+    rng = np.random.default_rng(5)
+    for i in range(args.warmup and 1):
+        miner_walk(das, [seed(1000 + i)], rng)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runs = [miner_walk(das, [seed(i)], rng) for i in range(steps)]
+    elapsed = time.perf_counter() - t0
+    tot = _miner_totals(runs)
+    cpu = None
+    if not args.no_cpu_baseline:
+        log("cpu baseline (getlinks)")
+        scale = 300                     # the oracle's pure-Python KB build: ~20 s at 1/300
+        g, r = max(args.fb_genes // scale, 100), max(args.fb_rows // scale, 200)
+        cruns = _pool_map(_gl_cpu_worker, [(g, args.fb_schema, r, args.cpu_baseline_seconds)])[0]
+        ct = _miner_totals(cruns)
+        cpu = {"value": ct["halo_queries"] / max(ct["halo_s"], 1e-9), "unit": "queries/s", "cores": 1,
+               "kind": "port",
+               "sample": f"miner_walk over the oracle's dict-backed DB-path restatement (no network) on "
+                         f"flybase_kb({g} genes, {args.fb_schema} schemas, {r} rows) = 1/{scale} of the GPU KB, "
+                         f"{len(cruns)} seeds, one process",
+               "halo_ms_per_query": round(ct["halo_ms_per_query"], 5),
+               "pattern_ms_per_get_links": round(ct["pattern_ms_per_get_links"], 5)}
+    lat = {"halo_ms_per_query": round(tot["halo_ms_per_query"], 5), "level_ms_per_query": tot["level_ms_per_query"],
+           "pattern_ms_per_get_links": round(tot["pattern_ms_per_get_links"], 5),
+           "pattern_ms_per_notebook_query": round(tot["pattern_ms_per_notebook_query"], 5),
+           "published_ms_per_query": {"halo_level1": 2.289, "halo_level2": [0.097, 0.131],
+                                      "pattern_count": [74, 104]}}
+    out = {"metric": "DBInterface lookups/s (SimplePatternMiner halo walk: get_links + get_link_targets)",
+           "value": tot["halo_queries"] / max(tot["halo_s"], 1e-9), "unit": "queries/s", "n_gpus": 1,
+           "steps": steps, "warmup": 1, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True,
+           "scaling": "replicas only", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic FlyBase-shaped KB (flybase_kb; the notebook's FlyBase dump needs a network fetch)",
+           "config": {"workload": "DBInterface surface: SimplePatternMiner.ipynb halo walk + pattern counts",
+                      "links": int(db.stats().n_links), "seeds": "one gene node per step",
+                      "prefetch_s": round(t_pre, 3)},
+           "roofline": None, "step_roofline": None, "cpu_baseline": cpu, "latency": lat,
+           "walks": [{"halo": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in h.items()}
+                               for h in r["halo"]],
+                      "pattern": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r["pattern"].items()}}
+                     for r in runs]}
+    del das, db, arrays
+    return out
+
+
 # kernel scopes that are scratch, not algorithmic bytes (SURVEY.md §8d: sort
 # passes and count -> offset scans count against the fraction)
 # (k_chunk_compact moves the filtered expansion's chunk runs out of its
@@ -1050,8 +1249,8 @@ def main():
         return
     if args.workload == "all":
         head = "bio"
-        legs = args.legs.split(",") if args.legs != "auto" else (["flybase", "hub", "build"] if world == 1
-                                                                 else ["build"])
+        legs = args.legs.split(",") if args.legs != "auto" else (["flybase", "hub", "build", "getlinks"]
+                                                                 if world == 1 else ["build"])
         legs = [w for w in legs if w]
     else:
         head, legs = args.workload, []
@@ -1059,6 +1258,8 @@ def main():
     def run_leg(w, a):
         if w == "build":
             return run_build(a, rank, world, dist, local_rank, backend)
+        if w == "getlinks":
+            return run_getlinks(a, rank, world, local_rank)
         return run_query(a, w, rank, world, dist, local_rank, backend)
 
     t_head = time.perf_counter()

@@ -109,6 +109,7 @@ _SIGS = {
     "das_link_targets": (C.c_int, [P, C.c_uint32, P, C.c_uint32, P]),
     "das_ctype_lookup": (C.c_int, [P, P, P]),
     "das_incoming": (C.c_int, [P, C.c_uint32, P, C.c_uint64, P]),
+    "das_export_outgoing": (C.c_int, [P, P, P, P, P]),
     "das_scan_link": (C.c_int, [P, C.POINTER(das_link_scan_t), C.POINTER(P)]),
     "das_scan_template": (C.c_int, [P, C.POINTER(das_template_scan_t), C.POINTER(P)]),
     "das_scan_type": (C.c_int, [P, C.c_uint32, P]),
@@ -478,6 +479,15 @@ class Context:
         n = C.c_uint32()
         check(lib().das_link_targets(self.h, int(atom_id), ptr(buf), 64, C.byref(n)), self.h)
         return buf[:n.value].copy()
+
+    def outgoing_csr(self):
+        """(tgt_off u64[n_atoms + 1], tgt u32[...]) host copies of the outgoing CSR."""
+        n_off, n_tgt = C.c_uint64(), C.c_uint64()
+        check(lib().das_export_outgoing(self.h, None, None, C.byref(n_off), C.byref(n_tgt)), self.h)
+        off = np.empty(n_off.value, dtype=np.uint64)
+        tgt = np.empty(max(n_tgt.value, 1), dtype=np.uint32)
+        check(lib().das_export_outgoing(self.h, ptr(off), ptr(tgt), C.byref(n_off), C.byref(n_tgt)), self.h)
+        return off, tgt[:n_tgt.value]
 
     def incoming(self, atom_id):
         n = C.c_uint64()

@@ -451,6 +451,24 @@ int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, u
   });
 }
 
+int das_export_outgoing(das_ctx_t* ctx, uint64_t* off, uint32_t* tgt, uint64_t* n_off, uint64_t* n_tgt) {
+  return guarded(ctx, [&] {
+    const das::Index& x = ctx->c.idx;
+    DAS_CHECK(x.built, das::DAS_E_NOT_BUILT, "index not built");
+    DAS_CHECK(n_off && n_tgt, das::DAS_E_INVALID, "null size argument");
+    uint64_t total = 0;
+    DAS_HIP(hipMemcpyAsync(&total, x.tgt_off + x.n_atoms, 8, hipMemcpyDeviceToHost, ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+    *n_off = x.n_atoms + 1;
+    *n_tgt = total;
+    if (!off && !tgt) return;
+    DAS_CHECK(off && tgt, das::DAS_E_INVALID, "null buffer");
+    DAS_HIP(hipMemcpyAsync(off, x.tgt_off, 8 * (x.n_atoms + 1), hipMemcpyDeviceToHost, ctx->c.s));
+    if (total) DAS_HIP(hipMemcpyAsync(tgt, x.tgt, 4 * total, hipMemcpyDeviceToHost, ctx->c.s));
+    DAS_HIP(hipStreamSynchronize(ctx->c.s));
+  });
+}
+
 int das_incoming(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint64_t cap, uint64_t* n) {
   return guarded(ctx, [&] {
     const das::Index& idx = ctx->c.idx;

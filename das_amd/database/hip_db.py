@@ -111,6 +111,7 @@ class HipDB(RelationalDB):
         self.generation = 0
         self.shard = None
         self._mirror = None
+        self._outgoing = None
         self.pattern_black_list = []
 
     def __repr__(self):
@@ -132,6 +133,7 @@ class HipDB(RelationalDB):
         self._hex_cache = {}
         self._handle_cache = {}
         self._mirror = None
+        self._outgoing = None
 
     def load_metta(self, texts):
         self.load_arrays(_loader.parse_metta(texts).finish())
@@ -261,10 +263,14 @@ class HipDB(RelationalDB):
     def get_link_targets(self, link_handle: str) -> List[str]:
         """redis_mongo_db.py:222-227: the outgoing set.  Redis returns a set, so
         order and repeats are not preserved there; here the stored order is
-        returned (a superset of what the reference guarantees)."""
+        returned (a superset of what the reference guarantees).  After
+        prefetch() the host copy of the outgoing CSR answers it."""
         aid, cat, _ = self._lookup(link_handle)
         if aid < 0 or cat not in (2, 3):
             raise ValueError(f"Invalid handle: {link_handle}")
+        if self._outgoing is not None:
+            off, tgt = self._outgoing
+            return self.hex_of(tgt[int(off[aid]):int(off[aid + 1])])
         return self.hex_of(self.ctx.link_targets(aid))
 
     def get_incoming_links(self, atom_handle: str) -> List[str]:
@@ -375,6 +381,8 @@ class HipDB(RelationalDB):
         aid, cat, _ = self._lookup(node_handle)
         if aid < 0 or cat != 1:
             raise ValueError(f"Invalid handle: {node_handle}")
+        if self._mirror is not None:
+            return self.arrays.node_name(int(self._mirror[4][aid]))
         _, _, _, _, nl = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
         return self.arrays.node_name(int(nl[0]))
 
@@ -422,19 +430,23 @@ class HipDB(RelationalDB):
             return {"type": tname, "name": self.arrays.node_name(int(nl[0]))}
         return {"type": tname, "targets": [self._deep(int(x)) for x in self.ctx.link_targets(aid)]}
 
-    def get_link_type(self, link_handle: str) -> str:
-        aid, cat, _ = self._lookup(link_handle)
-        if aid < 0 or cat != 2:
-            raise KeyError(link_handle)
+    def _type_of(self, aid):
+        if self._mirror is not None:
+            return self.arrays.type_names[int(self._mirror[3][aid])]
         _, _, _, ty, _ = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
         return self.arrays.type_names[int(ty[0])]
+
+    def get_link_type(self, link_handle: str) -> str:
+        aid, cat, _ = self._lookup(link_handle)
+        if aid < 0 or cat not in (2, 3):
+            raise KeyError(link_handle)
+        return self._type_of(aid)
 
     def get_node_type(self, node_handle: str) -> str:
         aid, cat, _ = self._lookup(node_handle)
         if aid < 0 or cat != 1:
             raise KeyError(node_handle)
-        _, _, _, ty, _ = self.ctx.atoms_info(np.array([aid], dtype=np.uint32))
-        return self.arrays.type_names[int(ty[0])]
+        return self._type_of(aid)
 
     def count_atoms(self) -> Tuple[int, int]:
         """redis_mongo_db.py:330-335"""
@@ -442,8 +454,16 @@ class HipDB(RelationalDB):
         return (int(st.n_nodes), int(st.n_links))
 
     def prefetch(self) -> None:
-        """redis_mongo_db.py:89-127 — the index is already resident in HBM."""
-        return None
+        """redis_mongo_db.py:89-127 caches the node / link type documents in
+        host memory for the per-atom metadata calls; here the index is
+        resident in HBM, and prefetch copies the per-atom metadata (handle,
+        category, arity, type, name leaf) and the outgoing CSR to the host, so
+        get_link_targets / get_link_type / get_node_type / get_node_name are
+        host lookups instead of a device round trip each (the
+        SimplePatternMiner.ipynb halo walk calls get_link_targets per link)."""
+        self._host_mirror()
+        if self._outgoing is None:
+            self._outgoing = self.ctx.outgoing_csr()
 
     # ------------------------------------------------ matcher entry points
     def _type_or_empty(self, link_type):

@@ -40,7 +40,9 @@ class DistributedAtomSpace:
     def __init__(self, **kwargs):
         self.database_name = kwargs.get("database_name", "das")
         device = int(kwargs.get("device", os.environ.get("DAS_DEVICE", 0)))
-        self.db = HipDB(device=device, tuple_targets=kwargs.get("tuple_targets", False))
+        # db: an existing DBInterface (a HipDB, or a parallel.ShardedDB over
+        # one process per GPU); default: a HipDB on `device`
+        self.db = kwargs.get("db") or HipDB(device=device, tuple_targets=kwargs.get("tuple_targets", False))
         self.pattern_black_list = []
         self._metta_sources = []
         self._canonical_sources = []

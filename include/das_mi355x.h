@@ -181,6 +181,11 @@ int das_atoms_info(das_ctx_t* ctx, const uint32_t* ids, uint64_t n, uint32_t* di
                    uint8_t* cat, uint32_t* arity, uint32_t* type, uint32_t* name_leaf);
 /* outgoing set of a link: targets in stored order (get_link_targets) */
 int das_link_targets(das_ctx_t* ctx, uint32_t id, uint32_t* out, uint32_t cap, uint32_t* n);
+/* The whole outgoing CSR to the host (a prefetch for per-link metadata calls,
+ * replacing redis_mongo_db.py:222-227's per-call `outgoing_set:<handle>`
+ * SMEMBERS): *n_off = n_atoms + 1 offsets, *n_tgt targets.  With null
+ * buffers only the sizes are returned; else `off` / `tgt` must hold them. */
+int das_export_outgoing(das_ctx_t* ctx, uint64_t* off, uint32_t* tgt, uint64_t* n_off, uint64_t* n_tgt);
 /* incoming set of an atom: the links whose outgoing set contains it, ascending
  * link id (`incomming_set:<handle>`, canonical_parser.py:141-143).  *n = the set
  * size; min(*n, cap) ids are copied to `out`. */

@@ -223,6 +223,30 @@ class RedisMongoSemantics:
     def count_atoms(self):
         return (len(self.kb.nodes), len(self.kb.links))
 
+    # per-atom metadata (the calls SimplePatternMiner.ipynb makes per link)
+    def get_link_targets(self, link_handle):
+        """redis_mongo_db.py:222-227 (`outgoing_set:<handle>`; Redis returns a
+        set, the stored order is returned here)."""
+        v = self.kb.links.get(link_handle)
+        if v is None:
+            raise ValueError(f"Invalid handle: {link_handle}")
+        return list(v[1])
+
+    def get_link_type(self, link_handle):
+        """redis_mongo_db.py:316-321 (link_type_cache: KeyError when absent)."""
+        return self.kb.links[link_handle][0]
+
+    def get_node_type(self, node_handle):
+        """redis_mongo_db.py:323-328 (node_type_cache)."""
+        return self.kb.nodes[node_handle][0]
+
+    def get_node_name(self, node_handle):
+        """redis_mongo_db.py:281-285 (`names:<handle>`)."""
+        v = self.kb.nodes.get(node_handle)
+        if v is None:
+            raise ValueError(f"Invalid handle: {node_handle}")
+        return v[1]
+
 
 class StubSemantics:
     """Restatement of StubDB (stub_db.py:8-188): readable handles, membership

@@ -974,3 +974,37 @@ def test_gpu_union_of_scans_matches_oracle(bits, monkeypatch):
     for q, want in zip(qs, _wants(("union_bits",), odb, qs)):
         got = record(q, db)
         assert same(got, want), (q, got.get("n"), want.get("n"))
+
+
+def test_gpu_miner_walk_matches_oracle():
+    """The DBInterface calls SimplePatternMiner.ipynb makes (bench.py's
+    getlinks leg: halo walk of get_links(None, None, template) +
+    get_link_targets, build_patterns' get_links counts), through the facade
+    over HipDB before and after prefetch() (host metadata mirrors), against
+    the same walk over the oracle: same queries, links and matched counts."""
+    import bench
+    from das_amd import synthetic
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    arrays = synthetic.flybase_kb(400, 10, 600, n_loc=30, n_do=40)
+    db = _hipdb(arrays)
+    das = DistributedAtomSpace(db=db)
+    api = bench.OracleFacade(O.RedisMongoSemantics(O.KB.from_arrays(arrays)))
+    seeds = [[O.terminal_hash("gene", f"g{g}")] for g in (0, 7, 123)]
+    seeds.append([O.terminal_hash("Verbatim", "FBgn0000042"), O.terminal_hash("Verbatim", "loc3")])
+
+    def strip(r):
+        return [(h["queries"], h["links"], h["nodes"]) for h in r["halo"]], \
+            (r["pattern"]["links"], r["pattern"]["get_links"], r["pattern"]["matched"])
+    for prefetched in (False, True):
+        if prefetched:
+            db.prefetch()
+        for s in seeds:
+            got = bench.miner_walk(das, s, np.random.default_rng(1), link_rate=0.2)
+            want = bench.miner_walk(api, s, np.random.default_rng(1), link_rate=0.2)
+            assert strip(got) == strip(want), (s, prefetched)
+            assert got["halo"][1]["links"] > 0
+    # per-link metadata after prefetch equals the device path's
+    link = sorted(api.get_links(None, None, ["*", seeds[1][0], "*"]))[0]
+    assert das.get_link_targets(link) == api.get_link_targets(link)
+    assert das.get_link_type(link) == "Execution"
+    assert das.get_node_name(seeds[1][0]) == "g7" and das.get_node_type(seeds[1][0]) == "gene"
