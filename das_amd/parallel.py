@@ -328,6 +328,7 @@ class ShardedDB(RelationalDB):
     # every shard.
     SMALL = 1 << 22
     GATHER_LIMIT = 1 << 26              # rows gathered per query at most (else the per-operator path)
+    GATHER_BUDGET = 1 << 28             # bytes of large terms gathered at most (else the per-operator fold)
 
     def plan_sharded(self, expr, answer):
         """Evaluates `expr` as ONE das_plan_execute_sharded call per GPU, or
@@ -403,32 +404,51 @@ class ShardedDB(RelationalDB):
                 if len(big) > 1:
                     # several large terms: all stay split when partition_spec
                     # places them by one variable (co-located joins), else the
-                    # largest does and the others are gathered
+                    # largest does and the others are gathered -- unless
+                    # gathering them would move more than the budget's bytes:
+                    # then the operator-by-operator fold joins them where they
+                    # are, placing each join by cost (broadcast of a small side,
+                    # or the all-to-all exchange by the shared variables with
+                    # the heavy-hitter split, _join_shared)
                     pv = {self._placement_var(db, rec[i]) for i in big}
-                    local = big if len(pv) == 1 and None not in pv else [max(big, key=lambda i: G[i])]
+                    if len(pv) == 1 and None not in pv:
+                        local = big
+                    else:
+                        top = max(big, key=lambda i: G[i])
+                        moved = sum(4 * int(rec[i, L.PLAN_SCAN]) * G[i] * (self.world - 1) for i in big if i != top)
+                        if moved > int(os.environ.get("DAS_SHARD_GATHER_BUDGET", self.GATHER_BUDGET)):
+                            self.plan_stats["split_fold"] = self.plan_stats.get("split_fold", 0) + 1
+                            return None
+                        local = [top]
                 else:
                     local = big
             gathered = [i for i in leaves if i not in local]
             if sum(G[i] for i in gathered) > self.GATHER_LIMIT:
                 return None
-        # gathered terms: this shard's rows, all-gathered into every shard (collective 2);
-        # a term whose rows may repeat ('*' type, repeated variable) is deduplicated after
+        # a wholly gathered top-level expression is evaluated by ONE shard
+        # (round robin over such plans, the same on every shard): its inputs
+        # go to that shard only, the others skip the native call and take
+        # the answer's size, flags and table schemas from one all-reduce
+        owner = None
+        if not local and expr is self._top and self.world > 1 and os.environ.get("DAS_GATHERED_OWNER") != "0":
+            owner = self._gather_seq % self.world
+            self._gather_seq += 1
+        # gathered terms: this shard's rows, all-gathered into every shard --
+        # or sent to the owner only (collective 2); a term whose rows may
+        # repeat ('*' type, repeated variable) is deduplicated after
         tables = [ctx.scan_words(nodes, i) for i in gathered]
-        inputs = self._gather_many(tables, [M[i] for i in gathered]) if gathered else []
-        if inputs is None:
+        inputs = self._gather_many(tables, [M[i] for i in gathered], owner) if gathered else []
+        if inputs is None and owner is None:
             return None                                  # an estimate below the rows: the operator fold
-        inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(gathered, inputs)]
+        if inputs is not None:
+            inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(gathered, inputs)]
         words = nodes.copy().reshape(n, W)
         for slot, i in enumerate(gathered):
             words[i, 0] = L.PLAN_INPUT
             words[i, 2] = slot
         words = words.reshape(-1)
-        if not local and expr is self._top and self.world > 1 and os.environ.get("DAS_GATHERED_OWNER") != "0":
-            # a wholly gathered top-level expression is evaluated by ONE shard
-            # (round robin over such plans, the same on every shard): the
-            # others skip the native call and take the answer's size, flags
-            # and table schemas from one all-reduce (collective 3)
-            return self._owner_plan(ctx, words, n, inputs, no_overload, answer)
+        if owner is not None:
+            return self._owner_plan(ctx, words, n, inputs, no_overload, answer, owner)          # collective 3
         matched, negation, out, checks = ctx.plan_execute_sharded(words, n, inputs, no_overload)
         del inputs, tables
         if not local:
@@ -471,48 +491,61 @@ class ShardedDB(RelationalDB):
 
     OWNER_TABLES = 16                       # answer tables an owner-evaluated plan describes
 
-    def _owner_plan(self, ctx, words, n, inputs, no_overload, answer):
+    def _owner_plan(self, ctx, words, n, inputs, no_overload, answer, owner):
+        """A wholly gathered top-level plan (every leaf's rows sent to the
+        owner shard only) evaluated by that shard: shards take turns (round
+        robin over such plans), so N independent gathered queries -- bench.py's
+        per-rank QUERY_1-3 instances -- run on N GPUs at once instead of each
+        on all of them.  The owner keeps the answer; one all-reduce hands every
+        shard its size, matched / negation and the answer tables' schemas
+        (kind, variables, composite members), so the others hold empty tables
+        of the same schemas (later collectives over the relation pair tables up
+        by position).  `inputs` None on the owner (a shard's rows exceeded
+        their slot): the all-reduce carries the fallback to every shard."""
         from . import _lib as L
-        """A wholly gathered top-level plan (every leaf's rows all-gathered,
-        the same on every shard) evaluated by one owner shard only: shards
-        take turns (round robin over such plans), so N independent gathered
-        queries -- bench.py's per-rank QUERY_1-3 instances -- run on N GPUs at
-        once instead of each on all of them.  The owner keeps the answer; one
-        all-reduce hands every shard its size, matched / negation and the
-        answer tables' schemas (kind, variables, composite members), so the
-        others hold empty tables of the same schemas (later collectives over
-        the relation pair tables up by position)."""
-        owner = self._gather_seq % self.world
-        self._gather_seq += 1
         K, W = self.OWNER_TABLES, 2 + 2 * L_MAXCOLS
-        vec = np.zeros(4 + K * W, dtype=np.int64)
+        vec = np.zeros(5 + K * W, dtype=np.int64)
         out = []
-        matched = negation = False
-        if self.rank == owner:
+
+        def describe(tables, v):
+            for i, t in enumerate(tables):
+                d = v[i * W:(i + 1) * W]
+                d[0], d[1] = int(t.kind), len(t.vars)
+                d[2:2 + len(t.vars)] = [int(x) + 1 for x in t.vars]          # +1: 0 = unused
+                mem = list(t.members) if t.members is not None else []
+                d[2 + L_MAXCOLS:2 + L_MAXCOLS + len(mem)] = [int(x) + 2 for x in mem]
+
+        def schemas(v, nt):
+            res = []
+            for i in range(nt):
+                d = v[i * W:(i + 1) * W]
+                kind, nv = int(d[0]), int(d[1])
+                vars_ = [int(x) - 1 for x in d[2:2 + nv]]
+                mem = [int(x) - 2 for x in d[2 + L_MAXCOLS:2 + L_MAXCOLS + nv]] if kind == L.TABLE_COMPOSITE else None
+                res.append(self.local.empty_table(kind, vars_, mem))
+            return res
+        if self.rank == owner and inputs is None:
+            vec[4] = 1
+        elif self.rank == owner:
             matched, negation, out, _ = ctx.plan_execute_sharded(words, n, inputs, no_overload)
             vec[0] = sum(t.nrows for t in out)
             vec[1], vec[2], vec[3] = int(matched), int(negation), len(out)
-            for i, t in enumerate(out[:K]):
-                v = vec[4 + i * W:4 + (i + 1) * W]
-                v[0], v[1] = int(t.kind), len(t.vars)
-                v[2:2 + len(t.vars)] = [int(x) + 1 for x in t.vars]          # +1: 0 = unused
-                mem = list(t.members) if t.members is not None else []
-                v[2 + L_MAXCOLS:2 + L_MAXCOLS + len(mem)] = [int(x) + 2 for x in mem]
+            describe(out[:K], vec[5:])
         got = self._allreduce_sum(vec)                                           # collective 3
+        if int(got[4]):
+            self.plan_stats["native_fallback"] += 1
+            return None
         nt = int(got[3])
-        if self.rank != owner:
-            if nt > K:
-                # more schemas than the vector describes: evaluate here too
-                # for the schemas (same inputs, same answer), keep no rows
-                _, _, res, _ = ctx.plan_execute_sharded(words, n, inputs, no_overload)
-                out = [self.local.empty_table(t.kind, list(t.vars), t.members) for t in res]
-                del res
-            for i in range(nt if nt <= K else 0):
-                v = got[4 + i * W:4 + (i + 1) * W]
-                kind, nv = int(v[0]), int(v[1])
-                vars_ = [int(x) - 1 for x in v[2:2 + nv]]
-                mem = [int(x) - 2 for x in v[2 + L_MAXCOLS:2 + L_MAXCOLS + nv]] if kind == L.TABLE_COMPOSITE else None
-                out.append(self.local.empty_table(kind, vars_, mem))
+        if nt > K:
+            # more schemas than the vector describes: a second all-reduce with all of them
+            big = np.zeros(nt * W, dtype=np.int64)
+            if self.rank == owner:
+                describe(out, big)
+            big = self._allreduce_sum(big)
+            if self.rank != owner:
+                out = schemas(big, nt)
+        elif self.rank != owner:
+            out = schemas(got[5:], nt)
         rel = DRel(out)
         rel._global = int(got[0])
         self.plan_stats["native"] += 1
@@ -547,12 +580,16 @@ class ShardedDB(RelationalDB):
 
     OVER = 0xFFFFFFFF                     # _gather_many header: rows over the slot
 
-    def _gather_many(self, tables, caps):
+    def _gather_many(self, tables, caps, owner=None):
         """Every shard's rows of each table, to every shard, in ONE
         all-gather: per shard a header (row count and column bounds per
         table) and each table's rows (row-major) in a slot of `caps[j]` rows
         (caps: the largest estimate any shard reported, an upper bound).
-        None on every shard when some shard's table exceeds its slot."""
+        None on every shard when some shard's table exceeds its slot.
+        owner: the rows go to that shard only, in ONE all-to-all whose sends
+        to every other shard are empty (an owner-evaluated plan: 1/N of the
+        all-gather's traffic); the other shards get None, and the owner None
+        on an overflow (its plan carries the fallback to the others)."""
         import torch
         lo_hi = [t.bounds() for t in tables]
         ncols = [max(len(t.vars), 1) for t in tables]
@@ -581,8 +618,19 @@ class ShardedDB(RelationalDB):
         if not loc.stream_ordered:
             loc.db.ctx.sync()
         stage = buf if loc.dev == gpu else buf.cpu()
-        out = torch.empty(self.world * width, dtype=torch.int32, device=stage.device)
-        self.dist.all_gather_into_tensor(out, stage, group=self.group)
+        if owner is None:
+            out = torch.empty(self.world * width, dtype=torch.int32, device=stage.device)
+            self.dist.all_gather_into_tensor(out, stage, group=self.group)
+        else:
+            mine = self.rank == owner
+            out = torch.empty(self.world * width if mine else 0, dtype=torch.int32, device=stage.device)
+            self.dist.all_to_all_single(out, stage, output_split_sizes=[width if mine else 0] * self.world,
+                                        input_split_sizes=[width if d == owner else 0 for d in range(self.world)],
+                                        group=self.group)
+            self.plan_stats["collectives"] += 1
+            if not mine:
+                return None
+            self.plan_stats["collectives"] -= 1
         self.plan_stats["collectives"] += 1
         out_dev = out.to(gpu)
         heads = out.view(self.world, width)[:, :H].cpu().numpy().view(np.uint32)

@@ -273,7 +273,7 @@ def _sharded_kb(kind):
     from tests.test_parallel_gloo import _fly_queries, _hub_queries, _queries
     if kind in ("default", "heavy", "small", "default_owner"):
         return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
-    if kind in ("hub", "hub_small"):
+    if kind in ("hub", "hub_small", "hub_exchange"):
         return MS.make_arrays("hub"), _hub_queries()
     if kind.startswith("bio_full"):
         # scripts/benchmark.py QUERY_1-3 (LinkTemplate leaves, template-target
@@ -292,7 +292,10 @@ def _sharded_kb(kind):
 # through each shard's index, the fold's emptiness checks, fallbacks)
 _SHARD_ENV = {"heavy": {"DAS_SHARDED_PLAN": "0", "DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
               "hub": {"DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
-              "small": {"DAS_SHARD_SMALL": "40"}, "hub_small": {"DAS_SHARD_SMALL": "30"}}
+              "small": {"DAS_SHARD_SMALL": "40"}, "hub_small": {"DAS_SHARD_SMALL": "30"},
+              # large terms over a gather budget scaled to the test KB: the
+              # planner folds them with the all-to-all exchange (no forcing)
+              "hub_exchange": {"DAS_SHARD_SMALL": "30", "DAS_SHARD_GATHER_BUDGET": "2000"}}
 
 
 def _sharded_worker(rank, world, port, out_path, mode):
@@ -339,8 +342,8 @@ def _sharded_worker(rank, world, port, out_path, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "flybase", "flybase_owner",
-                                  "default_owner", "bio_full", "bio_full_owner"])
+@pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "hub_exchange", "flybase",
+                                  "flybase_owner", "default_owner", "bio_full", "bio_full_owner"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
     """The multi-GPU path with two ranks sharing cuda:0 over gloo, against the
     single-process oracle: handle-sharded builds (each link indexed on exactly
@@ -367,6 +370,9 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
     stats = per_rank[0][-1]
     if mode == "heavy":
         assert stats["heavy"] > 0 and stats["native"] == 0, stats
+    elif mode == "hub_exchange":
+        # the default planner took the exchange for the two large terms
+        assert stats["exchange"] > 0 and stats.get("split_fold", 0) > 0, stats
     else:
         assert stats["native"] > 0, stats
     if mode in ("small", "hub_small"):

@@ -391,7 +391,12 @@ def _hub_queries():
     L = lambda t, a, b: ["Link", t, True, [a, b]]  # noqa: E731
     return [q for _, q in bench.hub_specs()] + [
         ["And", [L("T0", V("V1"), n(0)), L("T0", V("V1"), V("V2")), L("T0", V("V2"), n(1))]],
-        ["And", [L("T1", V("V1"), V("V2")), L("T1", V("V2"), n(0)), ["Not", L("T2", V("V1"), n(1))]]]]
+        ["And", [L("T1", V("V1"), V("V2")), L("T1", V("V2"), n(0)), ["Not", L("T2", V("V1"), n(1))]]],
+        # two large unanchored terms on the hub keys (config 5's skewed exchange)
+        ["And", [L("T1", V("V1"), V("V2")), L("T2", V("V2"), V("V3"))]],
+        # the open 4-clause chain of SURVEY.md §8d config 5
+        ["And", [L("T0", V("V1"), n(0)), L("T1", V("V1"), V("V2")), L("T2", V("V2"), n(1)),
+                 L("T3", V("V2"), V("V3"))]]]
 
 
 # kind -> (DAS_JOIN_PLACEMENT, DAS_HEAVY_FRAC)
