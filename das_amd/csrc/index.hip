@@ -386,9 +386,12 @@ __device__ __forceinline__ bool wave_run_tail(uint32_t id) {
   return __lane_id() == 63 || nid != id;
 }
 
+// local2id != nullptr: local2id[u] = id (a 4-byte random scatter per entry);
+// else ids[i] = id in sorted order, scattered later window by window
+// (scatter_partitioned: the random writes land in a MALL-sized window at a time)
 __global__ void __launch_bounds__(256) k_assign_ids(const uint32_t* idx, const uint32_t* first, const uint32_t* scan,
                                                     uint64_t n, const uint8_t* catl, const uint64_t* pkey,
-                                                    uint32_t* local2id, uint32_t* catmax, uint32_t* rep,
+                                                    uint32_t* local2id, uint32_t* ids, uint32_t* catmax, uint32_t* rep,
                                                     uint8_t* cat_sorted) {
   const int lane = __lane_id();
   for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
@@ -400,7 +403,8 @@ __global__ void __launch_bounds__(256) k_assign_ids(const uint32_t* idx, const u
       id = scan[i] + first[i] - 1;
       const uint32_t u = idx[i];
       const uint8_t c = pkey ? (uint8_t)(pkey[i] & 3u) : catl[u];   // pkey: the category rode in the sort key
-      local2id[u] = id;
+      if (local2id) local2id[u] = id;
+      else ids[i] = id;
       cat_sorted[i] = c;
       single = first[i] && (i + 1 == n || first[i + 1]);
       if (single) {
@@ -450,6 +454,15 @@ __global__ void k_rep_missing(const uint32_t* rep, uint64_t n, uint32_t* bad) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     miss |= rep[i] == kNone;
   if (__ballot(miss) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+
+// dst[key[i]] = val[i] over (key, val) pairs grouped by the key's top bits:
+// consecutive waves write into one key window at a time, so the random 4-byte
+// stores merge in the L2 / MALL before they reach HBM
+__global__ void k_scatter_pairs(const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n,
+                                uint32_t* __restrict__ dst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[key[i]] = val[i];
 }
 
 // named-type cluster key of a temp (digest-order) id; kNone types last
@@ -889,6 +902,36 @@ void col_bounds(Index& idx, const RowTable& t, uint64_t n_types, hipStream_t s) 
   idx.gbound[t.arity] = std::move(g);
 }
 
+// dst[keys[i]] = vals[i] for keys < key_range, as one radix partition pass of
+// the pairs by the keys' top 8 bits (LDS-staged scatter, contiguous runs per
+// bucket) followed by an in-order scatter: each bucket's keys span
+// key_range / 256 slots of dst, so the writes of the waves in flight share a
+// window of a few MB instead of the whole array.  keys / vals are consumed.
+void scatter_partitioned(uint32_t* keys, uint32_t* vals, uint64_t n, uint64_t key_range, uint32_t* dst,
+                         hipStream_t s) {
+  if (!n) return;
+  DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "scatter_partitioned: more than 2^32 pairs");
+  const int bits = std::max(1, bits_for(key_range ? key_range - 1 : 0));
+  const int shift = std::max(0, bits - 8);
+  const uint32_t tiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
+  DBuf<uint32_t> hist((uint64_t)tiles * 256, s), offs((uint64_t)tiles * 256, s), k2(n, s), v2(n, s);
+  {
+    KScope ks("k_radix_hist<u32>", 4.0 * n);
+    hipLaunchKernelGGL((k_radix_hist<uint32_t>), dim3(tiles), dim3(kSortBlock), 0, s, (const uint32_t*)keys, n, shift,
+                       hist.p, tiles);
+  }
+  exclusive_scan<uint32_t>(hist.p, (uint64_t)tiles * 256, offs.p, s);
+  {
+    KScope ks("k_radix_scatter_lds<u32,true>", 16.0 * n);
+    hipLaunchKernelGGL((k_radix_scatter_lds<uint32_t, true>), dim3(tiles), dim3(kSortBlock), 0, s, (const uint32_t*)keys,
+                       (const uint32_t*)vals, k2.p, v2.p, n, shift, (const uint32_t*)hist.p, (const uint32_t*)offs.p,
+                       tiles);
+  }
+  KScope ks("k_scatter_pairs", 12.0 * n);
+  hipLaunchKernelGGL(k_scatter_pairs, G(n), dim3(B), 0, s, (const uint32_t*)k2.p, (const uint32_t*)v2.p, n, dst);
+  DAS_HIP(hipGetLastError());
+}
+
 // Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact
 // fallback); key[i] = the high half of entry i's digest, sorted.  With
 // `prio` (category per unified index) the fast path carries it in the key's
@@ -1270,14 +1313,22 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   fill_dev(local2id.p, 0xFF, 4 * nu, s);
   fill_dev(catmax.p, 0, 4 * catmax.n, s);
   fill_dev(rep.p, 0xFF, 4 * rep.n, s);
+  // local2id by a partitioned scatter above 2^22 entries (DAS_L2I_PART=0: the
+  // direct 4-byte random scatter, which wrote ~10x its bytes at 10^9 links;
+  // =1: partitioned at every size, tests)
+  const char* l2p = std::getenv("DAS_L2I_PART");
+  const bool l2i_part = l2p && l2p[0] == '1' ? nc > 0 : nc >= (1ull << 22) && !(l2p && l2p[0] == '0');
+  DBuf<uint32_t> ids(l2i_part ? nc : 0, s);
   if (nc) {
     DBuf<uint8_t> cs(nc, s);
     {
-      // list, first, scan, catl in; local2id, sorted category out; catmax + rep per atom
-      KScope ks("k_assign_ids", 19.0 * nc + 8.0 * n_atoms);
+      // list, first, scan, catl in; local2id (or the ids in sorted order), sorted
+      // category out; catmax + rep per atom
+      KScope ks("k_assign_ids", (l2i_part ? 19.0 : 19.0) * nc + 8.0 * n_atoms);
       hipLaunchKernelGGL(k_assign_ids, G(nc), dim3(B), 0, s, (const uint32_t*)list.p, (const uint32_t*)first.p,
                          (const uint32_t*)scan.p, nc, (const uint8_t*)catl.p,
-                         prio_key ? (const uint64_t*)skey.p : nullptr, local2id.p, catmax.p, rep.p, cs.p);
+                         prio_key ? (const uint64_t*)skey.p : nullptr, l2i_part ? nullptr : local2id.p,
+                         l2i_part ? ids.p : nullptr, catmax.p, rep.p, cs.p);
     }
     skey.release();
     {
@@ -1294,7 +1345,9 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     DAS_HIP(hipGetLastError());
     DAS_CHECK(read_u32(bad.p, s) == 0, DAS_E_INTERNAL, "intern: a digest run has no representative");
   }
-  first.release(); scan.release(); list.release();
+  first.release(); scan.release();
+  if (l2i_part) scatter_partitioned(list.p, ids.p, nc, nu, local2id.p, s);     // after k_pick_rep read `list`
+  ids.release(); list.release();
 
   // 3b. final ids clustered by named type, so a variable's bindings occupy a
   // compact id range (direct-address joins); inside a type, atoms referenced

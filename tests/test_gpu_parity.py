@@ -360,13 +360,16 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # three ranks where the exchange must pay: at two, broadcasting the
+    # smaller side of a join never moves more rows than the exchange
+    world = 3 if mode == "hub_exchange" else 2
     arrays, queries = _sharded_kb(mode)
     okb = O.KB.from_arrays(arrays)
     odb = O.RedisMongoSemantics(okb)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.spawn(_sharded_worker, args=(2, port, out, mode), nprocs=2, join=True)
-        per_rank = [json.load(open(f"{out}.{r}")) for r in range(2)]
+        mp.spawn(_sharded_worker, args=(world, port, out, mode), nprocs=world, join=True)
+        per_rank = [json.load(open(f"{out}.{r}")) for r in range(world)]
     stats = per_rank[0][-1]
     if mode == "heavy":
         assert stats["heavy"] > 0 and stats["native"] == 0, stats
@@ -378,17 +381,17 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
     if mode in ("small", "hub_small"):
         # some queries keep terms split across the shards and still verify
         assert any(r.get("native") and r.get("collectives") == 3 for r in per_rank[0][:-2]), per_rank[0][:-2]
-    indexed = [set(per_rank[r][-2]) for r in range(2)]
+    indexed = [set(per_rank[r][-2]) for r in range(world)]
     assert not (indexed[0] & indexed[1]) and indexed[0] | indexed[1] == set(okb.links)
-    assert all(handle_owner(h, 2) == r for r in range(2) for h in indexed[r])
+    assert all(handle_owner(h, world) == r for r in range(world) for h in indexed[r])
     for qi, q in enumerate(queries):
         want = O.evaluate(q, odb)
         if "error" in want:
-            assert all(per_rank[r][qi] == {"error": want["error"]} for r in range(2)), q
+            assert all(per_rank[r][qi] == {"error": want["error"]} for r in range(world)), q
             continue
         want_rows = sorted(json.dumps(r, sort_keys=True) for r in want["rows"])
-        assert sum(per_rank[r][qi]["local"] for r in range(2)) == want["n"], q
-        for r in range(2):
+        assert sum(per_rank[r][qi]["local"] for r in range(world)) == want["n"], q
+        for r in range(world):
             got = per_rank[r][qi]
             assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
             assert got["rows"] == want_rows, q
@@ -397,7 +400,7 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
             assert got["native"] == 1 and got["collectives"] <= 3, (q, got["native"], got["collectives"])
     if mode.endswith("_owner"):
         # wholly gathered top-level plans were evaluated by one rank each, in turn
-        owners = [[r for r in range(2) if per_rank[r][qi].get("local")] for qi in range(len(queries))]
+        owners = [[r for r in range(world) if per_rank[r][qi].get("local")] for qi in range(len(queries))]
         assert any(o == [1] for o in owners) and any(o == [0] for o in owners), owners
 
 
