@@ -932,6 +932,163 @@ void scatter_partitioned(uint32_t* keys, uint32_t* vals, uint64_t n, uint64_t ke
   DAS_HIP(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// Digest sort on a key prefix.  Digests are uniform, so after an LSD sort on
+// the keys' top 40 bits (5 passes instead of 8) the entries are grouped in
+// runs of equal prefix that almost always hold one digest (its duplicates:
+// ~10^-3 of the distinct digests share a 40-bit prefix at 10^9 entries).  A
+// run holding several digests is put in order afterwards: descents inside a
+// run are listed (k_prefix_descents), each run with a descent is located once
+// (k_descent_runs, a wave walking to its ends), runs up to kRunSortMax entries
+// are sorted in LDS by one block each (k_sort_runs_lds), longer ones by a
+// radix sort of their low key bits.  The full key order results (equal keys,
+// i.e. copies of one digest with one category, in any order: nothing
+// downstream depends on their order).
+// ---------------------------------------------------------------------------
+constexpr int kPrefixShift = 24;                  // sorted bits [24, 64): 40 bits
+constexpr uint32_t kMaxDescents = 1u << 22;
+constexpr uint32_t kRunSortMax = 4096;
+
+__global__ void k_prefix_descents(const uint64_t* __restrict__ key, uint64_t n, int shift, uint32_t* list,
+                                  uint32_t* count, uint32_t cap) {
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x; b < n; b += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = b + threadIdx.x;        // block-uniform trip count: the wave ballots together
+    bool d = false;
+    if (i >= 1 && i < n) {
+      const uint64_t a = key[i - 1], c = key[i];
+      d = ((a ^ c) >> shift) == 0 && (a >> 2) > (c >> 2);
+    }
+    const uint64_t m = __ballot(d);
+    if (!m) continue;
+    uint32_t base = 0;
+    if (__lane_id() == 0) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    const uint32_t slot = base + (uint32_t)__popcll(m & __lanemask_lt());
+    if (d && slot < cap) list[slot] = (uint32_t)i;
+  }
+}
+
+// One wave per listed descent: the run [s, e) of equal prefix around it is
+// emitted by the wave whose descent is the run's first (a wave that meets an
+// earlier descent on its way left leaves the run to that one).
+__global__ void k_descent_runs(const uint64_t* __restrict__ key, uint64_t n, int shift, const uint32_t* list,
+                               uint32_t nd, uint2* runs, uint32_t* count) {
+  const uint32_t lane = __lane_id();
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t w = blockIdx.x * (uint64_t)(blockDim.x / 64) + (threadIdx.x >> 6); w < nd; w += waves) {
+    const uint64_t i = list[w];
+    const uint64_t P = key[i] >> shift;
+    // left: positions i-1, i-2, ... 64 per step
+    int64_t s = -1;
+    bool abort = false;
+    for (int64_t j = (int64_t)i - 1; s < 0 && !abort; j -= 64) {
+      const int64_t p = j - (int64_t)lane;
+      bool in = false, desc = false;
+      if (p >= 0) {
+        const uint64_t kp = key[p];
+        in = (kp >> shift) == P;
+        if (in && p >= 1) {
+          const uint64_t km = key[p - 1];
+          desc = (km >> shift) == P && (km >> 2) > (kp >> 2);
+        }
+      }
+      if (__ballot(desc)) abort = true;                  // an earlier descent of this run
+      const uint64_t out = __ballot(!in);                // lanes past the run's start (or p < 0)
+      if (out) s = j - (int64_t)__ffsll((long long)out) + 2;     // first lane out: p + 1
+    }
+    if (abort) continue;
+    uint64_t e = 0;
+    for (uint64_t j = i + 1; e == 0; j += 64) {
+      const uint64_t p = j + lane;
+      const bool in = p < n && (key[p] >> shift) == P;
+      const uint64_t out = __ballot(!in);
+      if (out) e = j + (uint64_t)__ffsll((long long)out) - 1;
+    }
+    if (lane == 0) {
+      const uint32_t r = atomicAdd(count, 1u);
+      runs[r] = make_uint2((uint32_t)s, (uint32_t)e);
+    }
+  }
+}
+
+// One block per run of at most kRunSortMax entries: bitonic sort of the
+// (key, value) pairs in LDS by the whole key.
+__global__ void __launch_bounds__(256) k_sort_runs_lds(uint64_t* key, uint32_t* val, const uint2* runs, uint32_t nr) {
+  __shared__ uint64_t sk[kRunSortMax];
+  __shared__ uint32_t sv[kRunSortMax];
+  for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+    const uint2 run = runs[r];
+    const uint32_t m = run.y - run.x;
+    if (m > kRunSortMax) continue;                      // block-uniform: the host sorts it
+    uint32_t np = 2;
+    while (np < m) np <<= 1;
+    for (uint32_t t = threadIdx.x; t < np; t += blockDim.x) {
+      sk[t] = t < m ? key[run.x + t] : ~0ull;
+      sv[t] = t < m ? val[run.x + t] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= np; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t t = threadIdx.x; t < np; t += blockDim.x) {
+          const uint32_t o = t ^ j;
+          if (o > t) {
+            const bool up = (t & k) == 0;
+            const uint64_t a = sk[t], b = sk[o];
+            if ((a > b) == up) {
+              sk[t] = b;
+              sk[o] = a;
+              const uint32_t x = sv[t];
+              sv[t] = sv[o];
+              sv[o] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+      key[run.x + t] = sk[t];
+      val[run.x + t] = sv[t];
+    }
+    __syncthreads();
+  }
+}
+
+// After radix_sort_pairs(key, idx, n, shift, 64): order the runs of equal
+// key >> shift that hold several keys.  false: too many descents to list
+// (the caller sorts the remaining bits instead).
+bool fix_prefix_runs(uint64_t* key, uint32_t* idx, uint64_t n, int shift, hipStream_t s) {
+  DBuf<uint32_t> cnt(2, s), list(kMaxDescents, s);
+  fill_dev(cnt.p, 0, 8, s);
+  {
+    KScope ks("k_prefix_descents", 8.0 * n);
+    hipLaunchKernelGGL(k_prefix_descents, G(n), dim3(B), 0, s, (const uint64_t*)key, n, shift, list.p, cnt.p,
+                       kMaxDescents);
+    DAS_HIP(hipGetLastError());
+  }
+  const uint32_t nd = read_u32(cnt.p, s);
+  if (nd == 0) return true;
+  if (nd > kMaxDescents) return false;
+  DBuf<uint2> runs(nd, s);
+  hipLaunchKernelGGL(k_descent_runs, dim3(grid_for(nd, B / 64, 65535u)), dim3(B), 0, s, (const uint64_t*)key, n,
+                     shift, (const uint32_t*)list.p, nd, runs.p, cnt.p + 1);
+  DAS_HIP(hipGetLastError());
+  const uint32_t nr = read_u32(cnt.p + 1, s);
+  if (!nr) return true;
+  {
+    KScope ks("k_sort_runs_lds", 24.0 * nr);
+    hipLaunchKernelGGL(k_sort_runs_lds, dim3(std::min<uint32_t>(nr, 65535u)), dim3(256), 0, s, key, idx,
+                       (const uint2*)runs.p, nr);
+    DAS_HIP(hipGetLastError());
+  }
+  std::vector<uint2> h(nr);
+  DAS_HIP(hipMemcpyAsync(h.data(), runs.p, sizeof(uint2) * nr, hipMemcpyDeviceToHost, s));
+  DAS_HIP(hipStreamSynchronize(s));
+  for (const uint2& r : h)
+    if (r.y - r.x > kRunSortMax) radix_sort_pairs<uint64_t>(key + r.x, idx + r.x, r.y - r.x, 0, shift, s);
+  return true;
+}
+
 // Sorts idx[0..n) by the 128-bit digest dig[idx[i]] (hi-only fast path, exact
 // fallback); key[i] = the high half of entry i's digest, sorted.  With
 // `prio` (category per unified index) the fast path carries it in the key's
@@ -951,7 +1108,17 @@ bool sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>
       KScope ks("k_digest_key", 29.0 * n);         // index, gathered digest half, category, key out
       hipLaunchKernelGGL(k_digest_key_prio, G(n), dim3(B), 0, s, dig, (const uint32_t*)idx, prio, n, key.p);
     }
-    radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
+    // large sorts: the top 40 key bits, then the runs that hold several keys
+    // (DAS_DIGEST_PREFIX=0: all 64 bits; =1: the prefix path at any size)
+    const char* pe = std::getenv("DAS_DIGEST_PREFIX");
+    const bool prefix = pe && pe[0] == '1' ? true : n >= (1ull << 22) && !(pe && pe[0] == '0');
+    // (DAS_DIGEST_PREFIX_SHIFT: a shorter prefix, so that most runs need
+    // ordering -- tests of the run fix-up)
+    const char* ps = std::getenv("DAS_DIGEST_PREFIX_SHIFT");
+    const int shift = ps ? std::max(2, std::min(56, std::atoi(ps))) : kPrefixShift;
+    radix_sort_pairs<uint64_t>(key.p, idx, n, prefix ? shift : 0, 64, s);
+    if (prefix && !fix_prefix_runs(key.p, idx, n, shift, s))
+      radix_sort_pairs<uint64_t>(key.p, idx, n, 0, 64, s);
     {
       KScope ks("k_prio_ties", 8.0 * n);            // sorted keys; digests only where the digest bits tie
       hipLaunchKernelGGL(k_prio_ties, G(n), dim3(B), 0, s, (const uint64_t*)key.p, dig, (const uint32_t*)idx, n,

@@ -192,12 +192,14 @@ def test_gpu_exchange_build_indexes_each_link_once(world):
     assert int(counts.sum()) == rows.shape[0]
 
 
-@pytest.mark.parametrize("onesweep", ["1", "0", "0-l2i"])
+@pytest.mark.parametrize("onesweep", ["1", "0", "0-part", "0-part48"])
 def test_gpu_large_build_sort_paths_agree(onesweep, monkeypatch):
     """A build whose sorts exceed 2^20 keys runs the onesweep passes (one
     histogram read up front, decoupled look-back per tile); with
-    DAS_ONESWEEP=0 the per-pass histogram sort; "0-l2i" also writes local2id
-    through the partitioned scatter (the default from 2^22 entries).  Same
+    DAS_ONESWEEP=0 the per-pass histogram sort; "0-part" also sorts the
+    digests on their top 40 bits and orders the runs sharing a prefix
+    afterwards, and writes local2id through the partitioned scatter (both the
+    default from 2^22 entries).  Same
     atoms, ids, links and answers either way, and the same as a small-sort
     reference build of the host copy checked against hashlib handles."""
     import torch
@@ -205,7 +207,14 @@ def test_gpu_large_build_sort_paths_agree(onesweep, monkeypatch):
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
     monkeypatch.setenv("DAS_ONESWEEP", onesweep[0])
-    monkeypatch.setenv("DAS_L2I_PART", "1" if onesweep.endswith("l2i") else "0")
+    monkeypatch.setenv("DAS_L2I_PART", "1" if "part" in onesweep else "0")
+    monkeypatch.setenv("DAS_DIGEST_PREFIX", "1" if "part" in onesweep else "0")
+    # part48: a 16-bit prefix -- nearly every run holds several digests (LDS
+    # run sorts), the hub links' duplicate runs exceed the LDS size (radix)
+    if onesweep.endswith("48"):
+        monkeypatch.setenv("DAS_DIGEST_PREFIX_SHIFT", "48")
+    else:
+        monkeypatch.delenv("DAS_DIGEST_PREFIX_SHIFT", raising=False)
     n_nodes, n_links = 1 << 18, 3 << 20
     db = HipDB(device=0)
     arrays = synthetic.powerlaw_kb_device(db.ctx, n_nodes, n_links)
