@@ -717,6 +717,31 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
+// The owner lanes of one round of 64 consecutive outputs ob + lane (the max
+// lane with pre <= o; pre non-decreasing over the lanes, cnt = each lane's
+// outputs).  Wave-uniform fast path: when no lane's range starts inside the
+// round (a skewed key's long run), its owner is the owner of ob for all 64
+// outputs (*uni = true, two ballots).  Otherwise each lane whose range starts
+// inside the round writes its id at that offset of the wave's 64-entry LDS row
+// (the owner of ob at offset 0) and an inclusive DPP max over the row gives
+// every output its owner: two LDS stores, one load and six VALU steps in place
+// of six dependent ds_bpermute rounds.
+__device__ __forceinline__ int owner_of_round(uint32_t ob, uint32_t pre, uint32_t cnt, uint32_t* row, int lane,
+                                              bool* uni) {
+  const uint64_t m0 = __ballot(pre <= ob);
+  const int l0 = 63 - __clzll((long long)m0);
+  const uint64_t m1 = __ballot(pre <= ob + 63u);
+  if (63 - __clzll((long long)m1) == l0) {
+    *uni = true;
+    return l0;
+  }
+  *uni = false;
+  row[lane] = lane == 0 ? (uint32_t)l0 : 0u;
+  if (cnt && pre > ob && pre - ob < 64u) row[pre - ob] = (uint32_t)lane;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  return (int)wave_incl_max_u32(row[lane]);
+}
+
 // Expands outputs [rs, re) of one 64-row group (relative to the group's first
 // output, written at obase + o): output o belongs to the max lane l with
 // pre[l] <= o and is build row ex[l] + (o - pre[l]).  kXUnroll rounds of 64
@@ -728,9 +753,13 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, int src) {
 #endif
 constexpr int kXUnroll = DAS_DJ_UNROLL;
 template <int NP, int NB, typename T, int V = 1>
-__device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, const uint32_t* pv,
+__device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
-                                             uint64_t obase, int lane) {
+                                             uint64_t obase, int lane, uint32_t* row, int search) {
+  // 32-bit groups: owner_of_round (unless DAS_OWNER_SEARCH=1); each lane's
+  // ex - pre travels as one value (br = (ex - pre)[owner] + o)
+  const bool fast = sizeof(T) == 4 && !search;
+  const uint32_t exp = ex - (uint32_t)pre;
   for (T o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
     // rounds of this iteration that hold outputs (wave-uniform): a group of
     // 64 rows at fan-out ~2 fills 2 of the 4, and the owner searches of an
@@ -738,13 +767,21 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, con
     const int nr = V == 0 ? kXUnroll : (re - o0) >= (T)(64 * kXUnroll) ? kXUnroll : (int)((re - o0 + 63) / 64);
     T o[kXUnroll];
     int l[kXUnroll];
+    bool un[kXUnroll];
     uint32_t br[kXUnroll];
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u) {
       o[u] = o0 + (T)(u * 64 + lane);
       l[u] = 0;
+      un[u] = false;
       br[u] = 0;
       if (u >= nr) continue;
+      if (fast) {
+        const int ll = owner_of_round((uint32_t)(o0 + (T)(u * 64)), (uint32_t)pre, cnt, row, lane, &un[u]);
+        l[u] = ll;
+        br[u] = (un[u] ? (uint32_t)__builtin_amdgcn_readlane((int)exp, ll) : lane_get(exp, ll)) + (uint32_t)o[u];
+        continue;
+      }
       int ll = 0;                                            // owner: max lane with pre <= o
 #pragma unroll
       for (int step = 32; step >= 1; step >>= 1) {
@@ -764,7 +801,7 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t ex, con
       if (u >= nr) continue;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        const uint32_t v = lane_get(pv[i], l[u]);
+        const uint32_t v = un[u] ? (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l[u]) : lane_get(pv[i], l[u]);
         if (o[u] < re) po[i][obase + o[u]] = v;
       }
 #pragma unroll
@@ -814,13 +851,23 @@ struct JoinCols {
   const uint32_t* b[kMaxCols];   // build-side source columns (rows of the sorted build table)
   int po[kMaxCols], bo[kMaxCols];  // their output column indices
   int np, nb;
+  int search;                    // 1: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B)
 };
+
+// DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
+// binary search over the lanes' prefixes (round 3); default: owner_of_round
+inline int owner_search_env() {
+  const char* e = std::getenv("DAS_OWNER_SEARCH");
+  return e && e[0] == '1' ? 1 : 0;
+}
 
 template <int NP, int NB, typename T, int V>
 __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                 uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                 const uint64_t* __restrict__ unit_off, JoinCols jc,
                                                 uint32_t* __restrict__ out, uint64_t cap) {
+  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint32_t* pp[NP > 0 ? NP : 1];
@@ -856,7 +903,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
       const T inc = wave_inclusive_scan(c);
       const T tot = (T)__shfl(inc, 63, 64);
       const T pre = inc - c;                                 // this lane's first output
-      expand_group<NP, NB, T, V>((T)0, tot, pre, e[g].x, pv[g], bb, po, bo, base, lane);
+      expand_group<NP, NB, T, V>((T)0, tot, pre, e[g].y, e[g].x, pv[g], bb, po, bo, base, lane, row, jc.search);
       base += tot;
     }
   }
@@ -883,6 +930,8 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
   for (int i = 0; i < NP; ++i) { pp[i] = jc.p[i]; po[i] = out + (uint64_t)jc.po[i] * cap; }
 #pragma unroll
   for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
+  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
     const uint64_t ob = w * kBalChunk;
@@ -923,7 +972,7 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
         uint32_t pv[NP > 0 ? NP : 1];
 #pragma unroll
         for (int i = 0; i < NP; ++i) pv[i] = r < np ? pp[i][r] : 0u;
-        expand_group<NP, NB, T>(rs, re, pre, e[g].x, pv, bb, po, bo, gb, lane);
+        expand_group<NP, NB, T>(rs, re, pre, (uint32_t)c, e[g].x, pv, bb, po, bo, gb, lane, row, jc.search);
       }
     }
   }
@@ -973,6 +1022,7 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
   int pi = 0, bi = 0;
   do {
     JoinCols part{};
+    part.search = owner_search_env();
     part.np = std::min(jc.np - pi, 4);
     part.nb = std::min(jc.nb - bi, 4);
     for (int i = 0; i < part.np; ++i) { part.p[i] = jc.p[pi + i]; part.po[i] = jc.po[pi + i]; }
@@ -1026,6 +1076,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
                                                const uint32_t* __restrict__ coff, JoinCols jc,
                                                uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo,
                                                uint64_t whi) {
+  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -1085,17 +1137,26 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
           for (int i = 0; i < 4; ++i)
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
         }
+        const uint32_t exp = e[g].x - pre;           // br = (ex - pre)[owner] + o
         // XU rounds of 64 outputs resolved before their loads issue
         for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
           const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
           uint32_t o[XU], br[XU];
           int ll[XU];
+          bool un[XU];
 #pragma unroll
           for (int q = 0; q < XU; ++q) {
             o[q] = o0 + (uint32_t)(q * 64 + lane);
             ll[q] = 0;
+            un[q] = false;
             br[q] = 0;
             if (q >= nr) continue;
+            if (!jc.search) {
+              const int l = owner_of_round(o0 + (uint32_t)(q * 64), pre, c, row, lane, &un[q]);
+              ll[q] = l;
+              br[q] = (un[q] ? (uint32_t)__builtin_amdgcn_readlane((int)exp, l) : lane_get(exp, l)) + o[q];
+              continue;
+            }
             int l = 0;                                 // owner: max lane with pre <= o
 #pragma unroll
             for (int st = 32; st >= 1; st >>= 1) {
@@ -1151,7 +1212,8 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 if (i >= ncp) break;
-                const uint32_t x = lane_get(pv[i], ll[q]);
+                const uint32_t x = un[q] ? (uint32_t)__builtin_amdgcn_readlane((int)pv[i], ll[q])
+                                         : lane_get(pv[i], ll[q]);
                 if (f[q]) po[i][pos] = x;
               }
               if (f[q]) {
@@ -3754,6 +3816,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
                                            const std::vector<const Table*>& Qs) {
   IjPlan pl;
   if (Qs.empty() || !ij_prepare(c, A, q, A.nrows, pl) || pl.empty) return nullptr;
+  pl.jc.search = owner_search_env();
   const JoinCols& jc = pl.jc;
   if (jc.np > 4 || jc.nb > 4) return nullptr;
   int fb = -1;
