@@ -940,6 +940,10 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     arrays, specs, cfg, scaling = make_kb(args, rank, world, db)
     log(f"building the device index ({arrays.n_expr} expressions)")
     db.load_arrays(arrays)
+    # the reference's loader ends with db.prefetch() (distributed_atom_space.py:
+    # 138-168, redis_mongo_db.py:89-127): host copies of the node directory and
+    # per-atom metadata, up to HipDB.PREFETCH_MAX_ATOMS (part of the load, untimed)
+    db.prefetch()
     if getattr(arrays, "expr_on_device", False):
         arrays.drop_expr()          # device-generated input: free it once indexed
     del arrays

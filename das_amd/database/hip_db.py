@@ -85,6 +85,8 @@ def _has_composite(tables):
 
 class HipDB(RelationalDB):
 
+    PREFETCH_MAX_ATOMS = 1 << 26            # host mirrors of prefetch() up to this many atoms
+
     def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False):
         """`tuple_targets=True` reproduces the reference DB path exactly,
         including returning targets as tuples from get_matched_links, which
@@ -112,6 +114,7 @@ class HipDB(RelationalDB):
         self.shard = None
         self._mirror = None
         self._outgoing = None
+        self._node_dir = None
         self.pattern_black_list = []
 
     def __repr__(self):
@@ -134,6 +137,7 @@ class HipDB(RelationalDB):
         self._handle_cache = {}
         self._mirror = None
         self._outgoing = None
+        self._node_dir = None
 
     def load_metta(self, texts):
         self.load_arrays(_loader.parse_metta(texts).finish())
@@ -159,7 +163,16 @@ class HipDB(RelationalDB):
     # --------------------------------------------------------------- helpers
     def _resolve(self, handles):
         """handle -> (id, category, arity) through a host cache of the device
-        index (handles are immutable once the index is built)."""
+        index (handles are immutable once the index is built).  After
+        prefetch() every node handle is in a host directory: a fresh query
+        anchor resolves without a device round trip."""
+        nd = self._node_dir
+        if nd is not None:
+            for h in handles:
+                if h not in self._handle_cache:
+                    i = nd.get(h)
+                    if i is not None:
+                        self._handle_cache[h] = (i, 1, 0)
         miss = [h for h in dict.fromkeys(handles) if h not in self._handle_cache]
         if miss and all(type(h) is str and len(h) == 32 for h in miss):
             try:
@@ -460,8 +473,17 @@ class HipDB(RelationalDB):
         category, arity, type, name leaf) and the outgoing CSR to the host, so
         get_link_targets / get_link_type / get_node_type / get_node_name are
         host lookups instead of a device round trip each (the
-        SimplePatternMiner.ipynb halo walk calls get_link_targets per link)."""
-        self._host_mirror()
+        SimplePatternMiner.ipynb halo walk calls get_link_targets per link),
+        and a host directory of the node handles lets a query's fresh node
+        anchors resolve without a device lookup.  KBs above
+        PREFETCH_MAX_ATOMS atoms keep every call on the device."""
+        st = self.ctx.stats()
+        if int(st.n_atoms) > self.PREFETCH_MAX_ATOMS:
+            return                          # (a 10^9-link KB: the device index answers every call)
+        dig, cat, _, _, _ = self._host_mirror()
+        if self._node_dir is None:
+            sel = np.nonzero(cat == 1)[0]
+            self._node_dir = dict(zip(_lib.digests_to_hex(dig[sel]), sel.tolist())) if sel.size else {}
         if self._outgoing is None:
             self._outgoing = self.ctx.outgoing_csr()
 
