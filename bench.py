@@ -989,16 +989,21 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         stage = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
         per_query = dict(zip(per_query, (int(x) for x in _sync_sum(dist, list(per_query.values()), stage))))
     # per-query wall time (the warm query set of the first timed step, 5 runs each)
-    per_query_ms = {}
+    per_query_ms, per_query_ops = {}, {}
+    from das_amd import _lib as _L
     for name, q in ([] if args.no_extras else qsets[args.warmup]):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+        c0 = _L.counters()
         t_q = time.perf_counter()
         for _ in range(5):
             run(q)
         torch.cuda.synchronize()
         per_query_ms[name] = round((time.perf_counter() - t_q) * 1e3 / 5, 4)
+        c1 = _L.counters()
+        # kernel scopes launched and host read-backs waited on, per query
+        per_query_ops[name] = [round((c1[0] - c0[0]) / 5, 1), round((c1[1] - c0[1]) / 5, 1)]
     db.ctx.prof_reset()
     db.ctx.prof_only(dominant["kernel"] if dominant else None)
     db.ctx.prof_enable(True)
@@ -1091,6 +1096,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                 "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
         cfg = dict(cfg, bindings_per_step=per_query, parallelism=f"links sharded x{world}")
         cfg["query_ms_rank0"] = per_query_ms
+        cfg["query_launches_readbacks_rank0"] = per_query_ops
         out = {
             "metric": "pattern matches/sec (bindings/s) + % HBM roofline",
             "value": value, "unit": "bindings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1100,6 +1106,13 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             "step_roofline": step_roofline(warm_stats if dominant else stats, ms_per_step, world,
                                            1 if dominant else args.steps),
             "cpu_baseline": cpu,
+            # latency-bound workloads: per query, its wall us and the kernel
+            # scopes / host read-backs it takes (FlyBase: launches and waits,
+            # not bytes, bound it)
+            "latency": {name.split(" ")[0]: {"us": round(per_query_ms[name] * 1e3, 1),
+                                             "launches": per_query_ops[name][0],
+                                             "readbacks": per_query_ops[name][1]}
+                        for name in per_query_ms} or None,
             "incl_materialisation": incl,
             "kernels": kernels_of(warm_stats if dominant else stats),
             "kernels_from": "last warmup step (every scope)" if dominant else "timed steps (every scope)",

@@ -110,6 +110,7 @@ _SIGS = {
     "das_ctype_lookup": (C.c_int, [P, P, P]),
     "das_incoming": (C.c_int, [P, C.c_uint32, P, C.c_uint64, P]),
     "das_export_outgoing": (C.c_int, [P, P, P, P, P]),
+    "das_counters": (C.c_int, [P]),
     "das_scan_link": (C.c_int, [P, C.POINTER(das_link_scan_t), C.POINTER(P)]),
     "das_scan_template": (C.c_int, [P, C.POINTER(das_template_scan_t), C.POINTER(P)]),
     "das_scan_type": (C.c_int, [P, C.c_uint32, P]),
@@ -272,6 +273,13 @@ def composite_digest(digests):
 
 def digest_to_hex(d):
     return np.asarray(d, dtype="<u4").tobytes().hex()
+
+
+def counters():
+    """(kernel launches, host read-backs) since the library loaded (das_counters)."""
+    out = (C.c_uint64 * 2)()
+    check(lib().das_counters(out))
+    return int(out[0]), int(out[1])
 
 
 def digests_to_hex(arr):

@@ -1,6 +1,7 @@
 // extern "C" boundary (include/das_mi355x.h).  Every entry point catches
 // das::Error / std::exception and returns a status; the message is kept per
 // context for das_last_error.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -203,6 +204,12 @@ int das_ctx_destroy(das_ctx_t* ctx) {
 }
 
 const char* das_last_error(const das_ctx_t* ctx) { return ctx ? ctx->c.err.c_str() : g_err.c_str(); }
+
+int das_counters(uint64_t out[2]) {
+  if (!out) return fail(nullptr, DAS_ERR_INVALID, "null out");
+  das::read_counters(out);
+  return DAS_OK;
+}
 
 int das_ctx_sync(das_ctx_t* ctx) {
   return guarded(ctx, [&] { DAS_HIP(hipStreamSynchronize(ctx->c.s)); });
@@ -780,10 +787,24 @@ Ctx*& active_ctx() {
   return c;
 }
 
+namespace {
+std::atomic<uint64_t> g_launches{0}, g_readbacks{0};
+}  // namespace
+void count_launch() { g_launches.fetch_add(1, std::memory_order_relaxed); }
+void count_readback() { g_readbacks.fetch_add(1, std::memory_order_relaxed); }
+void read_counters(uint64_t out[2]) {
+  out[0] = g_launches.load(std::memory_order_relaxed);
+  out[1] = g_readbacks.load(std::memory_order_relaxed);
+}
+
 KScope::KScope(const char* name, double algorithmic_bytes) {
   Ctx* c = active_ctx();
-  if (c && c->prof) impl = new ProfScope(*c, name, algorithmic_bytes);
-  else if (trace_on()) trace_mark("kernel", std::string(name) + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
+  if (c && c->prof) {
+    impl = new ProfScope(*c, name, algorithmic_bytes);      // (counts the launch)
+  } else {
+    count_launch();
+    if (trace_on()) trace_mark("kernel", std::string(name) + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
+  }
 }
 
 namespace {

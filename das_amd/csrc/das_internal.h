@@ -181,6 +181,11 @@ struct Ctx {
 // das_plan_execute.
 bool trace_on();
 void trace_mark(const char* what, const std::string& name = std::string());
+// process-wide counts of kernel scopes entered and of host read-backs waited
+// on (das_counters; bench.py reports them per query for latency-bound legs)
+void count_launch();
+void count_readback();
+void read_counters(uint64_t out[2]);
 void trace_dump(const char* title);
 
 struct ProfScope {
@@ -189,6 +194,7 @@ struct ProfScope {
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
+    count_launch();
     if (trace_on()) trace_mark("kernel", name + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
     if (!c.prof || (!c.prof_only.empty() && c.prof_only != name)) return;
     a = c.take_event();

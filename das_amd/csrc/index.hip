@@ -105,6 +105,7 @@ PubSlot pub_reserve() {
 }
 
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
+  count_readback();
   trace_mark("wait");
   for (uint64_t it = 1;; ++it) {
     if (__atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq) break;

@@ -56,6 +56,9 @@ int das_ctx_create(int device, void* stream, das_ctx_t** out);
 int das_ctx_destroy(das_ctx_t* ctx);
 const char* das_last_error(const das_ctx_t* ctx);
 int das_ctx_sync(das_ctx_t* ctx);
+/* Process-wide counters since load: out[0] = kernel launches (instrumented
+ * scopes), out[1] = host read-backs waited on (per-query latency accounting). */
+int das_counters(uint64_t out[2]);
 int das_version(void);
 
 /* ---- ExpressionHasher (expression_hasher.py:9-35) ------------------------ */
