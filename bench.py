@@ -1010,6 +1010,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    coll0 = engine.sdb.plan_stats["collectives"] if engine else 0
     t0 = time.perf_counter()
     log("timed steps")
     bindings = 0
@@ -1019,6 +1020,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    coll_per_step = (engine.sdb.plan_stats["collectives"] - coll0) / args.steps if engine else 0
     db.ctx.prof_enable(False)
     db.ctx.prof_only(None)
     stats = db.ctx.prof_stats()
@@ -1120,6 +1122,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         }
         if world > 1:
             out["sharded_plan_stats"] = dict(engine.sdb.plan_stats)
+            out["collectives_per_step"] = round(coll_per_step, 2)
         if variants:
             # the default's own And-join figure from the same timed steps' events
             variants["default (views)"] = {"ms_per_step": round(ms_per_step, 4),
@@ -1171,7 +1174,7 @@ def _compact_leg(d):
     sr = d.get("step_roofline")
     out["step_roofline"] = {"frac": sr.get("frac")} if sr else None
     out["cpu_baseline"] = _compact_cpu(d.get("cpu_baseline"), full=False)
-    for k in ("latency", "summary"):          # latency-bound legs: per-query us, launches / read-backs
+    for k in ("latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
         if d.get(k) is not None:
             out[k] = d[k]
     return out
@@ -1191,7 +1194,7 @@ def compact_line(full):
     line["roofline"] = _compact_roofline(full.get("roofline"))
     line["step_roofline"] = _compact_roofline(full.get("step_roofline"))
     line["cpu_baseline"] = _compact_cpu(full.get("cpu_baseline"))
-    for k in ("latency", "summary"):
+    for k in ("latency", "summary", "collectives_per_step"):
         if full.get(k) is not None:
             line[k] = full[k]
     if full.get("workloads"):

@@ -145,6 +145,7 @@ _SIGS = {
                                            C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
                                            C.POINTER(C.c_int32), P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "das_plan_estimates": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, P]),
+    "das_plan_bounds": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, P]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
@@ -551,6 +552,13 @@ class Context:
         out = np.zeros(max(n_nodes, 1), dtype=np.uint64)
         nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
         check(lib().das_plan_estimates(self.h, nodes, n_nodes, ptr(out)), self.h)
+        return out[:n_nodes]
+
+    def plan_bounds(self, words, n_nodes):
+        """Per node, an upper bound of plan_estimates over its shape (u64; 2^64-1 unknown)."""
+        out = np.zeros(max(n_nodes, 1), dtype=np.uint64)
+        nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
+        check(lib().das_plan_bounds(self.h, nodes, n_nodes, ptr(out)), self.h)
         return out[:n_nodes]
 
     def scan_words(self, words, node):

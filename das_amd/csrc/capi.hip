@@ -736,6 +736,23 @@ int das_plan_estimates(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n,
   });
 }
 
+int das_plan_bounds(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint64_t* rows) {
+  if (!ctx || (n && (!nodes || !rows))) return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    DAS_CHECK(ctx->c.idx.built, das::DAS_E_NOT_BUILT, "index not built");
+    const das::Index& idx = ctx->c.idx;
+    for (uint32_t i = 0; i < n; ++i) {
+      const das_plan_node_t& x = nodes[i];
+      if (x.op == DAS_PLAN_LINK || x.op == DAS_PLAN_INPUT)
+        rows[i] = das::scan_bound(ctx->c, x.scan);
+      else if (x.op == DAS_PLAN_TEMPLATE && x.scan.type_id < idx.ctype_range.size())
+        rows[i] = idx.ctype_range[x.scan.type_id].end - idx.ctype_range[x.scan.type_id].begin;
+      else
+        rows[i] = 0;
+    }
+  });
+}
+
 int das_prof_enable(das_ctx_t* ctx, int on) {
   return guarded(ctx, [&] {
     das::prof_collect(ctx->c);

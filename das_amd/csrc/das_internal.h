@@ -311,6 +311,10 @@ PlanOutput plan_execute_sharded(Ctx& c, const das_plan_node_t* nodes, uint32_t n
                                 const std::vector<const Table*>& inputs, std::vector<uint8_t>& checks);
 // Rows a das_scan_link would read (its index ranges; an upper bound of its output).
 uint64_t scan_estimate(Ctx& c, const das_link_scan_t& q);
+// An upper bound of scan_estimate over every choice of the scan's grounded
+// targets (its shape): the largest key range of its type at a grounded
+// position; the exact estimate when nothing is grounded; ~0 when unknown.
+uint64_t scan_bound(Ctx& c, const das_link_scan_t& q);
 // query.hip: an And of ordered Links (terms) and Not(Link) filters (anti)
 // evaluated by one single-workgroup launch when its running result stays
 // small.  0: not taken (the caller evaluates it operator by operator);

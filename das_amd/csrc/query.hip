@@ -2058,6 +2058,65 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
 }
 }  // namespace
 
+// Largest key range of P_{a,p} among the keys of named type `type`: an upper
+// bound of any single-key scan of that (type, position) whatever the key.
+__global__ void k_type_max_run(const uint64_t* __restrict__ ukey, const uint64_t* __restrict__ uoff, uint64_t nkeys,
+                               uint64_t klo, uint64_t khi, unsigned long long* out) {
+  __shared__ uint64_t s_b[2];
+  if (threadIdx.x < 2) {                         // this block's copy of the type's key bounds
+    const uint64_t v = threadIdx.x ? khi : klo;
+    uint64_t lo = 0, hi = nkeys;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (ukey[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    s_b[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  uint64_t m = 0;
+  for (uint64_t k = s_b[0] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < s_b[1];
+       k += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, uoff[k + 1] - uoff[k]);
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint64_t)__shfl_xor((unsigned long long)m, d, 64));
+  if (__lane_id() == 0 && m) atomicMax(out, (unsigned long long)m);
+}
+
+uint64_t type_max_run(Ctx& c, uint32_t a, uint32_t p, uint32_t type) {
+  Index& idx = c.idx;
+  const std::array<uint64_t, 4> key{a, p, type, ~0ull};          // (range_cache: these never collide)
+  auto it = idx.range_cache.find(key);
+  if (it != idx.range_cache.end()) return it->second.first;
+  const PosIndex& P = idx.pidx[a][p];
+  const uint64_t klo = (uint64_t)type << 32, khi = (uint64_t)(type + 1) << 32;
+  uint64_t m = 0;
+  if (!P.h_ukey.empty() || P.nkeys == 0) {
+    const uint64_t b = std::lower_bound(P.h_ukey.begin(), P.h_ukey.end(), klo) - P.h_ukey.begin();
+    const uint64_t e = std::lower_bound(P.h_ukey.begin(), P.h_ukey.end(), khi) - P.h_ukey.begin();
+    for (uint64_t k = b; k < e; ++k) m = std::max<uint64_t>(m, P.h_uoff[k + 1] - P.h_uoff[k]);
+  } else {
+    DBuf<unsigned long long> out(1, c.s);
+    fill_dev(out.p, 0, 8, c.s);
+    hipLaunchKernelGGL(k_type_max_run, dim3(grid_for(P.nkeys, B, 1024)), dim3(B), 0, c.s, (const uint64_t*)P.ukey,
+                       (const uint64_t*)P.uoff, P.nkeys, klo, khi, out.p);
+    DAS_HIP(hipGetLastError());
+    m = read_u64(reinterpret_cast<const uint64_t*>(out.p), c.s);
+  }
+  idx.range_cache[key] = {m, 0};
+  return m;
+}
+
+uint64_t scan_bound(Ctx& c, const das_link_scan_t& q) {
+  const uint32_t ar = q.arity;
+  bool grounded = false;
+  for (uint32_t p = 0; p < ar && p < 8; ++p) grounded |= q.target[p] != kNone;
+  if (!grounded) return scan_estimate(c, q);               // no anchor: the same rows every time
+  if (ar == 0 || ar > (uint32_t)kMaxPosArity || q.type_id == kNone || q.type_id >= c.idx.n_types) return ~0ull;
+  uint64_t best = ~0ull;
+  for (uint32_t p = 0; p < ar; ++p)
+    if (q.target[p] != kNone && c.idx.pidx[ar][p].nkeys) best = std::min(best, type_max_run(c, ar, p, q.type_id));
+  return best;
+}
+
 uint64_t scan_estimate(Ctx& c, const das_link_scan_t& q) {
   ScanPrep P;
   scan_prepare(c, q, P);

@@ -107,7 +107,12 @@ class ShardedDB(RelationalDB):
         # join placements taken; native = expressions evaluated by one sharded
         # native plan (fallback: its check failed), collectives issued
         self.plan_stats = {"colocated": 0, "broadcast": 0, "exchange": 0, "heavy": 0, "native": 0,
-                           "native_fallback": 0, "collectives": 0}
+                           "native_fallback": 0, "collectives": 0, "size_cache": 0}
+        # leaf sizes of sharded plans known without an exchange (generation,
+        # exact sizes by leaf words, upper bounds by leaf shape)
+        self._size_gen = None
+        self._exact_sizes = {}
+        self._shape_sizes = {}
         # DAS_JOIN_PLACEMENT=exchange|broadcast forces one placement (tests)
         self.force = os.environ.get("DAS_JOIN_PLACEMENT", "")
         # the top-level expression of the current ShardedMatcher call, and the
@@ -393,9 +398,7 @@ class ShardedDB(RelationalDB):
         elif not leaves:
             local, gathered = [], []                     # settled on the host: the same on every shard
         else:
-            est = self._allgather_i64(ctx.plan_estimates(nodes, n)[leaves])        # collective 1
-            G = dict(zip(leaves, est.sum(axis=0).tolist()))
-            M = dict(zip(leaves, est.max(axis=0).tolist()))
+            G, M = self._leaf_sizes(ctx, db, nodes, n, rec, leaves)                 # collective 1, or cached
             local = []
             if flat:
                 small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
@@ -488,6 +491,70 @@ class ShardedDB(RelationalDB):
         answer._set(self, rel)
         answer.negation = negation
         return matched
+
+    SIZE_CACHE = 1 << 12                    # leaf sizes kept per kind
+
+    @staticmethod
+    def _shape_key(words):
+        """A leaf record with its grounded targets masked (scan and index-join
+        target words, include/das_mi355x.h das_plan_node_t): its query shape."""
+        from . import _lib as L
+        w = np.array(words, dtype=np.uint32)
+        for base in (L.PLAN_SCAN, 28):
+            t = w[base + 2:base + 10]
+            t[t != np.uint32(L.DAS_NONE)] = 0xFFFFFFFE
+        return w.tobytes()
+
+    def _leaf_sizes(self, ctx, db, nodes, n, rec, leaves):
+        """(G, M) per leaf: its rows over all shards and on the largest one.
+        Exact from the estimate exchange (one all-gather of every shard's
+        das_plan_estimates, with its das_plan_bounds riding along), or --
+        when every leaf was seen before -- from the caches that exchange
+        fills: a leaf's exact sizes by its words (a term that repeats, e.g.
+        FlyBase's unanchored E(rec, V2, V1)), else its shape's upper bounds
+        (a fresh anchor of a known shape).  Then no collective: an anchored
+        query of a known shape takes 2 collectives instead of 3.  Bounds only
+        raise gather slot sizes and split decisions, never the answer.  The
+        caches fill from collective results, so every shard holds the same."""
+        if self._size_gen != db.generation:
+            self._size_gen = db.generation
+            self._exact_sizes, self._shape_sizes = {}, {}
+        keys = [rec[i].tobytes() for i in leaves]
+        skeys = [self._shape_key(rec[i]) for i in leaves]
+        G, M = {}, {}
+        if os.environ.get("DAS_SHARD_SIZE_CACHE") != "0":
+            small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
+            for i, k, sk in zip(leaves, keys, skeys):
+                hit = self._exact_sizes.get(k)
+                if hit is None:
+                    # a shape bound only where it settles the leaf as small
+                    # (gathered); a large bound (a hub key somewhere) needs the
+                    # exact sizes for the split decision
+                    hit = self._shape_sizes.get(sk)
+                    if hit is not None and hit[0] > small:
+                        hit = None
+                if hit is None:
+                    break
+                G[i], M[i] = hit
+            else:
+                self.plan_stats["size_cache"] += 1
+                return G, M
+        nl = len(leaves)
+        b = ctx.plan_bounds(nodes, n)[leaves]
+        local = np.concatenate([ctx.plan_estimates(nodes, n)[leaves].astype(np.int64),
+                                np.where(b == np.uint64(2 ** 64 - 1), -1, b.astype(np.int64))])
+        got = self._allgather_i64(local)
+        est, bnd = got[:, :nl], got[:, nl:]
+        if len(self._exact_sizes) > self.SIZE_CACHE:
+            self._exact_sizes.clear()
+        if len(self._shape_sizes) > self.SIZE_CACHE:
+            self._shape_sizes.clear()
+        for j, i in enumerate(leaves):
+            G[i], M[i] = int(est[:, j].sum()), int(est[:, j].max())
+            self._exact_sizes[keys[j]] = (G[i], M[i])
+            if (bnd[:, j] >= 0).all():
+                self._shape_sizes[skeys[j]] = (int(bnd[:, j].sum()), int(bnd[:, j].max()))
+        return G, M
 
     OWNER_TABLES = 16                       # answer tables an owner-evaluated plan describes
 

@@ -349,6 +349,12 @@ int das_plan_execute_sharded(das_ctx_t* ctx, const das_plan_node_t* nodes, uint3
 /* rows[i] = the index rows node i's scan would read (LINK / INPUT nodes; an
  * upper bound of its output on this shard), 0 for other nodes. */
 int das_plan_estimates(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint64_t* rows);
+/* Per LINK / TEMPLATE node, an upper bound of das_plan_estimates over every
+ * value of its grounded targets (its query shape): the largest pattern-key
+ * range of its type at a grounded position; UINT64_MAX when unknown.  A
+ * sharded plan caches these per shape, so a fresh anchor of a known shape
+ * needs no estimate exchange. */
+int das_plan_bounds(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint64_t* rows);
 
 /* ---- multi-GPU exchange (RCCL all-to-all of binding rows) ----- */
 /* Rows of `t` regrouped by destination = mix(key columns) % nparts (stable

@@ -398,6 +398,11 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
         if mode.startswith("flybase"):
             got = per_rank[0][qi]
             assert got["native"] == 1 and got["collectives"] <= 3, (q, got["native"], got["collectives"])
+    if mode.startswith("flybase"):
+        # the second gene's queries reuse the first's leaf sizes (shape cache):
+        # no estimate exchange, 2 collectives each
+        assert stats["size_cache"] > 0, stats
+        assert any(per_rank[0][qi]["collectives"] == 2 for qi in range(len(queries))), per_rank[0][:-2]
     if mode.endswith("_owner"):
         # wholly gathered top-level plans were evaluated by one rank each, in turn
         owners = [[r for r in range(world) if per_rank[r][qi].get("local")] for qi in range(len(queries))]
