@@ -736,10 +736,15 @@ __device__ __forceinline__ int owner_of_round(uint32_t ob, uint32_t pre, uint32_
     return l0;
   }
   *uni = false;
-  row[lane] = lane == 0 ? (uint32_t)l0 : 0u;
-  if (cnt && pre > ob && pre - ob < 64u) row[pre - ob] = (uint32_t)lane;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  return (int)wave_incl_max_u32(row[lane]);
+  // volatile: lanes exchange values through the row, which the compiler's
+  // per-lane memory model would otherwise let it forward (a lane's load
+  // replaced by its own earlier store, the load sunk under the branch of the
+  // other store); one wave's LDS accesses complete in program order
+  typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
+  lds_u32* vr = (lds_u32*)row;
+  vr[lane] = lane == 0 ? (uint32_t)l0 : 0u;
+  if (cnt && pre > ob && pre - ob < 64u) vr[pre - ob] = (uint32_t)lane;
+  return (int)wave_incl_max_u32(vr[lane]);
 }
 
 // Expands outputs [rs, re) of one 64-row group (relative to the group's first
