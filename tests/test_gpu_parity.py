@@ -561,6 +561,44 @@ def test_gpu_hub_join_expansion(force, monkeypatch):
         assert same(got, want), (q, got.get("n"), want.get("n"))
 
 
+@pytest.mark.parametrize("search", ["0", "1"])
+@pytest.mark.parametrize("shape", ["sparse", "fanout2", "skew", "wide"])
+def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
+    """das_join of two-column tables on one key through the direct-address
+    join, whose expansions find each output's owner lane per round of 64
+    outputs (owner_of_round: ballot fast path / LDS row + DPP max; search=1:
+    the ds_bpermute binary search): lanes without outputs, fan-out ~2, skewed
+    keys (the output-balanced expansion) and a wide fan-out, against a numpy
+    join with multiplicities."""
+    monkeypatch.setenv("DAS_OWNER_SEARCH", search)
+    from das_amd import _lib, synthetic
+    db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
+    rng = np.random.default_rng({"sparse": 1, "fanout2": 2, "skew": 3, "wide": 4}[shape])
+    nk = 5000
+    if shape == "sparse":
+        pk, qk = rng.integers(0, nk, 60000), rng.integers(0, nk, 300)
+    elif shape == "fanout2":
+        pk, qk = rng.integers(0, nk, 60000), rng.integers(0, nk, 2 * nk)
+    elif shape == "skew":
+        pk = np.where(rng.random(60000) < 0.3, 7, rng.integers(0, nk, 60000))
+        qk = np.concatenate([np.full(3000, 7), rng.integers(0, nk, 3000)])
+    else:
+        pk, qk = rng.integers(0, 50, 3000), rng.integers(0, 50, 4000)
+    pa = rng.integers(0, 1 << 20, len(pk)).astype(np.uint32)
+    qb = rng.integers(0, 1 << 20, len(qk)).astype(np.uint32)
+    P = db.ctx.table_from_host(_lib.TABLE_ORDERED, [0, 1], np.stack([pa, pk.astype(np.uint32)]))
+    Q = db.ctx.table_from_host(_lib.TABLE_ORDERED, [1, 2], np.stack([qk.astype(np.uint32), qb]))
+    P.set_bounds([0, 0], [(1 << 20) - 1, nk])
+    Q.set_bounds([0, 0], [nk, (1 << 20) - 1])
+    got = db.ctx.join(P, Q).fetch()
+    by = {}
+    for k, b in zip(qk.tolist(), qb.tolist()):
+        by.setdefault(k, []).append(b)
+    want = sorted((a, k, b) for a, k in zip(pa.tolist(), pk.tolist()) for b in by.get(k, ()))
+    assert len(want) > 1000
+    assert sorted(zip(*[c.tolist() for c in got])) == want
+
+
 @pytest.mark.parametrize("guard", ["1", "0"])
 @pytest.mark.parametrize("build", ["", "sparse", "dense"])
 @pytest.mark.parametrize("probe_rows", [5000, 40000])
