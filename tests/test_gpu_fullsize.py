@@ -280,7 +280,7 @@ def test_gpu_flybase_fullsize_counts():
     db = HipDB(device=0)
     db.load_arrays(arrays)
     db.prefetch()                        # anchors resolved through the host node directory (bench.py's path)
-    assert db._node_dir is not None and len(db._node_dir) > 2_000_000
+    assert db._node_dir is not None and len(db._node_dir) > 600_000          # every node (genes, FB ids, values)
     for gene in (7, 7 + 7919):
         do_terms = synthetic.flybase_do_terms(arrays, gene=gene)
         want = _flybase_counts(arrays, gene, do_terms)
