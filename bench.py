@@ -857,11 +857,15 @@ def run_getlinks(args, rank, world, local_rank):
     steps = max(1, min(args.steps, args.gl_steps))
     seed = lambda i: EH.terminal_hash("gene", f"g{(7 + 7919 * i) % args.fb_genes}")  # noqa: E731
     rng = np.random.default_rng(5)
+    log("getlinks warmup walk")
     for i in range(args.warmup and 1):
         miner_walk(das, [seed(1000 + i)], rng)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    runs = [miner_walk(das, [seed(i)], rng) for i in range(steps)]
+    runs = []
+    for i in range(steps):
+        runs.append(miner_walk(das, [seed(i)], rng))
+        log(f"getlinks walk {i}: {sum(h['queries'] for h in runs[-1]['halo'])} queries")
     elapsed = time.perf_counter() - t0
     tot = _miner_totals(runs)
     cpu = None

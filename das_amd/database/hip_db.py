@@ -350,6 +350,15 @@ class HipDB(RelationalDB):
         if cols.shape[1] == 0:
             return []
         links = self.hex_of(cols[0])
+        # the links of a pattern answer are indexed here (category 2): a
+        # caller's next get_link_targets / link lookups of them (the
+        # SimplePatternMiner halo walk) need no device lookup
+        hc = self._handle_cache
+        if len(hc) > (1 << 23):
+            hc.clear()
+        for h, i in zip(links, cols[0].tolist()):
+            if h not in hc:
+                hc[h] = (i, 2, arity)
         tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
         return [(links[i], self._fmt_targets([tg[k][i] for k in range(arity)])) for i in range(cols.shape[1])]
 
