@@ -205,9 +205,16 @@ class HipDB(RelationalDB):
         return np.array([r[0] for r in self._resolve(handles)], dtype=np.int64)
 
     def _lookup(self, handle):
-        return self._resolve([handle])[0]
+        r = self._handle_cache.get(handle)
+        return r if r is not None else self._resolve([handle])[0]
 
     def hex_of(self, ids) -> List[str]:
+        if len(ids) <= 16:
+            # a few ids (one link's targets): the cache, no numpy set ops
+            hc = self._hex_cache
+            out = [hc.get(int(i)) for i in ids]
+            if None not in out:
+                return out
         ids = np.asarray(ids, dtype=np.uint32).ravel()
         if ids.size == 0:
             return []
