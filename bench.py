@@ -218,29 +218,47 @@ def _pattern_templates(link_type, targets):
     return []
 
 
-def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_length=2):
+def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_length=2,
+               max_level_nodes=1000, max_level_links=50_000, progress=None):
     """SimplePatternMiner.ipynb cells 6 and 9 through the facade API `api`
     (get_links / get_link_targets / get_link_type / get_node_type /
     get_node_name): the halo walk (level by level, every template around
     every node handle, get_link_targets of every link found) and
     build_patterns' counts over the level-0 links plus a `link_rate` sample
-    of the deeper ones.  Returns per phase: seconds, calls, links."""
-    node_handles = sorted(set(seeds))
+    of the deeper ones.  Returns per phase: seconds, calls, links.
+
+    A FlyBase schema or predicate node sits in millions of links, so a
+    level expands at most `max_level_nodes` node handles and follows the
+    targets of at most `max_level_links` links (in handle order, so every
+    backend walks the same links); a level that hit a bound says so
+    ("bounded")."""
+    node_handles = sorted(set(seeds))[:max_level_nodes]
     levels, halo = [], []
-    for _ in range(halo_length):
+    for lv in range(halo_length):
         t0 = time.perf_counter()
-        new_nodes, level_links, n_queries = set(), set(), 0
-        for h in node_handles:
+        new_nodes, level_links, n_queries, bounded = set(), set(), 0, False
+        t_log = t0
+        for k, h in enumerate(node_handles):
+            if progress and time.perf_counter() - t_log > 30:
+                t_log = time.perf_counter()
+                progress(f"halo level {lv}: node {k} of {len(node_handles)}, {n_queries} queries")
             for tpl in _halo_templates(h):
-                found = set(api.get_links(None, None, tpl))
-                n_queries += len(found) + 1                       # the notebook's count (:411-413)
-                for link in found:
+                found = sorted(set(api.get_links(None, None, tpl)))
+                n_queries += 1                                    # the notebook's count (:411-413):
+                for link in found:                                # get_links + one per link found
+                    if link not in level_links and len(level_links) >= max_level_links:
+                        bounded = True
+                        break
+                    n_queries += 1
+                    level_links.add(link)
                     new_nodes.update(api.get_link_targets(link))
-                level_links |= found
+        bounded = bounded or len(new_nodes) > max_level_nodes
         halo.append({"s": time.perf_counter() - t0, "queries": n_queries, "links": len(level_links),
-                     "nodes": len(node_handles)})
+                     "nodes": len(node_handles), "bounded": bounded})
+        if progress:
+            progress(f"halo level {lv}: {len(node_handles)} nodes, {n_queries} queries, {len(level_links)} links")
         levels.append(level_links)
-        node_handles = sorted(new_nodes)
+        node_handles = sorted(new_nodes)[:max_level_nodes]
     sample = sorted(levels[0])
     for lv in levels[1:]:
         sample += [link for link in sorted(lv) if rng.random() < link_rate][:max_pattern_links]
@@ -859,12 +877,12 @@ def run_getlinks(args, rank, world, local_rank):
     rng = np.random.default_rng(5)
     log("getlinks warmup walk")
     for i in range(args.warmup and 1):
-        miner_walk(das, [seed(1000 + i)], rng)
+        miner_walk(das, [seed(1000 + i)], rng, progress=log)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     runs = []
     for i in range(steps):
-        runs.append(miner_walk(das, [seed(i)], rng))
+        runs.append(miner_walk(das, [seed(i)], rng, progress=log))
         log(f"getlinks walk {i}: {sum(h['queries'] for h in runs[-1]['halo'])} queries")
     elapsed = time.perf_counter() - t0
     tot = _miner_totals(runs)

@@ -416,7 +416,7 @@ __global__ void k_join_expand(const uint64_t* offs, uint64_t np, const uint32_t*
 // are 64-row aligned, so a partial last quad stays inside the capacity); one
 // division per thread: the grid stride S quads advances (i, j) by
 // (4S / nb, 4S % nb) with a carry.  A pure write stream at ~6 TB/s on MI355X
-// (4-byte stores: ~3.4 TB/s; tools/ubench/cart_bw.hip, profiles/r3_cart_bw.txt).
+// (4-byte stores: ~3.4 TB/s; tools/ubench/cart_bw.hip, profiles/archive/r3_cart_bw.txt).
 // NC: output columns, specialised up to 6.
 template <int NC>
 __global__ void __launch_bounds__(B) k_cartesian(OutMap om, uint64_t np, uint64_t nb, uint64_t total, uint64_t sq,
@@ -2286,7 +2286,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   // KBs: node ranges of 10^8 ids against 10^8-row probes).  (Small joins
   // over a wide range -- bio QUERY_3's 2*10^4-row sides keyed by Member link
   // ids over 1.4*10^7 slots -- measured no faster sorted: 2^22 instead of
-  // 2^26 below, bio step 1.994 vs 1.964 ms, profiles/r3_bio_range_floor_ab.json)
+  // 2^26 below, bio step 1.994 vs 1.964 ms, profiles/archive/r3_bio_range_floor_ab.json)
   if (range > std::max<uint64_t>(std::max<uint64_t>(8 * Q.nrows, 4 * P.nrows), 1ull << 26) ||
       range >= 0xFFFFFFFFull || Q.nrows >= 0xFFFFFFFFull)
     return nullptr;
@@ -3923,7 +3923,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   // DAS_FILT_FUSED=1: one pass, unsorted output, while the worst case (every
   // virtual output kept) fits the output buffer.  Off by default: at config 5
   // it ran 924 us against 337 + 296 us for the two ordered passes (round 3,
-  // profiles/r3_hub_filt_ab.json) -- the LDS flag tiles cut its occupancy
+  // profiles/archive/r3_hub_filt_ab.json) -- the LDS flag tiles cut its occupancy
   const char* ff = std::getenv("DAS_FILT_FUSED");
   if (ff && ff[0] == '1' && (uint64_t)nu * total * 4 <= (16ull << 30)) {
     const unsigned ugrid = grid_for((chunks + (B / 64) * kFuseChunks - 1) / ((B / 64) * kFuseChunks), 1, 65535u * 4u);
@@ -3973,7 +3973,7 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   // one walk writing kept outputs chunk-locally (k_dj_filt<2>) + a
   // compaction of the chunk runs: config 5's H4 0.82 -> 0.71 ms against the
   // flag pass and a second walk (DAS_FILT_LOCAL=0, A/B;
-  // profiles/r3_hub_local_ab.json)
+  // profiles/archive/r3_hub_local_ab.json)
   const char* fle = std::getenv("DAS_FILT_LOCAL");
   const bool local = !(fle && fle[0] == '0');
   // its scratch holds every virtual output's columns (4 nu B each, against one

@@ -1056,6 +1056,12 @@ def test_gpu_miner_walk_matches_oracle():
             want = bench.miner_walk(api, s, np.random.default_rng(1), link_rate=0.2)
             assert strip(got) == strip(want), (s, prefetched)
             assert got["halo"][1]["links"] > 0
+            # the bench's per-level bounds (hub schema nodes): same links walked
+            kw = dict(link_rate=0.2, max_level_nodes=5, max_level_links=40)
+            got = bench.miner_walk(das, s, np.random.default_rng(1), **kw)
+            want = bench.miner_walk(api, s, np.random.default_rng(1), **kw)
+            assert strip(got) == strip(want), (s, prefetched, "bounded")
+            assert got["halo"][1]["links"] <= 40 and got["halo"][1]["nodes"] <= 5
     # per-link metadata after prefetch equals the device path's
     link = sorted(api.get_links(None, None, ["*", seeds[1][0], "*"]))[0]
     assert das.get_link_targets(link) == api.get_link_targets(link)
