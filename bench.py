@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--fb-schema", type=int, default=60)
     ap.add_argument("--fb-rows", type=int, default=450_000)
     ap.add_argument("--gl-steps", type=int, default=3, help="getlinks: seed walks timed (at most --steps)")
+    ap.add_argument("--gl-pattern-s", type=float, default=10.0,
+                    help="getlinks: seconds of pattern counts per walk (the sample's first links)")
     # hub (config 5): H4's output grows ~ links^1.6 (Zipf hubs): 3M links -> ~4.3e8 bindings
     ap.add_argument("--hub-links", type=int, default=1_000_000_000)
     ap.add_argument("--hub-nodes", type=int, default=1 << 27)
@@ -219,7 +221,7 @@ def _pattern_templates(link_type, targets):
 
 
 def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_length=2,
-               max_level_nodes=1000, max_level_links=50_000, progress=None):
+               max_level_nodes=1000, max_level_links=50_000, progress=None, pattern_budget_s=None):
     """SimplePatternMiner.ipynb cells 6 and 9 through the facade API `api`
     (get_links / get_link_targets / get_link_type / get_node_type /
     get_node_name): the halo walk (level by level, every template around
@@ -231,7 +233,8 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
     level expands at most `max_level_nodes` node handles and follows the
     targets of at most `max_level_links` links (in handle order, so every
     backend walks the same links); a level that hit a bound says so
-    ("bounded")."""
+    ("bounded").  `pattern_budget_s` ends the pattern counts after that many
+    seconds (a count over a schema node materialises ~10^6 handles)."""
     node_handles = sorted(set(seeds))[:max_level_nodes]
     levels, halo = [], []
     for lv in range(halo_length):
@@ -263,8 +266,15 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
     for lv in levels[1:]:
         sample += [link for link in sorted(lv) if rng.random() < link_rate][:max_pattern_links]
     t0 = time.perf_counter()
-    calls, counted = 0, 0
+    calls, counted, done, t_log = 0, 0, 0, t0
     for link in sample:
+        now = time.perf_counter()
+        if pattern_budget_s is not None and now - t0 > pattern_budget_s:
+            break
+        if progress and now - t_log > 30:
+            t_log = now
+            progress(f"pattern counts: {done} of {len(sample)} links, {calls} get_links")
+        done += 1
         targets = api.get_link_targets(link)
         link_type = api.get_link_type(link)
         for tpl in _pattern_templates(link_type, targets):
@@ -277,8 +287,10 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
                 continue
             counted += len(api.get_links(tpl[0], None, tpl[1:]))
             calls += 1
-    return {"halo": halo, "pattern": {"s": time.perf_counter() - t0, "links": len(sample), "get_links": calls,
-                                      "matched": counted}}
+    if progress:
+        progress(f"pattern counts: {done} links, {calls} get_links, {counted} matched")
+    return {"halo": halo, "pattern": {"s": time.perf_counter() - t0, "links": done, "get_links": calls,
+                                      "matched": counted, "sampled": len(sample)}}
 
 
 class OracleFacade:
@@ -877,12 +889,12 @@ def run_getlinks(args, rank, world, local_rank):
     rng = np.random.default_rng(5)
     log("getlinks warmup walk")
     for i in range(args.warmup and 1):
-        miner_walk(das, [seed(1000 + i)], rng, progress=log)
+        miner_walk(das, [seed(1000 + i)], rng, progress=log, pattern_budget_s=args.gl_pattern_s)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     runs = []
     for i in range(steps):
-        runs.append(miner_walk(das, [seed(i)], rng, progress=log))
+        runs.append(miner_walk(das, [seed(i)], rng, progress=log, pattern_budget_s=args.gl_pattern_s))
         log(f"getlinks walk {i}: {sum(h['queries'] for h in runs[-1]['halo'])} queries")
     elapsed = time.perf_counter() - t0
     tot = _miner_totals(runs)

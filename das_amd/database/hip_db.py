@@ -86,6 +86,8 @@ def _has_composite(tables):
 class HipDB(RelationalDB):
 
     PREFETCH_MAX_ATOMS = 1 << 26            # host mirrors of prefetch() up to this many atoms
+    HEX_DIRECT = 4096                       # hex_of: larger id arrays skip the per-id cache
+    SEED_MAX = 1 << 16                      # _pairs: answers up to this size seed the handle cache
 
     def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False):
         """`tuple_targets=True` reproduces the reference DB path exactly,
@@ -218,6 +220,11 @@ class HipDB(RelationalDB):
         ids = np.asarray(ids, dtype=np.uint32).ravel()
         if ids.size == 0:
             return []
+        if ids.size > self.HEX_DIRECT:
+            # a large answer: its digests straight from the mirror (prefetch)
+            # or one device gather, formatted in one pass (no per-id cache work)
+            dig = self._mirror[0][ids] if self._mirror is not None else self.ctx.atoms_info(ids)[0]
+            return _lib.digests_to_hex(dig)
         uniq = np.unique(ids)
         missing = [int(i) for i in uniq if int(i) not in self._hex_cache]
         if missing:
@@ -363,11 +370,12 @@ class HipDB(RelationalDB):
         hc = self._handle_cache
         if len(hc) > (1 << 23):
             hc.clear()
-        for h, i in zip(links, cols[0].tolist()):
-            if h not in hc:
-                hc[h] = (i, 2, arity)
+        if len(links) <= self.SEED_MAX:
+            for h, i in zip(links, cols[0].tolist()):
+                if h not in hc:
+                    hc[h] = (i, 2, arity)
         tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
-        return [(links[i], self._fmt_targets([tg[k][i] for k in range(arity)])) for i in range(cols.shape[1])]
+        return list(zip(links, zip(*tg) if self.tuple_targets else map(list, zip(*tg))))
 
     def get_all_nodes(self, node_type: str, names: bool = False) -> List[str]:
         """redis_mongo_db.py:254-267"""
