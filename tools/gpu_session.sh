@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session (run through gpurun from the repo root).  MODES picks the
 # steps, in order (default "tests profile"):
-#   tests    the GPU parity suite (TESTS selects files / -k, default all)
+#   tests    the GPU parity suite (TESTS selects files, K a -k expression; default all)
 #   bench    the default bench.py run exactly as the driver runs it
 #            (BENCH_ARGS adds flags) -> gpurun_out/$TAG/bench.json + detail
 #   profile  tools/profile_bench.sh for each workload in WORKLOADS (rocprof
@@ -15,7 +15,7 @@ T=${TAG:-s}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
 run_tests() {
-    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 150 \
+    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} ${K:+-k "$K"} -m gpu -x -v --timeout 150 \
         --timeout-method thread --durations=15 > gpurun_out/$T/tests.txt 2>&1
 }
 run_bench() {
