@@ -1073,16 +1073,14 @@ struct FiltKey {
 
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
-template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk, int XU = kXUnroll>
-__global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
-                                               uint32_t range, const uint2* __restrict__ lc, uint64_t units,
-                                               const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
-                                               uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
-                                               const uint32_t* __restrict__ coff, JoinCols jc,
-                                               uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo,
-                                               uint64_t whi) {
-  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
-  uint32_t* row = s_row[threadIdx.x >> 6];
+template <int MODE, int NPC, int NBC, int CH, int XU>
+__device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                             uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                             const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
+                                             uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
+                                             const uint32_t* __restrict__ coff, const JoinCols& jc,
+                                             uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo, uint64_t whi,
+                                             uint32_t* row) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -1233,6 +1231,32 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
     }
     if (MODE != 1 && lane == 0) ccnt[w] = run;
   }
+}
+
+template <int MODE, int NPC = -1, int NBC = -1, int CH = (int)kBalChunk, int XU = kXUnroll>
+__global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                               uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                               const uint64_t* __restrict__ unit_off, uint64_t total, FiltKey fk,
+                                               uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
+                                               const uint32_t* __restrict__ coff, JoinCols jc,
+                                               uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo,
+                                               uint64_t whi) {
+  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  dj_filt_body<MODE, NPC, NBC, CH, XU>(pkey, np, kmin, range, lc, units, unit_off, total, fk, fl, ccnt, coff, jc, out,
+                                       cap, wlo, whi, s_row[threadIdx.x >> 6]);
+}
+
+// the one walk at 8 waves per SIMD (<= 64 VGPRs; DAS_FILT_OCC=8, A/B): more
+// waves in flight for a walk whose waves spend ~80 % of their cycles waiting
+template <int NPC, int NBC, int XU>
+__global__ void __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_dj_filt_o8(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin, uint32_t range,
+             const uint2* __restrict__ lc, uint64_t units, const uint64_t* __restrict__ unit_off, uint64_t total,
+             FiltKey fk, uint32_t* __restrict__ ccnt, JoinCols jc, uint32_t* __restrict__ out, uint64_t cap,
+             uint64_t wlo, uint64_t whi) {
+  __shared__ uint32_t s_row[B / 64][64];
+  dj_filt_body<2, NPC, NBC, 1024, XU>(pkey, np, kmin, range, lc, units, unit_off, total, fk, nullptr, ccnt, nullptr,
+                                      jc, out, cap, wlo, whi, s_row[threadIdx.x >> 6]);
 }
 
 // MODE 2's second step: chunk w's kept rows [(w - wlo) CH, + cnt[w]) of the
@@ -4010,11 +4034,27 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
   hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
                      (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks)
-      if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
+      // A/B variants of the (1, 1) walk: DAS_FILT_OCC=8 (8 waves per SIMD),
+      // DAS_FILT_XU=8 (8 rounds of 64 outputs per load batch)
+      static const int occ = std::getenv("DAS_FILT_OCC") ? std::atoi(std::getenv("DAS_FILT_OCC")) : 0;
+      static const int xu = std::getenv("DAS_FILT_XU") ? std::atoi(std::getenv("DAS_FILT_XU")) : 4;
+#define FILT_O8(XUV)                                                                                          \
+  hipLaunchKernelGGL((k_dj_filt_o8<1, 1, XUV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
+                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, ccnt.p, jc,    \
+                     scr.p, total, 0ull, fchunks)
+      if (jc.np == 1 && jc.nb == 1 && occ == 8) {
+        if (xu == 8) FILT_O8(8);
+        else FILT_O8(4);
+      } else if (jc.np == 1 && jc.nb == 1 && xu == 8) {
+        hipLaunchKernelGGL((k_dj_filt<2, 1, 1, 1024, 8>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
+                           A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total,
+                           fk, (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks);
+      } else if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
       else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
       else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
       else FILT_L(-1, -1);
 #undef FILT_L
+#undef FILT_O8
       DAS_HIP(hipGetLastError());
     }
     const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);

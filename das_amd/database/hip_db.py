@@ -11,6 +11,7 @@ Two extra, non-reference entry points feed the pattern matcher without
 materialising Python tuples: `match_link` and `match_template` return device
 binding tables (`Relation`).
 """
+import gc
 import itertools
 import os
 import re
@@ -363,19 +364,28 @@ class HipDB(RelationalDB):
         cols = t.fetch()
         if cols.shape[1] == 0:
             return []
-        links = self.hex_of(cols[0])
-        # the links of a pattern answer are indexed here (category 2): a
-        # caller's next get_link_targets / link lookups of them (the
-        # SimplePatternMiner halo walk) need no device lookup
-        hc = self._handle_cache
-        if len(hc) > (1 << 23):
-            hc.clear()
-        if len(links) <= self.SEED_MAX:
-            for h, i in zip(links, cols[0].tolist()):
-                if h not in hc:
-                    hc[h] = (i, 2, arity)
-        tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
-        return list(zip(links, zip(*tg) if self.tuple_targets else map(list, zip(*tg))))
+        # one container per row: with the collector on, every 700 of them start
+        # a collection that walks the handle cache and the caller's live
+        # objects (~1 us per row at 10^6 cached handles instead of ~0.15)
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            links = self.hex_of(cols[0])
+            # the links of a pattern answer are indexed here (category 2): a
+            # caller's next get_link_targets / link lookups of them (the
+            # SimplePatternMiner halo walk) need no device lookup
+            hc = self._handle_cache
+            if len(hc) > (1 << 23):
+                hc.clear()
+            if len(links) <= self.SEED_MAX:
+                for h, i in zip(links, cols[0].tolist()):
+                    if h not in hc:
+                        hc[h] = (i, 2, arity)
+            tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
+            return list(zip(links, zip(*tg) if self.tuple_targets else map(list, zip(*tg))))
+        finally:
+            if enabled:
+                gc.enable()
 
     def get_all_nodes(self, node_type: str, names: bool = False) -> List[str]:
         """redis_mongo_db.py:254-267"""

@@ -25,6 +25,7 @@ The collectives go through torch.distributed ("nccl" = RCCL on ROCm, over
 xGMI; "gloo" in the CPU tests).  `local` is a HipDB (or, in tests, a CPU
 double with the same surface).
 """
+import gc
 import os
 
 import numpy as np
@@ -244,7 +245,13 @@ class ShardedDB(RelationalDB):
             cols = cols[:, np.argsort(cols[0], kind="stable")]
             links = self.local.hex_of(cols[0])
             tg = [self.local.hex_of(cols[1 + k]) for k in range(a)]
-            out += [(links[i], fmt([tg[k][i] for k in range(a)])) for i in range(cols.shape[1])]
+            enabled = gc.isenabled()
+            gc.disable()                     # one container per row (HipDB._pairs)
+            try:
+                out += list(zip(links, map(fmt, zip(*tg))))
+            finally:
+                if enabled:
+                    gc.enable()
         return out
 
     def get_matched_links(self, link_type, target_handles):
