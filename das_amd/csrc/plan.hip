@@ -265,7 +265,29 @@ struct Exec {
 
   // And's fold of one positive term into the running result; false when the
   // term fails the And (:712-713).
-  bool step(uint32_t ti, Rel& acc, bool& have, std::vector<Rel>& forbidden) {
+  // The And's first two positive Link terms when the second one's rows are
+  // few against the first one's: instead of joining the first term's scan
+  // (probe, e.g. 2*10^7 Member rows) with the second's rows (build), the
+  // second's rows look their key up in the FIRST term's pattern index and
+  // expand its contiguous row ranges (index_join): the first term's rows
+  // without a partner are never read, and each output's fresh column comes
+  // from a contiguous P row.  Same rows as the join (a two-term join is
+  // symmetric, and an empty join empties acc either way), other row order.
+  // DAS_REV_IJ=0 off, =1 without the 2^16-row floor (tests).
+  TablePtr reverse_ij(int64_t t0, const Rel& acc, const Rel& s) {
+    const char* f = std::getenv("DAS_REV_IJ");
+    if (t0 < 0 || sharded() || (f && f[0] == '0')) return nullptr;
+    const das_plan_node_t& a = nd[t0];
+    if (a.op != DAS_PLAN_LINK || !a.index_join || a.dedup || acc.t.size() != 1 || s.t.size() != 1) return nullptr;
+    const Table& big = *acc.t[0];
+    const Table& small = *s.t[0];
+    if (small.kind != DAS_TABLE_ORDERED || !small.nrows || 4 * small.nrows > big.nrows) return nullptr;
+    if (!(f && f[0] == '1') && big.nrows < (1ull << 16)) return nullptr;
+    return index_join(c, small, a.ij);
+  }
+
+  // acc_term: the Link term whose scan alone is acc (-1: acc is anything else)
+  bool step(uint32_t ti, Rel& acc, bool& have, std::vector<Rel>& forbidden, int64_t& acc_term) {
     const das_plan_node_t& x = nd[ti];
     if (have && x.op == DAS_PLAN_LINK && x.index_join && ne(acc)) {
       // the term's rows looked up from the running result's keys; an empty
@@ -284,6 +306,7 @@ struct Exec {
       }
       if (ok && ne(r)) {
         acc = std::move(r);
+        acc_term = -1;
         return true;
       }
     }
@@ -297,8 +320,16 @@ struct Exec {
     if (!have || !ne(acc)) {
       acc = std::move(s.rel);
       have = true;
+      acc_term = x.op == DAS_PLAN_LINK ? (int64_t)ti : -1;
     } else {
-      acc = join_rel(acc, s.rel);
+      TablePtr r = reverse_ij(acc_term, acc, s.rel);
+      if (r) {
+        acc = Rel{};
+        acc.push(std::move(r));
+      } else {
+        acc = join_rel(acc, s.rel);
+      }
+      acc_term = -1;
     }
     return true;
   }
@@ -362,6 +393,7 @@ struct Exec {
       }
     }
     uint32_t seen = 0;                 // Link / other positive terms met so far
+    int64_t acc_term = -1;             // step(): the Link term whose scan alone is acc
     for (size_t k = 0; k < terms.size(); ++k) {
       const uint32_t ti = terms[k];
       const das_plan_node_t& x = nd[ti];
@@ -374,7 +406,7 @@ struct Exec {
       }
       if (x.op == DAS_PLAN_NOT) {
         // a negated term: its rows join `forbidden` (no fold of acc)
-        if (!step(ti, acc, have, forbidden)) return Res{};
+        if (!step(ti, acc, have, forbidden, acc_term)) return Res{};
         continue;
       }
       if (seen++ < skip) continue;
@@ -407,6 +439,7 @@ struct Exec {
           seen += (uint32_t)(e - k - 1);
           log(e - k);
           k = e - 1;
+          acc_term = -1;
           continue;
         }
       }
@@ -434,16 +467,17 @@ struct Exec {
             acc.partial = sharded();      // expanded through this shard's index
             acc.push(std::move(f));
           } else {
-            if (!step(ti, acc, have, forbidden)) return Res{};
+            if (!step(ti, acc, have, forbidden, acc_term)) return Res{};
             for (auto& r : rs) acc = ne(acc) ? join_rel(acc, r) : std::move(r);
           }
           seen += (uint32_t)(e - k - 1);
           log(e - k);
           k = e - 1;
+          acc_term = -1;
           continue;
         }
       }
-      if (!step(ti, acc, have, forbidden)) return Res{};
+      if (!step(ti, acc, have, forbidden, acc_term)) return Res{};
       log(1);
     }
     for (auto& f : forbidden)

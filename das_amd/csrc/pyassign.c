@@ -15,6 +15,7 @@
  *
  * format_set(s) returns str(s) for a set of assignments, taking repr() of an
  * OrderedAssignment's mapping in C instead of calling its Python __repr__.
+ * hex_list / hex_pairs format the handle rows of DBInterface answers.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -260,11 +261,196 @@ done:
   return res;
 }
 
+/* Handle strings of answer rows (HipDB.get_matched_links & co., the
+ * reference's [(handle, targets)] lists, redis_mongo_db.py:235-279): a
+ * 32-char lowercase hex str per digest, written straight into the str's
+ * buffer (the Python path formats ~3x slower through bytes.hex() + slicing),
+ * with a small direct-mapped cache so a target repeated across rows (a
+ * schema node) is one shared str. */
+static const char HEXD[] = "0123456789abcdef";
+
+static PyObject *hex_str(const uint32_t *w) {
+  PyObject *s = PyUnicode_New(32, 127);
+  if (!s) return NULL;
+  Py_UCS1 *p = PyUnicode_1BYTE_DATA(s);
+  const uint8_t *b = (const uint8_t *)w;          /* digest bytes in memory order (little-endian words) */
+  for (int i = 0; i < 16; ++i) {
+    p[2 * i] = (Py_UCS1)HEXD[b[i] >> 4];
+    p[2 * i + 1] = (Py_UCS1)HEXD[b[i] & 15];
+  }
+  return s;
+}
+
+#define HEX_CACHE 4096
+typedef struct {
+  uint32_t id[HEX_CACHE];
+  PyObject *s[HEX_CACHE];
+} HexCache;
+
+static void hc_init(HexCache *c) {
+  for (int i = 0; i < HEX_CACHE; ++i) {
+    c->id[i] = 0xFFFFFFFFu;
+    c->s[i] = NULL;
+  }
+}
+static void hc_free(HexCache *c) {
+  for (int i = 0; i < HEX_CACHE; ++i) Py_XDECREF(c->s[i]);
+}
+/* new reference to the str of atom `id` (digest words at w) */
+static PyObject *hc_get(HexCache *c, uint32_t id, const uint32_t *w) {
+  const uint32_t slot = (id * 2654435761u) >> 20;   /* 12 bits */
+  if (c->id[slot] == id && c->s[slot]) {
+    Py_INCREF(c->s[slot]);
+    return c->s[slot];
+  }
+  PyObject *s = hex_str(w);
+  if (!s) return NULL;
+  Py_XDECREF(c->s[slot]);
+  Py_INCREF(s);
+  c->s[slot] = s;
+  c->id[slot] = id;
+  return s;
+}
+
+/* digest words of row r of column col: dig indexed by ids (the host mirror,
+ * ids = (k, n) u32), or dig = (k, n, 4) gathered per column (ids None) */
+typedef struct {
+  const uint32_t *dig, *ids;
+  Py_ssize_t n_dig, n;
+} HexSrc;
+
+static const uint32_t *src_row(const HexSrc *h, int col, Py_ssize_t r, uint32_t *id) {
+  if (!h->ids) {
+    *id = 0xFFFFFFFFu;                              /* no id: uncached */
+    return h->dig + ((Py_ssize_t)col * h->n + r) * 4;
+  }
+  *id = h->ids[(Py_ssize_t)col * h->n + r];
+  if ((Py_ssize_t)*id >= h->n_dig) {
+    PyErr_SetString(PyExc_IndexError, "hex: atom id outside the digest table");
+    return NULL;
+  }
+  return h->dig + (Py_ssize_t)*id * 4;
+}
+
+static PyObject *src_str(HexCache *c, const HexSrc *h, int col, Py_ssize_t r) {
+  uint32_t id;
+  const uint32_t *w = src_row(h, col, r, &id);
+  if (!w) return NULL;
+  return id == 0xFFFFFFFFu ? hex_str(w) : hc_get(c, id, w);
+}
+
+static int open_src(PyObject *dig, PyObject *ids, int k, Py_ssize_t n, Py_buffer *db, Py_buffer *ib, HexSrc *h) {
+  if (get_u32(dig, db, "digests") < 0) return -1;
+  h->dig = (const uint32_t *)db->buf;
+  h->n_dig = db->len / 16;
+  h->n = n;
+  h->ids = NULL;
+  if (ids != Py_None) {
+    if (get_u32(ids, ib, "ids") < 0) {
+      PyBuffer_Release(db);
+      return -1;
+    }
+    if (ib->len / 4 < (Py_ssize_t)k * n) {
+      PyErr_SetString(PyExc_ValueError, "hex: ids shorter than k * n");
+      PyBuffer_Release(ib);
+      PyBuffer_Release(db);
+      return -1;
+    }
+    h->ids = (const uint32_t *)ib->buf;
+  } else if (h->n_dig < (Py_ssize_t)k * n) {
+    PyErr_SetString(PyExc_ValueError, "hex: digests shorter than k * n rows");
+    PyBuffer_Release(db);
+    return -1;
+  }
+  return 0;
+}
+
+/* hex_list(digests, ids | None, n) -> [str] of column 0 */
+static PyObject *hex_list(PyObject *self, PyObject *args) {
+  PyObject *dig, *ids;
+  Py_ssize_t n;
+  if (!PyArg_ParseTuple(args, "OOn", &dig, &ids, &n)) return NULL;
+  Py_buffer db, ib;
+  HexSrc h;
+  if (open_src(dig, ids, 1, n, &db, &ib, &h) < 0) return NULL;
+  HexCache *c = PyMem_Malloc(sizeof(HexCache));
+  PyObject *out = c ? PyList_New(n) : NULL;
+  if (c) hc_init(c);
+  else PyErr_NoMemory();
+  for (Py_ssize_t r = 0; out && r < n; ++r) {
+    PyObject *s = src_str(c, &h, 0, r);
+    if (!s) {
+      Py_CLEAR(out);
+      break;
+    }
+    PyList_SET_ITEM(out, r, s);
+  }
+  if (c) {
+    hc_free(c);
+    PyMem_Free(c);
+  }
+  if (ids != Py_None) PyBuffer_Release(&ib);
+  PyBuffer_Release(&db);
+  return out;
+}
+
+/* hex_pairs(digests, ids | None, k, n, tuple_targets) ->
+ * [(link, [t0 .. t_{k-2}]) | (link, (t0 ..))] over k columns of n rows */
+static PyObject *hex_pairs(PyObject *self, PyObject *args) {
+  PyObject *dig, *ids;
+  int k, tup;
+  Py_ssize_t n;
+  if (!PyArg_ParseTuple(args, "OOinp", &dig, &ids, &k, &n, &tup)) return NULL;
+  if (k < 1) {
+    PyErr_SetString(PyExc_ValueError, "hex_pairs: k >= 1 columns");
+    return NULL;
+  }
+  Py_buffer db, ib;
+  HexSrc h;
+  if (open_src(dig, ids, k, n, &db, &ib, &h) < 0) return NULL;
+  HexCache *c = PyMem_Malloc(sizeof(HexCache));
+  PyObject *out = c ? PyList_New(n) : NULL;
+  if (c) hc_init(c);
+  else PyErr_NoMemory();
+  for (Py_ssize_t r = 0; out && r < n; ++r) {
+    PyObject *link = src_str(c, &h, 0, r);
+    PyObject *tg = link ? (tup ? PyTuple_New(k - 1) : PyList_New(k - 1)) : NULL;
+    PyObject *pair = tg ? PyTuple_New(2) : NULL;
+    if (!pair) {
+      Py_XDECREF(link);
+      Py_XDECREF(tg);
+      Py_CLEAR(out);
+      break;
+    }
+    PyTuple_SET_ITEM(pair, 0, link);
+    PyTuple_SET_ITEM(pair, 1, tg);
+    PyList_SET_ITEM(out, r, pair);
+    for (int col = 1; col < k; ++col) {
+      PyObject *s = src_str(c, &h, col, r);
+      if (!s) {
+        Py_CLEAR(out);
+        break;
+      }
+      if (tup) PyTuple_SET_ITEM(tg, col - 1, s);
+      else PyList_SET_ITEM(tg, col - 1, s);
+    }
+  }
+  if (c) {
+    hc_free(c);
+    PyMem_Free(c);
+  }
+  if (ids != Py_None) PyBuffer_Release(&ib);
+  PyBuffer_Release(&db);
+  return out;
+}
+
 static PyObject *fast_hash_enabled(PyObject *self, PyObject *noargs);
 
 static PyMethodDef methods[] = {
     {"add_rows", add_rows, METH_VARARGS, "Add Assignment objects built from a binding table to a set."},
     {"format_set", format_set, METH_VARARGS, "str() of a set of assignments."},
+    {"hex_list", hex_list, METH_VARARGS, "Handle strs of n atoms (digest table + ids, or gathered digests)."},
+    {"hex_pairs", hex_pairs, METH_VARARGS, "[(link, targets)] handle rows of k id columns."},
     {"fast_hash_enabled", fast_hash_enabled, METH_NOARGS, "True when the C restatement of the hashes is in use."},
     {NULL, NULL, 0, NULL}};
 

@@ -20,6 +20,10 @@ from typing import Any, List, Tuple
 import numpy as np
 
 from .. import _lib
+try:
+    from .. import _assign as _hex          # C handle formatting of large answers (csrc/pyassign.c)
+except ImportError:                         # pragma: no cover - built with the library
+    _hex = None
 from .. import loader as _loader
 from ..expression_hasher import ExpressionHasher
 from .db_interface import UNORDERED_LINK_TYPES, WILDCARD, DBInterface
@@ -224,6 +228,10 @@ class HipDB(RelationalDB):
         if ids.size > self.HEX_DIRECT:
             # a large answer: its digests straight from the mirror (prefetch)
             # or one device gather, formatted in one pass (no per-id cache work)
+            if _hex is not None:
+                if self._mirror is not None:
+                    return _hex.hex_list(self._mirror[0], ids, ids.size)
+                return _hex.hex_list(np.ascontiguousarray(self.ctx.atoms_info(ids)[0]), None, ids.size)
             dig = self._mirror[0][ids] if self._mirror is not None else self.ctx.atoms_info(ids)[0]
             return _lib.digests_to_hex(dig)
         uniq = np.unique(ids)
@@ -362,7 +370,8 @@ class HipDB(RelationalDB):
 
     def _pairs(self, t, arity):
         cols = t.fetch()
-        if cols.shape[1] == 0:
+        n = cols.shape[1]
+        if n == 0:
             return []
         # one container per row: with the collector on, every 700 of them start
         # a collection that walks the handle cache and the caller's live
@@ -370,19 +379,31 @@ class HipDB(RelationalDB):
         enabled = gc.isenabled()
         gc.disable()
         try:
-            links = self.hex_of(cols[0])
+            if n > self.HEX_DIRECT and _hex is not None:
+                # every handle str written in C (_assign.hex_pairs), from the
+                # mirror or from one device gather of the answer's digests
+                cols = np.ascontiguousarray(cols)
+                if self._mirror is not None:
+                    out = _hex.hex_pairs(self._mirror[0], cols, arity + 1, n, self.tuple_targets)
+                else:
+                    dig = np.ascontiguousarray(self.ctx.atoms_info(cols.ravel())[0])
+                    out = _hex.hex_pairs(dig, None, arity + 1, n, self.tuple_targets)
+                links = None
+            else:
+                links = self.hex_of(cols[0])
+                tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
+                out = list(zip(links, zip(*tg) if self.tuple_targets else map(list, zip(*tg))))
             # the links of a pattern answer are indexed here (category 2): a
             # caller's next get_link_targets / link lookups of them (the
             # SimplePatternMiner halo walk) need no device lookup
             hc = self._handle_cache
             if len(hc) > (1 << 23):
                 hc.clear()
-            if len(links) <= self.SEED_MAX:
-                for h, i in zip(links, cols[0].tolist()):
+            if n <= self.SEED_MAX:
+                for h, i in zip(links if links is not None else (p[0] for p in out), cols[0].tolist()):
                     if h not in hc:
                         hc[h] = (i, 2, arity)
-            tg = [self.hex_of(cols[1 + k]) for k in range(arity)]
-            return list(zip(links, zip(*tg) if self.tuple_targets else map(list, zip(*tg))))
+            return out
         finally:
             if enabled:
                 gc.enable()

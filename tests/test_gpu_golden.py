@@ -45,7 +45,7 @@ def _atom_tables(db):
     return nodes, [[h, t, tg, ct(h)] for h, (t, tg) in links.items()]
 
 
-@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "1-sparse", "1-dense", "0"])
+@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "1-sparse", "1-dense", "1-rev", "0"])
 @pytest.mark.parametrize("name", FIXTURES)
 def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
     """plan 1: And / Or / Not trees folded natively (das_plan_execute), small
@@ -53,10 +53,12 @@ def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
     1-multi: Ors of Link scans always through the multi-segment scan +
     dedup; 1-sparse / 1-dense: every direct join's build side through the
     in-place (lo, cnt) descriptors / the histogram + scan (the default picks
-    by size, and these KBs are below the sparse floor); plan 0: the
-    per-operator host path."""
+    by size, and these KBs are below the sparse floor); 1-rev: unfused, an
+    And's second Link term index-joined into the first term's index at every
+    size (DAS_REV_IJ=1); plan 0: the per-operator host path."""
     monkeypatch.setenv("DAS_PLAN", plan[0])
-    monkeypatch.setenv("DAS_FUSED", "0" if plan == "1-unfused" else "1")
+    monkeypatch.setenv("DAS_FUSED", "0" if plan in ("1-unfused", "1-rev") else "1")
+    monkeypatch.setenv("DAS_REV_IJ", "1" if plan == "1-rev" else "")
     monkeypatch.setenv("DAS_UNION_MULTI", "1" if plan == "1-multi" else "0")
     if plan in ("1-sparse", "1-dense"):
         monkeypatch.setenv("DAS_DJ_BUILD", plan[2:])

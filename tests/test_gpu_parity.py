@@ -139,6 +139,39 @@ def test_gpu_index_probes(golden):
         assert sorted(x if isinstance(x, str) else x[0] for x in r) == p["handles"], p["args"]
 
 
+@pytest.mark.parametrize("tuple_targets", [False, True])
+def test_gpu_answer_rows_formatting(tuple_targets, monkeypatch):
+    """get_matched_links / get_matched_type_template / get_matched_type rows
+    (handle, targets) against the oracle's DB path, through the per-id cache
+    path, the C formatter (_assign.hex_pairs: HEX_DIRECT=0) from one device
+    gather, and the C formatter from the prefetched host mirror."""
+    from das_amd import synthetic
+    from das_amd.database.hip_db import HipDB
+    arrays = synthetic.bio_kb(300, 120, 3000, seed=4)
+    db = HipDB(device=0, tuple_targets=tuple_targets)
+    db.load_arrays(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    bp = O.terminal_hash("BiologicalProcess", "bp3")
+    fmt = tuple if tuple_targets else list
+    norm = lambda rows: sorted((h, fmt(tg)) for h, tg in rows)  # noqa: E731
+    calls = [("get_matched_links", ("Member", ["*", "*"])), ("get_matched_links", ("Member", ["*", bp])),
+             ("get_matched_type_template", (["Member", "Gene", "BiologicalProcess"],)),
+             ("get_matched_type", ("Inheritance",))]
+    want = [norm(getattr(odb, f)(*a)) for f, a in calls]
+    assert len(want[0]) > 1000
+    for mode in ("cache", "c-gather", "c-mirror"):
+        monkeypatch.setattr(HipDB, "HEX_DIRECT", 1 << 30 if mode == "cache" else 0)
+        if mode == "c-mirror":
+            db.prefetch()
+        for (f, a), w in zip(calls, want):
+            got = getattr(db, f)(*a)
+            assert all(isinstance(tg, fmt) for _, tg in got), (mode, f)
+            assert norm(got) == w, (mode, f, a)
+    # a link of a C-formatted answer resolves from the seeded handle cache
+    h, tg = db.get_matched_links("Member", ["*", bp])[0]
+    assert db.get_link_targets(h) == list(tg)
+
+
 # ----------------------------------------------------------------- queries
 
 @pytest.mark.parametrize("fixture", KB_FIXTURES)
@@ -885,7 +918,7 @@ def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
 
 # ------------------------------------------------------------ index join
 
-@pytest.mark.parametrize("mode", ["1", "1-bsearch", "1-ranged", "0"])
+@pytest.mark.parametrize("mode", ["1", "1-bsearch", "1-ranged", "0", "rev"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw", "flybase"])
 def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
     """And with das_index_join forced on every eligible term (1: keys found
@@ -895,10 +928,14 @@ def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
     keys and empty joins that fall back to the scan path (reset-on-empty).
     1-ranged: grounded-key terms searched within the (type, t_q = v) rows of
     P_{a,q} (ranged mode) wherever the shape allows it; the other modes
-    never take it."""
+    never take it.  rev: unfused, an And's second Link term index-joined
+    into the first term's index at every size (DAS_REV_IJ=1)."""
     import bench
     from das_amd import synthetic
-    monkeypatch.setenv("DAS_INDEX_JOIN", mode[0])
+    monkeypatch.setenv("DAS_INDEX_JOIN", "" if mode == "rev" else mode[0])
+    monkeypatch.setenv("DAS_REV_IJ", "1" if mode == "rev" else "")
+    if mode == "rev":
+        monkeypatch.setenv("DAS_FUSED", "0")
     monkeypatch.setenv("DAS_IJ_RANGED", "1" if mode == "1-ranged" else "0")
     if mode == "1-bsearch":
         monkeypatch.setenv("DAS_NO_KEY_DIR", "1")
