@@ -1069,32 +1069,48 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         with open(args.cprofile, "w") as f:
             pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
     variants = None
-    join_k = "k_dj_write<2,1,u32,1>"
-    if workload == "bio" and world == 1 and join_k in warm_stats and not args.no_extras:
-        # the And join with the probe read straight from the index (scan
-        # views for every size): HBM-cold, and with the count pass warming the
-        # probe's payload columns -- beside the default (large probes copied
-        # first, the copy leaving them MALL-warm)
-        variants = {}
+    join_k = None
 
-        def q2_only(i):
-            # the And join of Q2 (Member x Inheritance) alone: its launch is then
-            # the only k_dj_write<2,1> of the measurement (QUERY_2 / QUERY_3
-            # launch small ones of the same instantiation)
-            return sum(run(q) for name, q in qsets[i] if name.startswith("Q2"))
-        for vname, env in (("default (views; the count pass warms the probe's payload), Q2 only", {}),
-                           ("views, no warming (HBM-cold probe), Q2 only", {"DAS_DJ_WARM": "0"}),
-                           ("large probes copied (MALL-warm), Q2 only", {"DAS_SCAN_VIEWS": "2"}),
-                           ("views, no warming (HBM-cold probe)", {"DAS_DJ_WARM": "0"}),
-                           ("large probes copied (MALL-warm)", {"DAS_SCAN_VIEWS": "2"})):
+    def q2_only(i):
+        # the And join of Q2 (Member x Inheritance) alone: its launch is then
+        # the only one of its kernel in the measurement (QUERY_2 / QUERY_3
+        # launch small ones of the same instantiations)
+        return sum(run(q) for name, q in qsets[i] if name.startswith("Q2"))
+
+    def q2_join_kernel():
+        # the expansion kernel Q2's join runs as (the direct join's
+        # k_dj_write<2,1> with Member as probe; with the reverse index join,
+        # Inheritance rows expanding Member's P_{2,1} ranges: k_dj_write_bal<2,1>)
+        db.ctx.prof_reset()
+        db.ctx.prof_enable(True)
+        q2_only(0)
+        torch.cuda.synchronize()
+        db.ctx.prof_enable(False)
+        st = {k: v for k, v in db.ctx.prof_stats().items() if k.startswith("k_dj_write")}
+        return max(st, key=lambda k: st[k]["ms"]) if st else None
+    if workload == "bio" and world == 1 and not args.no_extras:
+        join_k = q2_join_kernel()
+    if join_k is not None:
+        # Q2's And join alone: the default (reverse index join: the 10^5
+        # Inheritance rows expand their Member ranges of P_{2,1}), and the
+        # direct join of round 3 (the 2*10^7 Member rows as probe, read from
+        # the index HBM-cold, warmed by the count pass, or copied first)
+        variants = {}
+        for vname, env in (("default (Inheritance rows index-join Member's P_{2,1}), Q2 only", {}),
+                           ("direct join, views, count pass warms the probe, Q2 only", {"DAS_REV_IJ": "0"}),
+                           ("direct join, views, no warming (HBM-cold probe), Q2 only",
+                            {"DAS_REV_IJ": "0", "DAS_DJ_WARM": "0"}),
+                           ("direct join, large probes copied (MALL-warm), Q2 only",
+                            {"DAS_REV_IJ": "0", "DAS_SCAN_VIEWS": "2"})):
             fn = q2_only if vname.endswith("Q2 only") else step
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
                 for i in range(2):
                     fn(i)
+                vk = q2_join_kernel()               # this variant's expansion kernel
                 db.ctx.prof_reset()
-                db.ctx.prof_only(join_k)
+                db.ctx.prof_only(vk)
                 db.ctx.prof_enable(True)
                 torch.cuda.synchronize()
                 tv = time.perf_counter()
@@ -1105,7 +1121,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                 db.ctx.prof_enable(False)
                 db.ctx.prof_only(None)
                 variants[vname] = {"env": env, ("ms_per_query" if fn is q2_only else "ms_per_step"): round(tv, 4),
-                                   "roofline": roofline_of(db.ctx.prof_stats(), workload, join_k)}
+                                   "roofline": roofline_of(db.ctx.prof_stats(), workload, vk)}
             finally:
                 for k, v in saved.items():
                     if v is None:
@@ -1158,9 +1174,6 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             out["sharded_plan_stats"] = dict(engine.sdb.plan_stats)
             out["collectives_per_step"] = round(coll_per_step, 2)
         if variants:
-            # the default's own And-join figure from the same timed steps' events
-            variants["default (views)"] = {"ms_per_step": round(ms_per_step, 4),
-                                                         "roofline": roofline_of(warm_stats, workload, join_k)}
             out["join_probe_variants"] = variants
     del engine, qsets, db
     return out
@@ -1231,12 +1244,23 @@ def compact_line(full):
     for k in ("latency", "summary", "collectives_per_step"):
         if full.get(k) is not None:
             line[k] = full[k]
+    jv = full.get("join_probe_variants") or {}
+    if jv:
+        # Q2's And join (the north_star And-join target): the default's kernel
+        # and fraction, and the round-3 direct join HBM-cold beside it
+        d0 = next(iter(jv.values()))
+        cold = next((v for k, v in jv.items() if "HBM-cold" in k), None)
+        rf = d0.get("roofline") or {}
+        line["and_join_q2"] = {"kernel": rf.get("kernel"), "frac": rf.get("frac"), "us": rf.get("avg_launch_us"),
+                               "query_ms": d0.get("ms_per_query"),
+                               "direct_cold_frac": ((cold or {}).get("roofline") or {}).get("frac")}
     if full.get("workloads"):
         line["workloads"] = {w: _compact_leg(d) for w, d in full["workloads"].items()}
     line["detail"] = full.get("detail_file")
     s = json.dumps(line, separators=(",", ":"))
     # never exceed the bound: shed the optional parts, then shorten the strings
-    for drop in (("workloads", "summary"), ("workloads", "latency"), ("summary",), ("latency",), ("data",)):
+    for drop in (("workloads", "summary"), ("and_join_q2",), ("workloads", "latency"), ("summary",), ("latency",),
+                 ("data",)):
         if len(s.encode()) <= LINE_MAX_BYTES:
             break
         if len(drop) == 2:

@@ -1440,7 +1440,12 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
 
   // 1. digests + composite types of every unified index
   DBuf<Digest> dig(nu, s), ct(nu, s);
-  hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig.p, ct.p);
+  {
+    ProfScope ph(c, "phase_hash", 0.0);
+    hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig.p, ct.p);
+  }
+  // (phase_* scopes: the build's steps as the bench's kernel table lists them)
+  std::optional<ProfScope> phase(std::in_place, c, "phase_intern", 0.0);
 
   // 2. which unified indices are atoms (nodes, links, link targets)
   DBuf<uint8_t> catl(nu, s);
@@ -1517,6 +1522,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   if (l2i_part) scatter_partitioned(list.p, ids.p, nc, nu, local2id.p, s);     // after k_pick_rep read `list`
   ids.release(); list.release();
 
+  phase.emplace(c, "phase_id_order", 0.0);
   // 3b. final ids clustered by named type, so a variable's bindings occupy a
   // compact id range (direct-address joins); inside a type, atoms referenced
   // more often come first (a power-of-two bucket of their reference count,
@@ -1585,6 +1591,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     catmax = std::move(cat2);
   }
 
+  phase.emplace(c, "phase_atom_arrays", 0.0);
   // 4. atom arrays (id order: named type, reference bucket, handle)
   idx.n_atoms = n_atoms;
   idx.n_types = a.n_types;
@@ -1622,6 +1629,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   }
   dig.release(); ct.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
   d_child.release(); d_bytes.release();
+  phase.reset();
 
   // incoming CSR (the reference's `incomming_set:<target>` family,
   // canonical_parser.py:141-143): every (target, link) pair of the outgoing
@@ -1668,6 +1676,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   }
 
   // 6. composite-type ids over links
+  phase.emplace(c, "phase_ctypes", 0.0);
   uint64_t n_ctypes = 0;
   {
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), lids;
@@ -1723,6 +1732,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   idx.ctype_range.assign(n_ctypes, CtypeRange{0, 0, 0});
 
   // 7. per-arity tables
+  phase.emplace(c, "phase_tables", 0.0);
   for (uint32_t ar = 1; ar <= (uint32_t)kMaxArity; ++ar) {
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), ids;
     if (n_atoms) {
@@ -1937,6 +1947,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     }
     DAS_HIP(hipGetLastError());
   }
+  phase.reset();
   idx.h_node_dig.clear();
   idx.h_node_id.clear();
   idx.h_node_type.clear();
