@@ -924,7 +924,8 @@ template <int NP, int NB, typename T>
 __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                     uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                     const uint64_t* __restrict__ unit_off, JoinCols jc,
-                                                    uint32_t* __restrict__ out, uint64_t cap, uint64_t total) {
+                                                    uint32_t* __restrict__ out, uint64_t cap, uint64_t total,
+                                                    uint64_t chunk) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint32_t* pp[NP > 0 ? NP : 1];
@@ -937,10 +938,10 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
   for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
   __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
   uint32_t* row = s_row[threadIdx.x >> 6];
-  const uint64_t chunks = (total + kBalChunk - 1) / kBalChunk;
+  const uint64_t chunks = (total + chunk - 1) / chunk;
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
-    const uint64_t ob = w * kBalChunk;
-    const uint64_t oe = ob + kBalChunk < total ? ob + kBalChunk : total;
+    const uint64_t ob = w * chunk;
+    const uint64_t oe = ob + chunk < total ? ob + chunk : total;
     // last unit with unit_off[u] <= ob   (unit_off[units] == total > ob)
     uint64_t lo = 0, hi = units;
     while (hi - lo > 1) {
@@ -995,13 +996,19 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
              (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
                 .c_str(), bytes);
   if (balanced) {
-    const unsigned g = grid_for((total + kBalChunk - 1) / kBalChunk, B / 64, 65535u * 4u);
+    // outputs per wave (DAS_BAL_CHUNK, A/B: 512 .. 8192, a multiple of 64)
+    static const uint64_t chunk = [] {
+      const char* e = std::getenv("DAS_BAL_CHUNK");
+      const uint64_t v = e ? std::strtoull(e, nullptr, 10) : kBalChunk;
+      return v >= 64 && v <= 8192 && v % 64 == 0 ? v : kBalChunk;
+    }();
+    const unsigned g = grid_for((total + chunk - 1) / chunk, B / 64, 65535u * 4u);
     if (total < (1ull << 32) - (1ull << 16))
       hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint32_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
-                         toff, jc, out, cap, total);
+                         toff, jc, out, cap, total, chunk);
     else
       hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint64_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
-                         toff, jc, out, cap, total);
+                         toff, jc, out, cap, total, chunk);
     return;
   }
   if (total < (1ull << 32) - (1ull << 16)) {
