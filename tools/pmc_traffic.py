@@ -8,8 +8,8 @@ FETCH_SIZE and WRITE_SIZE are reported in KiB.  FETCH_SIZE counts 64 B per
 memory request (profiles/fetch_calibration.json, tools/ubench/fetch_cal.hip):
 a wide coalesced stream issues 128-B requests tallied at 64 B, so streaming
 kernels' reads are 2 x FETCH_SIZE (MI355X_MICROARCH.md, HBM); an isolated
-4-B load is one 64-B request counted exactly, so the random-probe kernels
-(RANDOM below) take FETCH_SIZE as is.  The raw figure is reported beside the
+4-B load is one 64-B request counted exactly, so the random-probe and
+random-gather kernels (RANDOM below) take FETCH_SIZE as is.  The raw figure is reported beside the
 corrected one.  WRITE_SIZE is used as is.
 TOPK=k (env) averages only each kernel's k largest launches (the timed
 full-size launches of a run whose warm-up step is a small KB, e.g. the build).
@@ -35,9 +35,14 @@ def short(name):
     return n.replace(" ", "")
 
 
-# kernels whose reads are dominated by isolated random loads (x1)
+# kernels whose reads are dominated by isolated random loads (x1): probes,
+# and the build's gathers through a permutation or a representative index
+# (k_fill_atoms reads two 16-byte digests at rep[id], k_fill_targets the ids
+# of each child, k_temp_type / k_apply_perm / k_remap_local 4-byte gathers)
 RANDOM = {"k_tile_count<BitsPred>", "k_ij_mid", "k_bits_probe", "k_ij_lc", "k_ij_small", "k_anti_ij", "k_hset_insert",
-          "k_hset_first", "k_hset_anti", "k_lookup", "k_lookup_pub"}
+          "k_hset_first", "k_hset_anti", "k_lookup", "k_lookup_pub",
+          "k_fill_atoms", "k_fill_targets", "k_temp_type", "k_apply_perm", "k_remap_local", "k_gather_u32",
+          "k_gather_u64", "k_scatter_pairs", "k_run_bucket"}
 
 
 def fetch_factor(kernel):
