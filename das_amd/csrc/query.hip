@@ -217,38 +217,48 @@ __device__ __forceinline__ void publish_u32(uint32_t* slot, uint32_t seq, uint32
 // in ONE launch.  Each scanned row that passes its scan's predicate (the
 // grounded targets outside the key range) tests and sets its value's bit in
 // a bitmap over the column's host-known id range; the row that set it
-// writes the value, at a position its wave reserves with one atomic (output
-// unsorted, one row per distinct value -- Python set semantics).  ctr[0]:
+// writes the value, at a position its block reserves with one atomic (output
+// unsorted, one row per distinct value -- Python set semantics).  One row
+// per thread (the segments are chunked by B rows, not kChunk): a block's
+// load -> test-and-set -> reserve chain runs once, so the launch is as deep
+// as one chain instead of kChunkIters of them (F9: 71 -> ~15 us).  ctr[0]:
 // rows written, ctr[1]: blocks done, ctr[2]: values outside [lo, lo + range)
 // (the host then takes the general path); the last block publishes ctr[0]
 // and ctr[2].
 __global__ void __launch_bounds__(B) k_union_first(MultiScan ms, uint32_t lo, uint32_t range,
                                                    uint32_t* __restrict__ bits, uint32_t* __restrict__ out,
                                                    uint32_t* __restrict__ ctr, uint32_t* slot, uint32_t seq) {
+  __shared__ uint32_t s_w[B / 64];
+  __shared__ uint32_t s_base;
   const MultiScan::Seg& sg = seg_of(ms, blockIdx.x);
-  const uint64_t cb = sg.begin + (uint64_t)(blockIdx.x - sg.chunk0) * kChunk;
+  const uint64_t r = sg.begin + (uint64_t)(blockIdx.x - sg.chunk0) * B + threadIdx.x;
   const uint32_t* src = sg.sp.col[1 + sg.sp.outpos[0]];
+  const int wave = threadIdx.x >> 6;
   uint32_t bad = 0;
-  for (int it = 0; it < kChunkIters; ++it) {
-    const uint64_t r = cb + (uint64_t)it * B + threadIdx.x;
-    bool first = false;
-    uint32_t v = 0;
-    if (r < sg.end && scan_keep(sg.sp, r)) {
-      v = src[r];
-      const uint32_t d = v - lo;
-      if (d < range) {
-        const uint32_t m = 1u << (d & 31);
-        first = (atomicOr(&bits[d >> 5], m) & m) == 0;
-      } else {
-        bad = 1;
-      }
+  bool first = false;
+  uint32_t v = 0;
+  if (r < sg.end && scan_keep(sg.sp, r)) {
+    v = src[r];
+    const uint32_t d = v - lo;
+    if (d < range) {
+      const uint32_t m = 1u << (d & 31);
+      first = (atomicOr(&bits[d >> 5], m) & m) == 0;
+    } else {
+      bad = 1;
     }
-    const uint64_t bal = __ballot(first);
-    uint32_t base = 0;
-    if (__lane_id() == 0 && bal) base = atomicAdd(&ctr[0], (uint32_t)__popcll(bal));
-    base = (uint32_t)__shfl(base, 0, 64);
-    if (first) out[base + __popcll(bal & __lanemask_lt())] = v;
   }
+  const uint64_t bal = __ballot(first);
+  if (__lane_id() == 0) s_w[wave] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < B / 64; ++w) t += s_w[w];
+    s_base = t ? atomicAdd(&ctr[0], t) : 0u;
+  }
+  __syncthreads();
+  uint32_t pos = s_base + (uint32_t)__popcll(bal & __lanemask_lt());
+  for (int w = 0; w < wave; ++w) pos += s_w[w];
+  if (first) out[pos] = v;
   if (__ballot(bad) && __lane_id() == 0) atomicOr(&ctr[2], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3610,6 +3620,14 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
       for (uint32_t i = 0; i < ms.nseg && proj; ++i)
         proj = !ms.seg[i].sp.unordered && !ms.seg[i].sp.emit_link && ms.seg[i].sp.nout == 1;
       const char* fb = std::getenv("DAS_UNION_BITS");                // A/B, tests: 0 never
+      // (its segments re-chunked by B rows: one row per thread)
+      MultiScan ms1 = ms;
+      uint64_t blocks = 0;
+      for (uint32_t i = 0; i < ms1.nseg; ++i) {
+        ms1.seg[i].chunk0 = blocks;
+        blocks += (ms1.seg[i].end - ms1.seg[i].begin + B - 1) / B;
+      }
+      proj = proj && blocks < (1ull << 31);
       if (proj && !(fb && fb[0] == '0')) {
         const uint32_t range = uhi[0] - ulo[0] + 1;
         auto res = new_table(c, DAS_TABLE_ORDERED, 1, preps[0].vars, scanned);
@@ -3619,7 +3637,7 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
         const PubSlot ps = pub_reserve();
         {
           ProfScope pf(c, "k_union_first", 8.0 * scanned);
-          hipLaunchKernelGGL(k_union_first, dim3((unsigned)chunks), dim3(B), 0, c.s, ms, ulo[0], range, bits.p,
+          hipLaunchKernelGGL(k_union_first, dim3((unsigned)blocks), dim3(B), 0, c.s, ms1, ulo[0], range, bits.p,
                              res->data, ctr.p, ps.p, ps.seq);
           DAS_HIP(hipGetLastError());
         }
