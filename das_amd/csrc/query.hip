@@ -767,19 +767,56 @@ __device__ __forceinline__ int owner_of_round(uint32_t ob, uint32_t pre, uint32_
 #define DAS_DJ_UNROLL 4
 #endif
 constexpr int kXUnroll = DAS_DJ_UNROLL;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-byte load
+
 template <int NP, int NB, typename T, int V = 1>
 __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
                                              uint64_t obase, int lane, uint32_t* row, int search) {
   // 32-bit groups: owner_of_round (unless DAS_OWNER_SEARCH=1); each lane's
   // ex - pre travels as one value (br = (ex - pre)[owner] + o)
-  const bool fast = sizeof(T) == 4 && !search;
+  const bool fast = sizeof(T) == 4 && !(search & 1);
+  // Run path (not with DAS_DJ_VEC=0, search bit 1): 256 consecutive outputs of
+  // ONE probe row -- a skewed key's run, an index join's P range -- are
+  // consecutive build rows: each lane moves 4 of them per column with one
+  // 16-byte load and one 16-byte nontemporal store (4-byte stores top out at
+  // ~3.1-3.4 TB/s on this part, 16-byte ones reach ~7, k_cartesian), and
+  // writes the probe values as 16-byte splats.  Needs 16-byte aligned output
+  // positions: a head of up to 3 outputs goes through the rounds first.
+  const bool runs = fast && !(search & 2) && (re - rs) > (T)(64 * kXUnroll);
   const uint32_t exp = ex - (uint32_t)pre;
-  for (T o0 = rs; o0 < re; o0 += 64 * kXUnroll) {
+  const T head = runs ? (T)((4u - ((uint32_t)(obase + rs) & 3u)) & 3u) : (T)0;
+  for (T o0 = rs; o0 < re;) {
+    const T lim = (head && o0 == rs) ? rs + head : re;
+    if (runs && lim == re && (re - o0) >= (T)(64 * kXUnroll)) {
+      const uint64_t m0 = __ballot((uint32_t)pre <= (uint32_t)o0);
+      const int l0 = 63 - __clzll((long long)m0);
+      const uint64_t m1 = __ballot((uint32_t)pre <= (uint32_t)o0 + 255u);
+      if (63 - __clzll((long long)m1) == l0) {
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)exp, l0) + (uint32_t)o0 + 4u * (uint32_t)lane;
+        const uint64_t op = obase + (uint64_t)o0 + 4ull * (uint64_t)lane;
+        u32x4 bv4[NB > 0 ? NB : 1];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const u32x4_a4 x = *reinterpret_cast<const u32x4_a4*>(bb[i] + b0);
+          bv4[i] = u32x4{x.x, x.y, x.z, x.w};
+        }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l0);
+          __builtin_nontemporal_store(u32x4{v, v, v, v}, reinterpret_cast<u32x4*>(po[i] + op));
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(bv4[i], reinterpret_cast<u32x4*>(bo[i] + op));
+        o0 += (T)(64 * kXUnroll);
+        continue;
+      }
+    }
     // rounds of this iteration that hold outputs (wave-uniform): a group of
     // 64 rows at fan-out ~2 fills 2 of the 4, and the owner searches of an
     // empty round would be a third of the kernel's LDS instructions
-    const int nr = V == 0 ? kXUnroll : (re - o0) >= (T)(64 * kXUnroll) ? kXUnroll : (int)((re - o0 + 63) / 64);
+    const int nr = V == 0 ? kXUnroll : (lim - o0) >= (T)(64 * kXUnroll) ? kXUnroll : (int)((lim - o0 + 63) / 64);
     T o[kXUnroll];
     int l[kXUnroll];
     bool un[kXUnroll];
@@ -810,19 +847,20 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u)
 #pragma unroll
-      for (int i = 0; i < NB; ++i) bv[u][i] = (u < nr && o[u] < re) ? bb[i][br[u]] : 0u;
+      for (int i = 0; i < NB; ++i) bv[u][i] = (u < nr && o[u] < lim) ? bb[i][br[u]] : 0u;
 #pragma unroll
     for (int u = 0; u < kXUnroll; ++u) {
       if (u >= nr) continue;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const uint32_t v = un[u] ? (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l[u]) : lane_get(pv[i], l[u]);
-        if (o[u] < re) po[i][obase + o[u]] = v;
+        if (o[u] < lim) po[i][obase + o[u]] = v;
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        if (o[u] < re) bo[i][obase + o[u]] = bv[u][i];
+        if (o[u] < lim) bo[i][obase + o[u]] = bv[u][i];
     }
+    o0 = lim != re ? lim : o0 + (T)(64 * kXUnroll);
   }
 }
 
@@ -866,14 +904,17 @@ struct JoinCols {
   const uint32_t* b[kMaxCols];   // build-side source columns (rows of the sorted build table)
   int po[kMaxCols], bo[kMaxCols];  // their output column indices
   int np, nb;
-  int search;                    // 1: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B)
+  int search;                    // bit 0: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B);
+                                 // bit 1: no 16-byte run path (DAS_DJ_VEC=0)
 };
 
 // DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
-// binary search over the lanes' prefixes (round 3); default: owner_of_round
+// binary search over the lanes' prefixes (round 3); default: owner_of_round.
+// DAS_DJ_VEC=0 (bit 1): no 16-byte run path in expand_group (A/B).
 inline int owner_search_env() {
   const char* e = std::getenv("DAS_OWNER_SEARCH");
-  return e && e[0] == '1' ? 1 : 0;
+  const char* v = std::getenv("DAS_DJ_VEC");
+  return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0);
 }
 
 template <int NP, int NB, typename T, int V>
@@ -1171,7 +1212,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
             un[q] = false;
             br[q] = 0;
             if (q >= nr) continue;
-            if (!jc.search) {
+            if (!(jc.search & 1)) {
               const int l = owner_of_round(o0 + (uint32_t)(q * 64), pre, c, row, lane, &un[q]);
               ll[q] = l;
               br[q] = (un[q] ? (uint32_t)__builtin_amdgcn_readlane((int)exp, l) : lane_get(exp, l)) + o[q];
