@@ -777,13 +777,16 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
   // 32-bit groups: owner_of_round (unless DAS_OWNER_SEARCH=1); each lane's
   // ex - pre travels as one value (br = (ex - pre)[owner] + o)
   const bool fast = sizeof(T) == 4 && !(search & 1);
+  (void)cnt;
   // Run path (not with DAS_DJ_VEC=0, search bit 1): 256 consecutive outputs of
   // ONE probe row -- a skewed key's run, an index join's P range -- are
   // consecutive build rows: each lane moves 4 of them per column with one
   // 16-byte load and one 16-byte nontemporal store (4-byte stores top out at
   // ~3.1-3.4 TB/s on this part, 16-byte ones reach ~7, k_cartesian), and
-  // writes the probe values as 16-byte splats.  Needs 16-byte aligned output
-  // positions: a head of up to 3 outputs goes through the rounds first.
+  // writes the probe values as 16-byte splats; 256 outputs of several probe
+  // rows take the quad path below (not with DAS_DJ_VEC=1, search bit 2).
+  // Needs 16-byte aligned output positions: a head of up to 3 outputs goes
+  // through the rounds first.  `row`: the wave's 256-entry LDS row.
   const bool runs = fast && !(search & 2) && (re - rs) > (T)(64 * kXUnroll);
   const uint32_t exp = ex - (uint32_t)pre;
   const T head = runs ? (T)((4u - ((uint32_t)(obase + rs) & 3u)) & 3u) : (T)0;
@@ -809,6 +812,52 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(bv4[i], reinterpret_cast<u32x4*>(bo[i] + op));
+        o0 += (T)(64 * kXUnroll);
+        continue;
+      }
+      if (!(search & 4)) {
+        // Quad path: the 256 outputs span several probe rows.  Lane `lane`
+        // takes outputs o0 + 4 lane .. + 3: every probe row starting inside
+        // the block writes its lane id at its start offset of the wave's
+        // 256-entry LDS row (the owner of o0 at offset 0), and a max scan
+        // over the row -- 4 entries per lane, then an inclusive DPP max over
+        // the lanes -- gives each output its owner.  The build values are 4
+        // dword gathers per column; every column is written with ONE 16-byte
+        // nontemporal store per lane instead of four 4-byte ones.
+        typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
+        lds_u32* vr = (lds_u32*)row;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vr[4 * lane + k] = (lane == 0 && k == 0) ? (uint32_t)l0 : 0u;
+        if (cnt && (uint32_t)pre > (uint32_t)o0 && (uint32_t)pre - (uint32_t)o0 < 256u)
+          vr[(uint32_t)pre - (uint32_t)o0] = (uint32_t)lane;
+        uint32_t m[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = vr[4 * lane + k];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) m[k] = m[k] > m[k - 1] ? m[k] : m[k - 1];
+        const uint32_t incl = wave_incl_max_u32(m[3]);
+        const uint32_t prev = (uint32_t)__shfl_up((int)incl, 1, 64);
+        const uint32_t ex0 = lane ? prev : 0u;
+        const uint32_t q0 = (uint32_t)o0 + 4u * (uint32_t)lane;
+        const uint64_t op = obase + (uint64_t)q0;
+        int own[4];
+        uint32_t brk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          own[k] = (int)(m[k] > ex0 ? m[k] : ex0);
+          brk[k] = lane_get(exp, own[k]) + q0 + (uint32_t)k;
+        }
+        u32x4 bq[NB > 0 ? NB : 1];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) bq[i] = u32x4{bb[i][brk[0]], bb[i][brk[1]], bb[i][brk[2]], bb[i][brk[3]]};
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const u32x4 pq{lane_get(pv[i], own[0]), lane_get(pv[i], own[1]), lane_get(pv[i], own[2]),
+                         lane_get(pv[i], own[3])};
+          __builtin_nontemporal_store(pq, reinterpret_cast<u32x4*>(po[i] + op));
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(bq[i], reinterpret_cast<u32x4*>(bo[i] + op));
         o0 += (T)(64 * kXUnroll);
         continue;
       }
@@ -910,11 +959,12 @@ struct JoinCols {
 
 // DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
 // binary search over the lanes' prefixes (round 3); default: owner_of_round.
-// DAS_DJ_VEC=0 (bit 1): no 16-byte run path in expand_group (A/B).
+// DAS_DJ_VEC=0 (bit 1): no 16-byte paths in expand_group; =1 (bit 2): the
+// single-row run path only, no quad path (A/B).
 inline int owner_search_env() {
   const char* e = std::getenv("DAS_OWNER_SEARCH");
   const char* v = std::getenv("DAS_DJ_VEC");
-  return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0);
+  return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0) | (v && v[0] == '1' ? 4 : 0);
 }
 
 template <int NP, int NB, typename T, int V>
@@ -922,7 +972,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
                                                 uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                 const uint64_t* __restrict__ unit_off, JoinCols jc,
                                                 uint32_t* __restrict__ out, uint64_t cap) {
-  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  __shared__ uint32_t s_row[B / 64][256];                   // the wave's LDS row (owner_of_round, quad path)
   uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
@@ -987,7 +1037,7 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
   for (int i = 0; i < NP; ++i) { pp[i] = jc.p[i]; po[i] = out + (uint64_t)jc.po[i] * cap; }
 #pragma unroll
   for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
-  __shared__ uint32_t s_row[B / 64][64];                    // owner_of_round's row per wave
+  __shared__ uint32_t s_row[B / 64][256];                   // the wave's LDS row (owner_of_round, quad path)
   uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t chunks = (total + chunk - 1) / chunk;
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {

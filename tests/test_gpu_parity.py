@@ -595,7 +595,7 @@ def test_gpu_hub_join_expansion(force, monkeypatch):
         assert same(got, want), (q, got.get("n"), want.get("n"))
 
 
-@pytest.mark.parametrize("search", ["0", "1"])
+@pytest.mark.parametrize("search", ["0", "1", "0-vec1", "0-vec0"])
 @pytest.mark.parametrize("shape", ["sparse", "fanout2", "skew", "wide"])
 def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     """das_join of two-column tables on one key through the direct-address
@@ -603,8 +603,10 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     outputs (owner_of_round: ballot fast path / LDS row + DPP max; search=1:
     the ds_bpermute binary search): lanes without outputs, fan-out ~2, skewed
     keys (the output-balanced expansion) and a wide fan-out, against a numpy
-    join with multiplicities."""
-    monkeypatch.setenv("DAS_OWNER_SEARCH", search)
+    join with multiplicities.  The 16-byte paths of 256-output blocks: both
+    (default), the single-row run path only (vec1), none (vec0)."""
+    monkeypatch.setenv("DAS_OWNER_SEARCH", search[0])
+    monkeypatch.setenv("DAS_DJ_VEC", search[-1] if "vec" in search else "")
     from das_amd import _lib, synthetic
     db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
     rng = np.random.default_rng({"sparse": 1, "fanout2": 2, "skew": 3, "wide": 4}[shape])
