@@ -167,6 +167,9 @@ struct Ctx {
   std::mutex mu;
   Index idx;
   HostScalar scratch;
+  // (lo, cnt) descriptor array of the sparse direct-join build, all-zero
+  // between joins (direct_join clears the slots it wrote)
+  DBuf<uint2> zlc;
   // loader-side host copies kept for metadata calls
   std::vector<uint8_t> leaf_bytes;
   std::vector<uint64_t> leaf_off;

@@ -698,6 +698,17 @@ __global__ void __launch_bounds__(B) k_lc_base(const uint32_t* key, const uint32
   }
 }
 
+// the slots k_lc_count / k_lc_base wrote (and the running base at lc[range])
+// back to zero: the context's descriptor array stays all-zero between joins
+__global__ void __launch_bounds__(B) k_lc_clear(const uint32_t* key, uint64_t n, uint32_t kmin, uint32_t range,
+                                                uint2* lc) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = key[i] - kmin;
+    if (d < range) lc[d] = make_uint2(0u, 0u);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) lc[range] = make_uint2(0u, 0u);
+}
+
 __global__ void __launch_bounds__(B) k_lc_scatter(ColSet src, const uint32_t* key, const uint32_t* rank, uint64_t n,
                                                   uint32_t kmin, uint32_t range, const uint2* lc, uint32_t* out,
                                                   uint64_t cap) {
@@ -2429,7 +2440,7 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
   // sparse build's running base.  The sparse build (fewer launches, ~8 B per
   // slot instead of ~36) takes at most 2^18 build rows: its bases come from
   // one atomic per wave on one counter
-  DBuf<uint2> lc(range + 1, c.s);
+  DBuf<uint2> lc;
   auto expand = [&](const Table& Qb, const uint2* lcp) {
     const int nu = (int)uni.size();
     JoinCols jc{};
@@ -2445,25 +2456,56 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
       (bm && !std::strcmp(bm, "sparse") ? true
        : bm && !std::strcmp(bm, "dense") ? false : range > 16 * Q.nrows && range >= (1ull << 16) && Q.nrows <= (1ull << 18));
   if (sparse) {
-    // few build rows over a wide slot range: descriptors written in place
+    // few build rows over a wide slot range: descriptors written in place --
+    // into the context's descriptor array, which stays all-zero between joins
+    // (the build's own slots are cleared after the expansion: 2*10^4 slot
+    // writes instead of a 112 MB fill per bio QUERY_3 join; DAS_ZLC=0: a
+    // fresh array filled per join, A/B)
     const bool srt = Q.sorted_col == qk;
-    ProfScope ps(c, "join_build", (srt ? 4.0 : 8.0 + 8.0 * Q.ncols) * Q.nrows + 8.0 * range);
-    fill_dev(lc.p, 0, 8 * (range + 1), c.s);
-    DBuf<uint32_t> rk(srt ? 1 : Q.nrows, c.s);
-    hipLaunchKernelGGL(k_lc_count, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lc.p, rk.p,
-                       srt ? 1 : 0);
-    if (!srt) {
-      hipLaunchKernelGGL(k_lc_base, G(Q.nrows), dim3(B), 0, c.s, qkey, rk.p, Q.nrows, kmin, (uint32_t)range, lc.p,
-                         reinterpret_cast<uint32_t*>(lc.p + range));
-      Qs = new_table_like(c, Q, Q.nrows);
-      Qs->nrows = Q.nrows;
-      hipLaunchKernelGGL(k_lc_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, rk.p, Q.nrows, kmin,
-                         (uint32_t)range, lc.p, Qs->data, Qs->cap);
-      Qb = Qs.get();
+    const char* zf = std::getenv("DAS_ZLC");
+    const bool reuse = !(zf && zf[0] == '0');
+    uint2* lcp = nullptr;
+    {
+      const bool fresh = !reuse || c.zlc.n < range + 1;
+      ProfScope ps(c, "join_build", (srt ? 4.0 : 8.0 + 8.0 * Q.ncols) * Q.nrows + (fresh ? 8.0 * range : 0.0));
+      if (reuse) {
+        if (c.zlc.n < range + 1) {
+          c.zlc.alloc(std::max<uint64_t>(range + 1, 2 * c.zlc.n), c.s);
+          fill_dev(c.zlc.p, 0, 8 * c.zlc.n, c.s);
+        }
+        lcp = c.zlc.p;
+      } else {
+        lc.alloc(range + 1, c.s);
+        fill_dev(lc.p, 0, 8 * (range + 1), c.s);
+        lcp = lc.p;
+      }
+      DBuf<uint32_t> rk(srt ? 1 : Q.nrows, c.s);
+      hipLaunchKernelGGL(k_lc_count, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lcp, rk.p,
+                         srt ? 1 : 0);
+      if (!srt) {
+        hipLaunchKernelGGL(k_lc_base, G(Q.nrows), dim3(B), 0, c.s, qkey, rk.p, Q.nrows, kmin, (uint32_t)range, lcp,
+                           reinterpret_cast<uint32_t*>(lcp + range));
+        Qs = new_table_like(c, Q, Q.nrows);
+        Qs->nrows = Q.nrows;
+        hipLaunchKernelGGL(k_lc_scatter, G(Q.nrows), dim3(B), 0, c.s, cols_of(Q), qkey, rk.p, Q.nrows, kmin,
+                           (uint32_t)range, lcp, Qs->data, Qs->cap);
+        Qb = Qs.get();
+      }
+      DAS_HIP(hipGetLastError());
     }
+    if (!reuse) return expand(*Qb, lcp);
+    std::unique_ptr<Table> out;
+    try {
+      out = expand(*Qb, lcp);
+    } catch (...) {
+      c.zlc.release();              // slots possibly left set: the next join starts from a fresh array
+      throw;
+    }
+    hipLaunchKernelGGL(k_lc_clear, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lcp);
     DAS_HIP(hipGetLastError());
-    return expand(*Qb, lc.p);
+    return out;
   }
+  lc.alloc(range + 1, c.s);
   // bucket offsets of the build side: already grouped by key when it comes
   // sorted (an order-aware scan), else a counting sort
   DBuf<uint32_t> off(range + 1, c.s);

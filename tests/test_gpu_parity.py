@@ -635,6 +635,38 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     assert sorted(zip(*[c.tolist() for c in got])) == want
 
 
+@pytest.mark.parametrize("zlc", ["1", "0"])
+def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
+    """The sparse direct-join build writes its (lo, cnt) slots into the
+    context's descriptor array and clears them after the expansion (DAS_ZLC=1,
+    default; 0: a fresh array per join): five joins in a row on one context,
+    over overlapping and growing key ranges (build keys in sorted order or
+    not), each against a numpy join with multiplicities."""
+    monkeypatch.setenv("DAS_DJ_BUILD", "sparse")
+    monkeypatch.setenv("DAS_ZLC", zlc)
+    from das_amd import _lib, synthetic
+    db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
+    rng = np.random.default_rng(11)
+    for nk, nq, srt in ((20000, 300, False), (20000, 500, True), (90000, 800, False), (5000, 200, False),
+                        (90000, 1000, True)):
+        pk = rng.integers(0, nk, 30000)
+        qk = rng.integers(0, nk, nq)
+        if srt:
+            qk = np.sort(qk)
+        pa = rng.integers(0, 1 << 20, len(pk)).astype(np.uint32)
+        qb = rng.integers(0, 1 << 20, len(qk)).astype(np.uint32)
+        P = db.ctx.table_from_host(_lib.TABLE_ORDERED, [0, 1], np.stack([pa, pk.astype(np.uint32)]))
+        Q = db.ctx.table_from_host(_lib.TABLE_ORDERED, [1, 2], np.stack([qk.astype(np.uint32), qb]))
+        P.set_bounds([0, 0], [(1 << 20) - 1, nk])
+        Q.set_bounds([0, 0], [nk, (1 << 20) - 1])
+        got = db.ctx.join(P, Q).fetch()
+        by = {}
+        for k, b in zip(qk.tolist(), qb.tolist()):
+            by.setdefault(k, []).append(b)
+        want = sorted((a, k, b) for a, k in zip(pa.tolist(), pk.tolist()) for b in by.get(k, ()))
+        assert sorted(zip(*[c.tolist() for c in got])) == want, (nk, nq, srt)
+
+
 @pytest.mark.parametrize("guard", ["1", "0"])
 @pytest.mark.parametrize("build", ["", "sparse", "dense"])
 @pytest.mark.parametrize("probe_rows", [5000, 40000])
