@@ -781,6 +781,15 @@ constexpr int kXUnroll = DAS_DJ_UNROLL;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-byte load
 
+// 16-byte output store: nontemporal for large outputs, plain when the table
+// is small and read again right away (search bit 3): nontemporally written
+// lines were re-read ~30 % slower by the k_cartesian that consumes a small
+// join result (r4_dj_nt_ab)
+__device__ __forceinline__ void store16(uint32_t* p, u32x4 v, bool plain) {
+  if (plain) *reinterpret_cast<u32x4*>(p) = v;
+  else __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+}
+
 template <int NP, int NB, typename T, int V = 1>
 __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
@@ -819,10 +828,10 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
           const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l0);
-          __builtin_nontemporal_store(u32x4{v, v, v, v}, reinterpret_cast<u32x4*>(po[i] + op));
+          store16(po[i] + op, u32x4{v, v, v, v}, search & 8);
         }
 #pragma unroll
-        for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(bv4[i], reinterpret_cast<u32x4*>(bo[i] + op));
+        for (int i = 0; i < NB; ++i) store16(bo[i] + op, bv4[i], search & 8);
         o0 += (T)(64 * kXUnroll);
         continue;
       }
@@ -865,10 +874,10 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
         for (int i = 0; i < NP; ++i) {
           const u32x4 pq{lane_get(pv[i], own[0]), lane_get(pv[i], own[1]), lane_get(pv[i], own[2]),
                          lane_get(pv[i], own[3])};
-          __builtin_nontemporal_store(pq, reinterpret_cast<u32x4*>(po[i] + op));
+          store16(po[i] + op, pq, search & 8);
         }
 #pragma unroll
-        for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(bq[i], reinterpret_cast<u32x4*>(bo[i] + op));
+        for (int i = 0; i < NB; ++i) store16(bo[i] + op, bq[i], search & 8);
         o0 += (T)(64 * kXUnroll);
         continue;
       }
@@ -965,7 +974,8 @@ struct JoinCols {
   int po[kMaxCols], bo[kMaxCols];  // their output column indices
   int np, nb;
   int search;                    // bit 0: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B);
-                                 // bit 1: no 16-byte run path (DAS_DJ_VEC=0)
+                                 // bit 1: no 16-byte paths (DAS_DJ_VEC=0); bit 2: no quad path
+                                 // (DAS_DJ_VEC=1); bit 3: plain (not nontemporal) 16-byte stores
 };
 
 // DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
@@ -1146,7 +1156,11 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
   int pi = 0, bi = 0;
   do {
     JoinCols part{};
-    part.search = owner_search_env();
+    // 16-byte stores nontemporal only for outputs of 2^22 rows or more
+    // (DAS_DJ_NT=1 always, 0 never)
+    static const char* nt = std::getenv("DAS_DJ_NT");
+    const bool plain = nt && nt[0] == '0' ? true : nt && nt[0] == '1' ? false : total < (1ull << 22);
+    part.search = owner_search_env() | (plain ? 8 : 0);
     part.np = std::min(jc.np - pi, 4);
     part.nb = std::min(jc.nb - bi, 4);
     for (int i = 0; i < part.np; ++i) { part.p[i] = jc.p[pi + i]; part.po[i] = jc.po[pi + i]; }
