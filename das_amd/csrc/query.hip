@@ -782,12 +782,19 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-byte load
 
 // 16-byte output store: nontemporal for large outputs, plain when the table
-// is small and read again right away (search bit 3): nontemporally written
-// lines were re-read ~30 % slower by the k_cartesian that consumes a small
-// join result (r4_dj_nt_ab)
+// is small and read again right away (search bit 3): with nontemporal stores
+// in every join, bio QUERY_3's k_cartesian -- which reads a small join result
+// once per output row -- ran 1221 instead of 928 us (profiles/r4_dj_vec_ab.jsonl);
+// the 25 M-row Q2 join runs 64-72 us with them, 87 us with plain 16-byte stores
 __device__ __forceinline__ void store16(uint32_t* p, u32x4 v, bool plain) {
-  if (plain) *reinterpret_cast<u32x4*>(p) = v;
-  else __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  if (plain) {
+    *reinterpret_cast<u32x4*>(p) = v;
+  } else {
+    // (a vector store written out: with __builtin_nontemporal_store in one
+    // branch and a plain store in the other the compiler sinks both into one
+    // store and drops the nontemporal flag)
+    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+  }
 }
 
 template <int NP, int NB, typename T, int V = 1>
@@ -1400,25 +1407,34 @@ __global__ void __launch_bounds__(B) k_chunk_compact(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint32_t* __restrict__ off, uint64_t wlo, uint64_t whi,
                                                      int ncols, uint32_t* __restrict__ dst, uint64_t dcap) {
+  // 16-byte moves: a head of up to 3 rows aligns the destination, then each
+  // lane moves 4 rows per dwordx4 load (dword-aligned) and nontemporal
+  // dwordx4 store, then a tail of up to 3 rows (dcap is a multiple of 64)
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
-  const int lane = __lane_id();
+  const uint32_t lane = (uint32_t)__lane_id();
   for (uint64_t w = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < whi; w += waves) {
     const uint32_t n = cnt[w];
     const uint64_t s0 = (w - wlo) * CH, d0 = off[w];
+    const uint32_t h = (4u - (uint32_t)(d0 & 3u)) & 3u;
+    const uint32_t head = h < n ? h : n;
+    const uint32_t nq = (n - head) / 4u;
+    const uint32_t t0 = head + 4u * nq;
     for (int k = 0; k < ncols; ++k) {
       const uint32_t* sc = src + (uint64_t)k * scap + s0;
       uint32_t* dc = dst + (uint64_t)k * dcap + d0;
-      uint32_t x[CH / 64];
+      if (lane < head) dc[lane] = sc[lane];
+      u32x4_a4 x[CH / 256];
 #pragma unroll
-      for (int j = 0; j < CH / 64; ++j) {
-        const uint32_t i = (uint32_t)(j * 64 + lane);
-        x[j] = i < n ? __builtin_nontemporal_load(sc + i) : 0u;
+      for (int j = 0; j < CH / 256; ++j) {
+        const uint32_t q = (uint32_t)j * 64u + lane;
+        if (q < nq) x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(sc + head + 4u * q));
       }
 #pragma unroll
-      for (int j = 0; j < CH / 64; ++j) {
-        const uint32_t i = (uint32_t)(j * 64 + lane);
-        if (i < n) dc[i] = x[j];
+      for (int j = 0; j < CH / 256; ++j) {
+        const uint32_t q = (uint32_t)j * 64u + lane;
+        if (q < nq) store16(dc + head + 4u * q, u32x4{x[j].x, x[j].y, x[j].z, x[j].w}, false);
       }
+      if (t0 + lane < n) dc[t0 + lane] = sc[t0 + lane];
     }
   }
 }
