@@ -799,23 +799,20 @@ constexpr int kXUnroll = DAS_DJ_UNROLL;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-byte load
 
-// 16-byte output store: nontemporal for large outputs, plain when the table
-// is small and read again right away (search bit 3): with nontemporal stores
-// in every join, bio QUERY_3's k_cartesian -- which reads a small join result
-// once per output row -- ran 1221 instead of 928 us (profiles/r4_dj_vec_ab.jsonl);
-// the 25 M-row Q2 join runs 64-72 us with them, 87 us with plain 16-byte stores
-__device__ __forceinline__ void store16(uint32_t* p, u32x4 v, bool plain) {
-  if (plain) {
-    *reinterpret_cast<u32x4*>(p) = v;
-  } else {
-    // (a vector store written out: with __builtin_nontemporal_store in one
-    // branch and a plain store in the other the compiler sinks both into one
-    // store and drops the nontemporal flag)
-    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
-  }
+// 16-byte output store, nontemporal in the instantiations for large outputs
+// (>= 2^22 rows): with nontemporal stores in every join, bio QUERY_3's
+// k_cartesian -- which reads a small join result once per output row -- ran
+// 1221 instead of 928 us (profiles/r4_dj_vec_ab.jsonl); the 25 M-row Q2 join
+// runs 64-72 us with them, 87 us with plain 16-byte stores.  A template
+// parameter, not a run-time branch: the compiler sinks a nontemporal and a
+// plain store of two branches into one plain store.
+template <bool NT>
+__device__ __forceinline__ void store16(uint32_t* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = v;
 }
 
-template <int NP, int NB, typename T, int V = 1>
+template <int NP, int NB, typename T, int V = 1, bool NT = false>
 __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, uint32_t ex, const uint32_t* pv,
                                              const uint32_t* const* bb, uint32_t* const* po, uint32_t* const* bo,
                                              uint64_t obase, int lane, uint32_t* row, int search) {
@@ -853,10 +850,10 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
           const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l0);
-          store16(po[i] + op, u32x4{v, v, v, v}, search & 8);
+          store16<NT>(po[i] + op, u32x4{v, v, v, v});
         }
 #pragma unroll
-        for (int i = 0; i < NB; ++i) store16(bo[i] + op, bv4[i], search & 8);
+        for (int i = 0; i < NB; ++i) store16<NT>(bo[i] + op, bv4[i]);
         o0 += (T)(64 * kXUnroll);
         continue;
       }
@@ -899,10 +896,10 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
         for (int i = 0; i < NP; ++i) {
           const u32x4 pq{lane_get(pv[i], own[0]), lane_get(pv[i], own[1]), lane_get(pv[i], own[2]),
                          lane_get(pv[i], own[3])};
-          store16(po[i] + op, pq, search & 8);
+          store16<NT>(po[i] + op, pq);
         }
 #pragma unroll
-        for (int i = 0; i < NB; ++i) store16(bo[i] + op, bq[i], search & 8);
+        for (int i = 0; i < NB; ++i) store16<NT>(bo[i] + op, bq[i]);
         o0 += (T)(64 * kXUnroll);
         continue;
       }
@@ -1000,7 +997,7 @@ struct JoinCols {
   int np, nb;
   int search;                    // bit 0: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B);
                                  // bit 1: no 16-byte paths (DAS_DJ_VEC=0); bit 2: no quad path
-                                 // (DAS_DJ_VEC=1); bit 3: plain (not nontemporal) 16-byte stores
+                                 // (DAS_DJ_VEC=1)
 };
 
 // DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
@@ -1013,7 +1010,7 @@ inline int owner_search_env() {
   return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0) | (v && v[0] == '1' ? 4 : 0);
 }
 
-template <int NP, int NB, typename T, int V>
+template <int NP, int NB, typename T, int V, bool NT = false>
 __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                 uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                 const uint64_t* __restrict__ unit_off, JoinCols jc,
@@ -1055,7 +1052,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
       const T inc = wave_inclusive_scan(c);
       const T tot = (T)__shfl(inc, 63, 64);
       const T pre = inc - c;                                 // this lane's first output
-      expand_group<NP, NB, T, V>((T)0, tot, pre, e[g].y, e[g].x, pv[g], bb, po, bo, base, lane, row, jc.search);
+      expand_group<NP, NB, T, V, NT>((T)0, tot, pre, e[g].y, e[g].x, pv[g], bb, po, bo, base, lane, row, jc.search);
       base += tot;
     }
   }
@@ -1067,7 +1064,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
 // offsets, then expands only the slice of each group that falls in its chunk.
 constexpr uint64_t kBalChunk = 1024;
 
-template <int NP, int NB, typename T>
+template <int NP, int NB, typename T, bool NT = false>
 __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                                     uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                     const uint64_t* __restrict__ unit_off, JoinCols jc,
@@ -1125,7 +1122,7 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
         uint32_t pv[NP > 0 ? NP : 1];
 #pragma unroll
         for (int i = 0; i < NP; ++i) pv[i] = r < np ? pp[i][r] : 0u;
-        expand_group<NP, NB, T>(rs, re, pre, (uint32_t)c, e[g].x, pv, bb, po, bo, gb, lane, row, jc.search);
+        expand_group<NP, NB, T, 1, NT>(rs, re, pre, (uint32_t)c, e[g].x, pv, bb, po, bo, gb, lane, row, jc.search);
       }
     }
   }
@@ -1137,10 +1134,15 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
                      uint64_t cap, uint64_t total, bool balanced, double bytes) {
   const bool wide = total >= (1ull << 32) - (1ull << 16);
   static const int fixed = std::getenv("DAS_DJ_FIXED") && std::getenv("DAS_DJ_FIXED")[0] == '1';
+  // 16-byte stores nontemporal for outputs of 2^22 rows or more (DAS_DJ_NT=1
+  // always, 0 never); 64-bit-offset and fixed-round launches: plain
+  static const char* nte = std::getenv("DAS_DJ_NT");
+  const bool nt = !wide && (nte && nte[0] == '1' ? true : nte && nte[0] == '0' ? false : total >= (1ull << 22)) &&
+                  (balanced || !fixed);
   // scope names = rocprof's names of the instantiation launched below
   KScope ks((std::string(balanced ? "k_dj_write_bal<" : "k_dj_write<") + std::to_string(NP) + "," +
-             std::to_string(NB) + (wide ? ",u64" : ",u32") +
-             (balanced ? ">" : (fixed && !wide) ? ",0>" : ",1>"))
+             std::to_string(NB) + (wide ? ",u64" : ",u32") + (balanced ? "" : (fixed && !wide) ? ",0" : ",1") +
+             (nt ? ",true>" : ",false>"))
                 .c_str(), bytes);
   if (balanced) {
     // outputs per wave (DAS_BAL_CHUNK, A/B: 512 .. 8192, a multiple of 64)
@@ -1150,24 +1152,29 @@ void launch_dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_
       return v >= 64 && v <= 8192 && v % 64 == 0 ? v : kBalChunk;
     }();
     const unsigned g = grid_for((total + chunk - 1) / chunk, B / 64, 65535u * 4u);
-    if (total < (1ull << 32) - (1ull << 16))
-      hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint32_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
-                         toff, jc, out, cap, total, chunk);
-    else
+    if (wide)
       hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint64_t>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
                          toff, jc, out, cap, total, chunk);
+    else if (nt)
+      hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint32_t, true>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                         units, toff, jc, out, cap, total, chunk);
+    else
+      hipLaunchKernelGGL((k_dj_write_bal<NP, NB, uint32_t, false>), dim3(g), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                         units, toff, jc, out, cap, total, chunk);
     return;
   }
-  if (total < (1ull << 32) - (1ull << 16)) {
-    if (fixed)
-      hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 0>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
-                         units, toff, jc, out, cap);
-    else
-      hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 1>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
-                         units, toff, jc, out, cap);
-  } else {
+  if (wide) {
     hipLaunchKernelGGL((k_dj_write<NP, NB, uint64_t, 1>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
                        toff, jc, out, cap);
+  } else if (fixed) {
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 0>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc, units,
+                       toff, jc, out, cap);
+  } else if (nt) {
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 1, true>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                       units, toff, jc, out, cap);
+  } else {
+    hipLaunchKernelGGL((k_dj_write<NP, NB, uint32_t, 1, false>), dim3(grid), dim3(B), 0, s, pkey, np, kmin, range, lc,
+                       units, toff, jc, out, cap);
   }
 }
 
@@ -1181,11 +1188,7 @@ void dj_write(unsigned grid, hipStream_t s, const uint32_t* pkey, uint64_t np, u
   int pi = 0, bi = 0;
   do {
     JoinCols part{};
-    // 16-byte stores nontemporal only for outputs of 2^22 rows or more
-    // (DAS_DJ_NT=1 always, 0 never)
-    static const char* nt = std::getenv("DAS_DJ_NT");
-    const bool plain = nt && nt[0] == '0' ? true : nt && nt[0] == '1' ? false : total < (1ull << 22);
-    part.search = owner_search_env() | (plain ? 8 : 0);
+    part.search = owner_search_env();
     part.np = std::min(jc.np - pi, 4);
     part.nb = std::min(jc.nb - bi, 4);
     for (int i = 0; i < part.np; ++i) { part.p[i] = jc.p[pi + i]; part.po[i] = jc.po[pi + i]; }
@@ -1450,7 +1453,7 @@ __global__ void __launch_bounds__(B) k_chunk_compact(const uint32_t* __restrict_
 #pragma unroll
       for (int j = 0; j < CH / 256; ++j) {
         const uint32_t q = (uint32_t)j * 64u + lane;
-        if (q < nq) store16(dc + head + 4u * q, u32x4{x[j].x, x[j].y, x[j].z, x[j].w}, false);
+        if (q < nq) store16<true>(dc + head + 4u * q, u32x4{x[j].x, x[j].y, x[j].z, x[j].w});
       }
       if (t0 + lane < n) dc[t0 + lane] = sc[t0 + lane];
     }

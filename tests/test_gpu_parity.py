@@ -595,6 +595,16 @@ def test_gpu_hub_join_expansion(force, monkeypatch):
         assert same(got, want), (q, got.get("n"), want.get("n"))
 
 
+def _assert_same_rows(got, want, what=""):
+    """got == want for long row lists, reported by counts and the first
+    difference (pytest's own diff of 10^7-row lists runs for minutes)."""
+    if got == want:
+        return
+    i = next((k for k, (a, b) in enumerate(zip(got, want)) if a != b), min(len(got), len(want)))
+    raise AssertionError(f"{what}: {len(got)} rows, want {len(want)}; first difference at {i}: "
+                         f"{got[i] if i < len(got) else None} vs {want[i] if i < len(want) else None}")
+
+
 @pytest.mark.parametrize("search", ["0", "1", "0-vec1", "0-vec0"])
 @pytest.mark.parametrize("shape", ["sparse", "fanout2", "skew", "wide"])
 def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
@@ -632,7 +642,7 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
         by.setdefault(k, []).append(b)
     want = sorted((a, k, b) for a, k in zip(pa.tolist(), pk.tolist()) for b in by.get(k, ()))
     assert len(want) > 1000
-    assert sorted(zip(*[c.tolist() for c in got])) == want
+    _assert_same_rows(sorted(zip(*[c.tolist() for c in got])), want)
 
 
 @pytest.mark.parametrize("zlc", ["1", "0"])
@@ -664,7 +674,7 @@ def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
         for k, b in zip(qk.tolist(), qb.tolist()):
             by.setdefault(k, []).append(b)
         want = sorted((a, k, b) for a, k in zip(pa.tolist(), pk.tolist()) for b in by.get(k, ()))
-        assert sorted(zip(*[c.tolist() for c in got])) == want, (nk, nq, srt)
+        _assert_same_rows(sorted(zip(*[c.tolist() for c in got])), want, (nk, nq, srt))
 
 
 @pytest.mark.parametrize("guard", ["1", "0"])
