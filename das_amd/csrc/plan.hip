@@ -339,8 +339,11 @@ struct Exec {
   // running result must have more than 4096 rows (DAS_SEMI_MULTI as above).
   size_t filt_run(const std::vector<uint32_t>& terms, size_t k, const Table& a, int32_t& v) const {
     const char* f = std::getenv("DAS_SEMI_MULTI");
-    if ((f && f[0] == '0') || a.kind != DAS_TABLE_ORDERED || (!(f && f[0] == '1') && a.nrows <= 4096) ||
-        k + 1 >= terms.size())
+    // DAS_FILT_EXPAND=0 (A/B): the join written out, then filtered by the
+    // key-set intersection (semi_join_multi) instead of the filtered expansion
+    const char* fx = std::getenv("DAS_FILT_EXPAND");
+    if ((f && f[0] == '0') || (fx && fx[0] == '0') || a.kind != DAS_TABLE_ORDERED ||
+        (!(f && f[0] == '1') && a.nrows <= 4096) || k + 1 >= terms.size())
       return k;
     v = one_var(terms[k + 1]);
     if (v < 0) return k;
