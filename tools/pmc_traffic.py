@@ -60,7 +60,14 @@ def _last_counts():
         return None
     with open(path) as f:
         line = [l for l in f if l.startswith("{")][-1]
-    return {k: v["launches"] for k, v in json.loads(line).get("kernels", {}).items()}
+    rec = json.loads(line)
+    det = rec.get("detail")          # the compact last line names the full record
+    if det:
+        p = det if os.path.isabs(det) else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), det)
+        if os.path.exists(p):
+            with open(p) as f:
+                rec = json.load(f)
+    return {k: v["launches"] for k, v in rec.get("kernels", {}).items()}
 
 
 def per_kernel(db_dir, counter):

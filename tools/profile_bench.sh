@@ -21,12 +21,12 @@ mkdir -p $D
 export TMPDIR=/tmp
 ARGS="--workload $W --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-}"
 PARGS="$ARGS --no-cpu-baseline --no-materialise --no-extras"
-timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
-timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS > $D/kt.log 2>&1 &&
+timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS --detail gpurun_out/${T}_bench_${W}_detail.json > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
+timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS --detail $D/kt_detail.json > $D/kt.log 2>&1 &&
 cp "$(find $D/kt -name 'run_kernel_stats.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_stats.csv &&
 cp "$(find $D/kt -name 'run_kernel_trace.csv' | head -n 1)" gpurun_out/${T}_${W}_kernel_trace.csv &&
-timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/fetch -o run -- python bench.py $PARGS > $D/fetch.log 2>&1 &&
-timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $PARGS > $D/write.log 2>&1 &&
+timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc FETCH_SIZE -f rocpd -d $D/fetch -o run -- python bench.py $PARGS --detail $D/fetch_detail.json > $D/fetch.log 2>&1 &&
+timeout -s KILL ${PROF_TIMEOUT:-300} rocprofv3 --pmc WRITE_SIZE -f rocpd -d $D/write -o run -- python bench.py $PARGS --detail $D/write_detail.json > $D/write.log 2>&1 &&
 if [ "$W" = build ]; then export LAST_FROM=gpurun_out/${T}_bench_$W.json; fi &&
 python tools/pmc_traffic.py $D/fetch $D/write > gpurun_out/${T}_pmc_traffic_$W.json &&
 cp $D/kt.log gpurun_out/${T}_bench_${W}_under_rocprof.log &&

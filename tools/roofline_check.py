@@ -17,6 +17,16 @@ def main():
     with open(sys.argv[1]) as f:
         line = [l for l in f if l.startswith("{")][-1]
     bench = json.loads(line)
+    # the bench's last line is the compact record; the full one (per-launch
+    # bytes, kernel tables) is in the detail file it names
+    detail = bench.get("detail")
+    if detail:
+        import os
+        path = detail if os.path.isabs(detail) else os.path.join(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))), detail)
+        if os.path.exists(path):
+            with open(path) as f:
+                bench = json.load(f)
     rf = bench["roofline"]
     if "avg_launch_us" not in rf:
         # the build line: its roofline is the whole build's (SURVEY §8d
