@@ -55,6 +55,14 @@ struct PosIndex {
   // in place of the whole type's keys (index joins of sparse key ranges).
   std::vector<uint32_t*> bdir;
   std::vector<uint32_t> bshift, bn;
+  // Rank directory (in place of a dense one over >= 2^20 ids): one bit per
+  // id of the span (rbits, 64-bit words) and each word's count of earlier
+  // set bits (rpre); key (ty, t) is ukey[rklo + rpre[w] + popc(bits below
+  // t's bit)] -- 1.5 bits per id instead of 32, so a probe's directory lines
+  // are shared with its neighbours and the directory stays MALL-resident.
+  std::vector<uint64_t*> rbits;
+  std::vector<uint32_t*> rpre;
+  std::vector<uint64_t> rklo;
   // host mirror of ukey / uoff (nkeys <= kHostKeyMirror), else empty
   std::vector<uint64_t> h_ukey, h_uoff;
 };

@@ -1218,6 +1218,31 @@ void free_index(Index& idx) {
   idx = Index();
 }
 
+// rank directory: the bit of every key of ukey[klo, klo + n) (sorted, so
+// neighbouring lanes mostly set bits of one word: one atomic per word run)
+__global__ void k_rank_bits(const uint64_t* ukey, uint64_t klo, uint64_t n, uint32_t tmin, unsigned long long* bits) {
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x; b < n; b += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = b + threadIdx.x;             // block-uniform trip count: the whole wave shuffles
+    const bool act = i < n;
+    const uint32_t d = act ? (uint32_t)(ukey[klo + i] & 0xFFFFFFFFull) - tmin : 0u;
+    const uint32_t w = act ? d >> 6 : 0xFFFFFFFFu;
+    unsigned long long m = act ? 1ull << (d & 63) : 0ull;
+    // OR the bits of the lanes sharing this lane's word (runs: sorted keys)
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const unsigned long long om = __shfl_down(m, s, 64);
+      const uint32_t ow = __shfl_down(w, s, 64);
+      if ((int)__lane_id() + s < 64 && ow == w) m |= om;
+    }
+    const uint32_t pw = __shfl_up(w, 1, 64);
+    if (act && (__lane_id() == 0 || pw != w)) atomicOr(&bits[w], m);   // the run's first lane
+  }
+}
+__global__ void k_rank_popc(const uint64_t* bits, uint64_t nw, uint32_t* pc) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x)
+    pc[i] = (uint32_t)__popcll(bits[i]);
+}
+
 void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
   const uint32_t nt = (uint32_t)idx.n_types;
   P.dir.assign(nt, nullptr);
@@ -1226,6 +1251,9 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
   P.bdir.assign(nt, nullptr);
   P.bshift.assign(nt, 0);
   P.bn.assign(nt, 0);
+  P.rbits.assign(nt, nullptr);
+  P.rpre.assign(nt, nullptr);
+  P.rklo.assign(nt, 0);
   if (!P.nkeys || !nt || P.nkeys >= 0xFFFFFFFFull) return;
   DBuf<uint64_t> kb(4ull * nt, s);
   hipLaunchKernelGGL(k_type_key_bounds, dim3((nt + 63) / 64), dim3(64), 0, s, (const uint64_t*)P.ukey, P.nkeys, nt,
@@ -1260,6 +1288,32 @@ void build_key_dir(PosIndex& P, Index& idx, hipStream_t s) {
       P.bshift[ty] = shift;
       P.bn[ty] = nb;
       P.dir_lo[ty] = (uint32_t)tmin;
+      continue;
+    }
+    // large spans: the rank directory (DAS_KEY_RANK=0: dense, A/B; =1 at any span)
+    const char* rk = std::getenv("DAS_KEY_RANK");
+    if (rk && rk[0] == '1' ? true : span >= (1ull << 20) && !(rk && rk[0] == '0')) {
+      const uint64_t nw = (span + 63) / 64;
+      uint64_t* rb = dalloc<uint64_t>(idx, nw);
+      uint32_t* rp = dalloc<uint32_t>(idx, nw + 1);
+      fill_dev(rb, 0, 8 * nw, s);
+      {
+        KScope ks("k_rank_bits", 8.0 * (khi - klo) + 8.0 * nw);
+        hipLaunchKernelGGL(k_rank_bits, dim3(grid_for(khi - klo, 256, 8192)), dim3(256), 0, s,
+                           (const uint64_t*)P.ukey, klo, khi - klo, (uint32_t)tmin, (unsigned long long*)rb);
+      }
+      {
+        DBuf<uint32_t> pc(nw, s);
+        KScope ks("k_rank_popc", 12.0 * nw);
+        hipLaunchKernelGGL(k_rank_popc, dim3(grid_for(nw, 256, 8192)), dim3(256), 0, s, (const uint64_t*)rb, nw, pc.p);
+        exclusive_scan<uint32_t>(pc.p, nw, rp, s);
+      }
+      DAS_HIP(hipGetLastError());
+      P.rbits[ty] = rb;
+      P.rpre[ty] = rp;
+      P.rklo[ty] = klo;
+      P.dir_lo[ty] = (uint32_t)tmin;
+      P.dir_n[ty] = (uint32_t)span;
       continue;
     }
     uint32_t* d = dalloc<uint32_t>(idx, span);

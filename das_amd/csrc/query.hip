@@ -2627,12 +2627,24 @@ struct IjKeys {
   int fixed;
   const uint32_t* bdir; // bucket directory (no dense one): keys of bucket (t - dlo) >> bshift
   uint32_t bshift, bn;
+  const uint64_t* rbits; // rank directory (in place of a dense one over dn ids): bits, word prefixes
+  const uint32_t* rpre;
+  uint64_t rklo;
 };
 
 // Index in ukey of key (type, t) through the dense directory (one load), the
 // bucket directory (two adjacent loads + a search of ~2 keys) or a binary
 // search over every key; false if absent.
 __device__ __forceinline__ bool ij_key_index(uint32_t t, const IjKeys& kx, uint64_t& lo) {
+  if (kx.rbits) {
+    const uint32_t d = t - kx.dlo;
+    if (d >= kx.dn) return false;
+    const uint64_t w = kx.rbits[d >> 6];          // the word and its prefix: two independent loads
+    const uint32_t p = kx.rpre[d >> 6];
+    const uint64_t below = w & ((1ull << (d & 63)) - 1ull);
+    lo = kx.rklo + p + (uint64_t)__popcll(below);
+    return (w >> (d & 63)) & 1ull;
+  }
   if (kx.dir) {
     const uint32_t d = t - kx.dlo;
     const uint32_t j = d < kx.dn ? kx.dir[d] : 0xFFFFFFFFu;
@@ -2959,13 +2971,16 @@ int colof_t(const Table& t, int32_t v) {
 
 IjKeys ij_keys(const PosIndex& PI, uint32_t type_id) {
   static const bool no_dir = std::getenv("DAS_NO_KEY_DIR") != nullptr;
-  const bool use_dir = type_id < PI.dir.size() && PI.dir[type_id] && !no_dir;
-  const bool use_bdir = !use_dir && type_id < PI.bdir.size() && PI.bdir[type_id] && !no_dir;
+  const bool use_rank = type_id < PI.rbits.size() && PI.rbits[type_id] && !no_dir;
+  const bool use_dir = !use_rank && type_id < PI.dir.size() && PI.dir[type_id] && !no_dir;
+  const bool use_bdir = !use_rank && !use_dir && type_id < PI.bdir.size() && PI.bdir[type_id] && !no_dir;
   return IjKeys{(uint64_t)type_id << 32, (const uint64_t*)PI.ukey, (const uint64_t*)PI.uoff, PI.nkeys,
-                use_dir ? PI.dir[type_id] : nullptr, use_dir || use_bdir ? PI.dir_lo[type_id] : 0u,
-                use_dir ? PI.dir_n[type_id] : 0u, 0u, 0u, 0,
+                use_dir ? PI.dir[type_id] : nullptr, use_dir || use_bdir || use_rank ? PI.dir_lo[type_id] : 0u,
+                use_dir || use_rank ? PI.dir_n[type_id] : 0u, 0u, 0u, 0,
                 use_bdir ? PI.bdir[type_id] : nullptr, use_bdir ? PI.bshift[type_id] : 0u,
-                use_bdir ? PI.bn[type_id] : 0u};
+                use_bdir ? PI.bn[type_id] : 0u,
+                use_rank ? (const uint64_t*)PI.rbits[type_id] : nullptr,
+                use_rank ? (const uint32_t*)PI.rpre[type_id] : nullptr, use_rank ? PI.rklo[type_id] : 0ull};
 }
 
 // Anti index join of A by a Not(Link) term, resolved on the host.

@@ -962,7 +962,7 @@ def test_gpu_keyspace_export_matches_oracle(gen, tmp_path):
 
 # ------------------------------------------------------------ index join
 
-@pytest.mark.parametrize("mode", ["1", "1-bsearch", "1-ranged", "0", "rev"])
+@pytest.mark.parametrize("mode", ["1", "1-bsearch", "1-ranged", "1-rank", "0", "rev"])
 @pytest.mark.parametrize("gen", ["bio", "powerlaw", "flybase"])
 def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
     """And with das_index_join forced on every eligible term (1: keys found
@@ -973,10 +973,13 @@ def test_gpu_index_join_forced_matches_oracle(gen, mode, monkeypatch):
     1-ranged: grounded-key terms searched within the (type, t_q = v) rows of
     P_{a,q} (ranged mode) wherever the shape allows it; the other modes
     never take it.  rev: unfused, an And's second Link term index-joined
-    into the first term's index at every size (DAS_REV_IJ=1)."""
+    into the first term's index at every size (DAS_REV_IJ=1).  1-rank: keys
+    found through the rank directory (bit per id + word prefixes) at every
+    key span (DAS_KEY_RANK=1; by default only spans of >= 2^20 ids)."""
     import bench
     from das_amd import synthetic
     monkeypatch.setenv("DAS_INDEX_JOIN", "" if mode == "rev" else mode[0])
+    monkeypatch.setenv("DAS_KEY_RANK", "1" if mode == "1-rank" else "")
     monkeypatch.setenv("DAS_REV_IJ", "1" if mode == "rev" else "")
     if mode == "rev":
         monkeypatch.setenv("DAS_FUSED", "0")
