@@ -3857,17 +3857,20 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
                              res->data, ctrp, ps.p, ps.seq);
           DAS_HIP(hipGetLastError());
         }
+        if (reuse) {
+          // queued right behind the union (it reads the row count on the
+          // device), so its launch overlaps the union instead of following
+          // the read-back
+          hipLaunchKernelGGL(k_union_clear, dim3(1), dim3(1024), 0, c.s, (const uint32_t*)res->data, ctrp, ulo[0],
+                             range, bitsp);
+          DAS_HIP(hipGetLastError());
+        }
         uint32_t n = 0;
         try {
           pub_wait(ps, c.s, &n, 1);
         } catch (...) {
           c.zbits.release();
           throw;
-        }
-        if (reuse) {
-          hipLaunchKernelGGL(k_union_clear, dim3(1), dim3(1024), 0, c.s, (const uint32_t*)res->data, ctrp, ulo[0],
-                             range, bitsp);
-          DAS_HIP(hipGetLastError());
         }
         if (n != 0xFFFFFFFFu) {
           out.reset();
