@@ -178,9 +178,6 @@ struct Ctx {
   // (lo, cnt) descriptor array of the sparse direct-join build, all-zero
   // between joins (direct_join clears the slots it wrote)
   DBuf<uint2> zlc;
-  // bitmap + counters of the one-launch Or union (k_union_first), all-zero
-  // between unions (k_union_clear)
-  DBuf<uint32_t> zbits;
   // loader-side host copies kept for metadata calls
   std::vector<uint8_t> leaf_bytes;
   std::vector<uint64_t> leaf_off;

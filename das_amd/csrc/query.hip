@@ -271,24 +271,6 @@ __global__ void __launch_bounds__(B) k_union_first(MultiScan ms, uint32_t lo, ui
 }
 
 
-// After k_union_first: the bits it set (one per row it wrote) and its three
-// counters back to zero, so the context's union bitmap stays all-zero
-// between unions (one workgroup, off the query's critical path)
-__global__ void __launch_bounds__(1024) k_union_clear(const uint32_t* __restrict__ out, uint32_t* ctr, uint32_t lo,
-                                                      uint32_t range, uint32_t* bits) {
-  const uint32_t n = ctr[0];
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t d = out[i] - lo;
-    if (d < range) bits[d >> 5] = 0u;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ctr[0] = 0u;
-    ctr[1] = 0u;
-    ctr[2] = 0u;
-  }
-}
-
 __global__ void __launch_bounds__(kSmallBlock) k_scan_small(ScanSpec sp, uint64_t begin, uint64_t end, uint32_t* out,
                                                             uint64_t cap, uint32_t* slot, uint32_t seq) {
   constexpr int W = kSmallBlock / 64;
@@ -3873,25 +3855,13 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
       if (proj && !(fb && fb[0] == '0')) {
         const uint32_t range = uhi[0] - ulo[0] + 1;
         auto res = new_table(c, DAS_TABLE_ORDERED, 1, preps[0].vars, scanned);
-        // the bitmap + 3 counters: the context's all-zero scratch, cleared
-        // again after the union (k_union_clear) instead of two fills on the
-        // query's critical path (DAS_ZLC=0: fresh and filled per union)
+        // (a fresh, filled bitmap per union: a context-level all-zero bitmap
+        // cleared after each union was slower -- the clear of ~10^5 set bits
+        // ran behind the union on the stream, F9 40 -> 53-59 us)
         const uint64_t words = (range + 31) / 32;
-        const char* zf = std::getenv("DAS_ZLC");
-        const bool reuse = !(zf && zf[0] == '0');
-        DBuf<uint32_t> own;
-        uint32_t* bitsp;
-        if (reuse) {
-          if (c.zbits.n < words + 3) {
-            c.zbits.alloc(std::max<uint64_t>(words + 3, 2 * c.zbits.n), c.s);
-            fill_dev(c.zbits.p, 0, 4 * c.zbits.n, c.s);
-          }
-          bitsp = c.zbits.p;
-        } else {
-          own.alloc(words + 3, c.s);
-          fill_dev(own.p, 0, 4 * (words + 3), c.s);
-          bitsp = own.p;
-        }
+        DBuf<uint32_t> own(words + 3, c.s);
+        fill_dev(own.p, 0, 4 * (words + 3), c.s);
+        uint32_t* bitsp = own.p;
         uint32_t* ctrp = bitsp + words;
         const PubSlot ps = pub_reserve();
         {
@@ -3900,21 +3870,8 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
                              res->data, ctrp, ps.p, ps.seq);
           DAS_HIP(hipGetLastError());
         }
-        if (reuse) {
-          // queued right behind the union (it reads the row count on the
-          // device), so its launch overlaps the union instead of following
-          // the read-back
-          hipLaunchKernelGGL(k_union_clear, dim3(1), dim3(1024), 0, c.s, (const uint32_t*)res->data, ctrp, ulo[0],
-                             range, bitsp);
-          DAS_HIP(hipGetLastError());
-        }
         uint32_t n = 0;
-        try {
-          pub_wait(ps, c.s, &n, 1);
-        } catch (...) {
-          c.zbits.release();
-          throw;
-        }
+        pub_wait(ps, c.s, &n, 1);
         if (n != 0xFFFFFFFFu) {
           out.reset();
           matched = n > 0;

@@ -1091,18 +1091,16 @@ def test_gpu_ij_mid_matches_multi_launch(monkeypatch):
             assert same(got, want), (q, got.get("n"), want.get("n"))
 
 
-@pytest.mark.parametrize("bits", ["1", "1-fresh", "0"])
+@pytest.mark.parametrize("bits", ["1", "0"])
 def test_gpu_union_of_scans_matches_oracle(bits, monkeypatch):
     """Or of anchored one-column scans above the fused chain's size (FlyBase
     cell 9's DO-term Or over hot terms: thousands of rows, genes repeated
-    across terms): the one-launch bitmap union (k_union_first, unsorted; its
-    bitmap the context's all-zero scratch, cleared after each union, or a
-    fresh one per union: 1-fresh) and the count / write / hash-dedup path
-    (DAS_UNION_BITS=0) against the oracle; the queries run back to back, twice."""
+    across terms): the one-launch bitmap union (k_union_first, unsorted) and
+    the count / write / hash-dedup path (DAS_UNION_BITS=0) against the
+    oracle; the queries run back to back, twice."""
     import bench
     from das_amd import synthetic
-    monkeypatch.setenv("DAS_UNION_BITS", bits[0])
-    monkeypatch.setenv("DAS_ZLC", "0" if bits.endswith("fresh") else "")
+    monkeypatch.setenv("DAS_UNION_BITS", bits)
     arrays = synthetic.flybase_kb(3000, 5, 500, n_loc=10, n_do=4, seed=9)
     db = _hipdb(arrays)
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
