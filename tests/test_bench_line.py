@@ -42,6 +42,9 @@ def _check(full):
             continue
         for k in LEG_KEYS:
             assert k in got, (w, k)
+        if leg.get("roofline") is None:                 # a latency / DBInterface leg (getlinks)
+            assert got["roofline"] is None
+            continue
         assert got["roofline"]["kernel"] == leg["roofline"]["kernel"]
         assert got["roofline"]["frac"] == leg["roofline"]["frac"]
     return d
@@ -51,6 +54,17 @@ def test_bench_line_from_recorded_full_record():
     full = _recorded()
     assert len(json.dumps(full)) > 8000         # the record that went unparsed in round 3
     _check(full)
+
+
+def test_bench_line_from_round4_detail_record():
+    """A round-4 detail record (the full dict bench.py writes to --detail,
+    getlinks leg, join variants, latency objects included) compacts to a
+    line within the bound that carries the Q2 And-join summary."""
+    with open(os.path.join(ROOT, "profiles", "r4_bench_detail_s23.json")) as f:
+        full = json.load(f)
+    d = _check(full)
+    assert d["and_join_q2"]["kernel"].startswith("k_dj_write") and d["and_join_q2"]["frac"] > 0.5
+    assert "getlinks" in d["workloads"] and d["workloads"]["getlinks"]["unit"] == "queries/s"
 
 
 def test_bench_line_bounded_when_record_grows():
