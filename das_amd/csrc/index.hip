@@ -1713,6 +1713,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   }
 
   // 5. counts per arity, node count
+  uint64_t links_of_arity[kMaxArity + 1] = {};
   {
     DBuf<unsigned long long> h(64, s);
     fill_dev(h.p, 0, 64 * 8, s);
@@ -1722,6 +1723,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     unsigned long long hh[64];
     DAS_HIP(hipMemcpyAsync(hh, h.p, sizeof(hh), hipMemcpyDeviceToHost, s));
     DAS_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i <= kMaxArity; ++i) links_of_arity[i] = hh[i];
     idx.n_nodes = hh[63];
     idx.n_links = 0;
     for (int i = 0; i < 63; ++i) idx.n_links += hh[i];
@@ -1788,6 +1790,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   // 7. per-arity tables
   phase.emplace(c, "phase_tables", 0.0);
   for (uint32_t ar = 1; ar <= (uint32_t)kMaxArity; ++ar) {
+    if (!links_of_arity[ar]) continue;        // no link of this arity (step 5's counts): no flag pass
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), ids;
     if (n_atoms) {
       KScope ks("k_link_flags", 9.0 * n_atoms);
