@@ -124,6 +124,7 @@ _SIGS = {
     "das_table_members": (C.c_int, [P, P]),
     "das_table_set_bounds": (C.c_int, [P, P, P]),
     "das_table_get_bounds": (C.c_int, [P, P, P]),
+    "das_table_checksum": (C.c_int, [P, P, P, P]),
     "das_table_info": (C.c_int, [P, P, P, P, P]),
     "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
@@ -348,6 +349,14 @@ class Table:
         if n and k:
             check(lib().das_table_fetch(self.ctx.h, self.h, row0, n, ptr(out)), self.ctx.h)
         return out
+
+    def checksum(self, salts):
+        """(sum, bad) of das_table_checksum with one 64-bit salt per column."""
+        s = np.asarray([int(x) & ((1 << 64) - 1) for x in salts], dtype=np.uint64)
+        assert len(s) == len(self.vars)
+        out = np.zeros(2, dtype=np.uint64)
+        check(lib().das_table_checksum(self.ctx.h, self.h, ptr(s), ptr(out)), self.ctx.h)
+        return int(out[0]), int(out[1])
 
     def free(self):
         if self.h is not None:

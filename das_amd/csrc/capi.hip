@@ -196,6 +196,7 @@ int das_ctx_destroy(das_ctx_t* ctx) {
     for (hipEvent_t e : ctx->c.ev_pool) (void)hipEventDestroy(e);
     ctx->c.ev_pool.clear();
     das::free_index(ctx->c.idx);
+    ctx->c.zlc.release();                 // back to the cache while the stream still exists
     das::cache_release_stream(ctx->c.s);
     if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
   });
@@ -646,6 +647,13 @@ int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi)
     t->t.hi[c] = hi ? hi[c] : 0xFFFFFFFFu;
   }
   return DAS_OK;
+}
+
+int das_table_checksum(das_ctx_t* ctx, const das_table_t* t, const uint64_t* salt, uint64_t out[2]) {
+  return guarded(ctx, [&] {
+    DAS_CHECK(t && salt && out, das::DAS_E_INVALID, "null argument");
+    das::table_checksum(ctx->c, t->t, salt, out);
+  });
 }
 
 int das_table_get_bounds(const das_table_t* t, uint32_t* lo, uint32_t* hi) {

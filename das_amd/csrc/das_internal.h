@@ -304,6 +304,10 @@ inline std::unique_ptr<Table> new_table_like(Ctx& c, const Table& a, uint64_t ca
 std::unique_ptr<Table> partition(Ctx& c, const Table& t, const int32_t* key_vars, uint32_t nkey, uint32_t nparts,
                                  uint64_t* counts);
 void export_rows(Ctx& c, const Table& t, uint32_t* dst);
+// Order-independent checksum of an ordered table (checksum.hip): out[0] = sum
+// over rows of the product over columns of g(salt[c], digest), out[1] = values
+// that are not atom ids.
+void table_checksum(Ctx& c, const Table& t, const uint64_t* salt, uint64_t out[2]);
 std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
                                    const uint32_t* src, uint64_t n);
 

@@ -811,6 +811,11 @@ __device__ __forceinline__ int owner_of_round(uint32_t ob, uint32_t pre, uint32_
 #define DAS_DJ_UNROLL 4
 #endif
 constexpr int kXUnroll = DAS_DJ_UNROLL;
+// the 16-byte run and quad paths move one block of 4 outputs per lane (256 per
+// wave) whatever the rounds' unroll is: their guard, advance and LDS row size
+constexpr int kVecBlock = 256;
+// largest descriptor array (slots) the context keeps zeroed between sparse joins
+constexpr uint64_t kZlcMax = 1ull << 26;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-byte load
 
@@ -844,12 +849,12 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
   // rows take the quad path below (not with DAS_DJ_VEC=1, search bit 2).
   // Needs 16-byte aligned output positions: a head of up to 3 outputs goes
   // through the rounds first.  `row`: the wave's 256-entry LDS row.
-  const bool runs = fast && !(search & 2) && (re - rs) > (T)(64 * kXUnroll);
+  const bool runs = fast && !(search & 2) && (re - rs) > (T)kVecBlock;
   const uint32_t exp = ex - (uint32_t)pre;
   const T head = runs ? (T)((4u - ((uint32_t)(obase + rs) & 3u)) & 3u) : (T)0;
   for (T o0 = rs; o0 < re;) {
     const T lim = (head && o0 == rs) ? rs + head : re;
-    if (runs && lim == re && (re - o0) >= (T)(64 * kXUnroll)) {
+    if (runs && lim == re && (re - o0) >= (T)kVecBlock) {
       const uint64_t m0 = __ballot((uint32_t)pre <= (uint32_t)o0);
       const int l0 = 63 - __clzll((long long)m0);
       const uint64_t m1 = __ballot((uint32_t)pre <= (uint32_t)o0 + 255u);
@@ -869,7 +874,7 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i) store16<NT>(bo[i] + op, bv4[i]);
-        o0 += (T)(64 * kXUnroll);
+        o0 += (T)kVecBlock;
         continue;
       }
       if (!(search & 4)) {
@@ -915,7 +920,7 @@ __device__ __forceinline__ void expand_group(T rs, T re, T pre, uint32_t cnt, ui
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i) store16<NT>(bo[i] + op, bq[i]);
-        o0 += (T)(64 * kXUnroll);
+        o0 += (T)kVecBlock;
         continue;
       }
     }
@@ -1030,7 +1035,7 @@ __global__ void __launch_bounds__(B) k_dj_write(const uint32_t* __restrict__ pke
                                                 uint32_t range, const uint2* __restrict__ lc, uint64_t units,
                                                 const uint64_t* __restrict__ unit_off, JoinCols jc,
                                                 uint32_t* __restrict__ out, uint64_t cap) {
-  __shared__ uint32_t s_row[B / 64][256];                   // the wave's LDS row (owner_of_round, quad path)
+  __shared__ uint32_t s_row[B / 64][kVecBlock];             // the wave's LDS row (owner_of_round, quad path)
   uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
@@ -1095,7 +1100,7 @@ __global__ void __launch_bounds__(B) k_dj_write_bal(const uint32_t* __restrict__
   for (int i = 0; i < NP; ++i) { pp[i] = jc.p[i]; po[i] = out + (uint64_t)jc.po[i] * cap; }
 #pragma unroll
   for (int i = 0; i < NB; ++i) { bb[i] = jc.b[i]; bo[i] = out + (uint64_t)jc.bo[i] * cap; }
-  __shared__ uint32_t s_row[B / 64][256];                   // the wave's LDS row (owner_of_round, quad path)
+  __shared__ uint32_t s_row[B / 64][kVecBlock];             // the wave's LDS row (owner_of_round, quad path)
   uint32_t* row = s_row[threadIdx.x >> 6];
   const uint64_t chunks = (total + chunk - 1) / chunk;
   for (uint64_t w = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < chunks; w += waves) {
@@ -2539,17 +2544,31 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     // fresh array filled per join, A/B)
     const bool srt = Q.sorted_col == qk;
     const char* zf = std::getenv("DAS_ZLC");
-    const bool reuse = !(zf && zf[0] == '0');
+    // the context keeps the zeroed array for ranges up to 2^26 slots (512 MB);
+    // a wider range takes a fresh array filled for this join
+    const bool reuse = !(zf && zf[0] == '0') && range + 1 <= kZlcMax;
+    // from the first slot write until the build's own slots are cleared
+    // again, any unwind (an allocation or launch failure, an expansion
+    // throwing) leaves slots set: the guard drops the context's array, so the
+    // next join starts from a fresh one
+    struct ZlcGuard {
+      Ctx& c;
+      bool armed;
+      ~ZlcGuard() {
+        if (armed) c.zlc.release();
+      }
+    } zg{c, false};
     uint2* lcp = nullptr;
     {
       const bool fresh = !reuse || c.zlc.n < range + 1;
       ProfScope ps(c, "join_build", (srt ? 4.0 : 8.0 + 8.0 * Q.ncols) * Q.nrows + (fresh ? 8.0 * range : 0.0));
       if (reuse) {
         if (c.zlc.n < range + 1) {
-          c.zlc.alloc(std::max<uint64_t>(range + 1, 2 * c.zlc.n), c.s);
+          c.zlc.alloc(std::min<uint64_t>(std::max<uint64_t>(range + 1, 2 * c.zlc.n), kZlcMax), c.s);
           fill_dev(c.zlc.p, 0, 8 * c.zlc.n, c.s);
         }
         lcp = c.zlc.p;
+        zg.armed = true;
       } else {
         lc.alloc(range + 1, c.s);
         fill_dev(lc.p, 0, 8 * (range + 1), c.s);
@@ -2570,15 +2589,12 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
       DAS_HIP(hipGetLastError());
     }
     if (!reuse) return expand(*Qb, lcp);
-    std::unique_ptr<Table> out;
-    try {
-      out = expand(*Qb, lcp);
-    } catch (...) {
-      c.zlc.release();              // slots possibly left set: the next join starts from a fresh array
-      throw;
-    }
+    if (const char* t = std::getenv("DAS_TEST_ZLC_THROW"); t && t[0] == '1')   // tests: an unwind mid-join
+      DAS_CHECK(false, DAS_E_INTERNAL, "DAS_TEST_ZLC_THROW");
+    std::unique_ptr<Table> out = expand(*Qb, lcp);
     hipLaunchKernelGGL(k_lc_clear, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lcp);
     DAS_HIP(hipGetLastError());
+    zg.armed = false;
     return out;
   }
   lc.alloc(range + 1, c.s);
@@ -3851,7 +3867,7 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
         ms1.seg[i].chunk0 = blocks;
         blocks += (ms1.seg[i].end - ms1.seg[i].begin + B - 1) / B;
       }
-      proj = proj && blocks < (1ull << 31);
+      proj = proj && blocks < (1ull << 32) / B;                 // the dispatch grid counts work-items in 32 bits
       if (proj && !(fb && fb[0] == '0')) {
         const uint32_t range = uhi[0] - ulo[0] + 1;
         auto res = new_table(c, DAS_TABLE_ORDERED, 1, preps[0].vars, scanned);

@@ -277,6 +277,13 @@ int das_table_column(const das_table_t* t, int32_t c, uint32_t** dptr);
  * it (values outside are dropped by the build).  Scan and join results carry
  * bounds derived from the index, so callers only set them on imported tables. */
 int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi);
+/* Order-independent checksum of an ORDERED table under the reference's set
+ * identity (pattern_matcher.py:41-51, 741-748), for parity checks at sizes no
+ * host copy of the rows fits: out[0] = sum over rows of prod over columns c of
+ * (splitmix64(d64(value) ^ salt[c]) | 1) mod 2^64, d64 = the value's first 8
+ * digest bytes little-endian, salt[c] = the caller's key of column c's
+ * variable name; out[1] = values that are not atom ids (0 for a valid table). */
+int das_table_checksum(das_ctx_t* ctx, const das_table_t* t, const uint64_t* salt, uint64_t out[2]);
 /* The declared / derived inclusive bounds per column ([0, DAS_NONE] = unknown). */
 int das_table_get_bounds(const das_table_t* t, uint32_t* lo, uint32_t* hi);
 /* Member id per column: -1 ordered, m = unordered member m (DAS_TABLE_COMPOSITE;

@@ -2,9 +2,15 @@
 the bench workloads' binding counts (config 2 bio at 20 M Member links,
 config 5 hub at 10^9 links generated in HBM) against closed-form counts (numpy / torch)
 from the generator's own arrays (distinct-pair joins as degree sums), so a
-wrong row anywhere in a 10^7-10^8-row join changes the count."""
+wrong row anywhere in a 10^7-10^8-row join changes the count -- and, next to
+every count, an order-independent checksum of the answer's rows
+(tests/checksum.py: das_table_checksum on the device against the same
+function's closed form over the generator's arrays), so a wrong answer with
+the right count fails too (pattern_matcher.py:41-51, 741-748)."""
 import numpy as np
 import pytest
+
+from tests import checksum as CK
 
 pytestmark = pytest.mark.gpu
 
@@ -26,11 +32,19 @@ def _pairs(arrays, type_name):
 
 
 def _count(db, spec):
+    """(rows, checksum) of the device answer."""
     import bench
     from das_amd.pattern_matcher import pattern_matcher as pm
     ans = pm.PatternMatchingAnswer()
     bench.build_expr(pm, spec).matched(db, ans)
-    return ans.count()
+    ck, rows = CK.answer_checksum(ans)
+    assert rows == ans.count()
+    return rows, ck
+
+
+def _leaf_d64(arrays, n):
+    """d64 (tests/checksum.py) of leaves 0 .. n-1 by hashlib over their strings."""
+    return np.array([CK.d64_text(arrays.leaf_string(i)) for i in range(n)], dtype=np.uint64)
 
 
 def test_gpu_bio_fullsize_counts(monkeypatch):
@@ -55,34 +69,51 @@ def test_gpu_bio_fullsize_counts(monkeypatch):
     nl = base + n_genes + n_bps + 10_000                # every node index below the Concept blocks
     gdeg = np.bincount(mg, minlength=nl)
     outdeg = np.bincount(inh >> 32, minlength=nl)
+    D = _leaf_d64(arrays, arrays.n_leaf)
+    G = lambda v, x: CK.g_np(v, D[x])  # noqa: E731
+    gsum = lambda k, v, n=nl: CK.group_sum_np(k, v, n)  # noqa: E731
+    in_nl = mb < nl
+    s_inh = gsum(inh >> 32, G("V_p", inh & 0xFFFFFFFF))               # per V_bp: sum over its parents
+    s_mem = gsum(mb[in_nl], G("V_g", mg[in_nl]))                      # per V_bp: sum over its genes
+    both = np.flatnonzero((s_inh != 0) | (s_mem != 0))
+    inter = np.intersect1d(mb[mg == base + ga], mb[mg == base + gb])
+    s0 = np.zeros(nl, dtype=bool)
+    s0[mg[mb == bp0]] = True
+    q4 = s0[mg] & in_nl
     want = {
-        "Q1 Member(Vg,Vbp)": len(m),
-        "Q2 Member*Inheritance": int(outdeg[mb[mb < nl]].sum()),
-        "Q3 same_biological_process (QUERY_1)": len(np.intersect1d(mb[mg == base + ga], mb[mg == base + gb])),
-        "Q4 hub join": int(gdeg[mg[mb == bp0]].sum()),
+        "Q1 Member(Vg,Vbp)": (len(m), CK.sum_np(CK.prod_np(G("V_g", mg), G("V_bp", mb)))),
+        "Q2 Member*Inheritance": (int(outdeg[mb[in_nl]].sum()),
+                                  CK.sum_np(CK.prod_np(s_mem[both], G("V_bp", both), s_inh[both]))),
+        "Q3 same_biological_process (QUERY_1)": (len(inter), CK.sum_np(G("V_BiologicalProcess", inter))),
+        "Q4 hub join": (int(gdeg[mg[mb == bp0]].sum()), CK.sum_np(CK.prod_np(G("V_g", mg[q4]), G("V_bp", mb[q4])))),
     }
-    want.update(_query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh))
+    want.update(_query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, D=D))
     for name, spec in specs.items():
         assert _count(db, spec) == want[name], name
-    # QUERY_2 / QUERY_3 through the per-operator fold as well (same counts)
+    # QUERY_2 / QUERY_3 through the per-operator fold as well (same answers)
     monkeypatch.setenv("DAS_PLAN", "0")
     for name in ("Q5 same_or_inherited_biological_process (QUERY_2)", "Q6 linked_reactome_uniprot (QUERY_3)"):
         assert _count(db, specs[name]) == want[name], name
 
 
-def _query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, n_up=5000, n_r=1000, n_loc=40):
+def _query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, n_up=5000, n_r=1000, n_loc=40, D=None):
     """Closed forms of scripts/benchmark.py QUERY_2 / QUERY_3 (bench Q5 / Q6)
     over the generator's distinct link pairs, following the reference fold
-    (pattern_matcher.py:491-500, 644-687, 705-748).  The anchors' intermediate
-    results are asserted non-empty, so reset-on-empty never applies."""
+    (pattern_matcher.py:491-500, 644-687, 705-748): (rows, checksum) per
+    query.  The anchors' intermediate results are asserted non-empty, so
+    reset-on-empty never applies.  D: d64 per leaf (_leaf_d64)."""
     from das_amd import synthetic
     _, off = synthetic.bio_nodes(n_genes, n_bps, n_up, n_r, n_loc)
     rng_of = lambda k, n: (base + off[k], base + off[k] + n)  # noqa: E731
     inside = lambda x, r: (x >= r[0]) & (x < r[1])  # noqa: E731
-    G, BP = rng_of("g", n_genes), rng_of("bp", n_bps)
+    G_, BP = rng_of("g", n_genes), rng_of("bp", n_bps)
     UP, R = rng_of("up", n_up), rng_of("r", n_r)
     concept = [rng_of(k, n) for k, n in (("upname", n_up), ("rname", n_r), ("loc", n_loc))]
     is_concept = lambda x: np.logical_or.reduce([inside(x, r) for r in concept])  # noqa: E731
+    nl = arrays.n_leaf
+    if D is None:
+        D = _leaf_d64(arrays, nl)
+    G = lambda v, x: CK.g_np(v, D[np.asarray(x, dtype=np.int64)])  # noqa: E731
     mg, mb = m >> 32, m & 0xFFFFFFFF
     A = set(mb[mg == base + ga].tolist())                  # Member(ga, V1)
     B = set(mb[mg == base + gb].tolist())                  # Member(gb, V2)
@@ -96,18 +127,33 @@ def _query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, n_up=5000, n_r
     inner1 = [(c, p) for c, p in zip(ic.tolist(), ip.tolist()) if c in B]         # (V2, V3)
     assert A and B and inner1
     inner = {(v1, v2, v3) for v2, v3 in inner1 for v1 in by_parent[v3]}          # (V1, V2, V3)
-    q2 = sum(1 for v1, _, _ in inner if v1 in A) + len(A & B)
+    rows3 = np.array(sorted(r for r in inner if r[0] in A), dtype=np.int64).reshape(-1, 3)
+    ab = np.array(sorted(A & B), dtype=np.int64)
+    ck2 = (CK.sum_np(CK.prod_np(G("V1_BiologicalProcess", rows3[:, 0]), G("V2_BiologicalProcess", rows3[:, 1]),
+                                G("V3_BiologicalProcess", rows3[:, 2])))
+           + CK.sum_np(G("V1_BiologicalProcess", ab))) & CK.M64
+    q2 = len(rows3) + len(ab)
     # QUERY_3: same_bp x MemberT(Up, BP) x ListT(Up, .) x ListT(Up, .) x ListT(Reactome, Concept)
     S = A & B
     up = m[inside(mg, UP) & inside(mb, BP)]
-    ups = (up >> 32)[np.isin(up & 0xFFFFFFFF, np.array(sorted(S), dtype=np.int64))]
+    up = up[np.isin(up & 0xFFFFFFFF, np.array(sorted(S), dtype=np.int64))]
+    ups, upb = up >> 32, up & 0xFFFFFFFF
     lst = _pairs(arrays, "List")
     la, lb = lst >> 32, lst & 0xFFFFFFFF
-    nl_up = np.bincount(la[inside(la, UP) & is_concept(lb)], minlength=int(UP[1]))
+    lu = inside(la, UP) & is_concept(lb)
+    nl_up = np.bincount(la[lu], minlength=int(UP[1]))
     j = int((nl_up[ups] ** 2).sum())
-    lr = int((inside(la, R) & is_concept(lb)).sum())
-    assert S and len(ups) and j and lr
-    return {"Q5 same_or_inherited_biological_process (QUERY_2)": q2, "Q6 linked_reactome_uniprot (QUERY_3)": j * lr}
+    lr = inside(la, R) & is_concept(lb)
+    assert S and len(ups) and j and lr.sum()
+    # rows (bp, up, c1, c2, r, c3): per (up, bp) the List sums of V_UniprotName
+    # and V_Location over up's Concept lists, times the Reactome lists' sum
+    sn = CK.group_sum_np(la[lu], G("V_UniprotName", lb[lu]), nl)
+    sl = CK.group_sum_np(la[lu], G("V_Location", lb[lu]), nl)
+    left = CK.sum_np(CK.prod_np(G("V_BiologicalProcess", upb), G("V_Uniprot", ups), sn[ups], sl[ups]))
+    right = CK.sum_np(CK.prod_np(G("V_Reactome", la[lr]), G("V_ReactomeName", lb[lr])))
+    ck3 = int(CK.prod_np(np.uint64(left), np.uint64(right)))
+    return {"Q5 same_or_inherited_biological_process (QUERY_2)": (q2, ck2),
+            "Q6 linked_reactome_uniprot (QUERY_3)": (j * int(lr.sum()), ck3)}
 
 
 def _dev_pairs(arrays, k):
@@ -162,13 +208,39 @@ def test_gpu_hub_fullsize_counts(kb1g):
     s1 = member(0, h0)
     s23 = member(2, h1) & member(3, h0)
     in1 = s1[src[1]]
+    keep4 = in1 & s23[dst[1]]
+    D = _dev_leaf_d64(db, arrays)
+    ck = lambda sel: CK.sum_torch(CK.g_torch("V1", D[src[1][sel]]) * CK.g_torch("V2", D[dst[1][sel]]))  # noqa: E731
     want = {
-        "H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)": int((in1 & s23[dst[1]]).sum()),
-        "H2 T0(V1,h0) T1(V1,V2)": int(in1.sum()),
+        "H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)": (int(keep4.sum()), ck(keep4)),
+        "H2 T0(V1,h0) T1(V1,V2)": (int(in1.sum()), ck(in1)),
     }
-    assert want["H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)"] > 10_000_000
+    assert want["H4 T0(V1,h0) T1(V1,V2) T2(V2,h1) T3(V2,h0)"][0] > 10_000_000
+    del pairs, src, dst, s1, s23, in1, keep4
     for name, spec in bench.hub_specs():
         assert _count(db, spec) == want[name], name
+
+
+def _dev_leaf_d64(db, arrays):
+    """d64 (tests/checksum.py) of every leaf of a device-generated KB: the
+    leaf strings hashed on the GPU (das_hash_strings_dev, the MD5 kernel
+    test_gpu_md5_kernel_matches_hashlib pins), 1000 sampled against hashlib."""
+    import torch
+    from das_amd import _lib
+    n = int(arrays.n_leaf)
+    dev = torch.device("cuda:0")
+    b = torch.from_numpy(np.asarray(arrays.leaf_bytes, dtype=np.uint8)).to(dev)
+    o = torch.from_numpy(np.asarray(arrays.leaf_off).view(np.int64)).to(dev)
+    words = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    _lib.check(_lib.lib().das_hash_strings_dev(db.ctx.h, b.data_ptr(), o.data_ptr(), n, words.data_ptr()), db.ctx.h)
+    torch.cuda.synchronize()
+    del b, o
+    D = CK.d64_from_words_torch(words)
+    del words
+    for i in np.random.default_rng(5).integers(0, n, 1000).tolist() + [0, n - 1]:
+        assert (int(D[i]) & CK.M64) == CK.d64_text(arrays.leaf_string(i)), i
+    return D
 
 
 def test_gpu_build_fullsize_incoming_sets(kb1g):
@@ -234,9 +306,19 @@ def _flybase_counts(arrays, gene, do_terms):
     one gene anchor, from the generator's distinct Execution rows: And folds
     as joins (pattern_matcher.py:705-748; every running result is asserted
     non-empty, so reset-on-empty never applies), Not as the anti-join of
-    check_negation, Or as a union of distinct bindings."""
-    names = {s: i for i, s in enumerate(arrays.leaf_strings())}
+    check_negation, Or as a union of distinct bindings.  (rows, checksum)
+    per query; the checksum's per-key sums follow the same loops."""
+    strs = arrays.leaf_strings()
+    names = {s: i for i, s in enumerate(strs)}
     leaf = lambda t, n: names[f"{t} {n}"]  # noqa: E731
+    d64 = {}
+
+    def G(v, x):
+        d = d64.get(x)
+        if d is None:
+            d = d64[x] = CK.d64_text(strs[x])
+        return CK.g(v, d)
+    M = CK.M64
     rows = _exec_rows(arrays)
     s = lambda n: leaf("Schema", "Schema:" + n)  # noqa: E731
     tab = {k: np.unique(rows[rows[:, 0] == s(n)][:, 1:], axis=0) for k, n in (
@@ -250,22 +332,54 @@ def _flybase_counts(arrays, gene, do_terms):
             d.setdefault((a, b)[col], []).append((a, b)[1 - col])
         return d
     rec_by_val, uniq_by_val = by("rec", 1), by("uniq", 1)
+    # per v2: (number of uniquename keys v with value v2, sum of g(var, v))
+    u_sum = {}
+
+    def uniq_of(v2, var):
+        k = (v2, var)
+        if k not in u_sum:
+            us = uniq_by_val.get(v2, ())
+            u_sum[k] = (len(us), sum(G(var, u) for u in us) & M)
+        return u_sum[k]
     out = {}
     for name, t in (("F5 same recombination_loc", "rec"), ("F6 same cytogenetic_loc", "cyto")):
         r1 = set(tab[t][tab[t][:, 0] == fb][:, 1].tolist())
         t_by_val = by(t, 1)
         assert r1
-        out[name] = sum(len(uniq_by_val.get(v2, ())) for v1 in r1 for v2 in t_by_val.get(v1, ()))
+        n = ck = 0
+        for v1 in r1:
+            for v2 in t_by_val.get(v1, ()):
+                c, su = uniq_of(v2, "v3")
+                n += c
+                ck = (ck + G("v1", v1) * G("v2", v2) * su) & M
+        out[name] = (n, ck)
     r1 = set(tab["rec"][tab["rec"][:, 0] == fb][:, 1].tolist())
     c_fb = set(tab["cyto"][tab["cyto"][:, 0] == fb][:, 1].tolist())
     cyto = set(map(tuple, tab["cyto"].tolist()))
-    out["F7 same recomb, different cyto"] = sum(
-        len(uniq_by_val.get(v2, ())) * sum(1 for v3 in c_fb if (v2, v3) not in cyto)
-        for v1 in r1 for v2 in rec_by_val.get(v1, ()))
+    n = ck = 0
+    for v1 in r1:
+        for v2 in rec_by_val.get(v1, ()):
+            c, su = uniq_of(v2, "v4")
+            v3s = [v3 for v3 in c_fb if (v2, v3) not in cyto]
+            n += c * len(v3s)
+            s3 = sum(G("v3", v3) for v3 in v3s) & M
+            ck = (ck + G("v1", v1) * G("v2", v2) * s3 * su) & M
+    out["F7 same recomb, different cyto"] = (n, ck)
     terms = [leaf("Verbatim", d) for d in (do_terms or ["DOID:0"]) if f"Verbatim {d}" in names]
-    out["F9 DO-term Or"] = len(set(tab["do"][np.isin(tab["do"][:, 1], terms)][:, 0].tolist()))
+    v1s = set(tab["do"][np.isin(tab["do"][:, 1], terms)][:, 0].tolist())
+    out["F9 DO-term Or"] = (len(v1s), sum(G("v1", v) for v in v1s) & M)
     rec_by_key = by("rec", 0)
-    out["FJ uniquename x recombination_loc"] = sum(len(rec_by_key.get(v2, ())) for _, v2 in tab["uniq"].tolist())
+    r_sum = {}
+    n = ck = 0
+    for v3, v2 in tab["uniq"].tolist():
+        vs = rec_by_key.get(v2, ())
+        if not vs:
+            continue
+        if v2 not in r_sum:
+            r_sum[v2] = sum(G("v1", v) for v in vs) & M
+        n += len(vs)
+        ck = (ck + G("v3", v3) * G("v2", v2) * r_sum[v2]) & M
+    out["FJ uniquename x recombination_loc"] = (n, ck)
     return out
 
 

@@ -651,7 +651,9 @@ def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
     context's descriptor array and clears them after the expansion (DAS_ZLC=1,
     default; 0: a fresh array per join): five joins in a row on one context,
     over overlapping and growing key ranges (build keys in sorted order or
-    not), each against a numpy join with multiplicities."""
+    not), each against a numpy join with multiplicities.  With the reused array, a
+    join that unwinds between writing its slots and clearing them
+    (DAS_TEST_ZLC_THROW) must not leave them for the next join (advisor r4)."""
     monkeypatch.setenv("DAS_DJ_BUILD", "sparse")
     monkeypatch.setenv("DAS_ZLC", zlc)
     from das_amd import _lib, synthetic
@@ -669,6 +671,11 @@ def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
         Q = db.ctx.table_from_host(_lib.TABLE_ORDERED, [1, 2], np.stack([qk.astype(np.uint32), qb]))
         P.set_bounds([0, 0], [(1 << 20) - 1, nk])
         Q.set_bounds([0, 0], [nk, (1 << 20) - 1])
+        if zlc == "1" and nk == 90000 and not srt:
+            monkeypatch.setenv("DAS_TEST_ZLC_THROW", "1")
+            with pytest.raises(Exception, match="DAS_TEST_ZLC_THROW"):
+                db.ctx.join(P, Q)
+            monkeypatch.delenv("DAS_TEST_ZLC_THROW")
         got = db.ctx.join(P, Q).fetch()
         by = {}
         for k, b in zip(qk.tolist(), qb.tolist()):
@@ -1154,3 +1161,28 @@ def test_gpu_miner_walk_matches_oracle():
     assert das.get_link_targets(link) == api.get_link_targets(link)
     assert das.get_link_type(link) == "Execution"
     assert das.get_node_name(seeds[1][0]) == "g7" and das.get_node_type(seeds[1][0]) == "gene"
+
+
+def test_gpu_table_checksum_matches_oracle_rows():
+    """das_table_checksum (the full-size tests' set checksum) over the device
+    answers of the bench's bio and FlyBase queries on small instances equals
+    tests/checksum.py's function over the oracle's row sets."""
+    import bench
+    from das_amd import synthetic
+    from tests import checksum as CK
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    ng = 300
+    cases = [(synthetic.bio_full_kb(ng, 80, 6000, 300, n_uniprot=60, n_up_member=800, n_reactome=15,
+                                    n_context=300, n_loc=8), bench.bio_specs(np.arange(ng)))]
+    fa = synthetic.flybase_kb(300, 8, 400, n_loc=20, n_do=30)
+    cases.append((fa, bench.flybase_specs(7, synthetic.flybase_do_terms(fa, gene=7))))
+    for arrays, specs in cases:
+        db = _hipdb(arrays)
+        odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+        for name, spec in specs:
+            want = O.evaluate(spec, odb)
+            ans = pm.PatternMatchingAnswer()
+            bench.build_expr(pm, spec).matched(db, ans)
+            got = CK.answer_checksum(ans)
+            assert got[1] == want["n"], name
+            assert got[0] == CK.rows_checksum(dict(r[1]) for r in want["rows"]), name
