@@ -125,6 +125,7 @@ _SIGS = {
     "das_table_set_bounds": (C.c_int, [P, P, P]),
     "das_table_get_bounds": (C.c_int, [P, P, P]),
     "das_table_checksum": (C.c_int, [P, P, P, P]),
+    "das_set_pattern_black_list": (C.c_int, [P, P, C.c_uint32]),
     "das_table_info": (C.c_int, [P, P, P, P, P]),
     "das_table_fetch": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P]),
     "das_table_column": (C.c_int, [P, C.c_int32, P]),
@@ -410,6 +411,14 @@ class Context:
             expr_ctype_leaf=eptr(a.expr_ctype_leaf), n_levels=len(a.level_off) - 1, level_off=ptr(a.level_off),
             n_types=len(a.type_names))
         return s, (DAS_BUILD_EXPR_ON_DEVICE if dev else 0), keep
+
+    def set_pattern_black_list(self, type_names):
+        """Named types whose links the next build gives no pattern keys
+        (das_set_pattern_black_list; md5 of each name = named_type_hash)."""
+        import hashlib
+        names = sorted(set(type_names or ()))
+        d = np.frombuffer(b"".join(hashlib.md5(n.encode()).digest() for n in names), dtype="<u4").copy()
+        check(lib().das_set_pattern_black_list(self.h, ptr(d) if len(names) else None, len(names)), self.h)
 
     def build_index(self, arrays, shard=None):
         """Host arrays (das_build_index), or a KB whose expression arrays are

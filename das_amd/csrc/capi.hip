@@ -649,6 +649,14 @@ int das_table_set_bounds(das_table_t* t, const uint32_t* lo, const uint32_t* hi)
   return DAS_OK;
 }
 
+int das_set_pattern_black_list(das_ctx_t* ctx, const uint32_t* type_digests, uint32_t n) {
+  return guarded(ctx, [&] {
+    DAS_CHECK(n == 0 || type_digests, das::DAS_E_INVALID, "null digests");
+    ctx->c.black_list.assign(reinterpret_cast<const das::Digest*>(type_digests),
+                             reinterpret_cast<const das::Digest*>(type_digests) + n);
+  });
+}
+
 int das_table_checksum(das_ctx_t* ctx, const das_table_t* t, const uint64_t* salt, uint64_t out[2]) {
   return guarded(ctx, [&] {
     DAS_CHECK(t && salt && out, das::DAS_E_INVALID, "null argument");

@@ -103,6 +103,12 @@ struct Index {
   std::array<std::vector<uint32_t>, kMaxArity + 1> tbound, gbound;
   std::vector<Digest> ctype_digest;                            // host: sorted ctype digests
   std::vector<Digest> type_digest;                             // host: md5(type name) per named type
+  // host: 1 = the named type is in the pattern black list the build was
+  // given (its links get no pattern keys, canonical_parser.py:144 /
+  // parser_threads.py:185; template keys are kept)
+  std::vector<uint8_t> no_pattern;
+  bool no_pattern_any = false;
+  bool blocked(uint32_t ty) const { return ty < no_pattern.size() && no_pattern[ty]; }
   std::vector<uint32_t> type_name_len;                         // host: bytes of each type name
   std::vector<CtypeRange> ctype_range;                         // host
   // host mirror of the nodes in handle order (n_nodes <= kHostNodeMirror):
@@ -178,6 +184,8 @@ struct Ctx {
   // (lo, cnt) descriptor array of the sparse direct-join build, all-zero
   // between joins (direct_join clears the slots it wrote)
   DBuf<uint2> zlc;
+  // pattern black list for the next index build: md5 of each type name
+  std::vector<Digest> black_list;
   // loader-side host copies kept for metadata calls
   std::vector<uint8_t> leaf_bytes;
   std::vector<uint64_t> leaf_off;

@@ -1466,6 +1466,15 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     md5::digest_bytes(a.leaf_bytes + b, e - b, idx.type_digest[t].w);
     idx.type_name_len[t] = (uint32_t)(e - b);
   }
+  // the pattern black list given for this build (das_set_pattern_black_list)
+  idx.no_pattern.assign(a.n_types, 0);
+  idx.no_pattern_any = false;
+  for (uint32_t t = 0; t < a.n_types; ++t)
+    for (const Digest& d : c.black_list)
+      if (std::memcmp(d.w, idx.type_digest[t].w, 16) == 0) {
+        idx.no_pattern[t] = 1;
+        idx.no_pattern_any = true;
+      }
 
   std::optional<ProfScope> up(std::in_place, c, "upload",
                               (double)n_bytes + 8.0 * nl + 13.0 * nl + (dev_expr ? 0.0 : 8.0 * ne + 4.0 * n_child + 5.0 * ne));

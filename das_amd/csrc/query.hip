@@ -2157,6 +2157,8 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
   auto empty = [&]() { P.empty = true; };
   if (ar == 0 || ar > (uint32_t)kMaxArity || idx.ttab[ar].rows == 0) return empty();
   if (q.type_id != kNone && q.type_id >= idx.n_types) return empty();
+  // a black-listed type has no pattern keys (canonical_parser.py:144)
+  if (q.type_id != kNone && idx.blocked(q.type_id)) return empty();
   // Families the reference indexes (canonical_parser.py:144-178)
   if (ar > (uint32_t)kMaxPosArity) {
     if (q.type_id != kNone || any_wild) return empty();   // only [*, e0..en]
@@ -2177,8 +2179,21 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
     } else {
       rt = &idx.ttab[ar];
     }
-    if (!typed) ranges.push_back({0, rt->rows});
-    else ranges.push_back({idx.type_off[ar][q.type_id], idx.type_off[ar][q.type_id + 1]});
+    if (typed) {
+      ranges.push_back({idx.type_off[ar][q.type_id], idx.type_off[ar][q.type_id + 1]});
+    } else if (!idx.no_pattern_any) {
+      ranges.push_back({0, rt->rows});
+    } else {
+      // '*' keys hold no black-listed link: the type segments around them
+      uint64_t b = 0;
+      for (uint32_t ty = 0; ty < idx.n_types && ty + 1 < idx.type_off[ar].size(); ++ty) {
+        if (!idx.blocked(ty)) continue;
+        if (idx.type_off[ar][ty] > b) ranges.push_back({b, idx.type_off[ar][ty]});
+        b = std::max(b, idx.type_off[ar][ty + 1]);
+      }
+      if (rt->rows > b) ranges.push_back({b, rt->rows});
+      if (ranges.empty()) return empty();
+    }
   } else {
     // the cheapest P_{a,p} among the grounded positions: its key range(s)
     // (one per named type for a '*' type)
@@ -2186,7 +2201,7 @@ void scan_prepare(Ctx& c, const das_link_scan_t& q, ScanPrep& P) {
     if (q.type_id != kNone) types.push_back(q.type_id);
     else
       for (uint32_t ty = 0; ty < idx.n_types; ++ty)
-        if (idx.type_off[ar][ty + 1] > idx.type_off[ar][ty]) types.push_back(ty);
+        if (idx.type_off[ar][ty + 1] > idx.type_off[ar][ty] && !idx.blocked(ty)) types.push_back(ty);
     uint64_t best = ~0ull;
     for (uint32_t p : grounded) {
       const PosIndex& P = idx.pidx[ar][p];
@@ -3039,7 +3054,7 @@ bool anti_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, AntiPlan& pl
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
   if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
-      ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
+      idx.blocked(q.type_id) || ar == 0 || ar > (uint32_t)kMaxPosArity || A.nrows >= 0xFFFFFFFFull)
     return false;
   // every position grounded or bound by A (else the filter is not a lookup)
   int bp = -1;
@@ -3088,7 +3103,7 @@ bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows,
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
   if (A.kind != DAS_TABLE_ORDERED || !q.ordered || q.emit_link || q.type_id == kNone || q.type_id >= idx.n_types ||
-      ar == 0 || ar > (uint32_t)kMaxPosArity || rows >= 0xFFFFFFFFull)
+      idx.blocked(q.type_id) || ar == 0 || ar > (uint32_t)kMaxPosArity || rows >= 0xFFFFFFFFull)
     return false;
   // one bound position; every other position a fresh, distinct variable or
   // a grounded target that leads P_{a,p}'s secondary order

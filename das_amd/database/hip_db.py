@@ -137,6 +137,9 @@ class HipDB(RelationalDB):
         self.generation = next(_LOADS)      # invalidates lowered query plans (unique across HipDBs)
         self._plan_records = {}
         self.shard = shard if shard is not None else getattr(arrays, "shard", None)
+        # pattern_black_list is read at load time, as the reference's loaders
+        # read it (distributed_atom_space.py:346, 409)
+        self.ctx.set_pattern_black_list(self.pattern_black_list)
         self.ctx.build_index(arrays, self.shard)
         self.arrays = arrays
         self.type_id = dict(arrays.type_id)

@@ -68,6 +68,8 @@ class DistributedAtomSpace:
     def _rebuild(self):
         # canonical files through the native reader (canonical.cpp), general
         # MeTTa through the Python MettaYacc restatement, one device index
+        # the loaders honour pattern_black_list (distributed_atom_space.py:346, 409)
+        self.db.pattern_black_list = list(self.pattern_black_list)
         parts = []
         if self._canonical_sources:
             parts.append(_lib.parse_canonical(self._canonical_sources))

@@ -965,6 +965,15 @@ class HipLocal:
         self.stream_ordered = (not cpu_staging and bool(db.stream) and
                                db.stream == torch.cuda.current_stream().cuda_stream)
 
+    @property
+    def pattern_black_list(self):
+        """The local index's load-time pattern black list (HipDB.load_arrays)."""
+        return self.local.pattern_black_list
+
+    @pattern_black_list.setter
+    def pattern_black_list(self, value):
+        self.local.pattern_black_list = list(value)
+
     def __getattr__(self, name):     # DBInterface passthrough
         return getattr(self.db, name)
 

@@ -123,6 +123,17 @@ int das_parsed_atoms(const das_parsed_t* p, das_atoms_t* atoms, const uint32_t**
 int das_parsed_type_name(const das_parsed_t* p, uint32_t type_id, const char** name, uint64_t* len);
 int das_parsed_free(das_parsed_t* p);
 
+/* The reference's `pattern_black_list` (distributed_atom_space.py:38, 346,
+ * 409): named types (md5 of each type name, 4 words per type) whose links the
+ * NEXT index build gives no pattern keys -- typed and '*' Link queries with a
+ * wildcard (RedisMongoDB.get_matched_links :235-252) never return them --
+ * while their template keys, outgoing / incoming sets and existence stay
+ * (canonical_parser.py:144, 179-180; parser_threads.py:185).  (The reference
+ * also writes each black-listed link under the previous link's keys, a bug
+ * that depends on its load order; that is not reproduced: DESIGN.md §2.)
+ * n = 0 clears the list. */
+int das_set_pattern_black_list(das_ctx_t* ctx, const uint32_t* type_digests, uint32_t n);
+
 typedef struct {
   uint64_t n_atoms, n_nodes, n_links, n_types, n_ctypes;
   uint64_t device_bytes;

@@ -165,7 +165,15 @@ def keyspace_lines(kb):
 class RedisMongoSemantics:
     """Restatement of RedisMongoDB over an in-memory KB."""
 
-    def __init__(self, kb, pattern_black_list=(), tuple_targets=False):
+    def __init__(self, kb, pattern_black_list=(), tuple_targets=False, stale_key_order=None):
+        """pattern_black_list: named types whose links get no pattern keys
+        (the intent of canonical_parser.py:144 / parser_threads.py:185).
+        stale_key_order: the link handles in the order the reference's
+        pattern-key loop walks them -- the loop never resets `keys` for a
+        blacklisted link, so it is written under the previous link's keys
+        (canonical_parser.py:177-178, parser_threads.py:218-219), and a
+        blacklisted first link raises UnboundLocalError; given the order,
+        this restates that behaviour exactly."""
         self.kb = kb
         self.tuple_targets = tuple_targets
         self.patterns = {}
@@ -175,11 +183,21 @@ class RedisMongoSemantics:
             a = len(targets)
             self.collection[h] = "1" if a == 1 else ("2" if a == 2 else "N")
             value = (h, tuple(targets))
-            if t not in pattern_black_list:
+            if stale_key_order is None and t not in pattern_black_list:
                 for k in _pattern_keys(named_type_hash(t), targets):
                     self.patterns.setdefault(k, set()).add(value)
             self.templates.setdefault(ct, set()).add(value)
             self.templates.setdefault(named_type_hash(t), set()).add(value)
+        if stale_key_order is not None:
+            keys = None
+            for h in stale_key_order:
+                t, targets, _ = kb.links[h]
+                if t not in pattern_black_list:
+                    keys = _pattern_keys(named_type_hash(t), targets)
+                elif keys is None:
+                    raise UnboundLocalError("local variable 'keys' referenced before assignment")
+                for k in keys:
+                    self.patterns.setdefault(k, set()).add((h, tuple(targets)))
 
     def _fmt(self, values):
         if self.tuple_targets:

@@ -162,15 +162,17 @@ import das.distributed_atom_space as das_mod  # noqa: E402
 das_mod.sleep = lambda s: None
 
 
-def load_metta(paths):
+def load_metta(paths, black_list=()):
     das = new_das()
+    das.pattern_black_list = list(black_list)
     for p in paths:
         das.load_knowledge_base(p)
     return das
 
 
-def load_canonical(path):
+def load_canonical(path, black_list=()):
     das = new_das()
+    das.pattern_black_list = list(black_list)
     das.load_canonical_knowledge_base(path)
     das.db.prefetch()
     return das
@@ -596,6 +598,116 @@ def stubdb_fixture():
             "queries": [answer_record(db, q) for q in qs]}
 
 
+# A canonical KB whose link types interleave (canonical_parser.py:132-183
+# walks links_1, links_2, links_N in insertion order), for the
+# pattern_black_list fixture: a blacklisted type's links follow links of
+# every other type, arity 2 and 3.
+BLACKLIST_CANONICAL = "\n".join(
+    ["(: Concept Type)", "(: Inheritance Type)", "(: Similarity Type)", "(: List Type)", "(: Evaluation Type)",
+     "(: Predicate Type)", '(: "has" Predicate)']
+    + [f'(: "c{i}" Concept)' for i in range(12)]
+    + [f'(Inheritance "Concept c{a}" "Concept c{b}")' if k % 4 == 0 else
+       f'(Similarity "Concept c{a}" "Concept c{b}")' if k % 4 == 1 else
+       f'(List "Concept c{a}" "Concept c{b}" "Concept c{(a + b) % 12}")' if k % 4 == 2 else
+       f'(Evaluation "Predicate has" (List "Concept c{a}" "Concept c{b}"))'
+       for k, (a, b) in enumerate((i % 12, (5 * i + 3 + i // 12) % 12) for i in range(60))]) + "\n"
+
+
+def blacklist_queries():
+    c = [C(f"c{i}") for i in range(12)]
+    q = []
+    for t in ("Inheritance", "Similarity", "List", "Evaluation", "*"):
+        q += [L(t, [V("V1"), V("V2")]), L(t, [c[0], V("V1")]), L(t, [V("V1"), c[3]]),
+              L(t, [V("V1"), V("V2"), V("V3")]), L(t, [c[1], V("V1"), V("V2")]),
+              ["Template", t, True, [["TVar", "V1", "Concept"], ["TVar", "V2", "Concept"]]]]
+    q += [L("Similarity", [V("V1"), V("V2")], False), L("Similarity", [c[0], V("V1")], False),
+          ["And", [L("Inheritance", [V("V1"), V("V2")]), L("Similarity", [V("V2"), V("V3")])]],
+          ["And", [L("Inheritance", [V("V1"), V("V2")]), ["Not", L("Similarity", [V("V1"), V("V2")])]]],
+          ["Or", [L("Inheritance", [V("V1"), c[3]]), L("Similarity", [V("V1"), c[3]])]],
+          L("Similarity", [c[0], c[3]]), L("Inheritance", [c[0], c[3]])]
+    return q
+
+
+def blacklist_probes(das):
+    h = lambda n: das.db.get_node_handle("Concept", n)  # noqa: E731
+    P = []
+    for t in ["Inheritance", "Similarity", "List", "Evaluation", "*"]:
+        for targets in [["*", "*"], [h("c0"), "*"], ["*", h("c3")], ["*", "*", "*"], [h("c1"), "*", "*"]]:
+            P.append(("links", [t, targets]))
+        P.append(("type", t))
+    for tpl in [["Inheritance", "Concept", "Concept"], ["Similarity", "Concept", "Concept"],
+                ["List", "Concept", "Concept", "Concept"]]:
+        P.append(("template", tpl))
+    return P
+
+
+_PATTERN_ORDER = []
+
+
+def _record_pattern_order():
+    """The order BuildPatternsThread (parser_threads.py:181-219) walks the
+    MettaYacc loader's links, recorded before it runs (read only)."""
+    orig = parser_threads_mod.BuildPatternsThread.run
+
+    def run(self):
+        _PATTERN_ORDER.append([e.hash_code for e in self.shared_data.regular_expressions_list])
+        orig(self)
+    parser_threads_mod.BuildPatternsThread.run = run
+
+
+_record_pattern_order()
+
+
+def blacklist_fixture():
+    """pattern_black_list (distributed_atom_space.py:38, 346, 409): the
+    reference's loaders skip the pattern-key family of a blacklisted link
+    (canonical_parser.py:144, parser_threads.py:185) -- but `keys` is not
+    reset, so the link is written under the previous link's keys
+    (canonical_parser.py:177-178, parser_threads.py:218-219), or the load
+    fails when no earlier link set them.  Recorded for both loaders."""
+    out = {"cases": []}
+    p = os.path.join(SCRATCH, "blacklist.metta")
+    with open(p, "w") as f:
+        f.write(BLACKLIST_CANONICAL)
+    cases = [("metta", os.path.join(REF, "data/samples/animals.metta"), ["Similarity"], animals_queries, animals_probes),
+             ("metta", os.path.join(REF, "data/samples/animals.metta"), ["Inheritance"], animals_queries, animals_probes),
+             ("canonical", p, ["Similarity"], blacklist_queries, blacklist_probes),
+             ("canonical", p, ["Similarity", "Evaluation"], blacklist_queries, blacklist_probes),
+             ("canonical", p, ["Inheritance"], blacklist_queries, blacklist_probes),
+             ("canonical", os.path.join(REF, "data/samples/canonical_toy-example-mining.metta"), ["Inheritance"],
+              toy_mining_queries, None)]
+    for loader, path, bl, queries, probes in cases:
+        rec = {"loader": loader, "black_list": bl,
+               "source": "inline" if path == p else os.path.relpath(path, REF)}
+        _PATTERN_ORDER.clear()
+        das = new_das()
+        das.pattern_black_list = list(bl)
+        try:
+            if loader == "metta":
+                das.load_knowledge_base(path)
+            else:
+                das.load_canonical_knowledge_base(path)
+                das.db.prefetch()
+        except Exception as e:
+            rec["load_error"] = type(e).__name__
+        # the links in the order the pattern-key loop walked them
+        # (canonical_parser.py:136-137: links_1, links_2, links_N collections in
+        # insertion order; parser_threads.py:183: regular_expressions_list)
+        if loader == "metta":
+            rec["pattern_order"] = [h for order in _PATTERN_ORDER for h in order]
+        else:
+            rec["pattern_order"] = [d["_id"] for tag in ["1", "2", "N"]
+                                    for d in das.db.mongo_link_collection[tag].find()]
+        if "load_error" not in rec:
+            rec.update(kb_fixture("blacklist", das, queries(), probes(das) if probes else None, rec["source"]))
+        else:
+            nodes, links = atom_table(das)
+            rec["nodes"], rec["links"] = nodes, links
+        out["cases"].append(rec)
+    out["canonical_text"] = BLACKLIST_CANONICAL
+    return out
+
+
 def main():
     which = sys.argv[1:] or ["hash", "stubdb", "animals", "toy_mining", "stub_like", "synthetic"]
     if "hash" in which:
@@ -622,6 +734,8 @@ def main():
                 lines = sorted(l.rstrip("\n") for l in f if l.strip())
             with open(os.path.join(out_dir, f"{name}.txt"), "w") as f:
                 f.write("".join(l + "\n" for l in lines))
+    if "blacklist" in which:
+        write("kb_blacklist.json", blacklist_fixture())
     if "stub_like" in which:
         p = os.path.join(SCRATCH, "stub_like.metta")
         with open(p, "w") as f:

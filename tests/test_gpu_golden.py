@@ -112,3 +112,68 @@ def _has_ordered_templates_below_root(spec):
         return []
     ts = templates(spec)
     return spec[0] in ("And", "Or") and bool(ts) and all(t[2] for t in ts)
+
+
+@pytest.mark.parametrize("plan", ["1", "0"])
+def test_gpu_pattern_black_list(golden, plan, monkeypatch):
+    """pattern_black_list (kb_blacklist.json, reference-run with non-empty
+    black lists, both loaders): the product follows the intended semantics --
+    a black-listed type's links get no pattern keys (typed and '*' Link
+    queries with a wildcard never return them) and keep their template keys
+    (canonical_parser.py:144, 179-180; parser_threads.py:185) -- i.e. the
+    oracle without the reference's stale-key bug.  Every query and index probe
+    equals that oracle, and every query the bug does not touch equals the
+    reference's own answer (tests/test_oracle.py pins the bug's restatement
+    against the same fixture)."""
+    import os
+    from oracle import das_oracle as O
+    from das_amd import _lib, loader
+    from das_amd.database.hip_db import HipDB
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    monkeypatch.setenv("DAS_PLAN", plan)
+    d = golden("kb_blacklist.json")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
+    checked = reference_equal = 0
+    for case in d["cases"]:
+        if case.get("load_error"):
+            continue
+        bl = case["black_list"]
+        db = HipDB(device=0, tuple_targets=True)
+        db.pattern_black_list = list(bl)
+        if case["loader"] == "metta":
+            with open(os.path.join(here, os.path.basename(case["source"]))) as f:
+                db.load_arrays(loader.parse_metta([f.read()]).finish())
+        else:
+            db.load_arrays(_lib.parse_canonical([d["canonical_text"]]))
+        kb = O.KB.from_tables(case["nodes"], case["links"])
+        want_db = O.RedisMongoSemantics(kb, bl, tuple_targets=True)
+        stale_db = O.RedisMongoSemantics(kb, bl, tuple_targets=True, stale_key_order=case["pattern_order"])
+        assert list(db.count_atoms()) == case["count_atoms"]
+        for q in case["queries"]:
+            want = O.evaluate(q["query"], want_db)
+            got = record(q["query"], db)
+            assert same(got, want), (bl, q["query"])
+            checked += 1
+            if want == O.evaluate(q["query"], stale_db):
+                assert same(got, q), (bl, q["query"])
+                reference_equal += 1
+        for p in case.get("index") or []:
+            args = p["args"]
+            if p["kind"] == "links":
+                r, w = db.get_matched_links(*args), want_db.get_matched_links(*args)
+            elif p["kind"] == "template":
+                r, w = db.get_matched_type_template(args), want_db.get_matched_type_template(args)
+            else:
+                r, w = db.get_matched_type(args), want_db.get_matched_type(args)
+            key = lambda xs: sorted(x if isinstance(x, str) else x[0] for x in xs)  # noqa: E731
+            assert key(r) == key(w), (bl, p)
+    assert checked > 100 and reference_equal > checked // 2
+    # through the facade: the attribute the reference's loaders read
+    das = DistributedAtomSpace()
+    das.pattern_black_list = ["Similarity"]
+    p = os.path.join(here, "animals.metta")
+    das.load_knowledge_base(p)
+    assert das.get_links("Similarity", None, ["*", "*"]) == []
+    assert len(das.get_links("Similarity", ["Concept", "Concept"])) == 14
+    assert sorted(das.get_links("*", None, ["*", "*"])) == sorted(das.get_links("Inheritance", None, ["*", "*"]))
+    assert len(das.get_links("Inheritance", None, ["*", "*"])) == 12
