@@ -150,6 +150,7 @@ _SIGS = {
     "das_plan_bounds": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, P]),
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
+    "das_prof_tag": (C.c_int, [P, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
     "das_prof_names": (C.c_int, [P, P, C.c_uint64]),
@@ -722,6 +723,10 @@ class Context:
     def prof_only(self, name=None):
         """Record events only for scopes named `name` (None: every scope)."""
         check(lib().das_prof_only(self.h, name.encode() if name else None), self.h)
+
+    def prof_tag(self, tag=None):
+        """Name the scopes recorded from now on "<scope>@<tag>" (None: untagged)."""
+        check(lib().das_prof_tag(self.h, tag.encode() if tag else None), self.h)
 
     def prof_stats(self):
         buf = C.create_string_buffer(1 << 16)

@@ -783,6 +783,10 @@ int das_prof_only(das_ctx_t* ctx, const char* name) {
   });
 }
 
+int das_prof_tag(das_ctx_t* ctx, const char* tag) {
+  return guarded(ctx, [&] { ctx->c.prof_tag = tag ? tag : ""; });
+}
+
 int das_prof_reset(das_ctx_t* ctx) {
   return guarded(ctx, [&] {
     das::prof_collect(ctx->c);
@@ -869,8 +873,9 @@ void trace_dump(const char* title) {
 KScope::~KScope() { delete static_cast<ProfScope*>(impl); }
 
 void prof_add_bytes(Ctx& c, const std::string& name, double bytes) {
+  const std::string tagged = c.prof_tag.empty() ? name : name + "@" + c.prof_tag;
   for (auto it = c.pending.rbegin(); it != c.pending.rend(); ++it)
-    if (it->name == name) {
+    if (it->name == tagged) {
       it->bytes += bytes;
       return;
     }

@@ -160,7 +160,19 @@ struct Ctx {
   // a copy (2: scans up to kViewRows rows, 1: all, 0: none); views are
   // materialised before a table leaves the plan
   int scan_views = 0;
-  std::string prof_only;             // non-empty: only scopes of this name record events
+  std::string prof_only;             // non-empty: only scopes of these names (comma-separated) record events
+  std::string prof_tag;              // non-empty: recorded scopes are named "<scope>@<tag>" (one query's launches)
+  bool prof_selected(const std::string& name) const {
+    if (prof_only.empty()) return true;
+    size_t b = 0;
+    while (b <= prof_only.size()) {
+      size_t e = prof_only.find(',', b);
+      if (e == std::string::npos) e = prof_only.size();
+      if (prof_only.compare(b, e - b, name) == 0) return true;
+      b = e + 1;
+    }
+    return false;
+  }
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;   // recycled timing events (creation is not cheap on ROCm)
   hipEvent_t take_event() {
@@ -215,7 +227,8 @@ struct ProfScope {
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
     count_launch();
     if (trace_on()) trace_mark("kernel", name + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
-    if (!c.prof || (!c.prof_only.empty() && c.prof_only != name)) return;
+    if (!c.prof || !c.prof_selected(name)) return;
+    if (!c.prof_tag.empty()) name += "@" + c.prof_tag;
     a = c.take_event();
     b = c.take_event();
     DAS_HIP(hipEventRecord(a, c.s));

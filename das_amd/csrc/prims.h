@@ -312,15 +312,20 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_reduce_pub(In in, uint64_t 
   }
   block_sum_max(acc, m, s_sum, s_mx);
   if (threadIdx.x == 0) {
-    tsum[blockIdx.x] = acc;
-    tmax[blockIdx.x] = m;
-    const unsigned long long t =
-        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // the tile's sum and max written through to the coherence point (agent
+    // scope atomic stores), drained, then the arrival: no agent-scope
+    // release per block (on gfx950 each one writes this XCD's L2 back)
+    __hip_atomic_store(&tsum[blockIdx.x], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&tmax[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = t == last;
   }
   __syncthreads();
   if (!s_last) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the other tiles' sums
+  // the last block: an agent-scope acquire (this XCD's stale lines of the
+  // other tiles' sums invalidated), then plain reads
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   T total;
   uint64_t mx;
   block_scan_loop<T>(SpanIn<T>{tsum}, tiles, tsum, total, mx, s_sum, s_mx);   // in place, element-wise

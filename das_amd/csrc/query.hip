@@ -261,12 +261,14 @@ __global__ void __launch_bounds__(B) k_union_first(MultiScan ms, uint32_t lo, ui
   if (first) out[pos] = v;
   if (__ballot(bad) && __lane_id() == 0) atomicOr(&ctr[2], 1u);
   __syncthreads();
+  // arrival without an agent-scope release (on gfx950 each one writes this
+  // XCD's L2 back; one per block serialised ~2.5 us a block per XCD): the
+  // rows are read by later launches only, the last block reads counters,
+  // atomics performed at the coherence point once this thread's are done
   if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
-      __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1)
       publish_u32(slot, seq, atomicAdd(&ctr[2], 0u) ? 0xFFFFFFFFu : atomicAdd(&ctr[0], 0u));
-    }
   }
 }
 
@@ -2999,12 +3001,14 @@ __global__ void __launch_bounds__(B) k_ij_mid(const uint32_t* __restrict__ key, 
     }
   }
   __syncthreads();
+  // arrival without an agent-scope release (on gfx950 each one writes this
+  // XCD's L2 back; one per block serialised ~2.5 us a block per XCD): the
+  // rows are read by later launches only, the last block reads counters,
+  // atomics performed at the coherence point once this thread's are done
   if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
-      __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1)
       publish_u32(slot, seq, atomicAdd(&ctr[2], 0u) ? 0xFFFFFFFFu : atomicAdd(&ctr[0], 0u));
-    }
   }
 }
 
@@ -3375,6 +3379,9 @@ struct ChainStage {
   uint32_t append;               // SCAN: append to this stage's table (Or's union), or kChainNoStage
   uint32_t empty_ok;             // SCAN: no rows is not a failing term (Or)
   uint32_t begin, end;           // SCAN: row range of the index table
+  uint32_t ld;                   // column stride of dst (0: cap); grid chain: cap is per workgroup
+  uint32_t ncols;                // columns of dst
+  uint32_t part;                 // grid chain: the partition index join (each workgroup expands a slice)
   uint32_t* dst;                 // output table (ncols columns of `cap` rows)
   const uint32_t* key;           // IJ / ANTI: the probe key column
   ScanSpec sp;                   // SCAN
@@ -3388,9 +3395,18 @@ struct ChainStage {
   const uint32_t* copy[kMaxCols];
 };
 struct ChainDesc {
-  uint32_t nstage, pad;
+  uint32_t nstage;
+  uint32_t seg;                  // grid chain: rows per workgroup segment of every stage table (0: one workgroup)
+  uint32_t* fin;                 // grid chain: the final table (columns of fin_ld rows)
+  uint64_t fin_ld;
+  uint32_t* gsc;                 // grid chain: device counters (kGscWords, zeroed by k_chain_prep)
   ChainStage st[kChainStages];
 };
+// grid chain counters: per-stage global row counts, then the output cursor,
+// the finished-workgroup count and the redo flag
+constexpr uint32_t kGscOut = kChainStages, kGscDone = kChainStages + 1, kGscRedo = kChainStages + 2,
+                   kGscWords = kChainStages + 4;
+enum : uint32_t { CHS_REDO = 3 };
 
 // Block-wide ordered compaction step: this thread's output position among
 // the kept rows of the round (keep order = thread order); advances *run.
@@ -3412,9 +3428,25 @@ __device__ __forceinline__ uint32_t chain_rank(bool keep, uint32_t* s_w, uint32_
   return pos;
 }
 
-__global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restrict__ hdesc, uint32_t nwords,
-                                                       uint32_t* slot, uint32_t seq, uint64_t* tstamp) {
-  if (tstamp && threadIdx.x == 0) tstamp[0] = wall_clock64();
+// The stages, by one workgroup (GRID = false: the whole chain) or by each
+// workgroup of a grid (GRID = true).  In the grid form every workgroup runs
+// the stages before the partition index join itself (they are small: grounded
+// scans and their joins), writing its own segment [w * seg, (w + 1) * seg) of
+// every stage table; at the partition stage it expands only its slice of the
+// outputs (output-balanced over the workgroups), and every later stage is
+// row-local -- index joins, joins with a (replicated) scanned term, anti
+// index joins -- on the rows the workgroup holds.  No workgroup waits for
+// another: each appends its final rows to the output table at a cursor and
+// the last one to finish publishes the total.  A failure before or at the
+// partition is the same in every workgroup (the chain ends "partial" there,
+// as the one-workgroup chain does); after it -- a segment outgrowing its
+// capacity -- the whole chain is redone by the caller.
+template <bool GRID>
+__device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, uint32_t nwords, uint32_t* slot,
+                                           uint32_t seq, uint64_t* tstamp) {
+  const bool stamp = tstamp && (!GRID || blockIdx.x == 0);
+  const uint64_t t_start = wall_clock64();
+  if (stamp && threadIdx.x == 0) tstamp[0] = t_start;
   constexpr int W = kSmallBlock / 64;
   __shared__ ChainDesc d;
   __shared__ uint32_t s_cnt[kChainStages];
@@ -3422,21 +3454,28 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
   uint32_t* s_pre = s_buf;
   uint32_t* s_lo = s_buf + kIjSmall + 1;
   __shared__ uint32_t s_w[W];
-  __shared__ uint32_t s_run, s_state, s_acc;
+  __shared__ uint32_t s_run, s_state, s_acc, s_parted, s_base;
   uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
   for (uint32_t i = threadIdx.x; i < nwords; i += kSmallBlock) dw[i] = hdesc[i];
   if (threadIdx.x == 0) {
     s_state = CHS_OK;
     s_acc = 0;
+    s_parted = 0;
   }
   __syncthreads();
-  if (tstamp && threadIdx.x == 0) tstamp[1] = wall_clock64();
+  if (stamp && threadIdx.x == 0) tstamp[1] = wall_clock64();
+  const uint32_t G = GRID ? gridDim.x : 1u, wg = GRID ? blockIdx.x : 0u;
+  const uint64_t off = GRID ? (uint64_t)wg * d.seg : 0ull;   // this workgroup's rows of every stage table
   for (uint32_t si = 0; si < d.nstage && s_state == CHS_OK; ++si) {
     const ChainStage& st = d.st[si];
+    const uint64_t ld = st.ld ? st.ld : st.cap;
+    uint32_t* dst = st.dst + off;
+    const bool parted = GRID && s_parted;          // rows are this workgroup's share (uniform)
     if (threadIdx.x == 0) s_run = 0;
     __syncthreads();
     uint32_t n = 0;
     bool ok = true;                // uniform: the stage produced its full result
+    bool redo = false;             // grid, after the partition: a segment overflowed
     if (st.op == CH_SCAN) {
       const bool app = st.append != kChainNoStage;
       if (app && threadIdx.x == 0) s_run = s_cnt[st.append];
@@ -3445,7 +3484,8 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
         const uint32_t r = r0 + threadIdx.x;
         const bool keep = r < st.end && scan_keep(st.sp, r);
         const uint32_t pos = chain_rank(keep, s_w, &s_run);
-        if (keep) scan_emit(st.sp, r, st.dst, st.cap, pos);
+        if (keep)                                      // chain scans are ordered (no local sort buffer)
+          for (uint32_t c = 0; c < st.sp.nout; ++c) dst[c * ld + pos] = st.sp.col[1 + st.sp.outpos[c]][r];
       }
       n = s_run;
       if (app) {
@@ -3463,12 +3503,16 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
       } else {
         for (uint32_t i = threadIdx.x; i < kChainHash; i += kSmallBlock) s_buf[i] = 0u;
         __syncthreads();
-        bool first[(kChainHash / 2 + kSmallBlock - 1) / kSmallBlock];
-        for (uint32_t k = 0, r = threadIdx.x; r < kChainHash / 2; ++k, r += kSmallBlock) {
-          first[k] = false;
+        // this thread's rows r and r + kSmallBlock: first occurrences (two
+        // flags in registers, no indexed local array)
+        static_assert(kChainHash / 2 == 2 * kSmallBlock, "two rows per thread");
+        bool first[2] = {false, false};
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+          const uint32_t r = threadIdx.x + k * kSmallBlock;
           if (r >= nin) continue;
           uint32_t h = 0x9e3779b9u;
-          for (uint32_t c = 0; c < st.ncopy; ++c) h = mix32(h ^ (st.copy[c][r] + 0x7f4a7c15u * (c + 1)));
+          for (uint32_t c = 0; c < st.ncopy; ++c) h = mix32(h ^ (st.copy[c][off + r] + 0x7f4a7c15u * (c + 1)));
           for (uint32_t probe = h & (kChainHash - 1);; probe = (probe + 1) & (kChainHash - 1)) {
             const uint32_t cur = atomicCAS(&s_buf[probe], 0u, r + 1);
             if (cur == 0u) {
@@ -3476,32 +3520,36 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
               break;
             }
             bool same = true;
-            for (uint32_t c = 0; c < st.ncopy && same; ++c) same = st.copy[c][cur - 1] == st.copy[c][r];
+            for (uint32_t c = 0; c < st.ncopy && same; ++c) same = st.copy[c][off + cur - 1] == st.copy[c][off + r];
             if (same) break;
           }
         }
-        for (uint32_t k = 0, r0 = 0; r0 < nin; ++k, r0 += kSmallBlock) {
-          const uint32_t r = r0 + threadIdx.x;
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+          const uint32_t r = k * kSmallBlock + threadIdx.x;
+          if (k * kSmallBlock >= nin) break;
           const bool keep = r < nin && first[k];
           const uint32_t pos = chain_rank(keep, s_w, &s_run);
           if (keep)
-            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+            for (uint32_t c = 0; c < st.ncopy; ++c) dst[(uint64_t)c * ld + pos] = st.copy[c][off + r];
         }
         n = s_run;
       }
     } else if (st.op == CH_IJ) {
       // the probe in chunks of kIjSmall rows (the LDS prefix): lookups, a
       // block scan of the match counts, the chunk's outputs appended in
-      // probe order.  Inputs above kChainIjRows end the chain instead: one
-      // workgroup expanding them lost to the multi-workgroup index join
-      // (FlyBase F5 / F7 at hub genes, profiles/r2_flybase_host_split.json)
+      // probe order.  Inputs above kChainIjRows end the one-workgroup chain
+      // instead: one workgroup expanding them lost to the multi-workgroup
+      // index join (FlyBase F5 / F7 at hub genes, profiles/r2_flybase_host_split.json);
+      // the grid chain takes any input its segments hold
       const uint32_t nin = s_cnt[st.in];
       const int wave = threadIdx.x >> 6;
+      const bool part = GRID && st.part;
       uint32_t outn = 0;
-      if (nin > kChainIjRows) ok = false;
-      for (uint32_t c0 = 0; c0 < nin && ok; c0 += kIjSmall) {
+      if ((!parted && nin > kChainIjRows) || (part && nin > kIjSmall)) ok = false;
+      for (uint32_t c0 = 0; c0 < nin && ok && !redo; c0 += kIjSmall) {
         const uint32_t cn = nin - c0 < kIjSmall ? nin - c0 : kIjSmall;
-        lookups_small(st.key, st.kx, st.g, cn, s_lo, s_pre, c0);
+        lookups_small(st.key, st.kx, st.g, cn, s_lo, s_pre, (uint32_t)(off + c0));
         __syncthreads();
         // exclusive scan of s_pre[0..cn) in rounds of 1024
         uint32_t carry = 0;
@@ -3523,75 +3571,147 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
         }
         if (threadIdx.x == 0) s_pre[cn] = carry;
         __syncthreads();
-        if ((uint64_t)outn + carry > st.cap) {
-          ok = false;
+        // the partition stage expands outputs [o_lo, o_hi) of the total only
+        const uint32_t o_lo = part ? (uint32_t)(((uint64_t)carry * wg) / G) : 0u;
+        const uint32_t o_hi = part ? (uint32_t)(((uint64_t)carry * (wg + 1)) / G) : carry;
+        if (part && carry == 0) {
+          ok = false;                                  // empty everywhere: the chain ends partial
+        } else if ((uint64_t)outn + (o_hi - o_lo) > st.cap) {
+          if (parted || part) redo = true; else ok = false;
         } else {
-          for (uint32_t o = threadIdx.x; o < carry; o += kSmallBlock) {
+          for (uint32_t o = o_lo + threadIdx.x; o < o_hi; o += kSmallBlock) {
             uint32_t l = 0, h = cn;                    // last row r with s_pre[r] <= o
             while (h - l > 1) {
               const uint32_t m = (l + h) >> 1;
               if (s_pre[m] <= o) l = m; else h = m;
             }
             const uint32_t br = s_lo[l] + (o - s_pre[l]);
-            for (int i = 0; i < st.jc.np; ++i) st.dst[(uint64_t)st.jc.po[i] * st.cap + outn + o] = st.jc.p[i][c0 + l];
-            for (int i = 0; i < st.jc.nb; ++i) st.dst[(uint64_t)st.jc.bo[i] * st.cap + outn + o] = st.jc.b[i][br];
+            const uint64_t w = outn + (o - o_lo);
+            for (int i = 0; i < st.jc.np; ++i) dst[(uint64_t)st.jc.po[i] * ld + w] = st.jc.p[i][off + c0 + l];
+            for (int i = 0; i < st.jc.nb; ++i) dst[(uint64_t)st.jc.bo[i] * ld + w] = st.jc.b[i][br];
           }
-          outn += carry;
+          outn += o_hi - o_lo;
         }
         __syncthreads();                               // s_lo / s_pre are reused by the next chunk
       }
       n = outn;
-      if (n == 0) ok = false;
+      if (n == 0 && !parted && !part) ok = false;      // one workgroup: And's reset-on-empty path
+      if (part && ok && !redo && threadIdx.x == 0) s_parted = 1;
     } else if (st.op == CH_JOIN) {
       const uint32_t na = s_cnt[st.in], nb = s_cnt[st.rel];
       const uint64_t pairs = (uint64_t)na * nb;
       if (pairs > kChainJoinPairs) {
-        ok = false;
+        if (parted) redo = true; else ok = false;
       } else {
         for (uint64_t k0 = 0; k0 < pairs; k0 += kSmallBlock) {
           const uint64_t k = k0 + threadIdx.x;
           const uint32_t i = k < pairs ? (uint32_t)(k / nb) : 0u, j = k < pairs ? (uint32_t)(k % nb) : 0u;
           bool keep = k < pairs;
-          for (uint32_t x = 0; x < st.nsh && keep; ++x) keep = st.sha[x][i] == st.shb[x][j];
+          for (uint32_t x = 0; x < st.nsh && keep; ++x) keep = st.sha[x][off + i] == st.shb[x][off + j];
           const uint32_t pos = chain_rank(keep, s_w, &s_run);
           if (keep && pos < st.cap) {
-            for (int c = 0; c < st.jc.np; ++c) st.dst[(uint64_t)st.jc.po[c] * st.cap + pos] = st.jc.p[c][i];
-            for (int c = 0; c < st.jc.nb; ++c) st.dst[(uint64_t)st.jc.bo[c] * st.cap + pos] = st.jc.b[c][j];
+            for (int c = 0; c < st.jc.np; ++c) dst[(uint64_t)st.jc.po[c] * ld + pos] = st.jc.p[c][off + i];
+            for (int c = 0; c < st.jc.nb; ++c) dst[(uint64_t)st.jc.bo[c] * ld + pos] = st.jc.b[c][off + j];
           }
         }
         n = s_run;
-        if (n == 0 || n > st.cap) ok = false;
+        if (n > st.cap) {
+          if (parted) redo = true; else ok = false;
+        } else if (n == 0 && !parted) {
+          ok = false;
+        }
       }
     } else {   // CH_ANTI
       const uint32_t nin = s_cnt[st.in];
       if (nin <= kIjSmall) {
-        lookups_small(st.key, st.kx, st.g, nin, s_lo, s_pre);   // s_pre[r] = matches of row r's link (0 or 1)
+        lookups_small(st.key, st.kx, st.g, nin, s_lo, s_pre, (uint32_t)off);   // s_pre[r] = matches of row r's link (0 or 1)
         __syncthreads();
         for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
           const uint32_t r = r0 + threadIdx.x;
           const bool keep = r < nin && s_pre[r] == 0;
           const uint32_t pos = chain_rank(keep, s_w, &s_run);
           if (keep)
-            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+            for (uint32_t c = 0; c < st.ncopy; ++c) dst[(uint64_t)c * ld + pos] = st.copy[c][off + r];
         }
       } else {
         for (uint32_t r0 = 0; r0 < nin; r0 += kSmallBlock) {
           const uint32_t r = r0 + threadIdx.x;
-          const bool keep = r < nin && ij_lookup(st.key[r], st.kx, st.g, r).y == 0;
+          const bool keep = r < nin && ij_lookup(st.key[off + r], st.kx, st.g, off + r).y == 0;
           const uint32_t pos = chain_rank(keep, s_w, &s_run);
           if (keep)
-            for (uint32_t c = 0; c < st.ncopy; ++c) st.dst[(uint64_t)c * st.cap + pos] = st.copy[c][r];
+            for (uint32_t c = 0; c < st.ncopy; ++c) dst[(uint64_t)c * ld + pos] = st.copy[c][off + r];
         }
       }
       n = s_run;
     }
     if (threadIdx.x == 0) {
       s_cnt[si] = n;
-      if (!ok) s_state = CHS_PARTIAL;
-      else if (st.done) s_acc = si;
-      if (tstamp) tstamp[2 + si] = wall_clock64();
+      if (redo) {
+        s_state = CHS_REDO;
+      } else if (!ok) {
+        s_state = CHS_PARTIAL;
+      } else if (st.done) {
+        s_acc = si;
+      }
+      if (GRID && parted && ok && !redo) atomicAdd(&d.gsc[si], n);   // the stage's rows over all workgroups
+      if (stamp) tstamp[2 + si] = wall_clock64();
     }
     __syncthreads();
+  }
+  if constexpr (GRID) {
+    // the final rows of this workgroup go to the output table at a cursor;
+    // the last workgroup to finish publishes
+    const bool fin = s_state == CHS_OK;
+    const ChainStage& sa = d.st[s_acc];
+    const uint32_t n = fin ? s_cnt[s_acc] : 0u;
+    if (threadIdx.x == 0) {
+      if (s_state == CHS_REDO) atomicOr(&d.gsc[kGscRedo], 1u);
+      s_base = n ? atomicAdd(&d.gsc[kGscOut], n) : 0u;
+    }
+    __syncthreads();
+    if (n) {
+      const uint64_t ld = sa.ld ? sa.ld : sa.cap;
+      for (uint32_t c = 0; c < sa.ncols; ++c)
+        for (uint32_t r = threadIdx.x; r < n; r += kSmallBlock)
+          d.fin[c * d.fin_ld + s_base + r] = sa.dst[c * ld + off + r];
+    }
+    // No agent-scope fence here: on gfx950 each one writes this XCD's L2 back,
+    // and 32 workgroups per XCD doing so in turn cost ~80 us per chain.  The
+    // final rows are read by later launches (the kernel boundary makes them
+    // visible); the last workgroup reads only counters, which are atomics
+    // performed at the coherence point -- thread 0 waits for its own
+    // atomics to complete before it arrives.
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t prev = __hip_atomic_fetch_add(&d.gsc[kGscDone], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == G - 1) {
+        if (tstamp) {                                  // DAS_TRACE: the last workgroup's start and finish
+          tstamp[kChainStages + 2] = t_start;
+          tstamp[kChainStages + 3] = wall_clock64();
+        }
+        // every workgroup's counters and rows are in: the outcome
+        const uint32_t redo = __hip_atomic_load(&d.gsc[kGscRedo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t empty = 0;                            // a positive stage after the partition with no row anywhere
+        bool after = false;
+        for (uint32_t si = 0; si < d.nstage; ++si) {
+          if (after && d.st[si].op != CH_ANTI && d.st[si].op != CH_SCAN && d.st[si].done &&
+              __hip_atomic_load(&d.gsc[si], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            empty |= 1u << si;
+          after = after || d.st[si].part;
+        }
+        const uint32_t st = redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
+        const uint32_t total = st == CHS_OK ? __hip_atomic_load(&d.gsc[kGscOut], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : s_cnt[s_acc];
+        __hip_atomic_store(&slot[0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&slot[1], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&slot[2], s_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&slot[3], empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    return;
   }
   // every store of the chain is made visible before the host reads the
   // counts and (later, through other launches) the tables
@@ -3606,15 +3726,112 @@ __global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restric
   }
 }
 
+__global__ void __launch_bounds__(kSmallBlock) k_chain(const uint32_t* __restrict__ hdesc, uint32_t nwords,
+                                                       uint32_t* slot, uint32_t seq, uint64_t* tstamp) {
+  chain_body<false>(hdesc, nwords, slot, seq, tstamp);
+}
+
+// one workgroup per CU; the descriptor is read from device memory (k_chain_prep)
+__global__ void __launch_bounds__(kSmallBlock) k_chain_grid(const uint32_t* __restrict__ ddesc, uint32_t nwords,
+                                                            uint32_t* slot, uint32_t seq, uint64_t* tstamp) {
+  chain_body<true>(ddesc, nwords, slot, seq, tstamp);
+}
+
+// the grid chain's descriptor from pinned host memory into device memory
+// (every workgroup then reads it from L2, not over PCIe) and its counters zeroed
+// (the loads of one thread issued together: the host memory's latency paid once)
+__global__ void __launch_bounds__(kSmallBlock) k_chain_prep(const uint32_t* __restrict__ hdesc, uint32_t nwords,
+                                                            uint32_t* __restrict__ ddesc, uint32_t* __restrict__ gsc) {
+  constexpr uint32_t kPer = (sizeof(ChainDesc) / 4 + kSmallBlock - 1) / kSmallBlock;
+  uint32_t v[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * kSmallBlock;
+    v[k] = i < nwords ? hdesc[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * kSmallBlock;
+    if (i < nwords) ddesc[i] = v[k];
+  }
+  if (threadIdx.x < kGscWords) gsc[threadIdx.x] = 0u;
+}
+
 }  // namespace
+
+// Rows per workgroup segment of the grid chain's stage tables, and whether an
+// And's leading terms want the grid chain: a grounded scan (and scans joined
+// to it) feeding an index join whose output can outgrow the one-workgroup
+// chain -- bound = the scanned rows x the index join's largest key range
+// (type_max_run, an upper bound whatever the grounded targets) -- e.g. the
+// FlyBase F5 / F7 join on a recombination_loc shared by ~10^5 genes
+// (DESIGN.md §5).  DAS_CHAIN_GRID: 0 never, 1 whenever the shape allows.
+constexpr uint32_t kGridSeg = 4096;
+
+uint32_t cu_count(Ctx& c) {
+  static int n[64] = {0};
+  int& v = n[c.device & 63];
+  if (!v) DAS_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, c.device));
+  return (uint32_t)v;
+}
+
+bool chain_grid_wanted(Ctx& c, const std::vector<const das_plan_node_t*>& terms, size_t n_anti, bool force) {
+  if (terms.size() < 2) return false;
+  std::vector<int32_t> vars;
+  uint64_t bound = 1;
+  for (size_t k = 0; k < terms.size(); ++k) {
+    const das_plan_node_t* x = terms[k];
+    if (x->op != DAS_PLAN_LINK || !x->scan.ordered || x->dedup) return false;
+    if (k > 0 && x->index_join) {
+      const das_link_scan_t& q = x->ij;
+      int bp = -1;
+      for (uint32_t p = 0; p < q.arity && p < 8; ++p)
+        if (q.target[p] == kNone && q.var[p] >= 0 && std::find(vars.begin(), vars.end(), q.var[p]) != vars.end())
+          bp = (int)p;
+      if (bp >= 0 && q.type_id < c.idx.n_types && q.arity <= (uint32_t)kMaxPosArity) {
+        if (bound > kIjSmall) return false;           // the partition's probe is every workgroup's
+        bound *= std::max<uint64_t>(type_max_run(c, q.arity, (uint32_t)bp, q.type_id), 1);
+        const bool more = k + 1 < terms.size() || n_anti > 0;
+        return force || bound > kChainCap || (more && bound > kChainIjRows);
+      }
+    }
+    ScanPrep P;
+    scan_prepare(c, x->scan, P);
+    if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) return false;
+    const uint64_t r = P.ranges[0].second - P.ranges[0].first;
+    if (r > kGridSeg) return false;
+    bound *= std::max<uint64_t>(r, 1);
+    vars.insert(vars.end(), P.vars, P.vars + P.ncols);
+  }
+  return false;
+}
+
+int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, bool& matched,
+                  std::unique_ptr<Table>& out, uint32_t* consumed);
 
 int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
               std::unique_ptr<Table>& out, uint32_t* consumed) {
   const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
   if ((f && f[0] == '0') || no_overload || terms.empty()) return 0;
+  const char* gm = std::getenv("DAS_CHAIN_GRID");
+  const bool want_grid = !(gm && gm[0] == '0') && chain_grid_wanted(c, terms, anti.size(), gm && gm[0] == '1');
+  if (trace_on()) trace_mark(want_grid ? "chain grid" : "chain one workgroup");
+  for (int attempt = want_grid ? 0 : 1; attempt < 2; ++attempt) {
+    const int r = fused_and_run(c, terms, anti, attempt == 0, matched, out, consumed);
+    if (r >= 0) return r;                                     // -1: the grid form does not apply, try one workgroup
+  }
+  return 0;
+}
+
+int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, bool& matched,
+                  std::unique_ptr<Table>& out, uint32_t* consumed) {
   Index& idx = c.idx;
   ChainDesc d{};
+  const uint32_t G = grid ? cu_count(c) : 1u;
+  const uint64_t gcap = (uint64_t)G * kGridSeg;              // grid: every stage table holds G segments
   std::vector<std::unique_ptr<Table>> tabs;                  // one output table per stage
   std::vector<uint32_t> terms_done;                           // positive terms folded after each stage
   auto add = [&](uint32_t op) -> ChainStage* {
@@ -3624,6 +3841,14 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     st.append = kChainNoStage;
     return &st;
   };
+  // a stage's table: one workgroup -> `cap` rows; grid -> G segments of kGridSeg
+  auto place = [&](ChainStage* st, Table& t) {
+    st->cap = grid ? kGridSeg : (uint32_t)t.cap;
+    st->ld = grid ? (uint32_t)t.cap : 0u;
+    st->ncols = (uint32_t)t.ncols;
+    st->dst = t.data;
+  };
+  bool parted = false;
   // a chain ending early (too many stages) still folds the terms compiled so
   // far; the caller continues from there
   int acc = -1;                                               // stage holding the running result
@@ -3640,7 +3865,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
         if (pl.empty) { all_terms = false; break; }
         ChainStage* st = add(CH_IJ);
         if (!st) { all_terms = false; break; }
-        auto t = new_table(c, DAS_TABLE_ORDERED, (int)pl.uni.size(), pl.uni.data(), kChainCap);
+        auto t = new_table(c, DAS_TABLE_ORDERED, (int)pl.uni.size(), pl.uni.data(), grid ? gcap : kChainCap);
         if (trace_on()) trace_mark("prep new_table");
         for (size_t k = 0; k < pl.uni.size(); ++k) {
           t->lo[k] = pl.lo[k];
@@ -3648,8 +3873,9 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
         }
         st->in = (uint32_t)acc;
         st->done = 1;
-        st->cap = (uint32_t)t->cap;
-        st->dst = t->data;
+        place(st, *t);
+        st->part = grid && !parted;
+        parted = parted || grid;
         st->key = pl.akey;
         st->kx = pl.kx;
         st->g = pl.g;
@@ -3669,15 +3895,15 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
       all_terms = false;
       break;
     }
+    if (grid && e - b > kGridSeg) return -1;                 // every workgroup scans it into its segment
     ChainStage* st = add(CH_SCAN);
-    auto t = new_table(c, P.kind, P.ncols, P.vars, e - b);
+    auto t = new_table(c, P.kind, P.ncols, P.vars, grid ? gcap : e - b);
     scan_bounds(idx, P.sp, x->scan.type_id, *t);
     if (trace_on()) trace_mark("prep scan table");
     st->sp = P.sp;
     st->begin = (uint32_t)b;
     st->end = (uint32_t)e;
-    st->cap = (uint32_t)t->cap;
-    st->dst = t->data;
+    place(st, *t);
     st->done = acc < 0 ? 1 : 0;
     tabs.push_back(std::move(t));
     const int rel = (int)d.nstage - 1;
@@ -3696,12 +3922,11 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     std::set_union(va.begin(), va.end(), vb.begin(), vb.end(), std::back_inserter(uni));
     DAS_CHECK((int)uni.size() <= kMaxCols, DAS_E_UNSUPPORTED, "too many variables");
     ChainStage* js = add(CH_JOIN);
-    auto jt = new_table(c, DAS_TABLE_ORDERED, (int)uni.size(), uni.data(), kChainCap);
+    auto jt = new_table(c, DAS_TABLE_ORDERED, (int)uni.size(), uni.data(), grid ? gcap : kChainCap);
     js->in = (uint32_t)acc;
     js->rel = (uint32_t)rel;
     js->done = 1;
-    js->cap = (uint32_t)jt->cap;
-    js->dst = jt->data;
+    place(js, *jt);
     for (int32_t v : shared) {
       js->sha[js->nsh] = A.col(colof_t(A, v));
       js->shb[js->nsh++] = R.col(colof_t(R, v));
@@ -3721,6 +3946,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     acc = (int)d.nstage - 1;
   }
   if (acc < 0) return 0;
+  if (grid && !parted) return -1;                             // no index join to partition on
   const uint32_t n_anti_stage0 = d.nstage;
   bool anti_ok = all_terms;
   if (all_terms)
@@ -3744,8 +3970,7 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
       }
       st->in = (uint32_t)acc;
       st->done = 1;
-      st->cap = (uint32_t)t->cap;
-      st->dst = t->data;
+      place(st, *t);
       st->key = ap.key;
       st->kx = ap.kx;
       st->g = ap.g;
@@ -3757,15 +3982,32 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     }
   if (d.nstage < 2) return 0;                                 // one operator: nothing to fuse
   const bool complete = all_terms && anti_ok;
+  // grid: the final rows gather into one table; device copies of the
+  // descriptor and the counters
+  std::unique_ptr<Table> fin;
+  DBuf<uint32_t> gsc, dd;
+  if (grid) {
+    const Table& A = *tabs[acc];
+    fin = new_table(c, DAS_TABLE_ORDERED, A.ncols, A.vars, gcap);
+    for (int k = 0; k < A.ncols; ++k) {
+      fin->lo[k] = A.lo[k];
+      fin->hi[k] = A.hi[k];
+    }
+    gsc.alloc(kGscWords, c.s);
+    d.seg = kGridSeg;
+    d.fin = fin->data;
+    d.fin_ld = fin->cap;
+    d.gsc = gsc.p;
+  }
   // only the stages in use travel (the kernel copies them into LDS)
   const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
   static_assert(sizeof(ChainStage) % 4 == 0 && offsetof(ChainDesc, st) % 4 == 0, "word copy");
   // (DAS_TRACE: stage timestamps of the device clock after the descriptors)
   const uint64_t tsoff = (bytes + 63) & ~63ull;
-  uint8_t* hd = pinned_stage(tsoff + 8 * (kChainStages + 2));
+  uint8_t* hd = pinned_stage(tsoff + 8 * (kChainStages + 4));
   std::memcpy(hd, &d, bytes);
   uint64_t* ts = trace_on() ? reinterpret_cast<uint64_t*>(hd + tsoff) : nullptr;
-  if (ts) std::memset(ts, 0, 8 * (kChainStages + 2));
+  if (ts) std::memset(ts, 0, 8 * (kChainStages + 4));
   // algorithmic bytes known up front: the scanned index rows
   double sbytes = 0;
   for (uint32_t i = 0; i < d.nstage; ++i)
@@ -3773,26 +4015,63 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   if (trace_on()) trace_mark("prep staged");
   const PubSlot ps = pub_reserve();
   if (trace_on()) trace_mark("prep slot");
-  {
+  if (grid) {
+    dd.alloc(bytes / 4, c.s);
+    {
+      ProfScope pf(c, "k_chain_prep", 2.0 * bytes);
+      hipLaunchKernelGGL(k_chain_prep, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), dd.p,
+                         gsc.p);
+      DAS_HIP(hipGetLastError());
+    }
+    ProfScope pf(c, "k_chain_grid", sbytes);
+    hipLaunchKernelGGL(k_chain_grid, dim3(G), dim3(kSmallBlock), 0, c.s, (const uint32_t*)dd.p,
+                       (uint32_t)(bytes / 4), ps.p, ps.seq, ts);
+    DAS_HIP(hipGetLastError());
+  } else {
     ProfScope pf(c, "k_chain", sbytes);
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
                        ps.seq, ts);
     DAS_HIP(hipGetLastError());
   }
-  uint32_t w[3] = {0, 0, 0};
-  pub_wait(ps, c.s, w, 3);
+  uint32_t w[4] = {0, 0, 0, 0};
+  pub_wait(ps, c.s, w, 4);
   if (ts) {
     static const char* const kOp[] = {"?", "scan", "ij", "join", "anti"};
     trace_mark("chain copy", std::to_string((ts[1] - ts[0]) / 100.0) + " us");
     for (uint32_t i = 0; i < d.nstage && ts[2 + i]; ++i)
       trace_mark("chain stage", std::string(kOp[d.st[i].op < 5 ? d.st[i].op : 0]) + " " +
                                     std::to_string((ts[2 + i] - (i ? ts[1 + i] : ts[1])) / 100.0) + " us");
+    if (grid && ts[kChainStages + 3])
+      trace_mark("chain grid last workgroup",
+                 "started " + std::to_string(((int64_t)ts[kChainStages + 2] - (int64_t)ts[0]) / 100.0) +
+                     " us after workgroup 0, published at " +
+                     std::to_string(((int64_t)ts[kChainStages + 3] - (int64_t)ts[0]) / 100.0) + " us");
   }
   matched = false;
   out.reset();
   if (w[0] == CHS_EMPTY_SCAN) return 1;                       // a failing term: And is False
+  // grid: a segment overflowed after the partition, or a running result was
+  // empty on every workgroup (And's reset-on-empty path): the caller folds
+  // the whole And operator by operator
+  if (w[0] == CHS_REDO || (grid && w[0] == CHS_OK && w[3] != 0)) {
+    if (trace_on()) trace_mark("chain grid redo");
+    return 0;
+  }
   DAS_CHECK(w[2] < d.nstage && d.st[w[2]].done, DAS_E_INTERNAL, "fused chain: bad running result");
   const uint32_t last = w[2];
+  if (grid && w[0] == CHS_OK) {
+    DAS_CHECK(last == (uint32_t)acc, DAS_E_INTERNAL, "grid chain: bad running result");
+    if (complete && w[1] == 0) return 1;                      // nothing left after the Not filters
+    fin->nrows = w[1];
+    if (complete) {
+      matched = true;
+      out = std::move(fin);
+      return 1;
+    }
+    out = std::move(fin);
+    *consumed = terms_done[last];
+    return 2;
+  }
   if (w[0] == CHS_OK && last == d.nstage - 1 && complete) {
     if (w[1] == 0) return 1;                                  // nothing left after the Not filters
     tabs[last]->nrows = w[1];
@@ -3801,7 +4080,9 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     return 1;
   }
   // partial: the running result after terms_done[last] positive terms, no
-  // Not filter applied yet (anti stages never stop a chain)
+  // Not filter applied yet (anti stages never stop a chain); in the grid
+  // form only at or before the partition, where every workgroup holds the
+  // same rows (workgroup 0's segment is rows [0, n) of the table)
   if (d.st[last].op == CH_ANTI) return 0;                     // cannot happen (anti stages never stop); be safe
   tabs[last]->nrows = w[1];
   out = std::move(tabs[last]);

@@ -45,7 +45,7 @@ def _atom_tables(db):
     return nodes, [[h, t, tg, ct(h)] for h, (t, tg) in links.items()]
 
 
-@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "1-sparse", "1-dense", "1-rev", "0"])
+@pytest.mark.parametrize("plan", ["1", "1-unfused", "1-multi", "1-sparse", "1-dense", "1-rev", "1-grid", "0"])
 @pytest.mark.parametrize("name", FIXTURES)
 def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
     """plan 1: And / Or / Not trees folded natively (das_plan_execute), small
@@ -55,11 +55,16 @@ def test_gpu_matches_reference_on_synthetic(golden, name, plan, monkeypatch):
     in-place (lo, cnt) descriptors / the histogram + scan (the default picks
     by size, and these KBs are below the sparse floor); 1-rev: unfused, an
     And's second Link term index-joined into the first term's index at every
-    size (DAS_REV_IJ=1); plan 0: the per-operator host path."""
+    size (DAS_REV_IJ=1); 1-grid: every fused And the grid chain can take
+    through it (DAS_CHAIN_GRID=1); plan 0: the per-operator host path."""
     monkeypatch.setenv("DAS_PLAN", plan[0])
     monkeypatch.setenv("DAS_FUSED", "0" if plan in ("1-unfused", "1-rev") else "1")
     monkeypatch.setenv("DAS_REV_IJ", "1" if plan == "1-rev" else "")
     monkeypatch.setenv("DAS_UNION_MULTI", "1" if plan == "1-multi" else "0")
+    if plan == "1-grid":
+        monkeypatch.setenv("DAS_CHAIN_GRID", "1")
+    else:
+        monkeypatch.delenv("DAS_CHAIN_GRID", raising=False)
     if plan in ("1-sparse", "1-dense"):
         monkeypatch.setenv("DAS_DJ_BUILD", plan[2:])
     else:

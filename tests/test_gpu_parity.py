@@ -889,6 +889,71 @@ def test_gpu_chain_large_index_join_stage(fused, monkeypatch):
 _CHAIN_WANT = {}
 
 
+def test_gpu_grid_chain_matches_per_operator(monkeypatch):
+    """The grid form of the fused And (k_chain_grid, DAS_CHAIN_GRID=1): a
+    grounded scan feeding an index join whose output every workgroup expands a
+    slice of, then row-local stages -- index joins, a cross join with a
+    scanned term, an anti index join -- against the per-operator path
+    (DAS_FUSED=0) and, where it is cheap, the oracle.  Also: a running result
+    empty on every workgroup after the partition (reset-on-empty: redone
+    operator by operator), a segment overflowing after the partition (one
+    workgroup's rows fan out past kGridSeg = 4096: redone), and the automatic
+    choice (DAS_CHAIN_GRID unset)."""
+    from das_amd import loader
+    rng = np.random.default_rng(5)
+    b = loader.AtomBuilder()
+    C = lambda n: b.terminal("Concept", n, True)  # noqa: E731
+    hub = C("hub")
+    xs = [C(f"x{i}") for i in range(50)]
+    ys = [C(f"y{i}") for i in range(4000)]
+    zs = [C(f"z{i}") for i in range(6000)]
+    ws = [C(f"w{i}") for i in range(3)]
+    for x in xs:
+        b.expr("Rel", [hub, x])
+    for y in range(3000):                              # x0 is a hub of Rel2; the others link a few ys
+        b.expr("Rel2", [xs[0], ys[y]])
+    for i in range(1, 50):
+        for y in rng.choice(4000, 5, replace=False):
+            b.expr("Rel2", [xs[i], ys[int(y)]])
+    for y in range(4000):
+        b.expr("Rel3", [ys[y], zs[int(rng.integers(0, 6000))]])
+    for z in range(5000):                              # ys[7] fans out past a segment
+        b.expr("Rel6", [ys[7], zs[z]])
+    for w in ws[:2]:
+        b.expr("Rel4", [hub, w])
+    for y in rng.choice(4000, 1500, replace=False):
+        b.expr("Rel5", [ys[int(y)], ws[int(rng.integers(0, 2))]])
+    for z in range(20):
+        b.expr("Rel7", [zs[z], zs[z + 1]])             # keys no B reaches
+    arrays = b.finish()
+    db = _hipdb(arrays)
+    V = lambda x: ["Var", x]  # noqa: E731
+    h = ["Node", "Concept", "hub"]
+    L = lambda t, *a: ["Link", t, True, list(a)]  # noqa: E731
+    qs = [["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B"))]],
+          ["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B")), L("Rel3", V("B"), V("C"))]],
+          ["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B")), L("Rel4", h, V("W")),
+                   ["Not", L("Rel5", V("B"), V("W"))], L("Rel3", V("B"), V("C"))]],
+          ["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B")), L("Rel7", V("B"), V("C")),
+                   L("Rel3", V("B"), V("D"))]],
+          ["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B")), L("Rel6", V("B"), V("C"))]]]
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    for i, q in enumerate(qs):
+        monkeypatch.setenv("DAS_FUSED", "0")
+        want = record(q, db)
+        if i == 0:
+            assert same(want, O.evaluate(q, odb))
+        for grid in ("1", None):
+            monkeypatch.setenv("DAS_FUSED", "1")
+            if grid:
+                monkeypatch.setenv("DAS_CHAIN_GRID", grid)
+            else:
+                monkeypatch.delenv("DAS_CHAIN_GRID", raising=False)
+            got = record(q, db)
+            assert same(got, want), (i, grid, got.get("n"), want.get("n"))
+        assert want.get("n", 0) > 1000 or i == 3, (i, want.get("n"))
+
+
 def test_gpu_native_canonical_load_matches_oracle():
     """Canonical text -> native reader (canonical.cpp) -> device index: the
     queries answer as the oracle over the Python reader's atoms; nested
