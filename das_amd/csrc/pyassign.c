@@ -365,11 +365,18 @@ static int open_src(PyObject *dig, PyObject *ids, int k, Py_ssize_t n, Py_buffer
   return 0;
 }
 
-/* hex_list(digests, ids | None, n) -> [str] of column 0 */
+/* hex_list(digests, ids | None, n[, store]) -> [str] of column 0.  store:
+ * a list indexed by atom id holding each handle str made so far (None until
+ * then): repeated answers share their str objects instead of formatting
+ * them again (HipDB keeps one per prefetched KB) */
 static PyObject *hex_list(PyObject *self, PyObject *args) {
-  PyObject *dig, *ids;
+  PyObject *dig, *ids, *store = Py_None;
   Py_ssize_t n;
-  if (!PyArg_ParseTuple(args, "OOn", &dig, &ids, &n)) return NULL;
+  if (!PyArg_ParseTuple(args, "OOn|O", &dig, &ids, &n, &store)) return NULL;
+  if (store != Py_None && (!PyList_Check(store) || ids == Py_None)) {
+    PyErr_SetString(PyExc_TypeError, "hex_list: store must be a list (with ids)");
+    return NULL;
+  }
   Py_buffer db, ib;
   HexSrc h;
   if (open_src(dig, ids, 1, n, &db, &ib, &h) < 0) return NULL;
@@ -377,8 +384,28 @@ static PyObject *hex_list(PyObject *self, PyObject *args) {
   PyObject *out = c ? PyList_New(n) : NULL;
   if (c) hc_init(c);
   else PyErr_NoMemory();
+  const Py_ssize_t ns = store != Py_None ? PyList_GET_SIZE(store) : 0;
   for (Py_ssize_t r = 0; out && r < n; ++r) {
-    PyObject *s = src_str(c, &h, 0, r);
+    PyObject *s = NULL;
+    if (ns) {
+      const Py_ssize_t id = (Py_ssize_t)h.ids[r];
+      if (id < ns) {
+        PyObject *have = PyList_GET_ITEM(store, id);
+        if (have != Py_None) {
+          Py_INCREF(have);
+          PyList_SET_ITEM(out, r, have);
+          continue;
+        }
+        uint32_t aid;
+        const uint32_t *w = src_row(&h, 0, r, &aid);
+        s = w ? hex_str(w) : NULL;
+        if (s) {
+          Py_INCREF(s);
+          PyList_SetItem(store, id, s);                /* steals the extra reference; drops the None */
+        }
+      }
+    }
+    if (!s) s = PyErr_Occurred() ? NULL : src_str(c, &h, 0, r);
     if (!s) {
       Py_CLEAR(out);
       break;
@@ -444,9 +471,53 @@ static PyObject *hex_pairs(PyObject *self, PyObject *args) {
   return out;
 }
 
+/* seed(cache, strs, ids, arity) -> None: cache[strs[i]] = (ids[i], 2, arity)
+ * (strs[i] a handle str, or a (handle, targets) pair)
+ * for every handle not yet in the dict (HipDB's handle cache: the links of a
+ * pattern answer become host lookups for get_link_targets / get_link_type;
+ * the reference's Redis answers carry the same pairs, redis_mongo_db.py:235-252) */
+static PyObject *seed(PyObject *self, PyObject *args) {
+  PyObject *cache, *strs, *ids;
+  long arity;
+  if (!PyArg_ParseTuple(args, "O!O!Ol", &PyDict_Type, &cache, &PyList_Type, &strs, &ids, &arity)) return NULL;
+  Py_buffer ib;
+  if (get_u32(ids, &ib, "ids") < 0) return NULL;
+  const Py_ssize_t n = PyList_GET_SIZE(strs);
+  if (ib.len / 4 < n) {
+    PyBuffer_Release(&ib);
+    PyErr_SetString(PyExc_ValueError, "seed: fewer ids than handles");
+    return NULL;
+  }
+  const uint32_t *id = (const uint32_t *)ib.buf;
+  PyObject *two = PyLong_FromLong(2), *ar = PyLong_FromLong(arity);
+  int bad = !two || !ar;
+  for (Py_ssize_t i = 0; !bad && i < n; ++i) {
+    PyObject *h = PyList_GET_ITEM(strs, i);
+    if (PyTuple_Check(h) && PyTuple_GET_SIZE(h) > 0) h = PyTuple_GET_ITEM(h, 0);   /* a (link, targets) pair */
+    const int has = PyDict_Contains(cache, h);
+    if (has < 0) { bad = 1; break; }
+    if (has) continue;
+    PyObject *v = PyTuple_New(3), *x = v ? PyLong_FromUnsignedLong(id[i]) : NULL;
+    if (!x) { Py_XDECREF(v); bad = 1; break; }
+    PyTuple_SET_ITEM(v, 0, x);
+    Py_INCREF(two);
+    PyTuple_SET_ITEM(v, 1, two);
+    Py_INCREF(ar);
+    PyTuple_SET_ITEM(v, 2, ar);
+    if (PyDict_SetItem(cache, h, v) < 0) bad = 1;
+    Py_DECREF(v);
+  }
+  Py_XDECREF(two);
+  Py_XDECREF(ar);
+  PyBuffer_Release(&ib);
+  if (bad) return NULL;
+  Py_RETURN_NONE;
+}
+
 static PyObject *fast_hash_enabled(PyObject *self, PyObject *noargs);
 
 static PyMethodDef methods[] = {
+    {"seed", seed, METH_VARARGS, "Seed the handle cache with (id, 2, arity) per new link handle."},
     {"add_rows", add_rows, METH_VARARGS, "Add Assignment objects built from a binding table to a set."},
     {"format_set", format_set, METH_VARARGS, "str() of a set of assignments."},
     {"hex_list", hex_list, METH_VARARGS, "Handle strs of n atoms (digest table + ids, or gathered digests)."},

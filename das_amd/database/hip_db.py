@@ -120,6 +120,7 @@ class HipDB(RelationalDB):
         self.generation = 0
         self.shard = None
         self._mirror = None
+        self._hstore = None
         self._outgoing = None
         self._node_dir = None
         self.pattern_black_list = []
@@ -146,6 +147,7 @@ class HipDB(RelationalDB):
         self._hex_cache = {}
         self._handle_cache = {}
         self._mirror = None
+        self._hstore = None
         self._outgoing = None
         self._node_dir = None
 
@@ -228,6 +230,12 @@ class HipDB(RelationalDB):
         ids = np.asarray(ids, dtype=np.uint32).ravel()
         if ids.size == 0:
             return []
+        if _hex is not None and self._mirror is not None:
+            # digests on the host (prefetch): every handle formatted in C,
+            # once per atom (the store keeps the str objects made so far)
+            if self._hstore is None:
+                self._hstore = [None] * len(self._mirror[0])
+            return _hex.hex_list(self._mirror[0], ids, ids.size, self._hstore)
         if ids.size > self.HEX_DIRECT:
             # a large answer: its digests straight from the mirror (prefetch)
             # or one device gather, formatted in one pass (no per-id cache work)
@@ -399,14 +407,48 @@ class HipDB(RelationalDB):
             # the links of a pattern answer are indexed here (category 2): a
             # caller's next get_link_targets / link lookups of them (the
             # SimplePatternMiner halo walk) need no device lookup
-            hc = self._handle_cache
-            if len(hc) > (1 << 23):
-                hc.clear()
-            if n <= self.SEED_MAX:
-                for h, i in zip(links if links is not None else (p[0] for p in out), cols[0].tolist()):
-                    if h not in hc:
-                        hc[h] = (i, 2, arity)
+            self._seed(links if links is not None else out, cols[0], arity)
             return out
+        finally:
+            if enabled:
+                gc.enable()
+
+    def _seed(self, strs, ids, arity):
+        """The links of a pattern answer are indexed here (category 2): a
+        caller's next get_link_targets / link lookups of them (the
+        SimplePatternMiner halo walk) need no device lookup.  strs: handle
+        strs or (handle, targets) pairs, ids: their atom ids."""
+        hc = self._handle_cache
+        if len(hc) > (1 << 23):
+            hc.clear()
+        if len(strs) > self.SEED_MAX:
+            return
+        if _hex is not None:
+            _hex.seed(hc, strs, np.ascontiguousarray(ids, dtype=np.uint32), arity)
+            return
+        for h, i in zip(strs, np.asarray(ids).tolist()):
+            if not isinstance(h, str):
+                h = h[0]
+            if h not in hc:
+                hc[h] = (i, 2, arity)
+
+    def get_matched_link_handles(self, link_type: str, target_handles: List[str]) -> List[str]:
+        """[h for h, _ in get_matched_links(link_type, target_handles)]
+        without building the target lists: what the facade's get_links
+        returns in its default HANDLE format (distributed_atom_space.py:
+        259-284), e.g. SimplePatternMiner's len(get_links(...)) counts."""
+        if link_type != WILDCARD and WILDCARD not in target_handles:
+            return self.get_matched_links(link_type, target_handles)
+        t = self.matched_links_table(link_type, target_handles)
+        if t is None or t.nrows == 0:
+            return []
+        ids = np.ascontiguousarray(t.fetch()[0])
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            links = self.hex_of(ids)
+            self._seed(links, ids, len(target_handles))
+            return links
         finally:
             if enabled:
                 gc.enable()

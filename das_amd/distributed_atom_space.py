@@ -160,6 +160,10 @@ class DistributedAtomSpace:
             link_type = WILDCARD
         if target_types is not None and link_type != WILDCARD:
             db_answer = self.db.get_matched_type_template([link_type, *target_types])
+        elif targets is not None and output_format == QueryOutputFormat.HANDLE and \
+                hasattr(self.db, "get_matched_link_handles"):
+            # the handles alone: no (link, targets) rows built only to be dropped
+            return self.db.get_matched_link_handles(link_type, targets)
         elif targets is not None:
             db_answer = self.db.get_matched_links(link_type, targets)
         elif link_type != WILDCARD:

@@ -1251,3 +1251,46 @@ def test_gpu_table_checksum_matches_oracle_rows():
             got = CK.answer_checksum(ans)
             assert got[1] == want["n"], name
             assert got[0] == CK.rows_checksum(dict(r[1]) for r in want["rows"]), name
+
+
+@pytest.mark.parametrize("ranged", ["1", "0"])
+def test_gpu_ranged_index_join_long_ranges(ranged, monkeypatch):
+    """Index joins whose grounded key holds a long row range (the ranged
+    mode's interpolation window, narrow_eq): probe values below, above and
+    between the range's keys, keys with runs longer than the 32-value
+    window, repeated probe values, and keys at both ends of the range --
+    against the oracle, ranged mode forced (1) and off (0)."""
+    from das_amd import loader
+    monkeypatch.setenv("DAS_IJ_RANGED", ranged)
+    monkeypatch.setenv("DAS_INDEX_JOIN", "1")
+    rng = np.random.default_rng(21)
+    b = loader.AtomBuilder()
+    C = lambda n: b.terminal("Concept", n, True)  # noqa: E731
+    sch = C("schema")
+    other = C("other")
+    ks = [C(f"k{i}") for i in range(3000)]
+    vs = [C(f"v{i}") for i in range(50)]
+    probes = [C(f"p{i}") for i in range(40)]
+    for i in range(3000):
+        if i % 7 == 3:
+            continue                                   # keys absent from the range
+        reps = 120 if i in (0, 1500, 2999) else (40 if i % 97 == 0 else 1 + i % 3)
+        for r in range(reps):
+            b.expr("Exec", [sch, ks[i], vs[(i + r) % 50]])
+        b.expr("Exec", [other, ks[i], vs[i % 50]])
+    for p in probes:
+        for k in rng.choice(3000, 30, replace=False).tolist() + [0, 1500, 2999, 3, 97]:
+            b.expr("Has", [p, ks[int(k)]])
+    arrays = b.finish()
+    db = _hipdb(arrays)
+    odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    V = lambda x: ["Var", x]  # noqa: E731
+    L = lambda t, *a: ["Link", t, True, list(a)]  # noqa: E731
+    s = ["Node", "Concept", "schema"]
+    for pi in (0, 7, 39):
+        p = ["Node", "Concept", f"p{pi}"]
+        q = ["And", [L("Has", p, V("K")), L("Exec", s, V("K"), V("W"))]]
+        want = O.evaluate(q, odb)
+        got = record(q, db)
+        assert want.get("n", 0) > 100
+        assert same(got, want), (pi, got.get("n"), want.get("n"))
