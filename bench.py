@@ -1073,7 +1073,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if workload == "bio" and world == 1 and not args.no_extras and dominant:
         join_k = q2_join_kernel()
     db.ctx.prof_reset()
-    db.ctx.prof_only(",".join(k for k in ((dominant or {}).get("kernel"), join_k) if k) or None)
+    db.ctx.prof_only("|".join(k for k in ((dominant or {}).get("kernel"), join_k) if k) or None)
     tag_q2[0] = join_k is not None
     db.ctx.prof_enable(True)
     if dist:

@@ -160,13 +160,13 @@ struct Ctx {
   // a copy (2: scans up to kViewRows rows, 1: all, 0: none); views are
   // materialised before a table leaves the plan
   int scan_views = 0;
-  std::string prof_only;             // non-empty: only scopes of these names (comma-separated) record events
+  std::string prof_only;             // non-empty: only scopes of these names ('|'-separated) record events
   std::string prof_tag;              // non-empty: recorded scopes are named "<scope>@<tag>" (one query's launches)
   bool prof_selected(const std::string& name) const {
     if (prof_only.empty()) return true;
     size_t b = 0;
     while (b <= prof_only.size()) {
-      size_t e = prof_only.find(',', b);
+      size_t e = prof_only.find('|', b);
       if (e == std::string::npos) e = prof_only.size();
       if (prof_only.compare(b, e - b, name) == 0) return true;
       b = e + 1;

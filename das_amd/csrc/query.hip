@@ -1019,7 +1019,7 @@ struct JoinCols {
   int np, nb;
   int search;                    // bit 0: owner lanes by the 6-step ds_bpermute search (DAS_OWNER_SEARCH=1, A/B);
                                  // bit 1: no 16-byte paths (DAS_DJ_VEC=0); bit 2: no quad path
-                                 // (DAS_DJ_VEC=1)
+                                 // (DAS_DJ_VEC=1); bit 3: no run path in the filtered walk (DAS_FILT_RUN=0)
 };
 
 // DAS_OWNER_SEARCH=1: the expansions find each output's owner lane by the
@@ -1029,7 +1029,9 @@ struct JoinCols {
 inline int owner_search_env() {
   const char* e = std::getenv("DAS_OWNER_SEARCH");
   const char* v = std::getenv("DAS_DJ_VEC");
-  return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0) | (v && v[0] == '1' ? 4 : 0);
+  const char* fr = std::getenv("DAS_FILT_RUN");
+  return (e && e[0] == '1' ? 1 : 0) | (v && v[0] == '0' ? 2 : 0) | (v && v[0] == '1' ? 4 : 0) |
+         (fr && fr[0] == '0' ? 8 : 0);
 }
 
 template <int NP, int NB, typename T, int V, bool NT = false>
@@ -1324,8 +1326,52 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
             if (i < ncp) pv[i] = r < np ? pp[i][r] : 0u;
         }
         const uint32_t exp = e[g].x - pre;           // br = (ex - pre)[owner] + o
-        // XU rounds of 64 outputs resolved before their loads issue
-        for (uint32_t o0 = rs; o0 < re; o0 += 64 * XU) {
+        // Run path (one walk, one build column -- the filtered one): 256
+        // consecutive outputs of ONE probe row (a hub's run of P rows) are
+        // consecutive build rows: each lane tests 4 of them with one 16-byte
+        // load and 4 bitmap words, and the kept ones leave compacted by a
+        // wave prefix sum -- instead of 4 rounds of owner lanes, 4-byte
+        // gathers and ballots (DAS_DJ_VEC=0: off)
+        const bool runs = MODE == 2 && ncb == 1 && fk.bcol == 0 && !(jc.search & 10) && (re - rs) > 256u;
+        for (uint32_t o0 = rs; o0 < re;) {
+          if (runs && re - o0 >= 256u) {
+            const uint64_t m0 = __ballot(pre <= o0);
+            const int l0 = 63 - __clzll((long long)m0);
+            const uint64_t m1 = __ballot(pre <= o0 + 255u);
+            if (63 - __clzll((long long)m1) == l0) {
+              const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)exp, l0) + o0 + 4u * (uint32_t)lane;
+              const u32x4_a4 x = *reinterpret_cast<const u32x4_a4*>(fk.col + b0);
+              const uint32_t v[4] = {x.x - fk.lo, x.y - fk.lo, x.z - fk.lo, x.w - fk.lo};
+              uint32_t wd[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) wd[k] = v[k] < fk.range ? fk.bits[v[k] >> 5] : 0u;
+              bool f[4];
+              uint32_t cnt = 0;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                f[k] = v[k] < fk.range && ((wd[k] >> (v[k] & 31)) & 1u);
+                cnt += f[k] ? 1u : 0u;
+              }
+              const uint32_t inc = wave_inclusive_scan(cnt);
+              const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+              uint64_t pos = obase + run + (inc - cnt);
+              uint32_t pvl[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) pvl[i] = i < ncp ? (uint32_t)__builtin_amdgcn_readlane((int)pv[i], l0) : 0u;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                if (!f[k]) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  if (i < ncp) po[i][pos] = pvl[i];
+                bo[0][pos] = v[k] + fk.lo;
+                ++pos;
+              }
+              run += tot;
+              o0 += 256u;
+              continue;
+            }
+          }
           const int nr = (re - o0) >= 64u * XU ? XU : (int)((re - o0 + 63) / 64);
           uint32_t o[XU], br[XU];
           int ll[XU];
@@ -1409,6 +1455,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
               }
             }
           }
+          o0 += 64u * XU;
         }
       }
     }

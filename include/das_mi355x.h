@@ -401,7 +401,7 @@ int das_prof_enable(das_ctx_t* ctx, int on);
 /* Restrict event recording to the scopes named `name` (NULL or "" = every
  * scope): the bench times its dominant kernel live without paying two event
  * records per launch for every other kernel. */
-int das_prof_only(das_ctx_t* ctx, const char* name);   /* name: one scope or a comma-separated list */
+int das_prof_only(das_ctx_t* ctx, const char* name);   /* name: one scope or a '|'-separated list */
 /* Scopes recorded while a tag is set are named "<scope>@<tag>" (NULL or "" =
  * none): one query's launches of a kernel other queries launch too are timed
  * apart inside a step (bench.py's in-step And-join fraction). */
