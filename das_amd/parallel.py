@@ -119,12 +119,23 @@ class ShardedDB(RelationalDB):
         # the top-level expression of the current ShardedMatcher call, and the
         # round-robin owner of the next wholly gathered top-level plan
         self._top = None
+        self._tops = set()          # ids of the top-level expressions of a batch (ShardedMatcher.count_many)
+        self._no_plan = set()       # ids of batch expressions that fell back: the operator fold
         self._gather_seq = 0
         # a key bucket is heavy when its rows (both sides) exceed this fraction
         # of one rank's fair share of the join's rows (DAS_HEAVY_FRAC, tests)
         self.heavy_frac = float(os.environ.get("DAS_HEAVY_FRAC", "1.0"))
 
     # ------------------------------------------------------------ collectives
+    @property
+    def pattern_black_list(self):
+        """The local engine's load-time pattern black list (HipDB.load_arrays)."""
+        return self.local.pattern_black_list
+
+    @pattern_black_list.setter
+    def pattern_black_list(self, value):
+        self.local.pattern_black_list = list(value)
+
     def _allreduce_sum(self, values):
         t = self.local.xfer_tensor(np.asarray(values, dtype=np.int64))
         self.dist.all_reduce(t, group=self.group)
@@ -356,7 +367,56 @@ class ShardedDB(RelationalDB):
         all-gather (collective 2).  The fold assumes the split running result
         non-empty where it tests it; the final all-reduce of the result rows
         and of those tests' outcomes (collective 3) confirms it, or the
-        expression falls back (pattern_matcher.py:705-748 semantics either way)."""
+        expression falls back (pattern_matcher.py:705-748 semantics either way).
+        One expression of plan_many."""
+        return self.plan_many([(expr, answer)])[0]
+
+    def plan_many(self, items):
+        """plan_sharded for several independent expressions at once -- a
+        step's queries -- with their collectives shared: ONE estimate
+        all-gather for every leaf no cache settles, ONE all-to-all carrying
+        every expression's gathered terms (to every shard, or to the owner
+        of a wholly gathered top-level plan), ONE all-reduce of every
+        expression's outcome (result rows, schema / overflow flags, the
+        split running results' non-empty tests).  items: (expr, answer)
+        pairs; returns each expression's matched() or None (that expression
+        falls back to the operator fold, on every shard alike).  Every shard
+        takes the same decisions in the same order from collective results
+        only, so every shard issues the same collectives."""
+        res = [None] * len(items)
+        sts = []
+        for k, (expr, answer) in enumerate(items):
+            st = None if id(expr) in self._no_plan else self._plan_prepare(expr, answer)
+            if st is not None:
+                st["k"] = k
+                sts.append(st)
+        if not sts:
+            return res
+        self._plan_sizes([st for st in sts if st["leaves_sized"]])            # collective 1 (or none)
+        ready = []
+        for st in sts:
+            if self._plan_place(st):
+                ready.append(st)
+        self._plan_gather([st for st in ready if st["gathered"]])             # collective 2 (or none)
+        vecs = []
+        for st in ready:
+            self._plan_evaluate(st)
+            if st.get("vec") is not None:
+                vecs.append(st)
+        if vecs:                                                              # collective 3 (or none)
+            got = self._allreduce_sum(np.concatenate([st["vec"] for st in vecs]))
+            o = 0
+            for st in vecs:
+                m = len(st["vec"])
+                st["got"] = got[o:o + m]
+                o += m
+        for st in ready:
+            res[st["k"]] = self._plan_finish(st)
+        return res
+
+    def _plan_prepare(self, expr, answer):
+        """Phase 1 (local): the lowered plan and its shape; None when it is
+        not a sharded native plan."""
         from .pattern_matcher import pattern_matcher as pm
         from . import _lib as L
         db = getattr(self.local, "db", None)
@@ -396,18 +456,97 @@ class ShardedDB(RelationalDB):
                     flat = False
                     break
             flat = flat and i == n
-        ctx = db.ctx
         single = op[0] == L.PLAN_LINK and not rec[0, 3]
-        if single:
-            local, gathered = [0], []
-        elif op[0] == L.PLAN_LINK:
+        if op[0] == L.PLAN_LINK and not single:
             return None                                  # one '*'-type / repeated-variable Link: host fold
-        elif not leaves:
-            local, gathered = [], []                     # settled on the host: the same on every shard
-        else:
-            G, M = self._leaf_sizes(ctx, db, nodes, n, rec, leaves)                 # collective 1, or cached
+        st = {"expr": expr, "answer": answer, "db": db, "ctx": db.ctx, "nodes": nodes, "n": n, "rec": rec,
+              "op": op, "leaves": leaves, "pos": pos, "neg": neg, "flat": flat, "single": single,
+              "no_overload": no_overload, "top": expr is self._top or id(expr) in self._tops,
+              "gathered": [], "local": []}
+        st["leaves_sized"] = not single and bool(leaves)
+        if single:
+            st["local"] = [0]
+        return st
+
+    def _plan_sizes(self, sts):
+        """Phase 2: (G, M) per leaf of every plan -- its rows over all shards and
+        on the largest one.  Exact from the estimate exchange (one all-gather
+        of every shard's das_plan_estimates, with its das_plan_bounds riding
+        along, for every plan at once), or -- when every leaf of a plan was
+        seen before -- from the caches that exchange fills: a leaf's exact
+        sizes by its words (a term that repeats, e.g. FlyBase's unanchored
+        E(rec, V2, V1)), else its shape's upper bounds (a fresh anchor of a
+        known shape); then the plan needs no exchange.  Bounds only raise
+        gather slot sizes and split decisions, never the answer.  The caches
+        fill from collective results, so every shard holds the same."""
+        if not sts:
+            return
+        db = sts[0]["db"]
+        if self._size_gen != db.generation:
+            self._size_gen = db.generation
+            self._exact_sizes, self._shape_sizes = {}, {}
+        small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
+        miss = []
+        for st in sts:
+            rec, leaves = st["rec"], st["leaves"]
+            st["keys"] = [rec[i].tobytes() for i in leaves]
+            st["skeys"] = [self._shape_key(rec[i]) for i in leaves]
+            G, M = {}, {}
+            hit_all = os.environ.get("DAS_SHARD_SIZE_CACHE") != "0"
+            if hit_all:
+                for i, k, sk in zip(leaves, st["keys"], st["skeys"]):
+                    hit = self._exact_sizes.get(k)
+                    if hit is None:
+                        # a shape bound only where it settles the leaf as small
+                        # (gathered); a large bound (a hub key somewhere) needs
+                        # the exact sizes for the split decision
+                        hit = self._shape_sizes.get(sk)
+                        if hit is not None and hit[0] > small:
+                            hit = None
+                    if hit is None:
+                        hit_all = False
+                        break
+                    G[i], M[i] = hit
+            st["G"], st["M"] = G, M
+            if hit_all:
+                self.plan_stats["size_cache"] += 1
+            else:
+                miss.append(st)
+        if not miss:
+            return
+        parts = []
+        for st in miss:
+            ctx, nodes, n, leaves = st["ctx"], st["nodes"], st["n"], st["leaves"]
+            b = ctx.plan_bounds(nodes, n)[leaves]
+            parts.append(np.concatenate([ctx.plan_estimates(nodes, n)[leaves].astype(np.int64),
+                                         np.where(b == np.uint64(2 ** 64 - 1), -1, b.astype(np.int64))]))
+        got = self._allgather_i64(np.concatenate(parts))
+        if len(self._exact_sizes) > self.SIZE_CACHE:
+            self._exact_sizes.clear()
+        if len(self._shape_sizes) > self.SIZE_CACHE:
+            self._shape_sizes.clear()
+        o = 0
+        for st in miss:
+            nl = len(st["leaves"])
+            est, bnd = got[:, o:o + nl], got[:, o + nl:o + 2 * nl]
+            o += 2 * nl
+            for j, i in enumerate(st["leaves"]):
+                st["G"][i], st["M"][i] = int(est[:, j].sum()), int(est[:, j].max())
+                self._exact_sizes[st["keys"][j]] = (st["G"][i], st["M"][i])
+                if (bnd[:, j] >= 0).all():
+                    self._shape_sizes[st["skeys"][j]] = (int(bnd[:, j].sum()), int(bnd[:, j].max()))
+
+    def _plan_place(self, st):
+        """Phase 3 (local, from the sizes): which terms stay split, which are
+        gathered, and the owner of a wholly gathered top-level plan; False
+        when the plan does not apply (every shard decides alike)."""
+        from . import _lib as L
+        rec, op, leaves, pos = st["rec"], st["op"], st["leaves"], st["pos"]
+        db, ctx = st["db"], st["ctx"]
+        if not st["single"] and leaves:
+            G = st["G"]
             local = []
-            if flat:
+            if st["flat"]:
                 small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
                 # split candidates: Links whose rows are distinct across shards
                 big = [i for i in pos if op[i] == L.PLAN_LINK and not rec[i, 3] and G[i] > small]
@@ -428,51 +567,189 @@ class ShardedDB(RelationalDB):
                         moved = sum(4 * int(rec[i, L.PLAN_SCAN]) * G[i] * (self.world - 1) for i in big if i != top)
                         if moved > int(os.environ.get("DAS_SHARD_GATHER_BUDGET", self.GATHER_BUDGET)):
                             self.plan_stats["split_fold"] = self.plan_stats.get("split_fold", 0) + 1
-                            return None
+                            return False
                         local = [top]
                 else:
                     local = big
             gathered = [i for i in leaves if i not in local]
             if sum(G[i] for i in gathered) > self.GATHER_LIMIT:
-                return None
+                return False
+            st["local"], st["gathered"] = local, gathered
         # a wholly gathered top-level expression is evaluated by ONE shard
         # (round robin over such plans, the same on every shard): its inputs
         # go to that shard only, the others skip the native call and take
-        # the answer's size, flags and table schemas from one all-reduce
-        owner = None
-        if not local and expr is self._top and self.world > 1 and os.environ.get("DAS_GATHERED_OWNER") != "0":
-            owner = self._gather_seq % self.world
+        # the answer's size, flags and table schemas from the all-reduce
+        st["owner"] = None
+        if not st["local"] and st["top"] and self.world > 1 and os.environ.get("DAS_GATHERED_OWNER") != "0":
+            st["owner"] = self._gather_seq % self.world
             self._gather_seq += 1
         # gathered terms: this shard's rows, all-gathered into every shard --
-        # or sent to the owner only (collective 2); a term whose rows may
-        # repeat ('*' type, repeated variable) is deduplicated after
-        tables = [ctx.scan_words(nodes, i) for i in gathered]
-        inputs = self._gather_many(tables, [M[i] for i in gathered], owner) if gathered else []
-        if inputs is None and owner is None:
-            return None                                  # an estimate below the rows: the operator fold
-        if inputs is not None:
-            inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(gathered, inputs)]
-        words = nodes.copy().reshape(n, W)
-        for slot, i in enumerate(gathered):
+        # or sent to the owner only; a term whose rows may repeat ('*' type,
+        # repeated variable) is deduplicated after
+        st["tables"] = [ctx.scan_words(st["nodes"], i) for i in st["gathered"]]
+        st["caps"] = [st["M"][i] for i in st["gathered"]]
+        st["inputs"] = []
+        return True
+
+    def _plan_gather(self, sts):
+        """Phase 4: every plan's gathered terms in ONE all-to-all: a plan's
+        block (per table a header of row count and column bounds, then its
+        rows in a slot of its largest estimate, row-major) goes to every shard,
+        or to its owner only.  A table with more rows than its slot (an
+        estimate below the rows) is sent as the count OVER with no rows: the
+        receivers' plan falls back -- on every shard alike for an all-gathered
+        plan; an owner's plan carries the fallback in its all-reduce."""
+        if not sts:
+            return
+        import torch
+        loc = self.local
+        gpu = loc.gpu
+        lay = []                                  # per plan: (H, offsets, width) of its block
+        for st in sts:
+            tables = st["tables"]
+            H = sum(1 + 2 * len(t.vars) for t in tables)
+            offs, off = [], H
+            for c, t in zip(st["caps"], tables):
+                offs.append(off)
+                off += int(c) * max(len(t.vars), 1)
+            lay.append((H, offs, off))
+        dests = [[d for d in range(self.world) if st["owner"] is None or st["owner"] == d] for st in sts]
+        # the send buffer: for each destination, the blocks of the plans it
+        # receives, in plan order (the same layout on every shard)
+        send_sizes = [sum(lay[j][2] for j in range(len(sts)) if d in dests[j]) for d in range(self.world)]
+        blk = torch.zeros(sum(send_sizes), dtype=torch.int32, device=gpu)
+        base = {}
+        o = 0
+        for d in range(self.world):
+            for j in range(len(sts)):
+                if d in dests[j]:
+                    base[(j, d)] = o
+                    o += lay[j][2]
+        if not loc.stream_ordered:
+            torch.cuda.current_stream().synchronize()
+        for j, st in enumerate(sts):
+            H, offs, width = lay[j]
+            hdr = []
+            over = []
+            for t, c in zip(st["tables"], st["caps"]):
+                ov = t.nrows > int(c)
+                over.append(ov)
+                lo, hi = t.bounds()
+                hdr += [self.OVER if ov else t.nrows] + list(lo) + list(hi)
+            h = torch.from_numpy(np.array(hdr, dtype=np.uint32).view(np.int32)).to(gpu)
+            # one shard's block, then copied to each further destination
+            d0 = dests[j][0]
+            b0 = base[(j, d0)]
+            blk[b0:b0 + H] = h
+            for t, tof, ov in zip(st["tables"], offs, over):
+                if t.nrows and not ov:
+                    loc.db.ctx.export_rows(t, blk.data_ptr() + 4 * (b0 + tof))
+            if not loc.stream_ordered:
+                loc.db.ctx.sync()
+            for d in dests[j][1:]:
+                bd = base[(j, d)]
+                blk[bd:bd + width] = blk[b0:b0 + width]
+        if not loc.stream_ordered:
+            loc.db.ctx.sync()
+        stage = blk if loc.dev == gpu else blk.cpu()
+        mine = [j for j in range(len(sts)) if self.rank in dests[j]]
+        per_src = sum(lay[j][2] for j in mine)
+        out = torch.empty(self.world * per_src, dtype=torch.int32, device=stage.device)
+        self.dist.all_to_all_single(out, stage, output_split_sizes=[per_src] * self.world,
+                                    input_split_sizes=send_sizes, group=self.group)
+        self.plan_stats["collectives"] += 1
+        out_dev = out.to(gpu)
+        # the headers of the blocks this shard received, in one copy to the host
+        hcols, o = [], 0
+        for j in mine:
+            hcols += range(o, o + lay[j][0])
+            o += lay[j][2]
+        heads_all = (out.view(self.world, per_src)[:, torch.tensor(hcols, dtype=torch.long, device=out.device)]
+                     .cpu().numpy().view(np.uint32)) if hcols else None
+        if not loc.stream_ordered:
+            torch.cuda.current_stream().synchronize()
+        o = 0
+        ho = 0
+        for j in mine:
+            st = sts[j]
+            H, offs, width = lay[j]
+            heads = heads_all[:, ho:ho + H]
+            ho += H
+            tables = st["tables"]
+            cnt_cols = np.cumsum([0] + [1 + 2 * len(t.vars) for t in tables[:-1]])
+            if (heads[:, cnt_cols] == self.OVER).any():
+                self.plan_stats["gather_overflow"] = self.plan_stats.get("gather_overflow", 0) + 1
+                st["inputs"] = None
+                o += width
+                continue
+            result = []
+            h = 0
+            for t, tof in zip(tables, offs):
+                k = len(t.vars)
+                cnt = heads[:, h].astype(np.int64)
+                lo = heads[:, h + 1:h + 1 + k]
+                hi = heads[:, h + 1 + k:h + 1 + 2 * k]
+                h += 1 + 2 * k
+                parts = [loc.db.ctx.import_rows(t.kind, list(t.vars), out_dev.data_ptr() + 4 * (r * per_src + o + tof),
+                                                int(cnt[r]), t.members) for r in range(self.world) if cnt[r]]
+                g = parts[0] if len(parts) == 1 else (loc.db.ctx.concat(parts) if parts else
+                                                      loc.db.ctx.import_rows(t.kind, list(t.vars), None, 0, t.members))
+                has = cnt > 0
+                if has.any() and k:
+                    g.set_bounds(lo[has].min(axis=0), hi[has].max(axis=0))
+                result.append(g)
+            st["inputs"] = result
+            o += width
+        for j, st in enumerate(sts):
+            if j not in mine:
+                st["inputs"] = "elsewhere"
+        if not loc.stream_ordered:
+            loc.db.ctx.sync()
+        del out_dev
+
+    def _plan_evaluate(self, st):
+        """Phase 5 (local): the native call where this shard evaluates the
+        plan, and the vector this plan adds to the shared all-reduce (None
+        when it needs none)."""
+        from . import _lib as L
+        ctx, rec, op, n = st["ctx"], st["rec"], st["op"], st["n"]
+        st["vec"] = None
+        inputs = st["inputs"]
+        if inputs is not None and inputs != "elsewhere":
+            inputs = [ctx.dedup(t) if rec[i, 3] and t.nrows else t for i, t in zip(st["gathered"], inputs)]
+        words = st["nodes"].copy().reshape(n, L.PLAN_WORDS)
+        for slot, i in enumerate(st["gathered"]):
             words[i, 0] = L.PLAN_INPUT
             words[i, 2] = slot
         words = words.reshape(-1)
-        if owner is not None:
-            return self._owner_plan(ctx, words, n, inputs, no_overload, answer, owner)          # collective 3
-        matched, negation, out, checks = ctx.plan_execute_sharded(words, n, inputs, no_overload)
-        del inputs, tables
-        if not local:
-            # every shard holds the whole answer: shard 0 keeps it
-            total = sum(t.nrows for t in out)
-            if self.rank != 0:
-                out = [self.local.empty_table(t.kind, list(t.vars), t.members) for t in out]
-            rel = DRel(out)
-            rel._global = total
-        else:
+        st["tables"] = None
+        if st["owner"] is not None:
+            # an owner-evaluated plan: the owner evaluates, every shard learns
+            # the answer's size, flags and table schemas
+            K, Wd = self.OWNER_TABLES, 2 + 2 * L_MAXCOLS
+            vec = np.zeros(5 + K * Wd, dtype=np.int64)
+            st["out"] = []
+            if self.rank == st["owner"] and inputs is None:
+                vec[4] = 1
+            elif self.rank == st["owner"]:
+                matched, negation, out, _ = ctx.plan_execute_sharded(words, n, inputs, st["no_overload"])
+                vec[0] = sum(t.nrows for t in out)
+                vec[1], vec[2], vec[3] = int(matched), int(negation), len(out)
+                self._describe(out[:K], vec[5:])
+                st["out"] = out
+            st["vec"] = vec
+            return
+        if inputs is None:
+            st["fallback"] = True                        # an estimate below the rows: the operator fold
+            return
+        matched, negation, out, checks = ctx.plan_execute_sharded(words, n, inputs, st["no_overload"])
+        st["matched"], st["negation"], st["out"], st["checks"] = matched, negation, out, checks
+        if st["local"]:
             # the tested running results must hold rows on some shard: after
             # each positive term from the first split one up to (not
             # including) the last, whose emptiness is just the answer's
-            first = min(pos.index(i) for i in local) if not single else 0
+            single, pos = st["single"], st["pos"]
+            first = min(pos.index(i) for i in st["local"]) if not single else 0
             need = list(range(first, len(checks) - 1)) if not single else []
             # one ordered table per shard, the And's schema (sorted variable
             # ids of its positive terms), even where this shard has no rows:
@@ -485,8 +762,50 @@ class ShardedDB(RelationalDB):
             bad = int(len(out) > 1 or any(t.kind != L.TABLE_ORDERED or list(t.vars) != vars_ for t in out))
             if not out:
                 out = [self.local.empty_table(L.TABLE_ORDERED, vars_)]
-            got = self._allreduce_sum([sum(t.nrows for t in out), bad] +
-                                      [int(checks[j]) for j in need])                               # collective 3
+            st["out"] = out
+            st["vec"] = np.array([sum(t.nrows for t in out), bad] + [int(checks[j]) for j in need], dtype=np.int64)
+
+    def _plan_finish(self, st):
+        """Phase 6: the answer from the shared all-reduce (or, for a plan every
+        shard evaluated whole, shard 0's tables); None = fall back."""
+        from . import _lib as L
+        answer = st["answer"]
+        if st.get("fallback"):
+            return None
+        if st["owner"] is not None:
+            got, owner = st["got"], st["owner"]
+            if int(got[4]):
+                self.plan_stats["native_fallback"] += 1
+                return None
+            K, Wd = self.OWNER_TABLES, 2 + 2 * L_MAXCOLS
+            out = st["out"]
+            nt = int(got[3])
+            if nt > K:
+                # more schemas than the vector describes: a second all-reduce with all of them
+                big = np.zeros(nt * Wd, dtype=np.int64)
+                if self.rank == owner:
+                    self._describe(out, big)
+                big = self._allreduce_sum(big)
+                if self.rank != owner:
+                    out = self._schemas(big, nt)
+            elif self.rank != owner:
+                out = self._schemas(got[5:], nt)
+            rel = DRel(out)
+            rel._global = int(got[0])
+            self.plan_stats["native"] += 1
+            answer._set(self, rel)
+            answer.negation = bool(got[2])
+            return bool(got[1])
+        matched, negation, out = st["matched"], st["negation"], st["out"]
+        if not st["local"]:
+            # every shard holds the whole answer: shard 0 keeps it
+            total = sum(t.nrows for t in out)
+            if self.rank != 0:
+                out = [self.local.empty_table(t.kind, list(t.vars), t.members) for t in out]
+            rel = DRel(out)
+            rel._global = total
+        else:
+            got = st["got"]
             if int(got[1]) or any(int(x) == 0 for x in got[2:]):
                 self.plan_stats["native_fallback"] += 1
                 return None
@@ -512,120 +831,32 @@ class ShardedDB(RelationalDB):
             t[t != np.uint32(L.DAS_NONE)] = 0xFFFFFFFE
         return w.tobytes()
 
-    def _leaf_sizes(self, ctx, db, nodes, n, rec, leaves):
-        """(G, M) per leaf: its rows over all shards and on the largest one.
-        Exact from the estimate exchange (one all-gather of every shard's
-        das_plan_estimates, with its das_plan_bounds riding along), or --
-        when every leaf was seen before -- from the caches that exchange
-        fills: a leaf's exact sizes by its words (a term that repeats, e.g.
-        FlyBase's unanchored E(rec, V2, V1)), else its shape's upper bounds
-        (a fresh anchor of a known shape).  Then no collective: an anchored
-        query of a known shape takes 2 collectives instead of 3.  Bounds only
-        raise gather slot sizes and split decisions, never the answer.  The
-        caches fill from collective results, so every shard holds the same."""
-        if self._size_gen != db.generation:
-            self._size_gen = db.generation
-            self._exact_sizes, self._shape_sizes = {}, {}
-        keys = [rec[i].tobytes() for i in leaves]
-        skeys = [self._shape_key(rec[i]) for i in leaves]
-        G, M = {}, {}
-        if os.environ.get("DAS_SHARD_SIZE_CACHE") != "0":
-            small = int(os.environ.get("DAS_SHARD_SMALL", self.SMALL))
-            for i, k, sk in zip(leaves, keys, skeys):
-                hit = self._exact_sizes.get(k)
-                if hit is None:
-                    # a shape bound only where it settles the leaf as small
-                    # (gathered); a large bound (a hub key somewhere) needs the
-                    # exact sizes for the split decision
-                    hit = self._shape_sizes.get(sk)
-                    if hit is not None and hit[0] > small:
-                        hit = None
-                if hit is None:
-                    break
-                G[i], M[i] = hit
-            else:
-                self.plan_stats["size_cache"] += 1
-                return G, M
-        nl = len(leaves)
-        b = ctx.plan_bounds(nodes, n)[leaves]
-        local = np.concatenate([ctx.plan_estimates(nodes, n)[leaves].astype(np.int64),
-                                np.where(b == np.uint64(2 ** 64 - 1), -1, b.astype(np.int64))])
-        got = self._allgather_i64(local)
-        est, bnd = got[:, :nl], got[:, nl:]
-        if len(self._exact_sizes) > self.SIZE_CACHE:
-            self._exact_sizes.clear()
-        if len(self._shape_sizes) > self.SIZE_CACHE:
-            self._shape_sizes.clear()
-        for j, i in enumerate(leaves):
-            G[i], M[i] = int(est[:, j].sum()), int(est[:, j].max())
-            self._exact_sizes[keys[j]] = (G[i], M[i])
-            if (bnd[:, j] >= 0).all():
-                self._shape_sizes[skeys[j]] = (int(bnd[:, j].sum()), int(bnd[:, j].max()))
-        return G, M
-
     OWNER_TABLES = 16                       # answer tables an owner-evaluated plan describes
 
-    def _owner_plan(self, ctx, words, n, inputs, no_overload, answer, owner):
-        """A wholly gathered top-level plan (every leaf's rows sent to the
-        owner shard only) evaluated by that shard: shards take turns (round
-        robin over such plans), so N independent gathered queries -- bench.py's
-        per-rank QUERY_1-3 instances -- run on N GPUs at once instead of each
-        on all of them.  The owner keeps the answer; one all-reduce hands every
-        shard its size, matched / negation and the answer tables' schemas
-        (kind, variables, composite members), so the others hold empty tables
-        of the same schemas (later collectives over the relation pair tables up
-        by position).  `inputs` None on the owner (a shard's rows exceeded
-        their slot): the all-reduce carries the fallback to every shard."""
+    @staticmethod
+    def _describe(tables, v):
+        """An owner-evaluated answer's table schemas into its all-reduce
+        vector: kind, variables, composite members per table."""
+        W = 2 + 2 * L_MAXCOLS
+        for i, t in enumerate(tables):
+            d = v[i * W:(i + 1) * W]
+            d[0], d[1] = int(t.kind), len(t.vars)
+            d[2:2 + len(t.vars)] = [int(x) + 1 for x in t.vars]          # +1: 0 = unused
+            mem = list(t.members) if t.members is not None else []
+            d[2 + L_MAXCOLS:2 + L_MAXCOLS + len(mem)] = [int(x) + 2 for x in mem]
+
+    def _schemas(self, v, nt):
+        """Empty tables of the schemas an owner described."""
         from . import _lib as L
-        K, W = self.OWNER_TABLES, 2 + 2 * L_MAXCOLS
-        vec = np.zeros(5 + K * W, dtype=np.int64)
-        out = []
-
-        def describe(tables, v):
-            for i, t in enumerate(tables):
-                d = v[i * W:(i + 1) * W]
-                d[0], d[1] = int(t.kind), len(t.vars)
-                d[2:2 + len(t.vars)] = [int(x) + 1 for x in t.vars]          # +1: 0 = unused
-                mem = list(t.members) if t.members is not None else []
-                d[2 + L_MAXCOLS:2 + L_MAXCOLS + len(mem)] = [int(x) + 2 for x in mem]
-
-        def schemas(v, nt):
-            res = []
-            for i in range(nt):
-                d = v[i * W:(i + 1) * W]
-                kind, nv = int(d[0]), int(d[1])
-                vars_ = [int(x) - 1 for x in d[2:2 + nv]]
-                mem = [int(x) - 2 for x in d[2 + L_MAXCOLS:2 + L_MAXCOLS + nv]] if kind == L.TABLE_COMPOSITE else None
-                res.append(self.local.empty_table(kind, vars_, mem))
-            return res
-        if self.rank == owner and inputs is None:
-            vec[4] = 1
-        elif self.rank == owner:
-            matched, negation, out, _ = ctx.plan_execute_sharded(words, n, inputs, no_overload)
-            vec[0] = sum(t.nrows for t in out)
-            vec[1], vec[2], vec[3] = int(matched), int(negation), len(out)
-            describe(out[:K], vec[5:])
-        got = self._allreduce_sum(vec)                                           # collective 3
-        if int(got[4]):
-            self.plan_stats["native_fallback"] += 1
-            return None
-        nt = int(got[3])
-        if nt > K:
-            # more schemas than the vector describes: a second all-reduce with all of them
-            big = np.zeros(nt * W, dtype=np.int64)
-            if self.rank == owner:
-                describe(out, big)
-            big = self._allreduce_sum(big)
-            if self.rank != owner:
-                out = schemas(big, nt)
-        elif self.rank != owner:
-            out = schemas(got[5:], nt)
-        rel = DRel(out)
-        rel._global = int(got[0])
-        self.plan_stats["native"] += 1
-        answer._set(self, rel)
-        answer.negation = bool(got[2])
-        return bool(got[1])
+        W = 2 + 2 * L_MAXCOLS
+        res = []
+        for i in range(nt):
+            d = v[i * W:(i + 1) * W]
+            kind, nv = int(d[0]), int(d[1])
+            vars_ = [int(x) - 1 for x in d[2:2 + nv]]
+            mem = [int(x) - 2 for x in d[2 + L_MAXCOLS:2 + L_MAXCOLS + nv]] if kind == L.TABLE_COMPOSITE else None
+            res.append(self.local.empty_table(kind, vars_, mem))
+        return res
 
     def _placement_var(self, db, words):
         """The variable that places this Link term's rows (partition_spec:
@@ -652,88 +883,7 @@ class ShardedDB(RelationalDB):
     def get_atom_as_deep_representation(self, handle, arity=-1):
         return self.local.get_atom_as_deep_representation(handle, arity)
 
-    OVER = 0xFFFFFFFF                     # _gather_many header: rows over the slot
-
-    def _gather_many(self, tables, caps, owner=None):
-        """Every shard's rows of each table, to every shard, in ONE
-        all-gather: per shard a header (row count and column bounds per
-        table) and each table's rows (row-major) in a slot of `caps[j]` rows
-        (caps: the largest estimate any shard reported, an upper bound).
-        None on every shard when some shard's table exceeds its slot.
-        owner: the rows go to that shard only, in ONE all-to-all whose sends
-        to every other shard are empty (an owner-evaluated plan: 1/N of the
-        all-gather's traffic); the other shards get None, and the owner None
-        on an overflow (its plan carries the fallback to the others)."""
-        import torch
-        lo_hi = [t.bounds() for t in tables]
-        ncols = [max(len(t.vars), 1) for t in tables]
-        H = sum(1 + 2 * len(t.vars) for t in tables)
-        offs, off = [], H
-        for c, k in zip(caps, ncols):
-            offs.append(off)
-            off += int(c) * k
-        width = off
-        # a table with more rows than its slot (an estimate below the rows)
-        # is sent as the count OVER with no rows: every shard sees it after the
-        # all-gather and the plan falls back, on every shard alike
-        over = [t.nrows > int(c) for t, c in zip(tables, caps)]
-        hdr = []
-        for t, (lo, hi), ov in zip(tables, lo_hi, over):
-            hdr += [self.OVER if ov else t.nrows] + list(lo) + list(hi)
-        loc = self.local
-        gpu = loc.gpu
-        buf = torch.zeros(width, dtype=torch.int32, device=gpu)
-        buf[:H] = torch.from_numpy(np.array(hdr, dtype=np.uint32).view(np.int32)).to(gpu)
-        if not loc.stream_ordered:
-            torch.cuda.current_stream().synchronize()
-        for t, o, ov in zip(tables, offs, over):
-            if t.nrows and not ov:
-                loc.db.ctx.export_rows(t, buf.data_ptr() + 4 * o)
-        if not loc.stream_ordered:
-            loc.db.ctx.sync()
-        stage = buf if loc.dev == gpu else buf.cpu()
-        if owner is None:
-            out = torch.empty(self.world * width, dtype=torch.int32, device=stage.device)
-            self.dist.all_gather_into_tensor(out, stage, group=self.group)
-        else:
-            mine = self.rank == owner
-            out = torch.empty(self.world * width if mine else 0, dtype=torch.int32, device=stage.device)
-            self.dist.all_to_all_single(out, stage, output_split_sizes=[width if mine else 0] * self.world,
-                                        input_split_sizes=[width if d == owner else 0 for d in range(self.world)],
-                                        group=self.group)
-            self.plan_stats["collectives"] += 1
-            if not mine:
-                return None
-            self.plan_stats["collectives"] -= 1
-        self.plan_stats["collectives"] += 1
-        out_dev = out.to(gpu)
-        heads = out.view(self.world, width)[:, :H].cpu().numpy().view(np.uint32)
-        if not loc.stream_ordered:
-            torch.cuda.current_stream().synchronize()
-        cnt_cols = np.cumsum([0] + [1 + 2 * len(t.vars) for t in tables[:-1]])
-        if (heads[:, cnt_cols] == self.OVER).any():
-            self.plan_stats["gather_overflow"] = self.plan_stats.get("gather_overflow", 0) + 1
-            return None
-        result = []
-        h = 0
-        for j, (t, o) in enumerate(zip(tables, offs)):
-            k = len(t.vars)
-            cnt = heads[:, h].astype(np.int64)
-            lo = heads[:, h + 1:h + 1 + k]
-            hi = heads[:, h + 1 + k:h + 1 + 2 * k]
-            h += 1 + 2 * k
-            parts = [loc.db.ctx.import_rows(t.kind, list(t.vars), out_dev.data_ptr() + 4 * (r * width + o), int(cnt[r]),
-                                            t.members) for r in range(self.world) if cnt[r]]
-            g = parts[0] if len(parts) == 1 else (loc.db.ctx.concat(parts) if parts else
-                                                  loc.db.ctx.import_rows(t.kind, list(t.vars), None, 0, t.members))
-            has = cnt > 0
-            if has.any() and k:
-                g.set_bounds(lo[has].min(axis=0), hi[has].max(axis=0))
-            result.append(g)
-        if not loc.stream_ordered:
-            loc.db.ctx.sync()
-        del out_dev
-        return result
+    OVER = 0xFFFFFFFF                     # _plan_gather header: rows over the slot
 
     # ------------------------------------------------------- relation algebra
     def rel_empty(self):
@@ -968,11 +1118,11 @@ class HipLocal:
     @property
     def pattern_black_list(self):
         """The local index's load-time pattern black list (HipDB.load_arrays)."""
-        return self.local.pattern_black_list
+        return self.db.pattern_black_list
 
     @pattern_black_list.setter
     def pattern_black_list(self, value):
-        self.local.pattern_black_list = list(value)
+        self.db.pattern_black_list = list(value)
 
     def __getattr__(self, name):     # DBInterface passthrough
         return getattr(self.db, name)
@@ -1081,6 +1231,33 @@ class ShardedMatcher:
         finally:
             self.sdb._top = None
         return self.sdb.rel_local_count(ans._relation()) if ans._rel is not None else 0
+
+    def count_many(self, exprs):
+        """count() of a step's independent expressions, their sharded plans
+        sharing one estimate exchange, one gather and one outcome all-reduce
+        (ShardedDB.plan_many); an expression whose plan falls back is then
+        folded operator by operator, on every shard alike."""
+        from .pattern_matcher.pattern_matcher import PatternMatchingAnswer
+        sdb = self.sdb
+        answers = [PatternMatchingAnswer() for _ in exprs]
+        sdb._tops = {id(e) for e in exprs}
+        try:
+            res = sdb.plan_many(list(zip(exprs, answers)))
+        finally:
+            sdb._tops = set()
+        out = []
+        for e, a, r in zip(exprs, answers, res):
+            if r is None:
+                sdb._no_plan = {id(e)}
+                sdb._top = e
+                try:
+                    a = PatternMatchingAnswer()
+                    e.matched(sdb, a)
+                finally:
+                    sdb._no_plan = set()
+                    sdb._top = None
+            out.append(sdb.rel_local_count(a._relation()) if a._rel is not None else 0)
+        return out
 
 
 # ---------------------------------------------------------------------------

@@ -304,7 +304,7 @@ def _sharded_kb(kind):
     from das_amd import synthetic
     from tests.golden import make_synthetic as MS
     from tests.test_parallel_gloo import _fly_queries, _hub_queries, _queries
-    if kind in ("default", "heavy", "small", "default_owner"):
+    if kind in ("default", "heavy", "small", "default_owner", "small_batch"):
         return synthetic.bio_kb(60, 25, 600, 80, seed=3), _queries()
     if kind in ("hub", "hub_small", "hub_exchange"):
         return MS.make_arrays("hub"), _hub_queries()
@@ -325,7 +325,8 @@ def _sharded_kb(kind):
 # through each shard's index, the fold's emptiness checks, fallbacks)
 _SHARD_ENV = {"heavy": {"DAS_SHARDED_PLAN": "0", "DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
               "hub": {"DAS_JOIN_PLACEMENT": "exchange", "DAS_HEAVY_FRAC": "0.05"},
-              "small": {"DAS_SHARD_SMALL": "40"}, "hub_small": {"DAS_SHARD_SMALL": "30"},
+              "small": {"DAS_SHARD_SMALL": "40"}, "small_batch": {"DAS_SHARD_SMALL": "40"},
+              "hub_small": {"DAS_SHARD_SMALL": "30"},
               # large terms over a gather budget scaled to the test KB: the
               # planner folds them with the all-to-all exchange (no forcing)
               "hub_exchange": {"DAS_SHARD_SMALL": "30", "DAS_SHARD_GATHER_BUDGET": "2000"}}
@@ -350,6 +351,34 @@ def _sharded_worker(rank, world, port, out_path, mode):
     db.load_arrays(shard_arrays(arrays, rank, world))
     sdb = ShardedDB(HipLocal(db, cpu_staging=True), dist)
     res = []
+    if mode.endswith("_batch"):
+        # every query at once: their sharded plans share one estimate
+        # exchange, one gather and one outcome all-reduce (plan_many); the
+        # ones that fall back are folded operator by operator
+        exprs = [build(q) for q in queries]
+        answers = [pm.PatternMatchingAnswer() for _ in exprs]
+        c0 = sdb.plan_stats["collectives"]
+        sdb._tops = {id(e) for e in exprs}
+        got = sdb.plan_many(list(zip(exprs, answers)))
+        sdb._tops = set()
+        batch_coll = sdb.plan_stats["collectives"] - c0
+        for e, a, m in zip(exprs, answers, got):
+            if m is None:
+                sdb._no_plan, sdb._top = {id(e)}, e
+                a = pm.PatternMatchingAnswer()
+                try:
+                    m = e.matched(sdb, a)
+                except AttributeError as err:
+                    res.append({"error": type(err).__name__})
+                    continue
+                finally:
+                    sdb._no_plan, sdb._top = set(), None
+            rows = sorted(json.dumps(canon(x), sort_keys=True) for x in a.assignments)
+            res.append({"matched": bool(m), "negation": a.negation, "n": a.count(), "rows": rows,
+                        "local": sdb.rel_local_count(a._relation()), "native": 1, "collectives": 0})
+        sdb.plan_stats["batch_collectives"] = batch_coll
+        sdb.plan_stats["batch_fallbacks"] = sum(1 for m in got if m is None)
+        queries = []
     for q in queries:
         ans = pm.PatternMatchingAnswer()
         st0 = dict(sdb.plan_stats)
@@ -376,7 +405,8 @@ def _sharded_worker(rank, world, port, out_path, mode):
 
 
 @pytest.mark.parametrize("mode", ["default", "heavy", "small", "hub", "hub_small", "hub_exchange", "flybase",
-                                  "flybase_owner", "default_owner", "bio_full", "bio_full_owner"])
+                                  "flybase_owner", "default_owner", "bio_full", "bio_full_owner",
+                                  "flybase_batch", "bio_full_batch", "small_batch"])
 def test_gpu_sharded_two_ranks_one_gpu(mode):
     """The multi-GPU path with two ranks sharing cuda:0 over gloo, against the
     single-process oracle: handle-sharded builds (each link indexed on exactly
@@ -429,10 +459,15 @@ def test_gpu_sharded_two_ranks_one_gpu(mode):
             got = per_rank[r][qi]
             assert (got["matched"], got["negation"], got["n"]) == (want["matched"], want["negation"], want["n"]), q
             assert got["rows"] == want_rows, q
-        if mode.startswith("flybase"):
+        if mode.startswith("flybase") and not mode.endswith("_batch"):
             got = per_rank[0][qi]
             assert got["native"] == 1 and got["collectives"] <= 3, (q, got["native"], got["collectives"])
-    if mode.startswith("flybase"):
+    if mode.endswith("_batch"):
+        # the whole query list's sharded plans: at most 3 collectives together
+        assert stats["batch_collectives"] <= 3, stats
+        if mode.startswith("flybase"):
+            assert stats["batch_fallbacks"] == 0, stats
+    if mode in ("flybase", "flybase_owner"):
         # the second gene's queries reuse the first's leaf sizes (shape cache):
         # no estimate exchange, 2 collectives each
         assert stats["size_cache"] > 0, stats
@@ -605,6 +640,35 @@ def _assert_same_rows(got, want, what=""):
                          f"{got[i] if i < len(got) else None} vs {want[i] if i < len(want) else None}")
 
 
+def _np_join_rows(pa, pk, qk, qb):
+    """The natural join of P(a, k) and Q(k, b) with multiplicities, as (a, k, b)
+    uint64 columns sorted by (a, k, b) -- numpy, for joins of 10^7+ rows."""
+    pk, qk = np.asarray(pk, dtype=np.int64), np.asarray(qk, dtype=np.int64)
+    order = np.argsort(qk, kind="stable")
+    qk_s, qb_s = qk[order], np.asarray(qb, dtype=np.uint64)[order]
+    nk = int(max(pk.max(initial=0), qk.max(initial=0))) + 1
+    cnt = np.bincount(qk_s, minlength=nk)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    c = cnt[pk]
+    a = np.repeat(np.asarray(pa, dtype=np.uint64), c)
+    k = np.repeat(pk.astype(np.uint64), c)
+    first = np.repeat(start[pk], c)
+    within = np.arange(int(c.sum()), dtype=np.int64) - np.repeat(np.cumsum(c) - c, c)
+    b = qb_s[first + within]
+    o = np.lexsort((b, k, a))
+    return a[o], k[o], b[o]
+
+
+def _assert_same_join(got, want):
+    """got: (3, n) device join output columns (a, k, b); want: _np_join_rows."""
+    g = [np.asarray(x, dtype=np.uint64) for x in got]
+    o = np.lexsort((g[2], g[1], g[0]))
+    assert len(g[0]) == len(want[0]), (len(g[0]), len(want[0]))
+    for x, y in zip(g, want):
+        bad = np.flatnonzero(x[o] != y)
+        assert bad.size == 0, f"first difference at row {bad[0]}"
+
+
 @pytest.mark.parametrize("search", ["0", "1", "0-vec1", "0-vec0"])
 @pytest.mark.parametrize("shape", ["sparse", "fanout2", "skew", "wide"])
 def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
@@ -637,12 +701,9 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     P.set_bounds([0, 0], [(1 << 20) - 1, nk])
     Q.set_bounds([0, 0], [nk, (1 << 20) - 1])
     got = db.ctx.join(P, Q).fetch()
-    by = {}
-    for k, b in zip(qk.tolist(), qb.tolist()):
-        by.setdefault(k, []).append(b)
-    want = sorted((a, k, b) for a, k in zip(pa.tolist(), pk.tolist()) for b in by.get(k, ()))
-    assert len(want) > 1000
-    _assert_same_rows(sorted(zip(*[c.tolist() for c in got])), want)
+    want = _np_join_rows(pa, pk, qk, qb)
+    assert len(want[0]) > 1000
+    _assert_same_join(got, want)
 
 
 @pytest.mark.parametrize("zlc", ["1", "0"])
@@ -1118,8 +1179,9 @@ def test_gpu_scan_views_match_oracle(gen, views, monkeypatch):
     db = _hipdb(arrays)
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
     rng = np.random.default_rng(3)
-    for q in _random_queries(rng, arrays, 30):
-        want = O.evaluate(q, odb)
+    qs = _random_queries(rng, arrays, 30)
+    wants = _wants(("scan_views", gen), odb, qs)             # the oracle once for both settings
+    for q, want in zip(qs, wants):
         got = record(q, db)
         assert same(got, want), (q, got.get("n"), want.get("n"))
 

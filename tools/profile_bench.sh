@@ -11,8 +11,9 @@
 #      printed UNDER rocprof (same process, --no-extras: the timed steps are
 #      the last launches) recomputed from the rocprof trace of those launches
 # WORKLOAD selects bench.py --workload (default bio); BENCH_ARGS adds flags;
-# TAG names the outputs gpurun_out/<TAG>_<workload>*.  Copy what is worth
-# keeping into profiles/ afterwards.
+# TAG names the outputs gpurun_out/<TAG>_<workload>*, and <TAG>_<workload>_box.txt
+# records the card (serial, unique id, clocks).  Copy what is worth keeping
+# into profiles/ afterwards.
 set -o pipefail
 W=${WORKLOAD:-bio}
 T=${TAG:-r2}
@@ -20,6 +21,9 @@ D=gpurun_out/prof_${T}_$W
 mkdir -p $D
 export TMPDIR=/tmp
 ARGS="--workload $W --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-}"
+# which box: the card's serial / unique id and its clocks next to the records
+# (box-to-box spreads of the write-bound kernels are then attributable)
+{ date -u; hostname; rocm-smi --showserial --showuniqueid --showclocks 2>&1 || true; } > gpurun_out/${T}_${W}_box.txt
 PARGS="$ARGS --no-cpu-baseline --no-materialise --no-extras"
 timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py $ARGS --detail gpurun_out/${T}_bench_${W}_detail.json > gpurun_out/${T}_bench_$W.json 2> $D/bench.err &&
 timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d $D/kt -o run -- python bench.py $PARGS --detail $D/kt_detail.json > $D/kt.log 2>&1 &&
