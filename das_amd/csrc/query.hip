@@ -3287,6 +3287,15 @@ bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows,
         bq = qq;
       }
     }
+    // many probes against one long grounded key range: a binary search of
+    // log2(range) steps per probe costs more than reading the range once as
+    // the build side of a direct join (FlyBase FJ: 3*10^5 probes into the
+    // 4.5*10^5 rows of one schema, 73-76 vs 64-65 us per query) -- not an
+    // index join then (DAS_INDEX_JOIN=1 / DAS_IJ_RANGED=1 keep it)
+    const char* fij = std::getenv("DAS_INDEX_JOIN");
+    if (best != ~0ull && best > 0 && rows > 4096 && !(f && f[0] == '1') && !(fij && fij[0] == '1') &&
+        (double)rows * std::log2((double)best) > 2.0 * (double)best)
+      return false;
     const bool take = best != ~0ull &&
                       ((f && f[0] == '1') || (best <= (1ull << 22) && best <= 64ull * rows));
     if (take) {

@@ -50,4 +50,4 @@ pr.enable()
 for qs in sets[45:60]:
     run(qs, None)
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25); pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
