@@ -57,6 +57,9 @@ def parse():
                          "on one GPU; build at N > 1)")
     ap.add_argument("--leg-cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline budget of each extra workload of --workload all")
+    ap.add_argument("--batch", type=int, default=1, choices=[0, 1],
+                    help="1 (default): a step's queries in one das_plan_execute_many call (pm.matched_many); "
+                         "0: query.matched(db, answer) one by one")
     ap.add_argument("--events", default="dominant", choices=["dominant", "all"],
                     help="timed-step HIP events: around the dominant kernel only, or around every kernel scope")
     # bio (config 2)
@@ -1010,8 +1013,16 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         if engine is not None:
             # the step's queries share their collectives (ShardedMatcher.count_many)
             return sum(engine.count_many([q for _, q in qsets[i]]))
-        tot = 0
-        for name, q in qsets[i]:
+        if args.batch:
+            # the step's queries in one das_plan_execute_many call
+            # (pm.matched_many: a fused chain's GPU time overlaps the host
+            # work of the next query); Q2 alone while its launches are tagged
+            qs = [(name, q) for name, q in qsets[i] if not (tag_q2[0] and name.startswith("Q2"))]
+            tot = sum(a.count() for _, a in pm.matched_many(db, [q for _, q in qs]))
+            todo = [(name, q) for name, q in qsets[i] if tag_q2[0] and name.startswith("Q2")]
+        else:
+            tot, todo = 0, qsets[i]
+        for name, q in todo:
             if tag_q2[0] and name.startswith("Q2"):
                 db.ctx.prof_tag("Q2")
                 tot += run(q)

@@ -143,6 +143,7 @@ _SIGS = {
     "das_parsed_free": (C.c_int, [P]),
     "das_plan_execute": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32,
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "das_plan_execute_many": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]),
     "das_plan_execute_sharded": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32, P,
                                            C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
                                            C.POINTER(C.c_int32), P, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -546,6 +547,33 @@ class Context:
                 continue
             check(rc, self.h)
             return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
+
+    def plan_execute_many(self, plans, no_overload=False):
+        """das_plan_execute_many over [(words, n_nodes)] -> one (matched,
+        negation, [Table]) per plan, each as plan_execute's on it alone."""
+        m = len(plans)
+        if m == 0:
+            return []
+        ptrs = (P * m)(*[w.ctypes.data for w, _ in plans])
+        ns = np.array([k for _, k in plans], dtype=np.uint32)
+        cap = 8 * m
+        while True:
+            out = (P * cap)()
+            n_out = np.zeros(m, dtype=np.uint32)
+            matched = np.zeros(m, dtype=np.int32)
+            neg = np.zeros(m, dtype=np.int32)
+            rc = lib().das_plan_execute_many(self.h, m, ptrs, ptr(ns), 1 if no_overload else 0, out, cap, ptr(n_out),
+                                             ptr(matched), ptr(neg))
+            if rc == ERR_INVALID and int(n_out.sum()) > cap:
+                cap = int(n_out.sum())
+                continue
+            check(rc, self.h)
+            res, k = [], 0
+            for i in range(m):
+                j = int(n_out[i])
+                res.append((bool(matched[i]), bool(neg[i]), [Table(self, out[k + q]) for q in range(j)]))
+                k += j
+            return res
 
     def plan_execute_sharded(self, words, n_nodes, inputs, no_overload=False):
         """das_plan_execute_sharded: (matched, negation, [Table], checks)."""

@@ -198,6 +198,15 @@ int das_ctx_destroy(das_ctx_t* ctx) {
     das::free_index(ctx->c.idx);
     ctx->c.zlc.release();                 // back to the cache while the stream still exists
     das::cache_release_stream(ctx->c.s);
+    for (hipStream_t& ss : ctx->c.side)
+      if (ss) {
+        DAS_HIP(hipStreamSynchronize(ss));
+        das::cache_release_stream(ss);
+        DAS_HIP(hipStreamDestroy(ss));
+        ss = nullptr;
+      }
+    for (hipEvent_t e : ctx->c.side_ev) (void)hipEventDestroy(e);
+    ctx->c.side_ev.clear();
     if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
   });
   delete ctx;
@@ -710,6 +719,27 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
     *n_out = (uint32_t)r.tables.size();
     *matched = r.matched ? 1 : 0;
     *negation = r.negation ? 1 : 0;
+  });
+}
+
+int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,
+                          uint32_t no_overload, das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched,
+                          int32_t* negation) {
+  if (!ctx || (n_plans && (!nodes || !n || !n_out || !matched || !negation)))
+    return fail(ctx, DAS_ERR_INVALID, "null argument");
+  return guarded(ctx, [&] {
+    auto rs = das::plan_execute_many(ctx->c, nodes, n, n_plans, (int)no_overload);
+    uint64_t total = 0;
+    for (auto& r : rs) total += r.tables.size();
+    for (uint32_t i = 0; i < n_plans; ++i) n_out[i] = (uint32_t)rs[i].tables.size();
+    // on overflow every answer is dropped; n_out says the room each needs
+    DAS_CHECK(total <= cap, das::DAS_E_INVALID, "plans: more answer tables than `cap`");
+    uint64_t k = 0;
+    for (uint32_t i = 0; i < n_plans; ++i) {
+      for (auto& t : rs[i].tables) out[k++] = wrap(std::move(t));
+      matched[i] = rs[i].matched ? 1 : 0;
+      negation[i] = rs[i].negation ? 1 : 0;
+    }
   });
 }
 

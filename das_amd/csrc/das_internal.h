@@ -198,6 +198,23 @@ struct Ctx {
   DBuf<uint2> zlc;
   // pattern black list for the next index build: md5 of each type name
   std::vector<Digest> black_list;
+  // side streams for fused chains in flight together (das_plan_execute_many),
+  // each with two fence events per pooled run (created on first use)
+  static constexpr int kSide = 3;
+  hipStream_t side[kSide] = {};
+  std::vector<hipEvent_t> side_ev;
+  hipStream_t side_stream(int i) {
+    if (!side[i]) DAS_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
+    return side[i];
+  }
+  hipEvent_t fence_event(uint32_t i) {
+    while (side_ev.size() <= i) {
+      hipEvent_t e;
+      DAS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      side_ev.push_back(e);
+    }
+    return side_ev[i];
+  }
   // loader-side host copies kept for metadata calls
   std::vector<uint8_t> leaf_bytes;
   std::vector<uint64_t> leaf_off;
@@ -338,6 +355,12 @@ struct PlanOutput {
   std::vector<std::unique_ptr<Table>> tables;
 };
 PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload);
+// Several independent plans in one call (das_plan_execute_many): each result
+// equals plan_execute's on that plan alone.  Plans whose root And one fused
+// chain answers are launched first, without waiting; the other plans run
+// while the chains do; the chains' outcomes are read back last.
+std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* nodes, const uint32_t* n,
+                                          uint32_t n_plans, int no_overload);
 // Sharded evaluation (das_plan_execute_sharded): INPUT leaves are the
 // caller's tables (replicated relations), LINK leaves scan / index-join this
 // shard's index (partial relations, whose emptiness is assumed, not tested);
@@ -362,6 +385,21 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               std::unique_ptr<Table>& out, uint32_t* consumed);
 // query.hip: an Or of ordered Links with one schema (no Not terms): the
 // scans and the union's dedup in one launch.  0: not taken; 1: evaluated.
+// The fused And of a whole And operator launched without waiting for its
+// outcome (das_plan_execute_many): null when fused_and would not fuse every
+// term and Not filter of it; `k` picks the pooled read-back slot and
+// descriptor buffer (pub_reserve_pool), which stay the run's until
+// fused_and_finish.  fused_and_finish: 1 = answered (matched / out as
+// fused_and's), 0 = evaluate the And another way (a grid chain's redo, a
+// chain that stopped early).
+struct ChainRun;
+struct ChainRunDel {
+  void operator()(ChainRun* r) const;
+};
+using ChainRunPtr = std::unique_ptr<ChainRun, ChainRunDel>;
+ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k);
+int fused_and_finish(Ctx& c, ChainRun& r, bool& matched, std::unique_ptr<Table>& out);
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
              std::unique_ptr<Table>& out);
 

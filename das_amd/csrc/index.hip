@@ -104,6 +104,33 @@ PubSlot pub_reserve() {
   return PubSlot{sl.p, seq};
 }
 
+PubSlot pub_reserve_pool(uint32_t k) {
+  DAS_CHECK(k < kPubPool, DAS_E_INTERNAL, "read-back pool: bad slot");
+  thread_local std::unique_ptr<Slot> pool[kPubPool];
+  if (!pool[k]) pool[k] = std::make_unique<Slot>();
+  Slot& sl = *pool[k];
+  const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;
+  return PubSlot{sl.p, seq};
+}
+
+uint8_t* pinned_stage_pool(uint32_t k, uint64_t bytes) {
+  DAS_CHECK(k < kPubPool, DAS_E_INTERNAL, "staging pool: bad buffer");
+  struct Stage {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0;
+    ~Stage() { if (p) (void)hipHostFree(p); }
+  };
+  thread_local Stage pool[kPubPool];
+  Stage& st = pool[k];
+  if (bytes > st.cap) {
+    if (st.p) DAS_HIP(hipHostFree(st.p));
+    st.p = nullptr;
+    st.cap = std::max<uint64_t>(bytes, 1 << 14);
+    DAS_HIP(hipHostMalloc((void**)&st.p, st.cap, hipHostMallocCoherent | hipHostMallocMapped));
+  }
+  return st.p;
+}
+
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
   count_readback();
   trace_mark("wait");

@@ -51,6 +51,10 @@ bool same_schema(const Table& a, const Table& b) {
   return true;
 }
 
+struct Exec;
+void split_and(const Exec& ex, const std::vector<uint32_t>& terms, std::vector<const das_plan_node_t*>& pos,
+               std::vector<const das_plan_node_t*>& neg);
+
 struct Exec {
   Ctx& c;
   const das_plan_node_t* nd;
@@ -374,11 +378,7 @@ struct Exec {
       // the leading Link terms of the And (and its Not(Link) filters): one
       // fused launch while the running result stays small
       std::vector<const das_plan_node_t*> pos, neg;
-      for (uint32_t ti : terms) {
-        const das_plan_node_t& x = nd[ti];
-        if (x.op == DAS_PLAN_NOT && nd[ti + 1].op == DAS_PLAN_LINK && nd[ti + 1].index_join) neg.push_back(&nd[ti + 1]);
-        else pos.push_back(&x);
-      }
+      split_and(*this, terms, pos, neg);
       bool m = false;
       TablePtr t;
       const int r = fused_and(c, pos, neg, no_overload, m, t, &skip);
@@ -544,6 +544,49 @@ struct Exec {
   }
 };
 
+struct Views {                          // scans may return index views while plans run
+  Ctx& c;
+  explicit Views(Ctx& cc) : c(cc) {
+    // default (1): every predicate-free scan of consecutive index columns
+    // is a view.  2: views up to kViewRows rows only, larger probe sides
+    // copied (the copy leaves them MALL-warm for the join that reads them
+    // next: the join kernel runs at ~0.50 of the HBM peak instead of ~0.41,
+    // but the bio step is ~4 % slower with the copies, profiles/r3_*).
+    // 0: never.
+    const char* f = std::getenv("DAS_SCAN_VIEWS");
+    c.scan_views = f && f[0] == '2' ? 2 : f && f[0] == '0' ? 0 : 1;
+  }
+  ~Views() { c.scan_views = 0; }
+};
+
+// An And's terms as fused_and takes them: the Not(Link) terms that an anti
+// index join applies, and the others (eval_and)
+void split_and(const Exec& ex, const std::vector<uint32_t>& terms, std::vector<const das_plan_node_t*>& pos,
+               std::vector<const das_plan_node_t*>& neg) {
+  for (uint32_t ti : terms) {
+    const das_plan_node_t& x = ex.nd[ti];
+    if (x.op == DAS_PLAN_NOT && ex.nd[ti + 1].op == DAS_PLAN_LINK && ex.nd[ti + 1].index_join) neg.push_back(&ex.nd[ti + 1]);
+    else pos.push_back(&x);
+  }
+}
+
+// a plan's answer: a view must not outlive the index, so the caller gets a copy
+PlanOutput output(Ctx& c, Res r) {
+  PlanOutput out;
+  out.matched = r.matched;
+  out.negation = r.neg;
+  for (auto& t : r.rel.t) {
+    if (t->view) {
+      auto m = new_table_like(c, *t, t->nrows);
+      m->nrows = t->nrows;
+      for (int k = 0; k < t->ncols; ++k) copy_dev(m->col(k), t->col(k), 4 * t->nrows, c.s);
+      t = std::move(m);
+    }
+    out.tables.push_back(std::move(t));
+  }
+  return out;
+}
+
 }  // namespace
 
 PlanOutput plan_execute_sharded(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no_overload,
@@ -580,20 +623,6 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   Exec ex{c, nodes, n, no_overload};
   DAS_CHECK(ex.next(0) == n, DAS_E_INVALID, "plan: node array is not one expression tree");
   trace_mark("plan");
-  struct Views {                       // scans may return index views while the plan runs
-    Ctx& c;
-    explicit Views(Ctx& cc) : c(cc) {
-      // default (1): every predicate-free scan of consecutive index columns
-      // is a view.  2: views up to kViewRows rows only, larger probe sides
-      // copied (the copy leaves them MALL-warm for the join that reads them
-      // next: the join kernel runs at ~0.50 of the HBM peak instead of ~0.41,
-      // but the bio step is ~4 % slower with the copies, profiles/r3_*).
-      // 0: never.
-      const char* f = std::getenv("DAS_SCAN_VIEWS");
-      c.scan_views = f && f[0] == '2' ? 2 : f && f[0] == '0' ? 0 : 1;
-    }
-    ~Views() { c.scan_views = 0; }
-  };
   Res r;
   {
     Views v(c);
@@ -601,20 +630,57 @@ PlanOutput plan_execute(Ctx& c, const das_plan_node_t* nodes, uint32_t n, int no
   }
   trace_mark("done");
   trace_dump("das_plan_execute");
-  PlanOutput out;
-  out.matched = r.matched;
-  out.negation = r.neg;
-  for (auto& t : r.rel.t) {
-    if (t->view) {
-      // a view must not outlive the index: the caller gets a copy
-      auto m = new_table_like(c, *t, t->nrows);
-      m->nrows = t->nrows;
-      for (int k = 0; k < t->ncols; ++k) copy_dev(m->col(k), t->col(k), 4 * t->nrows, c.s);
-      t = std::move(m);
-    }
-    out.tables.push_back(std::move(t));
+  return output(c, std::move(r));
+}
+
+std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* nodes, const uint32_t* n,
+                                          uint32_t n_plans, int no_overload) {
+  DAS_CHECK(c.idx.built, DAS_E_NOT_BUILT, "index not built");
+  for (uint32_t i = 0; i < n_plans; ++i) {
+    DAS_CHECK(nodes[i] && n[i] > 0, DAS_E_INVALID, "plan: no nodes");
+    Exec ex{c, nodes[i], n[i], no_overload};
+    DAS_CHECK(ex.next(0) == n[i], DAS_E_INVALID, "plan: node array is not one expression tree");
   }
-  return out;
+  std::vector<PlanOutput> outs(n_plans);
+  std::vector<ChainRunPtr> runs(n_plans);
+  const char* f = std::getenv("DAS_DEFER");               // A/B: 0 = every plan in turn
+  const bool defer = !(f && f[0] == '0');
+  trace_mark("plans");
+  Views v(c);
+  // 1. root Ands one fused chain answers: launched, not waited on
+  uint32_t pooled = 0;
+  for (uint32_t i = 0; i < n_plans && defer && pooled < kPubPool; ++i) {
+    const das_plan_node_t* nd = nodes[i];
+    if (nd[0].op != DAS_PLAN_AND) continue;
+    Exec ex{c, nd, n[i], no_overload};
+    std::vector<const das_plan_node_t*> pos, neg;
+    split_and(ex, ex.children(0), pos, neg);
+    runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled);
+    if (runs[i]) ++pooled;
+  }
+  // 2. the other plans, their host work overlapping the chains on the GPU
+  for (uint32_t i = 0; i < n_plans; ++i) {
+    if (runs[i]) continue;
+    Exec ex{c, nodes[i], n[i], no_overload};
+    outs[i] = output(c, ex.eval(0));
+  }
+  // 3. the chains' outcomes (a redo: the plan evaluated in full)
+  for (uint32_t i = 0; i < n_plans; ++i) {
+    if (!runs[i]) continue;
+    bool m = false;
+    TablePtr t;
+    if (fused_and_finish(c, *runs[i], m, t)) {
+      outs[i].matched = m;
+      if (m && t && t->nrows) outs[i].tables.push_back(std::move(t));
+    } else {
+      Exec ex{c, nodes[i], n[i], no_overload};
+      outs[i] = output(c, ex.eval(0));
+    }
+    runs[i].reset();
+  }
+  trace_mark("done");
+  trace_dump("das_plan_execute_many");
+  return outs;
 }
 
 }  // namespace das

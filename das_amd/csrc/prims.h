@@ -212,6 +212,12 @@ void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
 // slot.  One launch per call, no runtime copies and no stream wait.  The
 // buffer is this thread's, reused by its next call.
 uint8_t* pinned_stage(uint64_t bytes);
+// Read-back slot and staging buffer number k (k < kPubPool) of this thread,
+// apart from the ones above: for launches in flight together whose read-backs
+// are taken later (das_plan_execute_many's deferred chains)
+constexpr uint32_t kPubPool = 16;
+PubSlot pub_reserve_pool(uint32_t k);
+uint8_t* pinned_stage_pool(uint32_t k, uint64_t bytes);
 // Per-(device, stream) completion counter of the reduce pass; `base` = its
 // value before the next launch (the host advances it by the launch's tiles).
 struct ScanCtr {

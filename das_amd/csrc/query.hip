@@ -3869,34 +3869,68 @@ bool chain_grid_wanted(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   return false;
 }
 
-int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                  const std::vector<const das_plan_node_t*>& anti, bool grid, bool& matched,
-                  std::unique_ptr<Table>& out, uint32_t* consumed);
+// A compiled fused And (one-workgroup or grid chain) between its launch and
+// the read-back of its outcome: fused_and runs compile -> launch -> finish in
+// a row; das_plan_execute_many launches several before it waits for any.
+struct ChainRun {
+  ChainDesc d{};
+  std::vector<std::unique_ptr<Table>> tabs;                  // one output table per stage
+  std::vector<uint32_t> terms_done;                          // positive terms folded after each stage
+  std::unique_ptr<Table> fin;                                // grid: the final rows
+  DBuf<uint32_t> gsc, dd;                                    // grid: counters, device descriptor
+  bool grid = false, complete = false;
+  int acc = -1;
+  PubSlot ps{};
+  uint64_t* ts = nullptr;
+  uint64_t bytes = 0;
+  hipStream_t ls = nullptr;                                   // the stream it was launched on
+  int fence = -1;                                             // side stream: its fence events (2k, 2k+1)
+  bool waited = false;                                        // chain_finish read its outcome
+};
+// 1: compiled; 0: nothing to fuse; -1: the grid form does not apply
+int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R);
+void chain_launch(Ctx& c, ChainRun& R, const PubSlot& ps, uint8_t* stage, int side = -1, uint32_t k = 0);
+int chain_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out, uint32_t* consumed);
+
+// whether fused_and applies, and the form it would take first (grid or not)
+int fused_and_form(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                   const std::vector<const das_plan_node_t*>& anti, int no_overload) {
+  const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
+  if ((f && f[0] == '0') || no_overload || terms.empty()) return -1;
+  const char* gm = std::getenv("DAS_CHAIN_GRID");
+  const bool want_grid = !(gm && gm[0] == '0') && chain_grid_wanted(c, terms, anti.size(), gm && gm[0] == '1');
+  if (trace_on()) trace_mark(want_grid ? "chain grid" : "chain one workgroup");
+  return want_grid ? 1 : 0;
+}
 
 int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               const std::vector<const das_plan_node_t*>& anti, int no_overload, bool& matched,
               std::unique_ptr<Table>& out, uint32_t* consumed) {
-  const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
-  if ((f && f[0] == '0') || no_overload || terms.empty()) return 0;
-  const char* gm = std::getenv("DAS_CHAIN_GRID");
-  const bool want_grid = !(gm && gm[0] == '0') && chain_grid_wanted(c, terms, anti.size(), gm && gm[0] == '1');
-  if (trace_on()) trace_mark(want_grid ? "chain grid" : "chain one workgroup");
-  for (int attempt = want_grid ? 0 : 1; attempt < 2; ++attempt) {
-    const int r = fused_and_run(c, terms, anti, attempt == 0, matched, out, consumed);
-    if (r >= 0) return r;                                     // -1: the grid form does not apply, try one workgroup
+  const int form = fused_and_form(c, terms, anti, no_overload);
+  if (form < 0) return 0;
+  for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
+    ChainRun R;
+    const int r = chain_compile(c, terms, anti, attempt == 0, R);
+    if (r < 0) continue;                                      // the grid form does not apply: one workgroup
+    if (r == 0) return 0;
+    // (the descriptor stages in this thread's pinned buffer, read by the
+    // launches before the read-back returns)
+    chain_launch(c, R, pub_reserve(), pinned_stage(((R.bytes + 63) & ~63ull) + 8 * (kChainStages + 4)));
+    return chain_finish(c, R, matched, out, consumed);
   }
   return 0;
 }
 
-int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                  const std::vector<const das_plan_node_t*>& anti, bool grid, bool& matched,
-                  std::unique_ptr<Table>& out, uint32_t* consumed) {
+int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R) {
   Index& idx = c.idx;
-  ChainDesc d{};
+  ChainDesc& d = R.d;
+  R.grid = grid;
   const uint32_t G = grid ? cu_count(c) : 1u;
   const uint64_t gcap = (uint64_t)G * kGridSeg;              // grid: every stage table holds G segments
-  std::vector<std::unique_ptr<Table>> tabs;                  // one output table per stage
-  std::vector<uint32_t> terms_done;                           // positive terms folded after each stage
+  std::vector<std::unique_ptr<Table>>& tabs = R.tabs;
+  std::vector<uint32_t>& terms_done = R.terms_done;
   auto add = [&](uint32_t op) -> ChainStage* {
     if (d.nstage >= (uint32_t)kChainStages) return nullptr;
     ChainStage& st = d.st[d.nstage++];
@@ -3914,7 +3948,7 @@ int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   bool parted = false;
   // a chain ending early (too many stages) still folds the terms compiled so
   // far; the caller continues from there
-  int acc = -1;                                               // stage holding the running result
+  int& acc = R.acc;                                           // stage holding the running result
   uint32_t nterm = 0;
   bool all_terms = true;
   for (const das_plan_node_t* x : terms) {
@@ -4044,60 +4078,99 @@ int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
       acc = (int)d.nstage - 1;
     }
   if (d.nstage < 2) return 0;                                 // one operator: nothing to fuse
-  const bool complete = all_terms && anti_ok;
+  R.complete = all_terms && anti_ok;
   // grid: the final rows gather into one table; device copies of the
   // descriptor and the counters
-  std::unique_ptr<Table> fin;
-  DBuf<uint32_t> gsc, dd;
   if (grid) {
     const Table& A = *tabs[acc];
-    fin = new_table(c, DAS_TABLE_ORDERED, A.ncols, A.vars, gcap);
+    R.fin = new_table(c, DAS_TABLE_ORDERED, A.ncols, A.vars, gcap);
     for (int k = 0; k < A.ncols; ++k) {
-      fin->lo[k] = A.lo[k];
-      fin->hi[k] = A.hi[k];
+      R.fin->lo[k] = A.lo[k];
+      R.fin->hi[k] = A.hi[k];
     }
-    gsc.alloc(kGscWords, c.s);
+    R.gsc.alloc(kGscWords, c.s);
     d.seg = kGridSeg;
-    d.fin = fin->data;
-    d.fin_ld = fin->cap;
-    d.gsc = gsc.p;
+    d.fin = R.fin->data;
+    d.fin_ld = R.fin->cap;
+    d.gsc = R.gsc.p;
   }
   // only the stages in use travel (the kernel copies them into LDS)
-  const uint64_t bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
+  R.bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
   static_assert(sizeof(ChainStage) % 4 == 0 && offsetof(ChainDesc, st) % 4 == 0, "word copy");
+  return 1;
+}
+
+// `stage`: pinned host memory of at least chain_stage_bytes(R) that stays
+// untouched until chain_finish (the launches read the descriptor from it).
+// side >= 0: launched on side stream `side` after the work the context's
+// stream holds so far (fence event 2k), so that it runs alongside later work
+// of the context's stream; chain_finish makes the context's stream wait for
+// it (fence event 2k + 1) before any of its tables is read or freed there.
+void chain_launch(Ctx& c, ChainRun& R, const PubSlot& ps, uint8_t* stage, int side, uint32_t k) {
+  struct Swap {                                               // the launches go to c.s: point it at the side stream
+    Ctx& c;
+    hipStream_t old;
+    ~Swap() { c.s = old; }
+  } sw{c, c.s};
+  if (side >= 0) {
+    hipStream_t ss = c.side_stream(side);
+    hipEvent_t in = c.fence_event(2 * k);
+    DAS_HIP(hipEventRecord(in, c.s));
+    DAS_HIP(hipStreamWaitEvent(ss, in, 0));
+    c.s = ss;
+    R.fence = (int)k;
+  }
+  R.ls = c.s;
+  const ChainDesc& d = R.d;
+  const uint64_t bytes = R.bytes;
   // (DAS_TRACE: stage timestamps of the device clock after the descriptors)
   const uint64_t tsoff = (bytes + 63) & ~63ull;
-  uint8_t* hd = pinned_stage(tsoff + 8 * (kChainStages + 4));
+  uint8_t* hd = stage;
   std::memcpy(hd, &d, bytes);
-  uint64_t* ts = trace_on() ? reinterpret_cast<uint64_t*>(hd + tsoff) : nullptr;
-  if (ts) std::memset(ts, 0, 8 * (kChainStages + 4));
+  R.ts = trace_on() ? reinterpret_cast<uint64_t*>(hd + tsoff) : nullptr;
+  if (R.ts) std::memset(R.ts, 0, 8 * (kChainStages + 4));
   // algorithmic bytes known up front: the scanned index rows
   double sbytes = 0;
   for (uint32_t i = 0; i < d.nstage; ++i)
     if (d.st[i].op == CH_SCAN) sbytes += 4.0 * (d.st[i].end - d.st[i].begin) * (d.st[i].sp.arity + 1);
   if (trace_on()) trace_mark("prep staged");
-  const PubSlot ps = pub_reserve();
-  if (trace_on()) trace_mark("prep slot");
-  if (grid) {
-    dd.alloc(bytes / 4, c.s);
+  R.ps = ps;
+  if (R.grid) {
+    const uint32_t G = cu_count(c);
+    R.dd.alloc(bytes / 4, c.s);
     {
       ProfScope pf(c, "k_chain_prep", 2.0 * bytes);
-      hipLaunchKernelGGL(k_chain_prep, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), dd.p,
-                         gsc.p);
+      hipLaunchKernelGGL(k_chain_prep, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4),
+                         R.dd.p, R.gsc.p);
       DAS_HIP(hipGetLastError());
     }
     ProfScope pf(c, "k_chain_grid", sbytes);
-    hipLaunchKernelGGL(k_chain_grid, dim3(G), dim3(kSmallBlock), 0, c.s, (const uint32_t*)dd.p,
-                       (uint32_t)(bytes / 4), ps.p, ps.seq, ts);
+    hipLaunchKernelGGL(k_chain_grid, dim3(G), dim3(kSmallBlock), 0, c.s, (const uint32_t*)R.dd.p,
+                       (uint32_t)(bytes / 4), ps.p, ps.seq, R.ts);
     DAS_HIP(hipGetLastError());
   } else {
     ProfScope pf(c, "k_chain", sbytes);
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd, (uint32_t)(bytes / 4), ps.p,
-                       ps.seq, ts);
+                       ps.seq, R.ts);
     DAS_HIP(hipGetLastError());
   }
+  if (R.fence >= 0) DAS_HIP(hipEventRecord(c.fence_event(2 * k + 1), c.s));
+}
+
+uint64_t chain_stage_bytes(const ChainRun& R) { return ((R.bytes + 63) & ~63ull) + 8 * (kChainStages + 4); }
+
+int chain_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out, uint32_t* consumed) {
+  const ChainDesc& d = R.d;
+  const bool grid = R.grid, complete = R.complete;
+  uint64_t* ts = R.ts;
+  auto& tabs = R.tabs;
   uint32_t w[4] = {0, 0, 0, 0};
-  pub_wait(ps, c.s, w, 4);
+  pub_wait(R.ps, R.ls ? R.ls : c.s, w, 4);
+  R.waited = true;
+  if (R.fence >= 0) {
+    DAS_HIP(hipStreamWaitEvent(c.s, c.fence_event(2 * R.fence + 1), 0));
+    R.fence = -1;
+  }
   if (ts) {
     static const char* const kOp[] = {"?", "scan", "ij", "join", "anti"};
     trace_mark("chain copy", std::to_string((ts[1] - ts[0]) / 100.0) + " us");
@@ -4123,16 +4196,16 @@ int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   DAS_CHECK(w[2] < d.nstage && d.st[w[2]].done, DAS_E_INTERNAL, "fused chain: bad running result");
   const uint32_t last = w[2];
   if (grid && w[0] == CHS_OK) {
-    DAS_CHECK(last == (uint32_t)acc, DAS_E_INTERNAL, "grid chain: bad running result");
+    DAS_CHECK(last == (uint32_t)R.acc, DAS_E_INTERNAL, "grid chain: bad running result");
     if (complete && w[1] == 0) return 1;                      // nothing left after the Not filters
-    fin->nrows = w[1];
+    R.fin->nrows = w[1];
     if (complete) {
       matched = true;
-      out = std::move(fin);
+      out = std::move(R.fin);
       return 1;
     }
-    out = std::move(fin);
-    *consumed = terms_done[last];
+    out = std::move(R.fin);
+    *consumed = R.terms_done[last];
     return 2;
   }
   if (w[0] == CHS_OK && last == d.nstage - 1 && complete) {
@@ -4149,8 +4222,43 @@ int fused_and_run(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   if (d.st[last].op == CH_ANTI) return 0;                     // cannot happen (anti stages never stop); be safe
   tabs[last]->nrows = w[1];
   out = std::move(tabs[last]);
-  *consumed = terms_done[last];
+  *consumed = R.terms_done[last];
   return 2;
+}
+
+void ChainRunDel::operator()(ChainRun* r) const {
+  // a run dropped before its outcome was read (an error in another plan of
+  // the batch): its kernels may still read its tables, its pinned descriptor
+  // and its slot, which the next run of the same pool entry reuses
+  if (r && r->ls && !r->waited) (void)hipStreamSynchronize(r->ls);
+  delete r;
+}
+
+ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k) {
+  const int form = fused_and_form(c, terms, anti, no_overload);
+  if (form < 0) return nullptr;
+  for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
+    ChainRunPtr R(new ChainRun);
+    const int r = chain_compile(c, terms, anti, attempt == 0, *R);
+    if (r < 0) continue;
+    if (r == 0 || !R->complete) return nullptr;
+    // DAS_CHAIN_SIDE=0 (A/B): on the context's stream, behind its other work
+    const char* sd = std::getenv("DAS_CHAIN_SIDE");
+    const int side = sd && sd[0] == '0' ? -1 : (int)(k % Ctx::kSide);
+    chain_launch(c, *R, pub_reserve_pool(k), pinned_stage_pool(k, chain_stage_bytes(*R)), side, k);
+    return R;
+  }
+  return nullptr;
+}
+
+int fused_and_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out) {
+  uint32_t consumed = 0;
+  const int r = chain_finish(c, R, matched, out, &consumed);
+  if (r == 1) return 1;
+  matched = false;
+  out.reset();
+  return 0;
 }
 
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,

@@ -646,6 +646,45 @@ def _try_plan(expr, db, answer):
     return matched
 
 
+def matched_many(db, exprs):
+    """[(matched, answer)] of independent expressions, each as
+    `expr.matched(db, answer)` with a fresh PatternMatchingAnswer would give.
+    On one HipDB the plannable ones go to ONE das_plan_execute_many call (the
+    GPU runs an expression's fused chain while the host prepares the next);
+    the rest, and every expression on other DBs, are evaluated one by one."""
+    res = [None] * len(exprs)
+    batch = []
+    if type(db) is HipDB and os.environ.get("DAS_PLAN") != "0":
+        no_overload = bool(CONFIG['no_overload'])
+        key = (db.generation, no_overload)
+        for i, e in enumerate(exprs):
+            # the operators whose matched() tries a whole-expression plan
+            # first, with its prelude (And.matched / Or.matched / Not.matched)
+            if type(e) not in (And, Or, Not) or (type(e) is not Not and not e.terms):
+                continue
+            if type(e) is And and not getattr(e, '_planned', False):
+                e._plan_orders()
+                e._planned = True
+            cached = getattr(e, '_plan', None)
+            if cached is None or cached[0] != key:
+                cached = (key, _lower(e, db, no_overload))
+                e._plan = cached
+            if cached[1] is not None:
+                batch.append((i, cached[1]))
+        if batch:
+            outs = db.ctx.plan_execute_many([(w, len(w) // _WORDS) for _, w in batch], no_overload)
+            for (i, _), (matched, negation, tables) in zip(batch, outs):
+                ans = PatternMatchingAnswer()
+                ans._set(db, Relation(tables))
+                ans.negation = negation
+                res[i] = (matched, ans)
+    for i, e in enumerate(exprs):
+        if res[i] is None:
+            ans = PatternMatchingAnswer()
+            res[i] = (e.matched(db, ans), ans)
+    return res
+
+
 # ---------------------------------------------------------------------------
 # Answers
 # ---------------------------------------------------------------------------

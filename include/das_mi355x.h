@@ -347,6 +347,19 @@ typedef struct {
 int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
                      das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation);
 
+/* n_plans independent plans in one call (no reference counterpart: a batch of
+ * the reference's Expression.matched calls, pattern_matcher.py:705-748 /
+ * :644-687, one per plan): plan i is nodes[i][0 .. n[i]), its answer tables
+ * out[sum(n_out[0..i)) ..], n_out[i] of them, matched[i] / negation[i] as
+ * das_plan_execute's.  Every answer equals das_plan_execute's on that plan
+ * alone; Ands one fused chain answers are launched before any other plan
+ * runs and read back last, so the host work of the batch overlaps their GPU
+ * time.  More than `cap` tables in all: DAS_ERR_INVALID with n_out set and
+ * no table returned. */
+int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,
+                          uint32_t no_overload, das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched,
+                          int32_t* negation);
+
 /* ---- sharded plans (links hash-partitioned by handle across GPUs) ---------- */
 /* One GPU's part of a plan over a KB sharded across GPUs (das_amd.parallel
  * ShardedDB): an INPUT leaf (`value` = index into `inputs`, `scan` = the term

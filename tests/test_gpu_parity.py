@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import das_oracle as O
-from tests.util import build, canon, record, same
+from tests.util import build, canon, record, record_many, same
 
 pytestmark = pytest.mark.gpu
 
@@ -999,9 +999,11 @@ def test_gpu_grid_chain_matches_per_operator(monkeypatch):
                    L("Rel3", V("B"), V("D"))]],
           ["And", [L("Rel", h, V("A")), L("Rel2", V("A"), V("B")), L("Rel6", V("B"), V("C"))]]]
     odb = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
+    wants = []
     for i, q in enumerate(qs):
         monkeypatch.setenv("DAS_FUSED", "0")
         want = record(q, db)
+        wants.append(want)
         if i == 0:
             assert same(want, O.evaluate(q, odb))
         for grid in ("1", None):
@@ -1013,6 +1015,46 @@ def test_gpu_grid_chain_matches_per_operator(monkeypatch):
             got = record(q, db)
             assert same(got, want), (i, grid, got.get("n"), want.get("n"))
         assert want.get("n", 0) > 1000 or i == 3, (i, want.get("n"))
+    # the same Ands as one batch (das_plan_execute_many): grid chains in
+    # flight together, the redo and reset-on-empty ones evaluated again
+    for grid in ("1", None):
+        if grid:
+            monkeypatch.setenv("DAS_CHAIN_GRID", grid)
+        else:
+            monkeypatch.delenv("DAS_CHAIN_GRID", raising=False)
+        for i, (g, w) in enumerate(zip(record_many(qs, db), wants)):
+            assert same(g, w), (i, grid, g.get("n"), w.get("n"))
+
+
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_gpu_plan_execute_many_matches_one_by_one(defer, monkeypatch):
+    """das_plan_execute_many (pm.matched_many, bench.py's step): each answer
+    equals the expression evaluated alone -- FlyBase And / And+Not / Or
+    shapes on several anchors (fused chains launched first, read back last),
+    grid chains including a redo (a segment overflow) and a reset-on-empty,
+    a failing term, a Not root, and an And the chain answers only in part;
+    DAS_DEFER=0 runs every plan in turn."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_DEFER", defer)
+    arrays = synthetic.flybase_kb(200, 6, 400, n_loc=20, n_do=15, seed=3)
+    db = _hipdb(arrays)
+    qs = []
+    for gene in (0, 7, 50, 199, 10 ** 6):
+        qs += [q for _, q in bench.flybase_specs(gene, synthetic.flybase_do_terms(arrays, gene))]
+    qs.append(["Not", qs[0][1][0]])
+    qs = qs + qs[:3]                                    # the same plan twice in one batch
+    want = [record(q, db) for q in qs]
+    got = record_many(qs, db)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert same(g, w), (i, g.get("n"), w.get("n"))
+    assert any(w["n"] for w in want) and any(not w["matched"] for w in want)
+    # more deferrable chains than pooled slots (kPubPool = 16): the rest in turn
+    big = [q for q in qs if q[0] == "And"] * 3
+    assert len(big) > 16
+    got = record_many(big, db)
+    for i, g in enumerate(got):
+        assert same(g, record(big[i], db)), i
 
 
 def test_gpu_native_canonical_load_matches_oracle():

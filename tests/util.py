@@ -63,6 +63,19 @@ def record(expr_spec, db):
             "count": ans.count()}
 
 
+def _rec(m, ans):
+    rows = sorted(json.dumps(canon(a), sort_keys=True) for a in ans.assignments)
+    return {"matched": bool(m), "negation": ans.negation, "n": len(ans.assignments),
+            "sha256": hashlib.sha256("\n".join(rows).encode()).hexdigest(),
+            "count": ans.count()}
+
+
+def record_many(expr_specs, db):
+    """record() of each spec, the batch evaluated by pm.matched_many (one
+    das_plan_execute_many call on a HipDB)."""
+    return [_rec(m, ans) for m, ans in pm.matched_many(db, [build(s) for s in expr_specs])]
+
+
 def same(got, want):
     if want.get("error") or got.get("error"):
         return got.get("error") == want.get("error")
