@@ -397,8 +397,12 @@ struct ChainRunDel {
   void operator()(ChainRun* r) const;
 };
 using ChainRunPtr = std::unique_ptr<ChainRun, ChainRunDel>;
+// side >= 0: compiled and launched on side stream `side` (its tables from
+// that stream's blocks), which first waits for `fence_in` (recorded on the
+// context's stream when the batch began) if *waited is false
 ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k);
+                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k,
+                             int side = -1, hipEvent_t fence_in = nullptr, bool* waited = nullptr);
 int fused_and_finish(Ctx& c, ChainRun& r, bool& matched, std::unique_ptr<Table>& out);
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
              std::unique_ptr<Table>& out);

@@ -15,6 +15,7 @@
 //   Not.matched  :627-631
 // Tables of one relation are kept one per schema, rows distinct, empty tables
 // dropped (das_amd.database.hip_db.Relation).
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -645,22 +646,60 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   std::vector<ChainRunPtr> runs(n_plans);
   const char* f = std::getenv("DAS_DEFER");               // A/B: 0 = every plan in turn
   const bool defer = !(f && f[0] == '0');
+  const char* fh = std::getenv("DAS_DEFER_HOOK");         // A/B: 0 = chains launched before the other plans
+  const char* sd = std::getenv("DAS_CHAIN_SIDE");         // A/B: 0 = chains on the context's stream
+  const bool side = !(sd && sd[0] == '0');
   trace_mark("plans");
   Views v(c);
-  // 1. root Ands one fused chain answers: launched, not waited on
-  uint32_t pooled = 0;
-  for (uint32_t i = 0; i < n_plans && defer && pooled < kPubPool; ++i) {
-    const das_plan_node_t* nd = nodes[i];
-    if (nd[0].op != DAS_PLAN_AND) continue;
-    Exec ex{c, nd, n[i], no_overload};
-    std::vector<const das_plan_node_t*> pos, neg;
-    split_and(ex, ex.children(0), pos, neg);
-    runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled);
-    if (runs[i]) ++pooled;
+  // root Ands are the chain candidates; a chain runs on a side stream (its
+  // tables that stream's blocks), ordered after the context's stream once,
+  // at this fence: blocks of earlier batches' answers were last read there
+  std::vector<uint8_t> cand(n_plans, 0), tried(n_plans, 0);
+  uint32_t n_cand = 0;
+  for (uint32_t i = 0; i < n_plans && defer; ++i)
+    if (nodes[i][0].op == DAS_PLAN_AND && n_cand < kPubPool) {
+      cand[i] = 1;
+      ++n_cand;
+    }
+  hipEvent_t fence_in = nullptr;
+  bool waited[Ctx::kSide] = {false, false, false};
+  if (n_cand && side) {
+    fence_in = c.fence_event(2 * kPubPool);
+    DAS_HIP(hipEventRecord(fence_in, c.s));
   }
-  // 2. the other plans, their host work overlapping the chains on the GPU
+  uint32_t pooled = 0;
+  auto launch_all = [&] {
+    for (uint32_t i = 0; i < n_plans; ++i) {
+      if (!cand[i] || tried[i]) continue;
+      tried[i] = 1;
+      Exec ex{c, nodes[i], n[i], no_overload};
+      std::vector<const das_plan_node_t*> pos, neg;
+      split_and(ex, ex.children(0), pos, neg);
+      const int sidx = side ? (int)(pooled % Ctx::kSide) : -1;
+      runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled, sidx, fence_in, sidx >= 0 ? &waited[sidx] : nullptr);
+      if (runs[i]) ++pooled;
+    }
+  };
+  // 1. the other plans first; the chains are compiled and launched by the
+  // first read-back one of them waits for (that host time is otherwise
+  // spent spinning), or right away without one
+  std::function<void()> hook = launch_all;
+  const bool hooked = n_cand && !(fh && fh[0] == '0');
+  if (!hooked) launch_all();
+  struct Unhook {
+    ~Unhook() { set_wait_hook(nullptr); }
+  } uh;
+  if (hooked) set_wait_hook(&hook);
   for (uint32_t i = 0; i < n_plans; ++i) {
-    if (runs[i]) continue;
+    if (cand[i]) continue;
+    Exec ex{c, nodes[i], n[i], no_overload};
+    outs[i] = output(c, ex.eval(0));
+  }
+  set_wait_hook(nullptr);
+  launch_all();                                           // (no-op once the hook ran)
+  // 2. candidates no chain answers, in turn
+  for (uint32_t i = 0; i < n_plans; ++i) {
+    if (!cand[i] || runs[i]) continue;
     Exec ex{c, nodes[i], n[i], no_overload};
     outs[i] = output(c, ex.eval(0));
   }

@@ -3,6 +3,7 @@
 // All launches go on the caller's stream; nothing here synchronises except
 // the explicit `read_scalar` helper.
 #pragma once
+#include <functional>
 #include "common.h"
 
 namespace das {
@@ -205,6 +206,11 @@ struct PubSlot {
 };
 PubSlot pub_reserve();
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
+// Host work to do while a read-back is outstanding: the next pub_wait of this
+// thread whose slot is not yet written runs it once (and clears it) before
+// it spins -- das_plan_execute_many compiles and launches its chains while a
+// synchronous plan waits for a size.  nullptr: none.
+void set_wait_hook(std::function<void()>* hook);
 // Pinned, device-mapped staging memory for small request / reply calls
 // (handle lookups, index key ranges): the host writes the request, one
 // kernel reads it over the mapping and writes its reply back with

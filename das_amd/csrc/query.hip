@@ -3156,7 +3156,7 @@ struct IjPlan {
 };
 
 // false: not an index join of A (the caller scans the term and joins)
-bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows, IjPlan& pl) {
+bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows, IjPlan& pl, bool dir_only = false) {
   Index& idx = c.idx;
   DAS_CHECK(idx.built, DAS_E_NOT_BUILT, "index not built");
   const uint32_t ar = q.arity;
@@ -3292,11 +3292,13 @@ bool ij_prepare(Ctx& c, const Table& A, const das_link_scan_t& q, uint64_t rows,
     // the build side of a direct join (FlyBase FJ: 3*10^5 probes into the
     // 4.5*10^5 rows of one schema, 73-76 vs 64-65 us per query) -- not an
     // index join then (DAS_INDEX_JOIN=1 / DAS_IJ_RANGED=1 keep it)
+    // (dir_only: the fused chain's probes after a partitioned scan -- the
+    // key-directory lookup instead of that search, no scan)
     const char* fij = std::getenv("DAS_INDEX_JOIN");
-    if (best != ~0ull && best > 0 && rows > 4096 && !(f && f[0] == '1') && !(fij && fij[0] == '1') &&
-        (double)rows * std::log2((double)best) > 2.0 * (double)best)
-      return false;
-    const bool take = best != ~0ull &&
+    const bool long_range = best != ~0ull && best > 0 && rows > 4096 && !(f && f[0] == '1') &&
+                            (double)rows * std::log2((double)best) > 2.0 * (double)best;
+    if (long_range && !dir_only && !(fij && fij[0] == '1')) return false;
+    const bool take = best != ~0ull && !(dir_only && long_range) &&
                       ((f && f[0] == '1') || (best <= (1ull << 22) && best <= 64ull * rows));
     if (take) {
       g = gb;
@@ -3543,9 +3545,16 @@ __device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, u
       const bool app = st.append != kChainNoStage;
       if (app && threadIdx.x == 0) s_run = s_cnt[st.append];
       __syncthreads();
-      for (uint32_t r0 = st.begin; r0 < st.end; r0 += kSmallBlock) {
+      // grid, partitioned scan (the chain's first term, too large to
+      // replicate): this workgroup's slice of the rows, then every later
+      // stage is row-local
+      const bool pscan = GRID && st.part;
+      const uint64_t span = st.end - st.begin;
+      const uint32_t sb = pscan ? st.begin + (uint32_t)(span * wg / G) : st.begin;
+      const uint32_t se = pscan ? st.begin + (uint32_t)(span * (wg + 1) / G) : st.end;
+      for (uint32_t r0 = sb; r0 < se; r0 += kSmallBlock) {
         const uint32_t r = r0 + threadIdx.x;
-        const bool keep = r < st.end && scan_keep(st.sp, r);
+        const bool keep = r < se && scan_keep(st.sp, r);
         const uint32_t pos = chain_rank(keep, s_w, &s_run);
         if (keep)                                      // chain scans are ordered (no local sort buffer)
           for (uint32_t c = 0; c < st.sp.nout; ++c) dst[c * ld + pos] = st.sp.col[1 + st.sp.outpos[c]][r];
@@ -3554,6 +3563,13 @@ __device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, u
       if (app) {
         if (threadIdx.x == 0) s_cnt[st.append] = n;
         n = 0;
+      } else if (pscan) {
+        // an empty slice is not a failing term: the last workgroup tells
+        // from the stage's total (kGscOut publish below)
+        if (threadIdx.x == 0) {
+          atomicAdd(&d.gsc[si], n);
+          s_parted = 1;
+        }
       } else if (n == 0 && !st.empty_ok && threadIdx.x == 0) {
         s_state = CHS_EMPTY_SCAN;
       }
@@ -3763,7 +3779,13 @@ __device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, u
             empty |= 1u << si;
           after = after || d.st[si].part;
         }
-        const uint32_t st = redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
+        // a partitioned scan with no row on any workgroup: a failing term
+        bool failed = false;
+        for (uint32_t si = 0; si < d.nstage; ++si)
+          if (d.st[si].op == CH_SCAN && d.st[si].part && d.st[si].append == kChainNoStage && !d.st[si].empty_ok &&
+              __hip_atomic_load(&d.gsc[si], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            failed = true;
+        const uint32_t st = failed ? CHS_EMPTY_SCAN : redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
         const uint32_t total = st == CHS_OK ? __hip_atomic_load(&d.gsc[kGscOut], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                             : s_cnt[s_acc];
         __hip_atomic_store(&slot[0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3838,6 +3860,10 @@ uint32_t cu_count(Ctx& c) {
   return (uint32_t)v;
 }
 
+// rows a partitioned first scan may have: half of the grid's segments (room
+// for an index join's fan-out on each slice)
+uint64_t part_scan_max(Ctx& c) { return (uint64_t)cu_count(c) * kGridSeg / 2; }
+
 bool chain_grid_wanted(Ctx& c, const std::vector<const das_plan_node_t*>& terms, size_t n_anti, bool force) {
   if (terms.size() < 2) return false;
   std::vector<int32_t> vars;
@@ -3862,6 +3888,16 @@ bool chain_grid_wanted(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     scan_prepare(c, x->scan, P);
     if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) return false;
     const uint64_t r = P.ranges[0].second - P.ranges[0].first;
+    // a first term too large to replicate, followed by an index join: the
+    // grid can partition the scan itself (each workgroup a slice of its
+    // rows).  Off unless DAS_CHAIN_PSCAN=1: on FlyBase FJ (3*10^5 probes, the
+    // key-directory lookups of a 4.5*10^5-row schema) the chain took 61 us
+    // on the GPU against 47 us for the scan + direct join, and the batched
+    // step 0.250-0.268 vs 0.212-0.226 ms (profiles/r5_flybase_env_ab.txt)
+    if (k == 0 && r > kGridSeg) {
+      const char* ps = std::getenv("DAS_CHAIN_PSCAN");
+      return ps && ps[0] == '1' && terms[1]->op == DAS_PLAN_LINK && terms[1]->index_join && r <= part_scan_max(c);
+    }
     if (r > kGridSeg) return false;
     bound *= std::max<uint64_t>(r, 1);
     vars.insert(vars.end(), P.vars, P.vars + P.ncols);
@@ -3946,6 +3982,7 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     st->dst = t.data;
   };
   bool parted = false;
+  uint64_t scan_rows = 0;                                     // a partitioned first scan's rows
   // a chain ending early (too many stages) still folds the terms compiled so
   // far; the caller continues from there
   int& acc = R.acc;                                           // stage holding the running result
@@ -3956,7 +3993,9 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     if (acc >= 0 && x->index_join) {
       IjPlan pl;
       const Table& A = *tabs[acc];
-      const bool ijok = ij_prepare(c, A, x->ij, kIjSmall, pl);
+      // (after a partitioned scan each workgroup probes its slice: the
+      // lookup through the key directory, never a search of one long range)
+      const bool ijok = scan_rows ? ij_prepare(c, A, x->ij, scan_rows, pl, true) : ij_prepare(c, A, x->ij, kIjSmall, pl);
       if (trace_on()) trace_mark("prep ij_prepare");
       if (ijok) {
         if (pl.empty) { all_terms = false; break; }
@@ -3988,11 +4027,14 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     if (trace_on()) trace_mark("prep scan_prepare");
     if (P.empty || P.kind != DAS_TABLE_ORDERED || P.ranges.size() != 1) { all_terms = false; break; }
     const uint64_t b = P.ranges[0].first, e = P.ranges[0].second;
-    if (e - b > kSmallScan || e >= 0xFFFFFFFFull || d.nstage + (acc >= 0 ? 2 : 1) > (uint32_t)kChainStages) {
+    // grid: every workgroup scans it into its segment, or (the first term,
+    // larger than a segment) each a slice of it
+    const bool pscan = grid && acc < 0 && e - b > kGridSeg && e - b <= part_scan_max(c);
+    if ((e - b > kSmallScan && !pscan) || e >= 0xFFFFFFFFull || d.nstage + (acc >= 0 ? 2 : 1) > (uint32_t)kChainStages) {
       all_terms = false;
       break;
     }
-    if (grid && e - b > kGridSeg) return -1;                 // every workgroup scans it into its segment
+    if (grid && e - b > kGridSeg && !pscan) return -1;
     ChainStage* st = add(CH_SCAN);
     auto t = new_table(c, P.kind, P.ncols, P.vars, grid ? gcap : e - b);
     scan_bounds(idx, P.sp, x->scan.type_id, *t);
@@ -4002,6 +4044,11 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
     st->end = (uint32_t)e;
     place(st, *t);
     st->done = acc < 0 ? 1 : 0;
+    if (pscan) {
+      st->part = 1;
+      parted = true;
+      scan_rows = e - b;
+    }
     tabs.push_back(std::move(t));
     const int rel = (int)d.nstage - 1;
     if (acc < 0) {
@@ -4102,24 +4149,11 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
 
 // `stage`: pinned host memory of at least chain_stage_bytes(R) that stays
 // untouched until chain_finish (the launches read the descriptor from it).
-// side >= 0: launched on side stream `side` after the work the context's
-// stream holds so far (fence event 2k), so that it runs alongside later work
-// of the context's stream; chain_finish makes the context's stream wait for
-// it (fence event 2k + 1) before any of its tables is read or freed there.
+// fence >= 0: launched on a side stream (c.s points at it, fused_and_launch);
+// fence event 2k + 1 marks its end, which chain_finish makes the context's
+// stream wait for before any of its tables is read there.
 void chain_launch(Ctx& c, ChainRun& R, const PubSlot& ps, uint8_t* stage, int side, uint32_t k) {
-  struct Swap {                                               // the launches go to c.s: point it at the side stream
-    Ctx& c;
-    hipStream_t old;
-    ~Swap() { c.s = old; }
-  } sw{c, c.s};
-  if (side >= 0) {
-    hipStream_t ss = c.side_stream(side);
-    hipEvent_t in = c.fence_event(2 * k);
-    DAS_HIP(hipEventRecord(in, c.s));
-    DAS_HIP(hipStreamWaitEvent(ss, in, 0));
-    c.s = ss;
-    R.fence = (int)k;
-  }
+  if (side >= 0) R.fence = (int)k;
   R.ls = c.s;
   const ChainDesc& d = R.d;
   const uint64_t bytes = R.bytes;
@@ -4235,17 +4269,30 @@ void ChainRunDel::operator()(ChainRun* r) const {
 }
 
 ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k) {
+                             const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k,
+                             int side, hipEvent_t fence_in, bool* waited) {
   const int form = fused_and_form(c, terms, anti, no_overload);
   if (form < 0) return nullptr;
+  // a side stream: the run's tables are that stream's blocks, so it needs no
+  // ordering after the context's stream beyond the batch's first fence
+  struct Swap {
+    Ctx& c;
+    hipStream_t old;
+    ~Swap() { c.s = old; }
+  } sw{c, c.s};
+  if (side >= 0) {
+    hipStream_t ss = c.side_stream(side);
+    if (waited && !*waited) {
+      DAS_HIP(hipStreamWaitEvent(ss, fence_in, 0));
+      *waited = true;
+    }
+    c.s = ss;
+  }
   for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
     ChainRunPtr R(new ChainRun);
     const int r = chain_compile(c, terms, anti, attempt == 0, *R);
     if (r < 0) continue;
     if (r == 0 || !R->complete) return nullptr;
-    // DAS_CHAIN_SIDE=0 (A/B): on the context's stream, behind its other work
-    const char* sd = std::getenv("DAS_CHAIN_SIDE");
-    const int side = sd && sd[0] == '0' ? -1 : (int)(k % Ctx::kSide);
     chain_launch(c, *R, pub_reserve_pool(k), pinned_stage_pool(k, chain_stage_bytes(*R)), side, k);
     return R;
   }

@@ -662,9 +662,6 @@ def matched_many(db, exprs):
             # first, with its prelude (And.matched / Or.matched / Not.matched)
             if type(e) not in (And, Or, Not) or (type(e) is not Not and not e.terms):
                 continue
-            if type(e) is And and not getattr(e, '_planned', False):
-                e._plan_orders()
-                e._planned = True
             cached = getattr(e, '_plan', None)
             if cached is None or cached[0] != key:
                 cached = (key, _lower(e, db, no_overload))
@@ -1125,12 +1122,14 @@ class And(LogicalExpression):
         db = _hip(db)
         if not self.terms:
             return False
-        if not getattr(self, '_planned', False):
-            self._plan_orders()
-            self._planned = True
+        # (the scan-order hints: _walk sets them when it lowers the And, and a
+        # query shape seen before needs none)
         r = _try_plan(self, db, answer)
         if r is not None:
             return r
+        if not getattr(self, '_planned', False):
+            self._plan_orders()
+            self._planned = True
         _prefetch(self, db)
         acc = None
         forbidden = []

@@ -1015,6 +1015,29 @@ def test_gpu_grid_chain_matches_per_operator(monkeypatch):
             got = record(q, db)
             assert same(got, want), (i, grid, got.get("n"), want.get("n"))
         assert want.get("n", 0) > 1000 or i == 3, (i, want.get("n"))
+    # a first term larger than a segment (Rel6: 5000 rows > kGridSeg) before
+    # an index join: the grid partitions the scan itself (DAS_CHAIN_PSCAN=1;
+    # 0, the default: scan + direct join); a join empty on every workgroup, a first term
+    # with no row at all
+    monkeypatch.delenv("DAS_CHAIN_GRID", raising=False)
+    ps = [["And", [L("Rel6", V("B"), V("C")), L("Rel7", V("C"), V("D"))]],
+          ["And", [L("Rel6", V("B"), V("C")), L("Rel3", V("D"), V("C"))]],
+          ["And", [L("Rel6", V("B"), V("C")), L("Rel4", V("C"), V("D"))]],
+          ["And", [L("Rel6", ["Node", "Concept", "y8"], V("C")), L("Rel7", V("C"), V("D"))]]]
+    for i, q in enumerate(ps):
+        monkeypatch.setenv("DAS_FUSED", "0")
+        want = record(q, db)
+        monkeypatch.setenv("DAS_FUSED", "1")
+        for pscan in ("1", "0"):
+            monkeypatch.setenv("DAS_CHAIN_PSCAN", pscan)
+            got = record(q, db)
+            assert same(got, want), ("pscan", i, pscan, got.get("n"), want.get("n"))
+        if i < 2:
+            assert want["n"] > 0, i
+    monkeypatch.setenv("DAS_CHAIN_PSCAN", "1")
+    for i, (g, w) in enumerate(zip(record_many(ps, db), [record(q, db) for q in ps])):
+        assert same(g, w), ("pscan batch", i)
+    monkeypatch.delenv("DAS_CHAIN_PSCAN", raising=False)
     # the same Ands as one batch (das_plan_execute_many): grid chains in
     # flight together, the redo and reset-on-empty ones evaluated again
     for grid in ("1", None):
