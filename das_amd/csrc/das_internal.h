@@ -404,6 +404,10 @@ ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& 
                              const std::vector<const das_plan_node_t*>& anti, int no_overload, uint32_t k,
                              int side = -1, hipEvent_t fence_in = nullptr, bool* waited = nullptr);
 int fused_and_finish(Ctx& c, ChainRun& r, bool& matched, std::unique_ptr<Table>& out);
+// false when fused_and_launch would surely return null (a first term too
+// large for the one-workgroup chain): host checks only, nothing allocated
+bool fused_and_viable(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                      const std::vector<const das_plan_node_t*>& anti, int no_overload);
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
              std::unique_ptr<Table>& out);
 

@@ -132,18 +132,19 @@ uint8_t* pinned_stage_pool(uint32_t k, uint64_t bytes) {
 }
 
 namespace {
-thread_local std::function<void()>* t_wait_hook = nullptr;
+thread_local WaitHook* t_wait_hook = nullptr;
 }
 
-void set_wait_hook(std::function<void()>* hook) { t_wait_hook = hook; }
+void set_wait_hook(WaitHook* hook) { t_wait_hook = hook; }
 
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
   count_readback();
   if (t_wait_hook && *t_wait_hook && __atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) != ps.seq) {
-    std::function<void()> f = std::move(*t_wait_hook);
-    *t_wait_hook = nullptr;
+    WaitHook* h = t_wait_hook;
+    t_wait_hook = nullptr;                       // no nested call from inside the hook
     trace_mark("wait hook");
-    f();
+    const bool done = (*h)([&] { return __atomic_load_n(&ps.p[15], __ATOMIC_ACQUIRE) == ps.seq; });
+    t_wait_hook = done ? nullptr : h;
   }
   trace_mark("wait");
   for (uint64_t it = 1;; ++it) {

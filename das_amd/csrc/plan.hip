@@ -656,21 +656,29 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   // at this fence: blocks of earlier batches' answers were last read there
   std::vector<uint8_t> cand(n_plans, 0), tried(n_plans, 0);
   uint32_t n_cand = 0;
-  for (uint32_t i = 0; i < n_plans && defer; ++i)
-    if (nodes[i][0].op == DAS_PLAN_AND && n_cand < kPubPool) {
-      cand[i] = 1;
-      ++n_cand;
-    }
+  for (uint32_t i = 0; i < n_plans && defer; ++i) {
+    if (nodes[i][0].op != DAS_PLAN_AND || n_cand >= kPubPool) continue;
+    Exec ex{c, nodes[i], n[i], no_overload};
+    std::vector<const das_plan_node_t*> pos, neg;
+    split_and(ex, ex.children(0), pos, neg);
+    if (!fused_and_viable(c, pos, neg, no_overload)) continue;   // runs with the other plans
+    cand[i] = 1;
+    ++n_cand;
+  }
   hipEvent_t fence_in = nullptr;
   bool waited[Ctx::kSide] = {false, false, false};
   if (n_cand && side) {
     fence_in = c.fence_event(2 * kPubPool);
     DAS_HIP(hipEventRecord(fence_in, c.s));
   }
-  uint32_t pooled = 0;
-  auto launch_all = [&] {
-    for (uint32_t i = 0; i < n_plans; ++i) {
+  uint32_t pooled = 0, next = 0;
+  // compiles and launches the next candidates' chains while ready() is false
+  // (every remaining one when it is null); true when none is left
+  auto launch_some = [&](const std::function<bool()>* ready) {
+    for (; next < n_plans; ++next) {
+      const uint32_t i = next;
       if (!cand[i] || tried[i]) continue;
+      if (ready && (*ready)()) return false;
       tried[i] = 1;
       Exec ex{c, nodes[i], n[i], no_overload};
       std::vector<const das_plan_node_t*> pos, neg;
@@ -679,11 +687,13 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled, sidx, fence_in, sidx >= 0 ? &waited[sidx] : nullptr);
       if (runs[i]) ++pooled;
     }
+    return true;
   };
-  // 1. the other plans first; the chains are compiled and launched by the
-  // first read-back one of them waits for (that host time is otherwise
-  // spent spinning), or right away without one
-  std::function<void()> hook = launch_all;
+  auto launch_all = [&] { launch_some(nullptr); };
+  // 1. the other plans first; the chains are compiled and launched in the
+  // gaps where those plans wait for a read-back (host time otherwise spent
+  // spinning), the rest after them
+  WaitHook hook = [&](const std::function<bool()>& ready) { return launch_some(&ready); };
   const bool hooked = n_cand && !(fh && fh[0] == '0');
   if (!hooked) launch_all();
   struct Unhook {

@@ -206,11 +206,14 @@ struct PubSlot {
 };
 PubSlot pub_reserve();
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
-// Host work to do while a read-back is outstanding: the next pub_wait of this
-// thread whose slot is not yet written runs it once (and clears it) before
-// it spins -- das_plan_execute_many compiles and launches its chains while a
-// synchronous plan waits for a size.  nullptr: none.
-void set_wait_hook(std::function<void()>* hook);
+// Host work to do while a read-back is outstanding: a pub_wait of this
+// thread whose slot is not yet written calls the hook with a predicate "the
+// slot is written" before it spins; the hook does work in pieces while the
+// predicate is false and returns true once it has none left (it is then
+// cleared) -- das_plan_execute_many compiles and launches its chains in the
+// gaps where a synchronous plan waits for a size.  nullptr: none.
+using WaitHook = std::function<bool(const std::function<bool()>& ready)>;
+void set_wait_hook(WaitHook* hook);
 // Pinned, device-mapped staging memory for small request / reply calls
 // (handle lookups, index key ranges): the host writes the request, one
 // kernel reads it over the mapping and writes its reply back with

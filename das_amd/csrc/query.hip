@@ -4229,6 +4229,10 @@ int chain_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out
   }
   DAS_CHECK(w[2] < d.nstage && d.st[w[2]].done, DAS_E_INTERNAL, "fused chain: bad running result");
   const uint32_t last = w[2];
+  // algorithmic bytes known only now: the final rows (grid: written to a
+  // workgroup segment, then gathered into the output table)
+  if (w[0] == CHS_OK && c.prof)
+    prof_add_bytes(c, grid ? "k_chain_grid" : "k_chain", (grid ? 12.0 : 4.0) * d.st[last].ncols * w[1]);
   if (grid && w[0] == CHS_OK) {
     DAS_CHECK(last == (uint32_t)R.acc, DAS_E_INTERNAL, "grid chain: bad running result");
     if (complete && w[1] == 0) return 1;                      // nothing left after the Not filters
@@ -4258,6 +4262,20 @@ int chain_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out
   out = std::move(tabs[last]);
   *consumed = R.terms_done[last];
   return 2;
+}
+
+bool fused_and_viable(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
+                      const std::vector<const das_plan_node_t*>& anti, int no_overload) {
+  const int form = fused_and_form(c, terms, anti, no_overload);
+  if (form < 0) return false;
+  if (form == 1) return true;
+  // the one-workgroup chain scans its first term whole: not past kSmallScan rows
+  const das_plan_node_t* x = terms[0];
+  if (x->op != DAS_PLAN_LINK || !x->scan.ordered || x->dedup) return false;
+  ScanPrep P;
+  scan_prepare(c, x->scan, P);
+  return !P.empty && P.kind == DAS_TABLE_ORDERED && P.ranges.size() == 1 &&
+         P.ranges[0].second - P.ranges[0].first <= kSmallScan;
 }
 
 void ChainRunDel::operator()(ChainRun* r) const {
