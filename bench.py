@@ -1181,6 +1181,11 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                            "network fetch)",
                 "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
         cfg = dict(cfg, bindings_per_step=per_query, parallelism=f"links sharded x{world}")
+        # how a step submits its queries: one das_plan_execute_many call
+        # (pm.matched_many; Q2 alone while its launches are tagged), or one
+        # matched() per query; N > 1: ShardedMatcher.count_many
+        cfg["step_calls"] = ("ShardedMatcher.count_many" if world > 1 else
+                             "pm.matched_many (das_plan_execute_many)" if args.batch else "matched() per query")
         cfg["query_ms_rank0"] = per_query_ms
         cfg["query_launches_readbacks_rank0"] = per_query_ops
         out = {

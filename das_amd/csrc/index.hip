@@ -764,6 +764,44 @@ __global__ void k_pack_key32(const uint32_t* __restrict__ col, uint64_t b, uint6
   }
 }
 
+// P_{a,p} (p > 0) from P_{a,0}'s rows [b, b + n) of one type, which are in
+// (t_0, .., t_{a-1}) order: key = (t_p - lo) << 32 | low, where low is the
+// other target (arity 2) or the row's place in the segment (arity 3); val =
+// the link id.  A stable sort on the high word alone then gives (t_p, the
+// other targets in position order) -- P_{a,p}'s order -- in ~27-bit passes.
+__global__ void k_derive_key(const uint32_t* __restrict__ P0, uint64_t ld, uint64_t b, uint64_t n, uint32_t ar,
+                             uint32_t p, uint32_t lo, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint32_t q = p == 0 ? 1u : 0u;               // arity 2: the other position
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = b + i;
+    const uint32_t low = ar == 2 ? P0[(uint64_t)(1 + q) * ld + r] : (uint32_t)i;
+    key[i] = ((uint64_t)(P0[(uint64_t)(1 + p) * ld + r] - lo) << 32) | low;
+    val[i] = P0[r];
+  }
+}
+
+// sorted derive keys -> P_{a,p} rows [b, b + n); arity 3 reads its two other
+// targets at P_{a,0} row b + low
+__global__ void k_derive_unpack(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n,
+                                uint32_t ar, uint32_t p, uint32_t lo, uint32_t ty, const uint32_t* __restrict__ P0,
+                                uint64_t ld0, uint64_t b, uint32_t* __restrict__ out, uint64_t ld,
+                                uint64_t* __restrict__ pk) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key[i];
+    const uint32_t tp = (uint32_t)(k >> 32) + lo, low = (uint32_t)k;
+    const uint64_t o = b + i;
+    out[o] = val[i];
+    out[(uint64_t)(1 + p) * ld + o] = tp;
+    if (ar == 2) {
+      out[(uint64_t)(1 + (p == 0 ? 1u : 0u)) * ld + o] = low;
+    } else {
+      for (uint32_t q = 0; q < ar; ++q)
+        if (q != p) out[(uint64_t)(1 + q) * ld + o] = P0[(uint64_t)(1 + q) * ld0 + b + low];
+    }
+    pk[o] = ((uint64_t)ty << 32) | tp;
+  }
+}
+
 // sorted (key, val) -> P rows [ob, ob + n): id, the key's targets, and the
 // target left out of the key (pos_rest, read at T row b + val; val is then a
 // row, else the link id); pk = type << 32 | t_p for the key directory
@@ -1936,7 +1974,33 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
         P.t.ld = col_stride(R);
         P.t.data = dalloc<uint32_t>(idx, (uint64_t)(ar + 1) * P.t.ld);
         DBuf<uint64_t> pk(R, s);
-        for (uint32_t ty = 0; ty < a.n_types; ++ty) {
+        // p > 0: from P_{a,0}'s rows (DAS_PIDX_DERIVE=0: each P_{a,p} sorted
+        // from the type table on its full key, A/B)
+        const char* dv = std::getenv("DAS_PIDX_DERIVE");
+        const bool derive = p > 0 && (ar == 2 || ar == 3) && !(dv && dv[0] == '0');
+        const PosIndex& P0 = idx.pidx[ar][0];
+        for (uint32_t ty = 0; ty < a.n_types && derive; ++ty) {
+          const uint64_t b = to[ty], n = to[ty + 1] - to[ty];
+          if (!n) continue;
+          const uint32_t lo = tb[((uint64_t)ty * ncol + 1 + p) * 2];
+          const uint32_t bits = (uint32_t)bits_for(tb[((uint64_t)ty * ncol + 1 + p) * 2 + 1] - lo);
+          DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "pattern index: a type segment of 2^32 links");
+          DBuf<uint64_t> key(n, s);
+          DBuf<uint32_t> val(n, s);
+          {
+            KScope ks("k_derive_key", 4.0 * (ar == 2 ? 3 : 2) * n + 12.0 * n);
+            hipLaunchKernelGGL(k_derive_key, G(n), dim3(B), 0, s, (const uint32_t*)P0.t.data, P0.t.ld, b, n, ar, p, lo,
+                               key.p, val.p);
+          }
+          if (bits) radix_sort_pairs<uint64_t>(key.p, val.p, n, 32, 32 + (int)bits, s);
+          {
+            KScope ks("k_derive_unpack", 12.0 * n + 4.0 * (ar + 1) * n + 8.0 * n + (ar == 3 ? 8.0 * n : 0.0));
+            hipLaunchKernelGGL(k_derive_unpack, G(n), dim3(B), 0, s, (const uint64_t*)key.p, (const uint32_t*)val.p, n,
+                               ar, p, lo, ty, (const uint32_t*)P0.t.data, P0.t.ld, b, P.t.data, P.t.ld, pk.p);
+          }
+          DAS_HIP(hipGetLastError());
+        }
+        for (uint32_t ty = 0; ty < a.n_types && !derive; ++ty) {
           const uint64_t b = to[ty], n = to[ty + 1] - to[ty];
           if (!n) continue;
           // fields: t_p, then the other positions in order

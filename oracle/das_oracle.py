@@ -524,6 +524,41 @@ def join(a, b):
     return _c_join(a, b)
 
 
+FAST_JOIN = True            # tests: False = the nested loop everywhere
+
+
+def _ordered_hash_join(acc, rows):
+    """The And fold's nested loop (:732-738) for ordered rows of one variable
+    set per side: only pairs agreeing on the shared variables can join
+    (_o_compat is INCOMPATIBLE otherwise, and join() returns None), so each
+    row of `acc` is joined with the rows of `rows` that carry its shared
+    values.  The same joined rows -- as a list in another order; the fold
+    keeps only their set and their emptiness -- at the cost of the output
+    instead of |acc| x |rows|.  None: not that case (the caller loops)."""
+    if CONFIG["no_overload"] or not FAST_JOIN:
+        return None
+    rows = list(rows)
+    if not acc or not rows or any(r[0] != "O" for r in acc) or any(r[0] != "O" for r in rows):
+        return None
+    va = {tuple(v for v, _ in r[1]) for r in acc}
+    vb = {tuple(v for v, _ in r[1]) for r in rows}
+    if len(va) != 1 or len(vb) != 1:
+        return None
+    shared = sorted(set(next(iter(va))) & set(next(iter(vb))))
+    index = {}
+    for b in rows:
+        m = dict(b[1])
+        index.setdefault(tuple(m[v] for v in shared), []).append(b)
+    out = []
+    for a in acc:
+        m = dict(a[1])
+        for b in index.get(tuple(m[v] for v in shared), ()):
+            j = _o_join(a, b)
+            if j is not None:
+                out.append(j)
+    return out
+
+
 def check_negation(a, tabu):
     """a.check_negation(tabu) — :112-117, :211-217, :353-362."""
     if a[0] == "O":
@@ -725,7 +760,9 @@ def matched(spec, db, answer):
             if not acc:
                 acc = list(sub.rows)
                 continue
-            acc = [j for a in acc for b in sub.rows for j in [join(a, b)] if j is not None]
+            fast = _ordered_hash_join(acc, sub.rows)
+            acc = fast if fast is not None else \
+                [j for a in acc for b in sub.rows for j in [join(a, b)] if j is not None]
         result = RowSet()
         for a in acc:
             if all(check_negation(a, t) for t in forbidden):

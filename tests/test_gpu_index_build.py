@@ -4,7 +4,9 @@ position order, link id) -- the `patterns:` key families of
 canonical_parser.py:148-176 with each key's links ordered so an anchored
 range comes out sorted by its first free target.  The packed-key build (one
 stable sort per type segment, two stages when the key exceeds 64 bits) must
-equal the permutation build (DAS_PIDX_PERM=1) row for row."""
+equal the permutation build (DAS_PIDX_PERM=1) row for row, and P_{a,p>0}
+derived from P_{a,0} (the default: a stable sort on t_p alone) the full-key
+sort of each (DAS_PIDX_DERIVE=0)."""
 import numpy as np
 import pytest
 
@@ -53,9 +55,10 @@ def test_gpu_pattern_index_order(kb, monkeypatch):
     from das_amd.database.hip_db import HipDB
     arrays = _kb(kb)
     got = {}
-    for mode in ("packed", "two", "perm"):
+    for mode in ("packed", "two", "perm", "noderive"):
         monkeypatch.setenv("DAS_PIDX_PERM", "1" if mode == "perm" else "0")
         monkeypatch.setenv("DAS_PIDX_TWO", "1" if mode == "two" else "0")
+        monkeypatch.setenv("DAS_PIDX_DERIVE", "0" if mode == "noderive" else "1")
         db = HipDB(device=0)
         db.load_arrays(arrays)
         got[mode] = _p_rows(db.ctx, db.stats().n_types)
@@ -71,5 +74,5 @@ def test_gpu_pattern_index_order(kb, monkeypatch):
         # np.lexsort: last key is the primary one
         order = np.lexsort([T[0]] + [T[c] for c in reversed(others)] + [T[1 + p]])
         assert np.array_equal(P, T[:, order]), key
-        for mode in ("two", "perm"):
+        for mode in ("two", "perm", "noderive"):
             assert np.array_equal(got[mode][key], P), (mode, key)
