@@ -1401,6 +1401,11 @@ def main():
             continue
         t_leg = time.perf_counter()
         a = argparse.Namespace(**dict(vars(args), cpu_baseline_seconds=args.leg_cpu_seconds))
+        if w == "flybase":
+            # a latency-bound step of ~0.25 ms: more untimed warmup steps (the
+            # side streams' blocks, pinned pools, shape caches) and more timed
+            # ones against scheduling noise -- milliseconds either way
+            a.warmup, a.steps = max(args.warmup, 5), max(args.steps, 40)
         try:
             r = run_leg(w, a)
         except Exception as e:            # one leg failing must not lose the headline line
