@@ -2,8 +2,7 @@
 // assignment identity (pattern_matcher.py:41-51: an OrderedAssignment is its
 // var -> handle mapping; PatternMatchingAnswer keeps a *set* of them,
 // :370-384, 741-748).  Parity at BASELINE sizes compares this value with the
-// same function computed from a generator's own arrays (tests/util.py
-// `checksum_*`), so a wrong row with the right row count is caught.
+// same function computed from a generator's own arrays (tests/checksum.py), so a wrong row with the right row count is caught.
 //
 //   g(v, d)  = splitmix64_final(d64 ^ salt[v]) | 1     (odd, so products stay informative)
 //   row(r)   = prod over columns c of g(var_c, digest(value_c))   mod 2^64

@@ -514,9 +514,203 @@ static PyObject *seed(PyObject *self, PyObject *args) {
   Py_RETURN_NONE;
 }
 
+/* ---- query-shape cache hits (pattern_matcher._lower) ---------------------
+ * shape(expr): the structure key pattern_matcher._shape builds, nodes
+ * appended to `nodes` in walk order; NULL with no exception set = no shape
+ * (_NoShape: an unordered link type, a link whose targets are all nodes, an
+ * unknown expression kind). */
+static PyObject *s_k, *s_atom_type, *s_name, *s_type, *s_ordered, *s_targets, *s_link_type, *s_term, *s_terms,
+    *s_handle, *s_copy, *s_tags;
+
+static PyObject *shape_of(PyObject *e, PyObject *nodes, PyObject *unordered, int depth) {
+  if (depth > 64) return NULL;
+  PyObject *k = PyObject_GetAttr(e, s_k);
+  if (!k) { PyErr_Clear(); return NULL; }
+  const char *ks = PyUnicode_Check(k) ? PyUnicode_AsUTF8(k) : NULL;
+  PyObject *out = NULL;
+  if (!ks) { PyErr_Clear(); Py_DECREF(k); return NULL; }
+  if (!strcmp(ks, "n")) {
+    if (PyList_Append(nodes, e) == 0) out = PyObject_GetAttr(e, s_atom_type);
+  } else if (!strcmp(ks, "v")) {
+    PyObject *n = PyObject_GetAttr(e, s_name);
+    if (n) out = Py_BuildValue("(sN)", "v", n);
+  } else if (!strcmp(ks, "tv")) {
+    PyObject *n = PyObject_GetAttr(e, s_name), *t = n ? PyObject_GetAttr(e, s_type) : NULL;
+    if (t) out = Py_BuildValue("(sNN)", "tv", n, t);
+    else Py_XDECREF(n);
+  } else if (!strcmp(ks, "l")) {
+    PyObject *at = PyObject_GetAttr(e, s_atom_type), *od = at ? PyObject_GetAttr(e, s_ordered) : NULL;
+    PyObject *ts = od ? PyObject_GetAttr(e, s_targets) : NULL;
+    PyObject *seq = ts ? PySequence_Fast(ts, "targets") : NULL;
+    int ok = seq != NULL;
+    if (ok) {
+      const int un = PySet_Contains(unordered, at);
+      ok = un == 0;
+    }
+    PyObject *tup = NULL;
+    if (ok) {
+      const Py_ssize_t m = PySequence_Fast_GET_SIZE(seq);
+      int all_nodes = 1;
+      tup = PyTuple_New(m);
+      for (Py_ssize_t i = 0; tup && i < m; ++i) {
+        PyObject *t = PySequence_Fast_GET_ITEM(seq, i);
+        PyObject *tk = PyObject_GetAttr(t, s_k);
+        if (!tk) { ok = 0; break; }
+        const char *tks = PyUnicode_Check(tk) ? PyUnicode_AsUTF8(tk) : NULL;
+        if (!tks || strcmp(tks, "n")) all_nodes = 0;
+        Py_DECREF(tk);
+        PyObject *x = shape_of(t, nodes, unordered, depth + 1);
+        if (!x) { ok = 0; break; }
+        PyTuple_SET_ITEM(tup, i, x);
+      }
+      if (!tup || all_nodes) ok = 0;
+    }
+    if (ok) {
+      out = PyTuple_Pack(4, PyTuple_GET_ITEM(s_tags, 0), at, od, tup);
+    }
+    Py_XDECREF(tup);
+    Py_XDECREF(seq);
+    Py_XDECREF(ts);
+    Py_XDECREF(od);
+    Py_XDECREF(at);
+  } else if (!strcmp(ks, "t")) {
+    PyObject *lt = PyObject_GetAttr(e, s_link_type), *od = lt ? PyObject_GetAttr(e, s_ordered) : NULL;
+    PyObject *ts = od ? PyObject_GetAttr(e, s_targets) : NULL;
+    PyObject *seq = ts ? PySequence_Fast(ts, "targets") : NULL;
+    PyObject *tup = seq ? PyTuple_New(PySequence_Fast_GET_SIZE(seq)) : NULL;
+    int ok = tup != NULL;
+    for (Py_ssize_t i = 0; ok && i < PyTuple_GET_SIZE(tup); ++i) {
+      PyObject *v = PySequence_Fast_GET_ITEM(seq, i);
+      PyObject *n = PyObject_GetAttr(v, s_name), *t = n ? PyObject_GetAttr(v, s_type) : NULL;
+      if (!t) { Py_XDECREF(n); ok = 0; break; }
+      PyObject *pair = PyTuple_New(2);
+      if (!pair) { Py_DECREF(n); Py_DECREF(t); ok = 0; break; }
+      PyTuple_SET_ITEM(pair, 0, n);
+      PyTuple_SET_ITEM(pair, 1, t);
+      PyTuple_SET_ITEM(tup, i, pair);
+    }
+    if (ok) out = PyTuple_Pack(4, PyTuple_GET_ITEM(s_tags, 1), lt, od, tup);
+    Py_XDECREF(tup);
+    Py_XDECREF(seq);
+    Py_XDECREF(ts);
+    Py_XDECREF(od);
+    Py_XDECREF(lt);
+  } else if (!strcmp(ks, "x")) {
+    PyObject *t = PyObject_GetAttr(e, s_term);
+    PyObject *x = t ? shape_of(t, nodes, unordered, depth + 1) : NULL;
+    if (x) out = PyTuple_Pack(2, PyTuple_GET_ITEM(s_tags, 2), x);
+    Py_XDECREF(x);
+    Py_XDECREF(t);
+  } else if (!strcmp(ks, "a") || !strcmp(ks, "o")) {
+    PyObject *ts = PyObject_GetAttr(e, s_terms);
+    PyObject *seq = ts ? PySequence_Fast(ts, "terms") : NULL;
+    PyObject *tup = seq ? PyTuple_New(PySequence_Fast_GET_SIZE(seq)) : NULL;
+    int ok = tup != NULL;
+    for (Py_ssize_t i = 0; ok && i < PyTuple_GET_SIZE(tup); ++i) {
+      PyObject *x = shape_of(PySequence_Fast_GET_ITEM(seq, i), nodes, unordered, depth + 1);
+      if (!x) { ok = 0; break; }
+      PyTuple_SET_ITEM(tup, i, x);
+    }
+    if (ok) out = PyTuple_Pack(2, k, tup);
+    Py_XDECREF(tup);
+    Py_XDECREF(seq);
+    Py_XDECREF(ts);
+  }
+  Py_DECREF(k);
+  if (!out) PyErr_Clear();
+  return out;
+}
+
+/* plan_words(expr, shapes, no_overload, node_handles, handle_cache, node_dir,
+ * unordered) -> a copy of the cached words of expr's query shape with its
+ * nodes' atom ids patched in, or None: pattern_matcher._lower's shape-cache
+ * hit, restated (the caller takes its Python path on None -- a shape not
+ * cached yet, a node whose handle or id is not cached, a node absent). */
+static PyObject *plan_words(PyObject *self, PyObject *args) {
+  PyObject *e, *shapes, *no_overload, *node_handles, *cache, *node_dir, *unordered;
+  if (!PyArg_ParseTuple(args, "OO!OO!O!OO", &e, &PyDict_Type, &shapes, &no_overload, &PyDict_Type, &node_handles,
+                        &PyDict_Type, &cache, &node_dir, &unordered))
+    return NULL;
+  if (!PyAnySet_Check(unordered)) { PyErr_SetString(PyExc_TypeError, "unordered: a set"); return NULL; }
+  PyObject *nodes = PyList_New(0);
+  if (!nodes) return NULL;
+  PyObject *shape = shape_of(e, nodes, unordered, 0), *res = NULL;
+  PyObject *key = shape ? PyTuple_Pack(2, no_overload, shape) : NULL;
+  PyObject *hit = key ? PyDict_GetItemWithError(shapes, key) : NULL;   /* borrowed */
+  Py_XDECREF(key);
+  Py_XDECREF(shape);
+  if (!hit || !PyTuple_Check(hit) || PyTuple_GET_SIZE(hit) != 2) goto done;
+  {
+    const Py_ssize_t nn = PyList_GET_SIZE(nodes);
+    uint32_t ids_small[64];
+    if (nn > 64) goto done;
+    for (Py_ssize_t i = 0; i < nn; ++i) {
+      PyObject *n = PyList_GET_ITEM(nodes, i);
+      PyObject *h = PyObject_GetAttr(n, s_handle);
+      if (!h) { PyErr_Clear(); goto done; }
+      if (!PyObject_IsTrue(h)) {
+        Py_DECREF(h);
+        PyObject *t = PyObject_GetAttr(n, s_atom_type), *nm = t ? PyObject_GetAttr(n, s_name) : NULL;
+        PyObject *tk = nm ? PyTuple_Pack(2, t, nm) : NULL;
+        Py_XDECREF(t);
+        Py_XDECREF(nm);
+        h = tk ? PyDict_GetItemWithError(node_handles, tk) : NULL;
+        Py_XDECREF(tk);
+        if (!h) { PyErr_Clear(); goto done; }
+        Py_INCREF(h);
+        if (PyObject_SetAttr(n, s_handle, h) < 0) { Py_DECREF(h); PyErr_Clear(); goto done; }
+      }
+      PyObject *r = PyDict_GetItemWithError(cache, h);              /* (id, category, arity) */
+      if (!r && !PyErr_Occurred() && node_dir != Py_None && PyDict_Check(node_dir)) {
+        PyObject *nid = PyDict_GetItemWithError(node_dir, h);
+        if (nid) {
+          PyObject *v = Py_BuildValue("(Oii)", nid, 1, 0);
+          if (v && PyDict_SetItem(cache, h, v) == 0) r = v;
+          Py_XDECREF(v);                                              /* the dict holds it */
+        }
+      }
+      Py_DECREF(h);
+      if (!r || !PyTuple_Check(r) || PyTuple_GET_SIZE(r) < 2) { PyErr_Clear(); goto done; }
+      const long aid = PyLong_AsLong(PyTuple_GET_ITEM(r, 0)), cat = PyLong_AsLong(PyTuple_GET_ITEM(r, 1));
+      if (PyErr_Occurred()) { PyErr_Clear(); goto done; }
+      if (aid < 0 || cat != 1) goto done;                            /* not a node of the KB */
+      ids_small[i] = (uint32_t)aid;
+    }
+    PyObject *w = PyObject_CallMethodObjArgs(PyTuple_GET_ITEM(hit, 0), s_copy, NULL);
+    if (!w) { PyErr_Clear(); goto done; }
+    Py_buffer wb;
+    if (PyObject_GetBuffer(w, &wb, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) < 0 || wb.itemsize != 4) {
+      PyErr_Clear();
+      Py_DECREF(w);
+      goto done;
+    }
+    uint32_t *wp = (uint32_t *)wb.buf;
+    const Py_ssize_t nw = wb.len / 4;
+    PyObject *patches = PySequence_Fast(PyTuple_GET_ITEM(hit, 1), "patches");
+    int ok = patches != NULL;
+    for (Py_ssize_t i = 0; ok && i < PySequence_Fast_GET_SIZE(patches); ++i) {
+      PyObject *pr = PySequence_Fast_GET_ITEM(patches, i);
+      if (!PyTuple_Check(pr) || PyTuple_GET_SIZE(pr) != 2) { ok = 0; break; }
+      const Py_ssize_t wi = PyLong_AsSsize_t(PyTuple_GET_ITEM(pr, 0)), ki = PyLong_AsSsize_t(PyTuple_GET_ITEM(pr, 1));
+      if (PyErr_Occurred() || wi < 0 || wi >= nw || ki < 0 || ki >= nn) { ok = 0; break; }
+      wp[wi] = ids_small[ki];
+    }
+    Py_XDECREF(patches);
+    PyBuffer_Release(&wb);
+    if (!ok) { PyErr_Clear(); Py_DECREF(w); goto done; }
+    res = w;
+  }
+done:
+  Py_DECREF(nodes);
+  if (PyErr_Occurred()) PyErr_Clear();
+  if (res) return res;
+  Py_RETURN_NONE;
+}
+
 static PyObject *fast_hash_enabled(PyObject *self, PyObject *noargs);
 
 static PyMethodDef methods[] = {
+    {"plan_words", plan_words, METH_VARARGS, "Cached plan words of an expression's query shape, node ids patched."},
     {"seed", seed, METH_VARARGS, "Seed the handle cache with (id, 2, arity) per new link handle."},
     {"add_rows", add_rows, METH_VARARGS, "Add Assignment objects built from a binding table to a set."},
     {"format_set", format_set, METH_VARARGS, "str() of a set of assignments."},
@@ -564,5 +758,17 @@ PyMODINIT_FUNC PyInit__assign(void) {
   s_mapping = PyUnicode_InternFromString("mapping");
   s_values = PyUnicode_InternFromString("values");
   s_symbols = PyUnicode_InternFromString("symbols");
+  s_k = PyUnicode_InternFromString("_k");
+  s_atom_type = PyUnicode_InternFromString("atom_type");
+  s_name = PyUnicode_InternFromString("name");
+  s_type = PyUnicode_InternFromString("type");
+  s_ordered = PyUnicode_InternFromString("ordered");
+  s_targets = PyUnicode_InternFromString("targets");
+  s_link_type = PyUnicode_InternFromString("link_type");
+  s_term = PyUnicode_InternFromString("term");
+  s_terms = PyUnicode_InternFromString("terms");
+  s_handle = PyUnicode_InternFromString("handle");
+  s_copy = PyUnicode_InternFromString("copy");
+  s_tags = Py_BuildValue("(sss)", "l", "t", "x");
   return PyModule_Create(&module);
 }

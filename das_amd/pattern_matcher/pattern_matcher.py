@@ -543,12 +543,21 @@ def _lower(expr, db, no_overload):
     records are cached per (index, signature), so a repeated query re-lowers
     only the links whose anchors changed; their handles are resolved in one
     batched lookup."""
+    shapes = db.__dict__.setdefault('_plan_shapes', {})
+    if shapes and _assign is not None and hasattr(_assign, "plan_words"):
+        # the shape-cache hit below, in C (das_amd/csrc/pyassign.c plan_words);
+        # None: take the Python path
+        nh, hc = getattr(db, "_node_handles", None), getattr(db, "_handle_cache", None)
+        if type(nh) is dict and type(hc) is dict:
+            w = _assign.plan_words(expr, shapes, no_overload, nh, hc, getattr(db, "_node_dir", None),
+                                   frozenset(UNORDERED_LINK_TYPES))
+            if w is not None:
+                return w
     nodes = []
     try:
         skey = (no_overload, _shape(expr, nodes))
     except _NoShape:
         skey = None
-    shapes = db.__dict__.setdefault('_plan_shapes', {})
     if skey is not None:
         hit = shapes.get(skey)
         if hit is not None:
