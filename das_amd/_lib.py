@@ -143,7 +143,7 @@ _SIGS = {
     "das_parsed_free": (C.c_int, [P]),
     "das_plan_execute": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32,
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
-    "das_plan_execute_many": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]),
+    "das_plan_execute_many": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P, P]),
     "das_plan_execute_sharded": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32, P,
                                            C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
                                            C.POINTER(C.c_int32), P, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -308,10 +308,16 @@ class Table:
 
     __slots__ = ("ctx", "h", "kind", "vars", "members", "nrows", "part")
 
-    def __init__(self, ctx, handle):
+    def __init__(self, ctx, handle, info=None):
         self.ctx = ctx
         self.h = handle
         self.part = None          # multi-GPU: how the rows are spread over ranks (das_amd.parallel)
+        if info is not None and info[0] != TABLE_COMPOSITE:
+            # (kind, ncols, nrows, 0, vars[16]) as das_plan_execute_many reports them
+            self.kind, self.nrows = info[0], info[2]
+            self.vars = tuple(info[4:4 + info[1]])
+            self.members = None
+            return
         kind = C.c_int32()
         ncols = C.c_int32()
         vars_ = (C.c_int32 * 16)()
@@ -562,16 +568,18 @@ class Context:
             n_out = np.zeros(m, dtype=np.uint32)
             matched = np.zeros(m, dtype=np.int32)
             neg = np.zeros(m, dtype=np.int32)
+            info = np.zeros((cap, 20), dtype=np.int64)
             rc = lib().das_plan_execute_many(self.h, m, ptrs, ptr(ns), 1 if no_overload else 0, out, cap, ptr(n_out),
-                                             ptr(matched), ptr(neg))
+                                             ptr(matched), ptr(neg), ptr(info))
             if rc == ERR_INVALID and int(n_out.sum()) > cap:
                 cap = int(n_out.sum())
                 continue
             check(rc, self.h)
             res, k = [], 0
+            inf = info.tolist()
             for i in range(m):
                 j = int(n_out[i])
-                res.append((bool(matched[i]), bool(neg[i]), [Table(self, out[k + q]) for q in range(j)]))
+                res.append((bool(matched[i]), bool(neg[i]), [Table(self, out[k + q], inf[k + q]) for q in range(j)]))
                 k += j
             return res
 

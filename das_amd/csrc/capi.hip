@@ -205,6 +205,10 @@ int das_ctx_destroy(das_ctx_t* ctx) {
         DAS_HIP(hipStreamDestroy(ss));
         ss = nullptr;
       }
+    if (ctx->c.gsc_pool) {
+      (void)hipFree(ctx->c.gsc_pool);
+      ctx->c.gsc_pool = nullptr;
+    }
     for (hipEvent_t e : ctx->c.side_ev) (void)hipEventDestroy(e);
     ctx->c.side_ev.clear();
     if (ctx->c.own_stream) DAS_HIP(hipStreamDestroy(ctx->c.s));
@@ -724,7 +728,7 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
 
 int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,
                           uint32_t no_overload, das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched,
-                          int32_t* negation) {
+                          int32_t* negation, int64_t* info) {
   if (!ctx || (n_plans && (!nodes || !n || !n_out || !matched || !negation)))
     return fail(ctx, DAS_ERR_INVALID, "null argument");
   return guarded(ctx, [&] {
@@ -736,7 +740,18 @@ int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_
     DAS_CHECK(total <= cap, das::DAS_E_INVALID, "plans: more answer tables than `cap`");
     uint64_t k = 0;
     for (uint32_t i = 0; i < n_plans; ++i) {
-      for (auto& t : rs[i].tables) out[k++] = wrap(std::move(t));
+      for (auto& t : rs[i].tables) {
+        if (info) {
+          // what das_table_info reports, so the caller needs no call per table
+          int64_t* f = info + 20 * k;
+          f[0] = t->kind;
+          f[1] = t->ncols;
+          f[2] = (int64_t)t->nrows;
+          f[3] = 0;
+          for (int c = 0; c < 16; ++c) f[4 + c] = c < t->ncols ? t->vars[c] : 0;
+        }
+        out[k++] = wrap(std::move(t));
+      }
       matched[i] = rs[i].matched ? 1 : 0;
       negation[i] = rs[i].negation ? 1 : 0;
     }

@@ -207,6 +207,17 @@ struct Ctx {
     if (!side[i]) DAS_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
     return side[i];
   }
+  // zeroed grid-chain counter blocks, one per pooled chain of a batch (the
+  // grid kernel leaves its block zero again)
+  static constexpr uint32_t kGscBlock = 64;               // words per block (>= the kernel's kGscWords)
+  uint32_t* gsc_pool = nullptr;
+  uint32_t* gsc_block(uint32_t k) {
+    if (!gsc_pool) {
+      DAS_HIP(hipMalloc((void**)&gsc_pool, 4ull * kGscBlock * 16));
+      DAS_HIP(hipMemset(gsc_pool, 0, 4ull * kGscBlock * 16));
+    }
+    return gsc_pool + (uint64_t)kGscBlock * (k % 16);
+  }
   hipEvent_t fence_event(uint32_t i) {
     while (side_ev.size() <= i) {
       hipEvent_t e;

@@ -3471,6 +3471,7 @@ struct ChainDesc {
 // the finished-workgroup count and the redo flag
 constexpr uint32_t kGscOut = kChainStages, kGscDone = kChainStages + 1, kGscRedo = kChainStages + 2,
                    kGscWords = kChainStages + 4;
+static_assert(kGscWords <= Ctx::kGscBlock, "pooled grid-chain counter block too small");
 enum : uint32_t { CHS_REDO = 3 };
 
 // Block-wide ordered compaction step: this thread's output position among
@@ -3788,6 +3789,9 @@ __device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, u
         const uint32_t st = failed ? CHS_EMPTY_SCAN : redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
         const uint32_t total = st == CHS_OK ? __hip_atomic_load(&d.gsc[kGscOut], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                             : s_cnt[s_acc];
+        // every workgroup is done with the counters: leave them zero for the
+        // next chain of a pooled counter block (no k_chain_prep launch)
+        for (uint32_t i = 0; i < kGscWords; ++i) __hip_atomic_store(&d.gsc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&slot[0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&slot[1], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&slot[2], s_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3922,10 +3926,11 @@ struct ChainRun {
   hipStream_t ls = nullptr;                                   // the stream it was launched on
   int fence = -1;                                             // side stream: its fence events (2k, 2k+1)
   bool waited = false;                                        // chain_finish read its outcome
+  bool noprep = false;                                        // grid: pooled counters, descriptor read from pinned memory
 };
 // 1: compiled; 0: nothing to fuse; -1: the grid form does not apply
 int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R);
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R, uint32_t* gsc_fixed = nullptr);
 void chain_launch(Ctx& c, ChainRun& R, const PubSlot& ps, uint8_t* stage, int side = -1, uint32_t k = 0);
 int chain_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>& out, uint32_t* consumed);
 
@@ -3958,8 +3963,11 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
   return 0;
 }
 
+// gsc_fixed: a pooled, zeroed counter block (the grid kernel leaves it zero
+// again), which lets the grid read its descriptor from the pinned buffer with
+// no k_chain_prep launch; null: fresh counters zeroed by k_chain_prep
 int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
-                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R) {
+                  const std::vector<const das_plan_node_t*>& anti, bool grid, ChainRun& R, uint32_t* gsc_fixed) {
   Index& idx = c.idx;
   ChainDesc& d = R.d;
   R.grid = grid;
@@ -4135,11 +4143,12 @@ int chain_compile(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
       R.fin->lo[k] = A.lo[k];
       R.fin->hi[k] = A.hi[k];
     }
-    R.gsc.alloc(kGscWords, c.s);
+    if (!gsc_fixed) R.gsc.alloc(kGscWords, c.s);
+    R.noprep = gsc_fixed != nullptr;
     d.seg = kGridSeg;
     d.fin = R.fin->data;
     d.fin_ld = R.fin->cap;
-    d.gsc = R.gsc.p;
+    d.gsc = gsc_fixed ? gsc_fixed : R.gsc.p;
   }
   // only the stages in use travel (the kernel copies them into LDS)
   R.bytes = offsetof(ChainDesc, st) + sizeof(ChainStage) * d.nstage;
@@ -4169,7 +4178,13 @@ void chain_launch(Ctx& c, ChainRun& R, const PubSlot& ps, uint8_t* stage, int si
     if (d.st[i].op == CH_SCAN) sbytes += 4.0 * (d.st[i].end - d.st[i].begin) * (d.st[i].sp.arity + 1);
   if (trace_on()) trace_mark("prep staged");
   R.ps = ps;
-  if (R.grid) {
+  if (R.grid && R.noprep) {
+    // every workgroup copies the descriptor from the pinned buffer itself
+    ProfScope pf(c, "k_chain_grid", sbytes);
+    hipLaunchKernelGGL(k_chain_grid, dim3(cu_count(c)), dim3(kSmallBlock), 0, c.s, (const uint32_t*)hd,
+                       (uint32_t)(bytes / 4), ps.p, ps.seq, R.ts);
+    DAS_HIP(hipGetLastError());
+  } else if (R.grid) {
     const uint32_t G = cu_count(c);
     R.dd.alloc(bytes / 4, c.s);
     {
@@ -4306,9 +4321,15 @@ ChainRunPtr fused_and_launch(Ctx& c, const std::vector<const das_plan_node_t*>& 
     }
     c.s = ss;
   }
+  // DAS_CHAIN_PREP=0: pooled zeroed counters and every workgroup reading the
+  // descriptor from pinned memory, no k_chain_prep launch -- measured no
+  // faster (FlyBase step 0.235 / 0.254 vs 0.230 / 0.234 ms with the prep,
+  // profiles/r5_flybase_env_ab.txt), so the prep stays the default
+  const char* fp = std::getenv("DAS_CHAIN_PREP");
+  uint32_t* gsc = fp && fp[0] == '0' ? c.gsc_block(k) : nullptr;
   for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
     ChainRunPtr R(new ChainRun);
-    const int r = chain_compile(c, terms, anti, attempt == 0, *R);
+    const int r = chain_compile(c, terms, anti, attempt == 0, *R, gsc);
     if (r < 0) continue;
     if (r == 0 || !R->complete) return nullptr;
     chain_launch(c, *R, pub_reserve_pool(k), pinned_stage_pool(k, chain_stage_bytes(*R)), side, k);

@@ -355,10 +355,11 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
  * alone; Ands one fused chain answers are launched before any other plan
  * runs and read back last, so the host work of the batch overlaps their GPU
  * time.  More than `cap` tables in all: DAS_ERR_INVALID with n_out set and
- * no table returned. */
+ * no table returned.  info (optional, 20 int64 per table): kind, ncols,
+ * nrows, 0, vars[16] -- das_table_info's fields without a call per table. */
 int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,
                           uint32_t no_overload, das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched,
-                          int32_t* negation);
+                          int32_t* negation, int64_t* info);
 
 /* ---- sharded plans (links hash-partitioned by handle across GPUs) ---------- */
 /* One GPU's part of a plan over a KB sharded across GPUs (das_amd.parallel
