@@ -198,6 +198,7 @@ int das_ctx_destroy(das_ctx_t* ctx) {
     das::free_index(ctx->c.idx);
     ctx->c.zlc.release();                 // back to the cache while the stream still exists
     das::cache_release_stream(ctx->c.s);
+    for (auto& z : ctx->c.zlc_side) z.release();
     for (hipStream_t& ss : ctx->c.side)
       if (ss) {
         DAS_HIP(hipStreamSynchronize(ss));

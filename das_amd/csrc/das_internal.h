@@ -3,6 +3,7 @@
 #pragma once
 #include <array>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -200,11 +201,31 @@ struct Ctx {
   std::vector<Digest> black_list;
   // side streams for fused chains in flight together (das_plan_execute_many),
   // each with two fence events per pooled run (created on first use)
-  static constexpr int kSide = 3;
+  static constexpr int kSide = 4;                     // 0..2: chains; 3: the batch's other plans
+  static constexpr int kChainSides = 3, kPlanSide = 3;
   hipStream_t side[kSide] = {};
+  DBuf<uint2> zlc_side[kSide];                        // the sparse-join scratch of each side stream
+  DBuf<uint2>& zlc_of(hipStream_t st) {
+    for (int i = 0; i < kSide; ++i)
+      if (side[i] && st == side[i]) return zlc_side[i];
+    return zlc;
+  }
+  // algorithmic bytes launched per query shape in its last batch (the batch's
+  // order: the heaviest plan first, on the context's stream)
+  std::unordered_map<uint64_t, double> plan_bytes;
   std::vector<hipEvent_t> side_ev;
   hipStream_t side_stream(int i) {
-    if (!side[i]) DAS_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
+    if (!side[i]) {
+      // the batch's other plans (kPlanSide) run beside the lead plan's long
+      // kernels: their queue gets the highest dispatch priority
+      // (DAS_PLAN_PRIO=0: default priority, A/B)
+      int lo = 0, hi = 0;
+      const char* pp = std::getenv("DAS_PLAN_PRIO");
+      if (i == kPlanSide && !(pp && pp[0] == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+        DAS_HIP(hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, hi));
+      else
+        DAS_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
+    }
     return side[i];
   }
   // zeroed grid-chain counter blocks, one per pooled chain of a batch (the
@@ -243,6 +264,12 @@ void trace_mark(const char* what, const std::string& name = std::string());
 // process-wide counts of kernel scopes entered and of host read-backs waited
 // on (das_counters; bench.py reports them per query for latency-bound legs)
 void count_launch();
+// algorithmic bytes of the kernel scopes this thread entered (a plan's
+// weight, das_plan_execute_many)
+inline double& launched_bytes() {
+  thread_local double b = 0;
+  return b;
+}
 void count_readback();
 void read_counters(uint64_t out[2]);
 void trace_dump(const char* title);
@@ -254,6 +281,7 @@ struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
     count_launch();
+    launched_bytes() += algorithmic_bytes;
     if (trace_on()) trace_mark("kernel", name + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");
     if (!c.prof || !c.prof_selected(name)) return;
     if (!c.prof_tag.empty()) name += "@" + c.prof_tag;

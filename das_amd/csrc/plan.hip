@@ -571,6 +571,21 @@ void split_and(const Exec& ex, const std::vector<uint32_t>& terms, std::vector<c
   }
 }
 
+// a plan's query shape: its node words with the scan / index-join targets
+// left out (the anchors a fresh query changes; words 7..14 and 30..37 of
+// each das_plan_node_t), FNV-1a
+uint64_t shape_hash(const das_plan_node_t* nd, uint32_t n) {
+  static_assert(sizeof(das_plan_node_t) == 51 * 4, "plan node layout");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(nd);
+  uint64_t h = 1469598103934665603ull;
+  for (uint64_t i = 0; i < 51ull * n; ++i) {
+    const uint32_t k = (uint32_t)(i % 51);
+    if ((k >= 7 && k < 15) || (k >= 30 && k < 38)) continue;
+    h = (h ^ w[i]) * 1099511628211ull;
+  }
+  return h;
+}
+
 // a plan's answer: a view must not outlive the index, so the caller gets a copy
 PlanOutput output(Ctx& c, Res r) {
   PlanOutput out;
@@ -666,8 +681,18 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
     ++n_cand;
   }
   hipEvent_t fence_in = nullptr;
-  bool waited[Ctx::kSide] = {false, false, false};
-  if (n_cand && side) {
+  bool waited[Ctx::kSide] = {};
+  // DAS_PLAN_SIDE=1: the heaviest other plan first, the rest on a side
+  // stream (below).  Off by default: no faster in the bench steps (bio
+  // 1.443 / 1.486 vs 1.430 / 1.469 ms, hub 0.891 / 0.888 vs 0.894 / 0.892;
+  // the lead's cross product holds the CUs and HBM the side plans need,
+  // even from a highest-priority queue; profiles/r5_plan_side_ab.txt)
+  const char* ps = std::getenv("DAS_PLAN_SIDE");
+  const bool plan_side = ps && ps[0] == '1' && n_plans - n_cand > 1;
+  if ((n_cand && side) || plan_side) {
+    // side streams are ordered after the context's stream as it stands when
+    // the batch begins (their blocks' last readers), never after this batch's
+    // own launches there
     fence_in = c.fence_event(2 * kPubPool);
     DAS_HIP(hipEventRecord(fence_in, c.s));
   }
@@ -683,7 +708,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       Exec ex{c, nodes[i], n[i], no_overload};
       std::vector<const das_plan_node_t*> pos, neg;
       split_and(ex, ex.children(0), pos, neg);
-      const int sidx = side ? (int)(pooled % Ctx::kSide) : -1;
+      const int sidx = side ? (int)(pooled % Ctx::kChainSides) : -1;
       runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled, sidx, fence_in, sidx >= 0 ? &waited[sidx] : nullptr);
       if (runs[i]) ++pooled;
     }
@@ -700,11 +725,52 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
     ~Unhook() { set_wait_hook(nullptr); }
   } uh;
   if (hooked) set_wait_hook(&hook);
-  for (uint32_t i = 0; i < n_plans; ++i) {
-    if (cand[i]) continue;
+  // the other plans: the heaviest (by the algorithmic bytes its shape
+  // launched last time) first, on the context's stream; the rest after it on
+  // a side stream, so a plan ending in a long kernel with no read-back (bio
+  // QUERY_3's cross product) does not hold their read-backs behind it
+  // (DAS_PLAN_SIDE=1 only; by default every plan in order on the context's stream)
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < n_plans; ++i)
+    if (!cand[i]) order.push_back(i);
+  std::vector<uint64_t> shape(n_plans, 0);
+  for (uint32_t i : order) shape[i] = shape_hash(nodes[i], n[i]);
+  auto weight = [&](uint32_t i) {
+    auto it = c.plan_bytes.find(shape[i]);
+    return it == c.plan_bytes.end() ? -1.0 : it->second;
+  };
+  if (plan_side)
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return weight(a) > weight(b); });
+  // the lead goes alone only when it outweighs the rest together (else every
+  // plan stays on the context's stream, in order)
+  double rest = 0;
+  for (size_t j = 1; j < order.size(); ++j) rest += std::max(weight(order[j]), 0.0);
+  const char* sm = std::getenv("DAS_PLAN_SPLIT_MIN");          // tests: 0 = any lead heavier than the rest
+  const double split_min = sm ? std::atof(sm) : (double)(64u << 20);
+  const bool split = plan_side && weight(order[0]) > std::max(rest, split_min) && weight(order[0]) >= 0;
+  bool on_side = false;
+  for (size_t j = 0; j < order.size(); ++j) {
+    const uint32_t i = order[j];
+    struct Swap {
+      Ctx& c;
+      hipStream_t old;
+      ~Swap() { c.s = old; }
+    } sw{c, c.s};
+    if (split && j > 0) {
+      hipStream_t ss = c.side_stream(Ctx::kPlanSide);
+      if (!waited[Ctx::kPlanSide]) {
+        DAS_HIP(hipStreamWaitEvent(ss, fence_in, 0));
+        waited[Ctx::kPlanSide] = true;
+      }
+      c.s = ss;
+      on_side = true;
+    }
+    const double b0 = launched_bytes();
     Exec ex{c, nodes[i], n[i], no_overload};
     outs[i] = output(c, ex.eval(0));
+    c.plan_bytes[shape[i]] = launched_bytes() - b0;
   }
+  if (c.plan_bytes.size() > 4096) c.plan_bytes.clear();
   set_wait_hook(nullptr);
   launch_all();                                           // (no-op once the hook ran)
   // 2. candidates no chain answers, in turn
@@ -726,6 +792,11 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       outs[i] = output(c, ex.eval(0));
     }
     runs[i].reset();
+  }
+  // the side stream's answers are read on the context's stream from here on
+  if (on_side) {
+    DAS_HIP(hipEventRecord(c.fence_event(2 * kPubPool + 2), c.side_stream(Ctx::kPlanSide)));
+    DAS_HIP(hipStreamWaitEvent(c.s, c.fence_event(2 * kPubPool + 2), 0));
   }
   trace_mark("done");
   trace_dump("das_plan_execute_many");

@@ -2615,23 +2615,26 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
     // again, any unwind (an allocation or launch failure, an expansion
     // throwing) leaves slots set: the guard drops the context's array, so the
     // next join starts from a fresh one
+    // (one array per stream the context launches on: a join on a side
+    // stream must not see another stream's slots before their clear ran)
+    DBuf<uint2>& zlc = c.zlc_of(c.s);
     struct ZlcGuard {
-      Ctx& c;
+      DBuf<uint2>& z;
       bool armed;
       ~ZlcGuard() {
-        if (armed) c.zlc.release();
+        if (armed) z.release();
       }
-    } zg{c, false};
+    } zg{zlc, false};
     uint2* lcp = nullptr;
     {
-      const bool fresh = !reuse || c.zlc.n < range + 1;
+      const bool fresh = !reuse || zlc.n < range + 1;
       ProfScope ps(c, "join_build", (srt ? 4.0 : 8.0 + 8.0 * Q.ncols) * Q.nrows + (fresh ? 8.0 * range : 0.0));
       if (reuse) {
-        if (c.zlc.n < range + 1) {
-          c.zlc.alloc(std::min<uint64_t>(std::max<uint64_t>(range + 1, 2 * c.zlc.n), kZlcMax), c.s);
-          fill_dev(c.zlc.p, 0, 8 * c.zlc.n, c.s);
+        if (zlc.n < range + 1) {
+          zlc.alloc(std::min<uint64_t>(std::max<uint64_t>(range + 1, 2 * zlc.n), kZlcMax), c.s);
+          fill_dev(zlc.p, 0, 8 * zlc.n, c.s);
         }
-        lcp = c.zlc.p;
+        lcp = zlc.p;
         zg.armed = true;
       } else {
         lc.alloc(range + 1, c.s);

@@ -1098,6 +1098,34 @@ def test_gpu_plan_execute_many_matches_one_by_one(defer, monkeypatch):
         assert same(g, record(big[i], db)), i
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_gpu_plan_execute_many_heavy_lead(split, monkeypatch):
+    """das_plan_execute_many's other plans: from the second batch on, the
+    plan whose shape launched the most bytes runs first on the context's
+    stream and the rest after it on a side stream (split=1, any lead heavier
+    than the rest, DAS_PLAN_SIDE=1; 0: all in order, the default).  Bio Q1-Q6 and hub
+    H4 / H2 shapes over fresh anchors, three batches each, every answer equal
+    to its one-by-one evaluation."""
+    import bench
+    from das_amd import synthetic
+    monkeypatch.setenv("DAS_PLAN_SPLIT_MIN", "0")
+    monkeypatch.setenv("DAS_PLAN_SIDE", split)
+    arrays = synthetic.bio_kb(300, 60, 4000, 200, seed=4)
+    db = _hipdb(arrays)
+    for rep in range(3):
+        qs = [q for _, q in bench.bio_specs(np.arange(300), anchor=rep)]
+        want = [record(q, db) for q in qs]
+        for i, (g, w) in enumerate(zip(record_many(qs, db), want)):
+            assert same(g, w), ("bio", rep, i, g.get("n"), w.get("n"))
+    arrays = synthetic.powerlaw_kb(3000, 300000, link_types=4, seed=21)
+    db = _hipdb(arrays)
+    qs = [q for _, q in bench.hub_specs()]
+    want = [record(q, db) for q in qs]
+    for rep in range(3):
+        for i, (g, w) in enumerate(zip(record_many(qs, db), want)):
+            assert same(g, w), ("hub", rep, i, g.get("n"), w.get("n"))
+
+
 def test_gpu_native_canonical_load_matches_oracle():
     """Canonical text -> native reader (canonical.cpp) -> device index: the
     queries answer as the oracle over the Python reader's atoms; nested
