@@ -8,6 +8,7 @@
 // step performs no runtime allocation calls once warm (the runtime's own
 // stream-ordered allocator costs microseconds per call and, under a step's
 // mix of sizes, occasionally hundreds of microseconds).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -97,19 +98,40 @@ void* cache_alloc(size_t bytes, hipStream_t s) {
   void* p = nullptr;
   hipError_t e = traced_malloc(&p, cls, "cache");
   if (e != hipSuccess) {
-    // out of memory with idle blocks cached: give them back and retry once
+    // out of memory with idle blocks cached: give back the largest ones
+    // until the request fits, keep the rest cached (every hipFree of a large
+    // block costs milliseconds: freeing the whole cache at once stalled a
+    // 10^9-link build for ~1.4 s, round 5)
     (void)hipGetLastError();
-    std::vector<void*> idle;
+    std::vector<std::pair<std::pair<hipStream_t, size_t>, void*>> idle;
     {
       std::lock_guard<std::mutex> lk(c.mu);
-      for (auto& kv : c.free_blocks) idle.insert(idle.end(), kv.second.begin(), kv.second.end());
+      for (auto& kv : c.free_blocks)
+        for (void* q : kv.second) idle.push_back({kv.first, q});
       c.free_blocks.clear();
       c.cached_bytes = 0;
     }
+    std::sort(idle.begin(), idle.end(), [](const auto& x, const auto& y) { return x.first.second > y.first.second; });
     DAS_HIP(hipDeviceSynchronize());
-    if (alloc_trace()) std::fprintf(stderr, "[das alloc] OOM fallback: freeing %zu idle blocks\n", idle.size());
-    for (void* q : idle) (void)hipFree(q);
-    DAS_HIP(traced_malloc(&p, cls, "cache-retry"));
+    if (alloc_trace()) std::fprintf(stderr, "[das alloc] OOM fallback: %zu idle blocks\n", idle.size());
+    size_t k = 0, freed = 0;
+    p = nullptr;
+    for (; k < idle.size() && !p; ++k) {
+      (void)hipFree(idle[k].second);
+      freed += idle[k].first.second;
+      if (freed >= cls && hipMalloc(&p, cls) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(c.mu);
+      for (size_t r = k; r < idle.size(); ++r) {
+        c.free_blocks[idle[r].first].push_back(idle[r].second);
+        c.cached_bytes += idle[r].first.second;
+      }
+    }
+    if (!p) DAS_HIP(traced_malloc(&p, cls, "cache-retry"));
   }
   std::lock_guard<std::mutex> lk(c.mu);
   c.live[p] = {s, cls};
