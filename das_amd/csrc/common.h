@@ -33,7 +33,10 @@ inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 8u)
 void* cache_alloc(size_t bytes, hipStream_t s);
 void cache_free(void* p);
 void cache_release_stream(hipStream_t s);
-void cache_trim();                        // returns every idle cached block to the driver
+void cache_trim();
+// idle blocks returned to the driver, smallest first, until at most `keep` bytes stay cached
+void cache_trim_to(size_t keep);
+                       // returns every idle cached block to the driver
 void cache_hold(bool on);                 // nested: while held, freed blocks stay cached (no budget)
 
 // Stream-ordered device buffer from the caching allocator (ctx stream).
