@@ -76,12 +76,23 @@ struct Slot {
   }
   ~Slot() { if (p) (void)hipHostFree(p); }
 };
+// level 1: a plan nested in another's read-back wait (das_plan_execute_many)
+// has its own slot and staging buffer, so the outer wait's sequence and
+// request stay untouched
+thread_local int t_pub_level = 0;
+
 Slot& slot() {
-  thread_local Slot s;
-  return s;
+  thread_local Slot s[2];
+  return s[t_pub_level];
 }
 
 }  // namespace
+
+PubLevel::PubLevel() {
+  DAS_CHECK(t_pub_level == 0, DAS_E_INTERNAL, "read-back level: nested twice");
+  t_pub_level = 1;
+}
+PubLevel::~PubLevel() { t_pub_level = 0; }
 
 uint8_t* pinned_stage(uint64_t bytes) {
   struct Stage {
@@ -89,7 +100,8 @@ uint8_t* pinned_stage(uint64_t bytes) {
     uint64_t cap = 0;
     ~Stage() { if (p) (void)hipHostFree(p); }
   };
-  thread_local Stage st;
+  thread_local Stage sts[2];
+  Stage& st = sts[t_pub_level];
   if (bytes > st.cap) {
     if (st.p) DAS_HIP(hipHostFree(st.p));
     st.cap = std::max<uint64_t>(bytes, 1 << 16);
@@ -133,9 +145,11 @@ uint8_t* pinned_stage_pool(uint32_t k, uint64_t bytes) {
 
 namespace {
 thread_local WaitHook* t_wait_hook = nullptr;
+thread_local double t_wait_mark = 0;           // launched_bytes() when the last wait ended
 }
 
 void set_wait_hook(WaitHook* hook) { t_wait_hook = hook; }
+double bytes_since_wait() { return launched_bytes() - t_wait_mark; }
 
 void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
   count_readback();
@@ -162,6 +176,7 @@ void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n) {
     __builtin_ia32_pause();
   }
   for (uint32_t i = 0; i < n; ++i) out[i] = __atomic_load_n(&ps.p[i], __ATOMIC_RELAXED);
+  t_wait_mark = launched_bytes();
   trace_mark("woke");
 }
 

@@ -689,7 +689,12 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   // even from a highest-priority queue; profiles/r5_plan_side_ab.txt)
   const char* ps = std::getenv("DAS_PLAN_SIDE");
   const bool plan_side = ps && ps[0] == '1' && n_plans - n_cand > 1;
-  if ((n_cand && side) || plan_side) {
+  // a plan nested in another's long read-back wait (below; DAS_PLAN_NEST=0 off)
+  const char* pn = std::getenv("DAS_PLAN_NEST");
+  const bool nest = !(pn && pn[0] == '0') && n_plans - n_cand > 1;
+  const char* nm = std::getenv("DAS_PLAN_NEST_MIN");             // tests: 0 = at every wait
+  const double nest_min = nm ? std::atof(nm) : (double)(128u << 20);
+  if ((n_cand && side) || plan_side || nest) {
     // side streams are ordered after the context's stream as it stands when
     // the batch begins (their blocks' last readers), never after this batch's
     // own launches there
@@ -718,21 +723,65 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   // 1. the other plans first; the chains are compiled and launched in the
   // gaps where those plans wait for a read-back (host time otherwise spent
   // spinning), the rest after them
-  WaitHook hook = [&](const std::function<bool()>& ready) { return launch_some(&ready); };
-  const bool hooked = n_cand && !(fh && fh[0] == '0');
+  // the other plans in order (below), with `order` / `done` shared with the
+  // hook: a plan whose read-back wait follows >= nest_min launched bytes (the
+  // hub's filtered walk) hosts the next pending plans, run whole inside that
+  // wait on the plan side stream with their own read-back slot (PubLevel),
+  // while the awaited slot is unwritten -- the hub's H2 expansion, bound by
+  // HBM writes, then runs beside H4's latency-bound walk
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < n_plans; ++i)
+    if (!cand[i]) order.push_back(i);
+  std::vector<uint8_t> done(n_plans, 0);
+  size_t cur = 0;                                          // the plan the main loop is in
+  bool on_side = false;
+  auto to_side = [&]() {
+    hipStream_t ss = c.side_stream(Ctx::kPlanSide);
+    if (!waited[Ctx::kPlanSide]) {
+      DAS_HIP(hipStreamWaitEvent(ss, fence_in, 0));
+      waited[Ctx::kPlanSide] = true;
+    }
+    on_side = true;
+    return ss;
+  };
+  struct Swap {
+    Ctx& c;
+    hipStream_t old;
+    ~Swap() { c.s = old; }
+  };
+  auto nest_some = [&](const std::function<bool()>& ready) {
+    if (!nest || bytes_since_wait() < nest_min) return;
+    for (size_t j = cur + 1; j < order.size() && !ready(); ++j) {
+      const uint32_t i = order[j];
+      if (done[i]) continue;
+      done[i] = 1;
+      if (trace_on()) trace_mark("nested plan");
+      PubLevel lv;
+      Swap sw{c, c.s};
+      c.s = to_side();
+      Exec ex{c, nodes[i], n[i], no_overload};
+      outs[i] = output(c, ex.eval(0));
+    }
+  };
+  // 1. the other plans first; the chains are compiled and launched in the
+  // gaps where those plans wait for a read-back (host time otherwise spent
+  // spinning), the rest after them
+  WaitHook hook = [&](const std::function<bool()>& ready) {
+    const bool chains_done = launch_some(&ready);
+    if (chains_done) nest_some(ready);
+    bool pending = false;
+    for (size_t j = cur + 1; j < order.size() && nest; ++j) pending = pending || !done[order[j]];
+    return chains_done && !pending;
+  };
+  const bool hooked = (n_cand && !(fh && fh[0] == '0')) || nest;
   if (!hooked) launch_all();
   struct Unhook {
     ~Unhook() { set_wait_hook(nullptr); }
   } uh;
   if (hooked) set_wait_hook(&hook);
-  // the other plans: the heaviest (by the algorithmic bytes its shape
-  // launched last time) first, on the context's stream; the rest after it on
-  // a side stream, so a plan ending in a long kernel with no read-back (bio
-  // QUERY_3's cross product) does not hold their read-backs behind it
-  // (DAS_PLAN_SIDE=1 only; by default every plan in order on the context's stream)
-  std::vector<uint32_t> order;
-  for (uint32_t i = 0; i < n_plans; ++i)
-    if (!cand[i]) order.push_back(i);
+  // (DAS_PLAN_SIDE=1: the heaviest plan by the algorithmic bytes its shape
+  // launched last time first, on the context's stream, the rest after it on
+  // the side stream -- measured no faster, off by default)
   std::vector<uint64_t> shape(n_plans, 0);
   for (uint32_t i : order) shape[i] = shape_hash(nodes[i], n[i]);
   auto weight = [&](uint32_t i) {
@@ -741,34 +790,23 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   };
   if (plan_side)
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return weight(a) > weight(b); });
-  // the lead goes alone only when it outweighs the rest together (else every
-  // plan stays on the context's stream, in order)
   double rest = 0;
   for (size_t j = 1; j < order.size(); ++j) rest += std::max(weight(order[j]), 0.0);
   const char* sm = std::getenv("DAS_PLAN_SPLIT_MIN");          // tests: 0 = any lead heavier than the rest
   const double split_min = sm ? std::atof(sm) : (double)(64u << 20);
   const bool split = plan_side && weight(order[0]) > std::max(rest, split_min) && weight(order[0]) >= 0;
-  bool on_side = false;
   for (size_t j = 0; j < order.size(); ++j) {
     const uint32_t i = order[j];
-    struct Swap {
-      Ctx& c;
-      hipStream_t old;
-      ~Swap() { c.s = old; }
-    } sw{c, c.s};
-    if (split && j > 0) {
-      hipStream_t ss = c.side_stream(Ctx::kPlanSide);
-      if (!waited[Ctx::kPlanSide]) {
-        DAS_HIP(hipStreamWaitEvent(ss, fence_in, 0));
-        waited[Ctx::kPlanSide] = true;
-      }
-      c.s = ss;
-      on_side = true;
-    }
+    if (done[i]) continue;                                 // ran nested in an earlier plan's wait
+    done[i] = 1;
+    cur = j;
+    Swap sw{c, c.s};
+    if (split && j > 0) c.s = to_side();
     const double b0 = launched_bytes();
     Exec ex{c, nodes[i], n[i], no_overload};
     outs[i] = output(c, ex.eval(0));
     c.plan_bytes[shape[i]] = launched_bytes() - b0;
+    if (hooked) set_wait_hook(&hook);                      // (re-armed for the next plan's waits)
   }
   if (c.plan_bytes.size() > 4096) c.plan_bytes.clear();
   set_wait_hook(nullptr);

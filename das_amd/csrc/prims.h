@@ -214,6 +214,17 @@ void pub_wait(const PubSlot& ps, hipStream_t s, uint32_t* out, uint32_t n);
 // gaps where a synchronous plan waits for a size.  nullptr: none.
 using WaitHook = std::function<bool(const std::function<bool()>& ready)>;
 void set_wait_hook(WaitHook* hook);
+// algorithmic bytes of the kernel scopes launched since this thread's last
+// read-back wait ended: how long the wait now starting can be expected to be
+double bytes_since_wait();
+// While alive: pub_reserve / pinned_stage hand out this thread's second slot
+// and staging buffer (a plan run inside another plan's read-back wait)
+struct PubLevel {
+  PubLevel();
+  ~PubLevel();
+  PubLevel(const PubLevel&) = delete;
+  PubLevel& operator=(const PubLevel&) = delete;
+};
 // Pinned, device-mapped staging memory for small request / reply calls
 // (handle lookups, index key ranges): the host writes the request, one
 // kernel reads it over the mapping and writes its reply back with

@@ -1098,18 +1098,22 @@ def test_gpu_plan_execute_many_matches_one_by_one(defer, monkeypatch):
         assert same(g, record(big[i], db)), i
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
-def test_gpu_plan_execute_many_heavy_lead(split, monkeypatch):
-    """das_plan_execute_many's other plans: from the second batch on, the
-    plan whose shape launched the most bytes runs first on the context's
-    stream and the rest after it on a side stream (split=1, any lead heavier
-    than the rest, DAS_PLAN_SIDE=1; 0: all in order, the default).  Bio Q1-Q6 and hub
+@pytest.mark.parametrize("mode", ["nest", "split", "plain"])
+def test_gpu_plan_execute_many_heavy_lead(mode, monkeypatch):
+    """das_plan_execute_many's other plans.  nest (the default, here at every
+    read-back wait: DAS_PLAN_NEST_MIN=0): the pending plans run whole inside
+    a plan's wait, on the plan side stream with their own read-back slot.
+    split (DAS_PLAN_SIDE=1, any lead heavier than the rest): from the second
+    batch on, the plan whose shape launched the most bytes first, the rest
+    after it on the side stream.  plain: all in order.  Bio Q1-Q6 and hub
     H4 / H2 shapes over fresh anchors, three batches each, every answer equal
     to its one-by-one evaluation."""
     import bench
     from das_amd import synthetic
     monkeypatch.setenv("DAS_PLAN_SPLIT_MIN", "0")
-    monkeypatch.setenv("DAS_PLAN_SIDE", split)
+    monkeypatch.setenv("DAS_PLAN_NEST_MIN", "0")
+    monkeypatch.setenv("DAS_PLAN_SIDE", "1" if mode == "split" else "0")
+    monkeypatch.setenv("DAS_PLAN_NEST", "1" if mode == "nest" else "0")
     arrays = synthetic.bio_kb(300, 60, 4000, 200, seed=4)
     db = _hipdb(arrays)
     for rep in range(3):
