@@ -447,8 +447,28 @@ int fused_and_finish(Ctx& c, ChainRun& r, bool& matched, std::unique_ptr<Table>&
 // large for the one-workgroup chain): host checks only, nothing allocated
 bool fused_and_viable(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
                       const std::vector<const das_plan_node_t*>& anti, int no_overload);
+// An Or of one-column scans launched as one bitmap union (k_union_first)
+// without waiting for its size (das_plan_execute_many): fused_or with
+// `defer` launches and returns 2 when that path applies (0 otherwise,
+// nothing launched); fused_or_finish reads the size back (1: answered, 0:
+// evaluate the Or another way).
+struct UnionRun {
+  std::unique_ptr<Table> res;
+  DBuf<uint32_t> own;                                 // bitmap + counters
+  PubSlot ps{};
+  uint32_t ulo = 0, uhi = 0, pool = 0;
+  hipStream_t ls = nullptr;
+  int fence = -1;
+  bool waited = false;
+  ~UnionRun() {
+    if (ls && !waited) (void)hipStreamSynchronize(ls);   // dropped before its read-back
+  }
+};
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
-             std::unique_ptr<Table>& out);
+             std::unique_ptr<Table>& out, struct UnionRun* defer = nullptr);
+std::unique_ptr<UnionRun> fused_or_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload,
+                                          uint32_t k, int side, hipEvent_t fence_in, bool* waited);
+int fused_or_finish(Ctx& c, UnionRun& u, bool& matched, std::unique_ptr<Table>& out);
 
 // export.hip: Redis key-space files (canonical_parser.py:119-183)
 struct ExportCounts {

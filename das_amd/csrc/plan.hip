@@ -659,6 +659,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   }
   std::vector<PlanOutput> outs(n_plans);
   std::vector<ChainRunPtr> runs(n_plans);
+  std::vector<std::unique_ptr<UnionRun>> uruns(n_plans);
   const char* f = std::getenv("DAS_DEFER");               // A/B: 0 = every plan in turn
   const bool defer = !(f && f[0] == '0');
   const char* fh = std::getenv("DAS_DEFER_HOOK");         // A/B: 0 = chains launched before the other plans
@@ -671,8 +672,18 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   // at this fence: blocks of earlier batches' answers were last read there
   std::vector<uint8_t> cand(n_plans, 0), tried(n_plans, 0);
   uint32_t n_cand = 0;
+  // (root Ors: their one-launch bitmap union, likewise launched early and
+  // read back last; DAS_DEFER_OR=0 off)
+  const char* fo = std::getenv("DAS_DEFER_OR");
+  const bool defer_or = !(fo && fo[0] == '0');
   for (uint32_t i = 0; i < n_plans && defer; ++i) {
-    if (nodes[i][0].op != DAS_PLAN_AND || n_cand >= kPubPool) continue;
+    if (n_cand >= kPubPool) break;
+    if (nodes[i][0].op == DAS_PLAN_OR && defer_or && nodes[i][0].nchild >= 2) {
+      cand[i] = 1;
+      ++n_cand;
+      continue;
+    }
+    if (nodes[i][0].op != DAS_PLAN_AND) continue;
     Exec ex{c, nodes[i], n[i], no_overload};
     std::vector<const das_plan_node_t*> pos, neg;
     split_and(ex, ex.children(0), pos, neg);
@@ -711,9 +722,16 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       if (ready && (*ready)()) return false;
       tried[i] = 1;
       Exec ex{c, nodes[i], n[i], no_overload};
+      const int sidx = side ? (int)(pooled % Ctx::kChainSides) : -1;
+      if (nodes[i][0].op == DAS_PLAN_OR) {
+        std::vector<const das_plan_node_t*> links;
+        for (uint32_t ti : ex.children(0)) links.push_back(&nodes[i][ti]);
+        uruns[i] = fused_or_launch(c, links, no_overload, pooled, sidx, fence_in, sidx >= 0 ? &waited[sidx] : nullptr);
+        if (uruns[i]) ++pooled;
+        continue;
+      }
       std::vector<const das_plan_node_t*> pos, neg;
       split_and(ex, ex.children(0), pos, neg);
-      const int sidx = side ? (int)(pooled % Ctx::kChainSides) : -1;
       runs[i] = fused_and_launch(c, pos, neg, no_overload, pooled, sidx, fence_in, sidx >= 0 ? &waited[sidx] : nullptr);
       if (runs[i]) ++pooled;
     }
@@ -811,13 +829,26 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   if (c.plan_bytes.size() > 4096) c.plan_bytes.clear();
   set_wait_hook(nullptr);
   launch_all();                                           // (no-op once the hook ran)
-  // 2. candidates no chain answers, in turn
+  // 2. candidates no chain / union launch answers, in turn
   for (uint32_t i = 0; i < n_plans; ++i) {
-    if (!cand[i] || runs[i]) continue;
+    if (!cand[i] || runs[i] || uruns[i]) continue;
     Exec ex{c, nodes[i], n[i], no_overload};
     outs[i] = output(c, ex.eval(0));
   }
-  // 3. the chains' outcomes (a redo: the plan evaluated in full)
+  // 3. the unions' and chains' outcomes (a redo: the plan evaluated in full)
+  for (uint32_t i = 0; i < n_plans; ++i) {
+    if (!uruns[i]) continue;
+    bool m = false;
+    TablePtr t;
+    if (fused_or_finish(c, *uruns[i], m, t)) {
+      outs[i].matched = m;
+      if (m && t && t->nrows) outs[i].tables.push_back(std::move(t));
+    } else {
+      Exec ex{c, nodes[i], n[i], no_overload};
+      outs[i] = output(c, ex.eval(0));
+    }
+    uruns[i].reset();
+  }
   for (uint32_t i = 0; i < n_plans; ++i) {
     if (!runs[i]) continue;
     bool m = false;

@@ -4296,6 +4296,55 @@ bool fused_and_viable(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
          P.ranges[0].second - P.ranges[0].first <= kSmallScan;
 }
 
+std::unique_ptr<UnionRun> fused_or_launch(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload,
+                                          uint32_t k, int side, hipEvent_t fence_in, bool* waited) {
+  struct Swap {
+    Ctx& c;
+    hipStream_t old;
+    ~Swap() { c.s = old; }
+  } sw{c, c.s};
+  if (side >= 0) {
+    hipStream_t ss = c.side_stream(side);
+    if (waited && !*waited) {
+      DAS_HIP(hipStreamWaitEvent(ss, fence_in, 0));
+      *waited = true;
+    }
+    c.s = ss;
+  }
+  auto u = std::make_unique<UnionRun>();
+  u->pool = k;
+  bool m = false;
+  std::unique_ptr<Table> t;
+  if (fused_or(c, terms, no_overload, m, t, u.get()) != 2) return nullptr;
+  if (side >= 0) {
+    DAS_HIP(hipEventRecord(c.fence_event(2 * k + 1), c.s));
+    u->fence = (int)k;
+  }
+  return u;
+}
+
+int fused_or_finish(Ctx& c, UnionRun& u, bool& matched, std::unique_ptr<Table>& out) {
+  uint32_t n = 0;
+  pub_wait(u.ps, u.ls ? u.ls : c.s, &n, 1);
+  u.waited = true;
+  if (u.fence >= 0) {
+    DAS_HIP(hipStreamWaitEvent(c.s, c.fence_event(2 * u.fence + 1), 0));
+    u.fence = -1;
+  }
+  matched = false;
+  out.reset();
+  if (n == 0xFFFFFFFFu) return 0;                             // the union did not fit: the Or another way
+  matched = n > 0;
+  if (matched) {
+    u.res->nrows = n;
+    u.res->lo[0] = u.ulo;
+    u.res->hi[0] = u.uhi;
+    u.res->sorted_col = -1;
+    out = std::move(u.res);
+  }
+  return 1;
+}
+
 void ChainRunDel::operator()(ChainRun* r) const {
   // a run dropped before its outcome was read (an error in another plan of
   // the batch): its kernels may still read its tables, its pinned descriptor
@@ -4351,7 +4400,7 @@ int fused_and_finish(Ctx& c, ChainRun& R, bool& matched, std::unique_ptr<Table>&
 }
 
 int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_overload, bool& matched,
-             std::unique_ptr<Table>& out) {
+             std::unique_ptr<Table>& out, UnionRun* defer) {
   const char* f = std::getenv("DAS_FUSED");                  // tests: 0 never
   if ((f && f[0] == '0') || no_overload || terms.size() < 2 || terms.size() + 1 > (size_t)kChainStages) return 0;
   Index& idx = c.idx;
@@ -4372,7 +4421,9 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
   bool single = true;
   for (auto& P : preps) single = single && (P.empty || P.ranges.size() == 1);
   const char* fm = std::getenv("DAS_UNION_MULTI");            // tests: 1 = always the multi-launch form
-  if (total > kChainHash / 2 || !single || (fm && fm[0] == '1')) {
+  const bool multi = total > kChainHash / 2 || !single || (fm && fm[0] == '1');
+  if (defer && !multi) return 0;                              // deferred: the union launch only
+  if (multi) {
     // larger: every range of every term counted in one launch, written in
     // one, then one dedup of the concatenation
     MultiScan ms{};
@@ -4424,6 +4475,7 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
         blocks += (ms1.seg[i].end - ms1.seg[i].begin + B - 1) / B;
       }
       proj = proj && blocks < (1ull << 32) / B;                 // the dispatch grid counts work-items in 32 bits
+      if (defer && !(proj && !(fb && fb[0] == '0'))) return 0;   // deferred: the union launch only
       if (proj && !(fb && fb[0] == '0')) {
         const uint32_t range = uhi[0] - ulo[0] + 1;
         auto res = new_table(c, DAS_TABLE_ORDERED, 1, preps[0].vars, scanned);
@@ -4435,12 +4487,21 @@ int fused_or(Ctx& c, const std::vector<const das_plan_node_t*>& terms, int no_ov
         fill_dev(own.p, 0, 4 * (words + 3), c.s);
         uint32_t* bitsp = own.p;
         uint32_t* ctrp = bitsp + words;
-        const PubSlot ps = pub_reserve();
+        const PubSlot ps = defer ? pub_reserve_pool(defer->pool) : pub_reserve();
         {
           ProfScope pf(c, "k_union_first", 8.0 * scanned);
           hipLaunchKernelGGL(k_union_first, dim3((unsigned)blocks), dim3(B), 0, c.s, ms1, ulo[0], range, bitsp,
                              res->data, ctrp, ps.p, ps.seq);
           DAS_HIP(hipGetLastError());
+        }
+        if (defer) {
+          defer->res = std::move(res);
+          defer->own = std::move(own);
+          defer->ps = ps;
+          defer->ulo = ulo[0];
+          defer->uhi = uhi[0];
+          defer->ls = c.s;
+          return 2;
         }
         uint32_t n = 0;
         pub_wait(ps, c.s, &n, 1);
