@@ -1438,7 +1438,7 @@ def main():
             # a latency-bound step of ~0.25 ms: more untimed warmup steps (the
             # side streams' blocks, pinned pools, shape caches) and more timed
             # ones against scheduling noise -- milliseconds either way
-            a.warmup, a.steps = max(args.warmup, 5), max(args.steps, 40)
+            a.warmup, a.steps = max(args.warmup, 20), max(args.steps, 60)
         try:
             r = run_leg(w, a)
         except Exception as e:            # one leg failing must not lose the headline line
