@@ -60,8 +60,6 @@ def parse():
     ap.add_argument("--build-warmup", default="full", choices=["full", "small"],
                     help="config 4 warm-up build: the same input (default; the timed build then reuses every "
                          "device block) or a 10^4-link KB")
-    ap.add_argument("--q2-first", type=int, default=1, choices=[0, 1],
-                    help="batched steps: the tagged Q2 before the batch (1) or after it (0)")
     ap.add_argument("--batch", type=int, default=1, choices=[0, 1],
                     help="1 (default): a step's queries in one das_plan_execute_many call (pm.matched_many); "
                          "0: query.matched(db, answer) one by one")
@@ -438,9 +436,12 @@ def _cpu_sample(workload, args_d):
 
 def _cpu_query_worker(job):
     """One process of the CPU baseline: evaluates whole queries, one at a
-    time, round-robin from its offset, until the budget is spent."""
-    workload, args_d, wid, budget = job
+    time, round-robin from its offset, until the budget is spent.  fast:
+    the oracle's And fold joins by hash on the shared variables (FAST_JOIN);
+    else the reference's nested loop (pattern_matcher.py:732-738)."""
+    workload, args_d, wid, budget, fast = job
     from oracle import das_oracle as O
+    O.FAST_JOIN = bool(fast)
     arrays, specs, _ = _cpu_sample(workload, args_d)
     db = O.RedisMongoSemantics(O.KB.from_arrays(arrays))
     total, done, i = 0, 0, wid
@@ -472,14 +473,17 @@ def _cpu_build_worker(job):
     return links, reps, time.perf_counter() - t0
 
 
-def _calibration():
+def _calibration(join="nested"):
+    """The oracle's time over the reference's on the reference-answered
+    fixtures, for the And join the baseline ran (tools/calibrate_cpu.py)."""
     path = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         c = json.load(f)
-    return {"oracle_over_reference_time": c.get("ratio_all"), "source": "profiles/cpu_calibration.json",
-            "how": c.get("what")}
+    r = (c.get("joins") or {}).get(join) or {}
+    return {"oracle_over_reference_time": r.get("ratio_all"), "join": join,
+            "source": "profiles/cpu_calibration.json", "how": c.get("what")}
 
 
 def _pool_map(fn, jobs):
@@ -489,26 +493,32 @@ def _pool_map(fn, jobs):
         return pool.map(fn, jobs)
 
 
-def cpu_baseline(args, budget_s):
-    """The oracle (CPU restatement keeping the reference's nested-loop join
-    complexity; its speed against the reference itself is in
-    profiles/cpu_calibration.json) on a bounded sample of the same workload:
-    one process per host core, each evaluating whole queries one at a time
-    (SURVEY.md §8d(ii))."""
+def cpu_baseline(args, budget_s, fast=False):
+    """The oracle on a bounded sample of the same workload, one process per
+    host core, each evaluating whole queries one at a time (SURVEY.md
+    §8d(ii)).  Default: the oracle's And fold as the reference's nested loop
+    over both sides' assignments (FAST_JOIN = False; pattern_matcher.py:
+    732-738), i.e. the reference's complexity -- its time against the
+    reference's own on the reference-answered fixtures is the calibration
+    (profiles/cpu_calibration.json, "nested").  fast: the oracle's hash join
+    on the shared variables (same rows), reported apart as cpu_fast."""
     cores = cpu_cores()
     args_d = vars(args)
     _, specs, what = _cpu_sample(args.workload, args_d)
     t0 = time.perf_counter()
-    res = _pool_map(_cpu_query_worker, [(args.workload, args_d, w, budget_s) for w in range(cores)])
+    res = _pool_map(_cpu_query_worker, [(args.workload, args_d, w, budget_s, fast) for w in range(cores)])
     wall = time.perf_counter() - t0
     total = sum(r[0] for r in res)
     done = sum(r[1] for r in res)
     span = max(r[2] for r in res)
+    join = ("hash join on the shared variables (oracle FAST_JOIN=True, not the reference's complexity)" if fast
+            else "nested-loop And (oracle FAST_JOIN=False, the reference's complexity)")
     return {"value": total / span, "unit": "bindings/s", "cores": cores, "kind": "port",
-            "sample": f"oracle (nested-loop And, reference complexity) on {what}; {len(specs)} query instances, "
+            "join": "hash" if fast else "nested",
+            "sample": f"oracle, {join}, on {what}; {len(specs)} query instances, "
                       f"{cores} processes x one whole query at a time, {done} queries in {span:.1f} s "
                       f"({wall:.1f} s with interpreter start-up)",
-            "calibration": _calibration()}
+            "calibration": _calibration("hash" if fast else "nested")}
 
 
 def cpu_baseline_build(args, budget_s):
@@ -983,6 +993,27 @@ def step_roofline(stats, ms_per_step, world, steps=1):
                     "scratch excluded) / ms_per_step"}
 
 
+def verify_steps(batched, single, names, dist, stage):
+    """Per timed step: the answer size of each query as the step computed it
+    (one das_plan_execute_many batch) against matched() one query at a time
+    on the same query set; summed over ranks at N > 1.  Raises on any
+    difference -- the bench's numbers are only reported for steps whose
+    answers the one-by-one path confirms."""
+    import numpy as np
+    a = np.array(batched, dtype=np.float64)
+    b = np.array(single, dtype=np.float64)
+    if dist:
+        a = np.array(_sync_sum(dist, a.ravel().tolist(), stage)).reshape(a.shape)
+        b = np.array(_sync_sum(dist, b.ravel().tolist(), stage)).reshape(b.shape)
+    bad = [(s, names[s][q], int(a[s, q]), int(b[s, q])) for s, q in zip(*np.nonzero(a != b))]
+    if bad:
+        raise AssertionError(f"batched step answers differ from matched() one by one (step, query, batched, "
+                             f"single): {bad[:8]}")
+    return {"steps": len(batched), "queries_per_step": len(names[0]) if names else 0,
+            "bindings_checked": int(a.sum()), "how": "each timed step's per-query answer sizes (and so its total) "
+                                                      "equal matched() one query at a time on the same query set"}
+
+
 def run_query(args, workload, rank, world, dist, local_rank, backend):
     """One query workload (bio / flybase / hub): KB, warmup, K timed steps
     between barriers, max over ranks.  Returns rank 0's JSON dict."""
@@ -1011,7 +1042,9 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     t_build = time.perf_counter() - t_build
     # one query set per step: anchored queries change their anchor every step
     n_sets = args.warmup + args.steps + 1
-    qsets = [[(name, build_expr(pm, s)) for name, s in specs(i)] for i in range(n_sets)]
+    # (and args.steps more, fresh anchors for the matched()-per-query timing)
+    qsets = [[(name, build_expr(pm, s)) for name, s in specs(i)] for i in range(n_sets + args.steps)]
+    stage_dev = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
     engine = None
     if world > 1:
         from das_amd import parallel
@@ -1027,42 +1060,36 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             q.matched(db, ans)
             return ans.count()
 
-    # Q2's launches are tagged inside the timed steps (das_prof_tag): its And
-    # join's fraction is then the in-step one, apart from QUERY_2 / QUERY_3's
-    # launches of the same kernel instantiation
+    # Q2's launches are tagged inside the timed steps (das_prof_tag_plan:
+    # Q2's own launches inside the batch, not those of the plans and chains
+    # that run in its read-back waits): its And join's fraction is then the
+    # in-step one, apart from QUERY_2 / QUERY_3's launches of the same kernel
+    # instantiation.  The step is the same batch with or without the tag.
     tag_q2 = [False]
 
-    def step(i):
+    def step(i, batch=None):
+        """One pass over query set i -> the answer size of each query."""
         if engine is not None:
+            if batch is False:
+                return [run(q) for _, q in qsets[i]]
             # the step's queries share their collectives (ShardedMatcher.count_many)
-            return sum(engine.count_many([q for _, q in qsets[i]]))
-        if args.batch:
+            return list(engine.count_many([q for _, q in qsets[i]]))
+        names = [name for name, _ in qsets[i]]
+        q2 = next((k for k, name in enumerate(names) if name.startswith("Q2")), None) if tag_q2[0] else None
+        if args.batch if batch is None else batch:
             # the step's queries in one das_plan_execute_many call
             # (pm.matched_many: a fused chain's GPU time overlaps the host
-            # work of the next query); Q2 alone while its launches are tagged
-            # -- before the batch by default (--q2-first 0: after it, where its
-            # read-back waits behind the batch's last kernels)
-            tagged = [(name, q) for name, q in qsets[i] if tag_q2[0] and name.startswith("Q2")]
-            qs = [(name, q) for name, q in qsets[i] if not (tag_q2[0] and name.startswith("Q2"))]
-            tot = 0
-            if args.q2_first:
-                for name, q in tagged:
-                    db.ctx.prof_tag("Q2")
-                    tot += run(q)
-                    db.ctx.prof_tag(None)
-                tagged = []
-            tot += sum(a.count() for _, a in pm.matched_many(db, [q for _, q in qs]))
-            todo = tagged
-        else:
-            tot, todo = 0, qsets[i]
-        for name, q in todo:
-            if tag_q2[0] and name.startswith("Q2"):
+            # work of the next query)
+            return [a.count() for _, a in pm.matched_many(db, [q for _, q in qsets[i]],
+                                                           tag=None if q2 is None else (q2, "Q2"))]
+        out = []
+        for k, (name, q) in enumerate(qsets[i]):
+            if k == q2:
                 db.ctx.prof_tag("Q2")
-                tot += run(q)
+            out.append(run(q))
+            if k == q2:
                 db.ctx.prof_tag(None)
-            else:
-                tot += run(q)
-        return tot
+        return out
 
     log("warmup")
     # the warmup steps record every kernel scope (the "kernels" table); the
@@ -1077,7 +1104,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     db.ctx.prof_enable(False)
     warm_stats = db.ctx.prof_stats()
     dominant = roofline_of(warm_stats, workload) if args.events == "dominant" else None
-    per_query = {name: run(q) for name, q in qsets[args.warmup]}
+    per_query = {name: run(q) for name, q in qsets[args.warmup]}          # one by one: matched() per query
     if world > 1:
         # the answer's size: each rank counts the bindings it holds
         stage = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
@@ -1129,13 +1156,14 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     coll0 = engine.sdb.plan_stats["collectives"] if engine else 0
     t0 = time.perf_counter()
     log("timed steps")
-    bindings = 0
+    step_counts = []
     for i in range(args.steps):
-        bindings += step(args.warmup + i)
+        step_counts.append(step(args.warmup + i))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    bindings = sum(sum(c) for c in step_counts)
     coll_per_step = (engine.sdb.plan_stats["collectives"] - coll0) / args.steps if engine else 0
     db.ctx.prof_enable(False)
     db.ctx.prof_only(None)
@@ -1146,6 +1174,24 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if and_join:
         and_join["note"] = "Q2's And join launches inside the timed steps (das_prof_tag)"
     stats = {k: v for k, v in stats.items() if "@" not in k}
+    # every timed step's answers against the same query set evaluated one
+    # query at a time through matched() (untimed): the batched executor's
+    # per-query answer sizes and the step's total must equal them
+    check = verify_steps(step_counts, [step(args.warmup + i, batch=False) for i in range(args.steps)],
+                         [[name for name, _ in qsets[args.warmup + i]] for i in range(args.steps)], dist, stage_dev)
+    # the reference's call pattern, timed: one expr.matched(db, answer) per
+    # query (scripts/benchmark.py:231-239, QueryFlyBase.ipynb cells 5-9) over
+    # query sets no earlier step used
+    matched_ms = None
+    if engine is None and args.batch and not args.no_extras:
+        for i in range(2):                         # the extra sets' shapes warm (no new anchors timed cold)
+            step(args.warmup + i, batch=False)
+        torch.cuda.synchronize()
+        tm = time.perf_counter()
+        for i in range(args.steps):
+            step(n_sets + i, batch=False)
+        torch.cuda.synchronize()
+        matched_ms = (time.perf_counter() - tm) * 1e3 / args.steps
     if args.cprofile and rank == 0:
         import cProfile
         import pstats
@@ -1195,7 +1241,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                         os.environ.pop(k, None)
                     else:
                         os.environ[k] = v
-    stage = torch.device("cuda", local_rank) if backend == "nccl" else "cpu"
+    stage = stage_dev
     elapsed = _sync_max(dist, [elapsed], stage)[0]
     bindings = _sync_sum(dist, [bindings], stage)[0]
     value = bindings / elapsed
@@ -1205,20 +1251,23 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         incl = materialised_rate(pm, db, qsets[n_sets - 1], args.materialise_cap)
     out = None
     if rank == 0:
-        cpu = None
+        cpu = cpu_fast = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
             cpu = cpu_baseline(args, args.cpu_baseline_seconds)
+            # the oracle's hash-join fold beside it (not the reference's complexity)
+            cpu_fast = cpu_baseline(args, max(args.cpu_baseline_seconds / 3, 2.0), fast=True)
         data = {"bio": "synthetic (seeded bio_kb in scripts/benchmark.py shape; bio_atomspace dump unavailable offline)",
                 "flybase": "synthetic FlyBase-shaped KB (flybase2metta Execution layout; the FlyBase dump needs a "
                            "network fetch)",
                 "hub": "synthetic power-law hypergraph (powerlaw_kb, Zipf(1.1) targets)"}[workload]
         cfg = dict(cfg, bindings_per_step=per_query, parallelism=f"links sharded x{world}")
         # how a step submits its queries: one das_plan_execute_many call
-        # (pm.matched_many; Q2 alone while its launches are tagged), or one
+        # (pm.matched_many; Q2's own launches tagged inside it), or one
         # matched() per query; N > 1: ShardedMatcher.count_many
         cfg["step_calls"] = ("ShardedMatcher.count_many" if world > 1 else
                              "pm.matched_many (das_plan_execute_many)" if args.batch else "matched() per query")
+        cfg["step_check"] = check
         cfg["query_ms_rank0"] = per_query_ms
         cfg["query_launches_readbacks_rank0"] = per_query_ops
         out = {
@@ -1230,6 +1279,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             "step_roofline": step_roofline(warm_stats if dominant else stats, ms_per_step, world,
                                            1 if dominant else args.steps),
             "cpu_baseline": cpu,
+            "cpu_fast": cpu_fast,
             # latency-bound workloads: per query, its wall us and the kernel
             # scopes / host read-backs it takes (FlyBase: launches and waits,
             # not bytes, bound it)
@@ -1241,6 +1291,9 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             "kernels": kernels_of(warm_stats if dominant else stats),
             "kernels_from": "last warmup step (every scope)" if dominant else "timed steps (every scope)",
             "build_s": round(t_build, 2),
+            # the same workload through the reference's call pattern: one
+            # matched() per query (no batching), fresh anchors
+            "step_ms_matched": None if matched_ms is None else round(matched_ms, 4),
         }
         if world > 1:
             out["sharded_plan_stats"] = dict(engine.sdb.plan_stats)
@@ -1281,8 +1334,8 @@ def _compact_cpu(c, full=True):
     if not c:
         return None
     if not full:
-        return {"value": _r(c.get("value"), 1)}
-    out = {k: _r(c.get(k), 1) for k in ("value", "unit", "cores", "kind") if k in c}
+        return {k: _r(c.get(k), 1) for k in ("value", "join") if k in c}
+    out = {k: _r(c.get(k), 1) for k in ("value", "unit", "cores", "kind", "join") if k in c}
     out["sample"] = (c.get("sample") or "")[:240]
     return out
 
@@ -1295,7 +1348,9 @@ def _compact_leg(d):
     sr = d.get("step_roofline")
     out["step_roofline"] = {"frac": sr.get("frac")} if sr else None
     out["cpu_baseline"] = _compact_cpu(d.get("cpu_baseline"), full=False)
-    for k in ("latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
+    if d.get("cpu_fast"):
+        out["cpu_fast"] = _compact_cpu(d.get("cpu_fast"), full=False)
+    for k in ("step_ms_matched", "latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
         if d.get(k) is not None:
             out[k] = d[k]
     return out
@@ -1315,7 +1370,9 @@ def compact_line(full):
     line["roofline"] = _compact_roofline(full.get("roofline"))
     line["step_roofline"] = _compact_roofline(full.get("step_roofline"))
     line["cpu_baseline"] = _compact_cpu(full.get("cpu_baseline"))
-    for k in ("latency", "summary", "collectives_per_step"):
+    if full.get("cpu_fast"):
+        line["cpu_fast"] = _compact_cpu(full.get("cpu_fast"), full=False)
+    for k in ("step_ms_matched", "box", "latency", "summary", "collectives_per_step"):
         if full.get(k) is not None:
             line[k] = full[k]
     jv = full.get("join_probe_variants") or {}

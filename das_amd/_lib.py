@@ -152,6 +152,7 @@ _SIGS = {
     "das_prof_enable": (C.c_int, [P, C.c_int]),
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_tag": (C.c_int, [P, C.c_char_p]),
+    "das_prof_tag_plan": (C.c_int, [P, C.c_uint32, C.c_char_p]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
     "das_prof_names": (C.c_int, [P, P, C.c_uint64]),
@@ -763,6 +764,12 @@ class Context:
     def prof_tag(self, tag=None):
         """Name the scopes recorded from now on "<scope>@<tag>" (None: untagged)."""
         check(lib().das_prof_tag(self.h, tag.encode() if tag else None), self.h)
+
+    def prof_tag_plan(self, plan=None, tag=None):
+        """Tag the launches of plan `plan` of each following plan_execute_many
+        batch "<scope>@<tag>" (None: untag)."""
+        on = plan is not None and tag
+        check(lib().das_prof_tag_plan(self.h, int(plan) if on else 0xFFFFFFFF, tag.encode() if on else None), self.h)
 
     def prof_stats(self):
         buf = C.create_string_buffer(1 << 16)

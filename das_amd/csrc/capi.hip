@@ -734,7 +734,7 @@ int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, u
 int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,
                           uint32_t no_overload, das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched,
                           int32_t* negation, int64_t* info) {
-  if (!ctx || (n_plans && (!nodes || !n || !n_out || !matched || !negation)))
+  if (!ctx || (n_plans && (!nodes || !n || !n_out || !matched || !negation)) || (cap && !out))
     return fail(ctx, DAS_ERR_INVALID, "null argument");
   return guarded(ctx, [&] {
     auto rs = das::plan_execute_many(ctx->c, nodes, n, n_plans, (int)no_overload);
@@ -835,6 +835,13 @@ int das_prof_only(das_ctx_t* ctx, const char* name) {
 
 int das_prof_tag(das_ctx_t* ctx, const char* tag) {
   return guarded(ctx, [&] { ctx->c.prof_tag = tag ? tag : ""; });
+}
+
+int das_prof_tag_plan(das_ctx_t* ctx, uint32_t plan, const char* tag) {
+  return guarded(ctx, [&] {
+    ctx->c.tag_plan = tag && tag[0] ? plan : ~0u;
+    ctx->c.tag_plan_name = tag ? tag : "";
+  });
 }
 
 int das_prof_reset(das_ctx_t* ctx) {

@@ -68,6 +68,10 @@ struct PosIndex {
   std::vector<uint64_t> h_ukey, h_uoff;
 };
 constexpr uint64_t kHostKeyMirror = 1ull << 24;   // keys per P_{a,p} mirrored on the host (256 MB at most)
+// the mirror's key limit for the next build: kHostKeyMirror, or
+// DAS_HOST_KEY_MIRROR (tests: 0 = no mirror, every anchored key range is
+// resolved on the device through a read-back)
+uint64_t host_key_mirror_max();
 constexpr uint64_t kHostNodeMirror = 1ull << 24;  // nodes mirrored on the host (384 MB at most)
 
 struct CtypeRange {
@@ -163,6 +167,8 @@ struct Ctx {
   int scan_views = 0;
   std::string prof_only;             // non-empty: only scopes of these names ('|'-separated) record events
   std::string prof_tag;              // non-empty: recorded scopes are named "<scope>@<tag>" (one query's launches)
+  uint32_t tag_plan = ~0u;           // das_plan_execute_many: the plan whose launches carry tag_plan_name
+  std::string tag_plan_name;
   bool prof_selected(const std::string& name) const {
     if (prof_only.empty()) return true;
     size_t b = 0;

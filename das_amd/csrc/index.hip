@@ -1531,6 +1531,11 @@ void partition_rows(Ctx& c, const uint32_t* d_rows, uint64_t n, uint32_t K, cons
 namespace {
 }  // namespace
 
+uint64_t host_key_mirror_max() {
+  const char* e = std::getenv("DAS_HOST_KEY_MIRROR");
+  return e ? std::strtoull(e, nullptr, 10) : kHostKeyMirror;
+}
+
 void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_rank, uint32_t shard_world) {
   DAS_CHECK(shard_world >= 1 && shard_rank < shard_world && shard_world <= 256, DAS_E_INVALID, "bad shard rank/world");
   // DAS_BUILD_EXPR_ON_DEVICE: expr_off / expr_child / expr_kind /
@@ -1891,6 +1896,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
 
   // 7. per-arity tables
   phase.emplace(c, "phase_tables", 0.0);
+  const uint64_t mirror_max = host_key_mirror_max();
   for (uint32_t ar = 1; ar <= (uint32_t)kMaxArity; ++ar) {
     if (!links_of_arity[ar]) continue;        // no link of this arity (step 5's counts): no flag pass
     DBuf<uint32_t> lf(n_atoms ? n_atoms : 1, s), ids;
@@ -2071,7 +2077,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
         }
         P.nkeys = rle<uint64_t>(pk.p, R, &P.ukey, &P.uoff, idx, s);
         build_key_dir(P, idx, s);
-        if (P.nkeys <= kHostKeyMirror) {
+        if (P.nkeys <= mirror_max) {
           P.h_ukey.resize(P.nkeys);
           P.h_uoff.resize(P.nkeys + 1);
           DAS_HIP(hipMemcpyAsync(P.h_ukey.data(), P.ukey, 8 * P.nkeys, hipMemcpyDeviceToHost, s));
@@ -2119,7 +2125,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
         }
         P.nkeys = rle<uint64_t>(key.p, R, &P.ukey, &P.uoff, idx, s);
         build_key_dir(P, idx, s);
-        if (P.nkeys <= kHostKeyMirror) {
+        if (P.nkeys <= mirror_max) {
           // host copy of the unique keys and offsets: an anchored scan finds
           // its key range without a device round trip
           P.h_ukey.resize(P.nkeys);

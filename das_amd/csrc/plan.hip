@@ -712,6 +712,23 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
     fence_in = c.fence_event(2 * kPubPool);
     DAS_HIP(hipEventRecord(fence_in, c.s));
   }
+  // das_prof_tag_plan: plan c.tag_plan's own launches are named
+  // "<scope>@<tag>" (restored on exit, so plans nested in its waits and the
+  // hook's chains stay untagged: the hook clears the tag, below)
+  struct TagScope {
+    Ctx& c;
+    std::string old;
+    bool on;
+    TagScope(Ctx& c_, uint32_t i) : c(c_), old(c_.prof_tag), on(i == c_.tag_plan) {
+      if (on) c.prof_tag = c.tag_plan_name;
+    }
+    ~TagScope() { if (on) c.prof_tag = old; }
+  };
+  auto eval_plan = [&](uint32_t i) {
+    TagScope ts(c, i);
+    Exec ex{c, nodes[i], n[i], no_overload};
+    return output(c, ex.eval(0));
+  };
   uint32_t pooled = 0, next = 0;
   // compiles and launches the next candidates' chains while ready() is false
   // (every remaining one when it is null); true when none is left
@@ -721,6 +738,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       if (!cand[i] || tried[i]) continue;
       if (ready && (*ready)()) return false;
       tried[i] = 1;
+      TagScope ts(c, i);
       Exec ex{c, nodes[i], n[i], no_overload};
       const int sidx = side ? (int)(pooled % Ctx::kChainSides) : -1;
       if (nodes[i][0].op == DAS_PLAN_OR) {
@@ -777,15 +795,28 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       PubLevel lv;
       Swap sw{c, c.s};
       c.s = to_side();
-      Exec ex{c, nodes[i], n[i], no_overload};
-      outs[i] = output(c, ex.eval(0));
+      outs[i] = eval_plan(i);
     }
   };
   // 1. the other plans first; the chains are compiled and launched in the
   // gaps where those plans wait for a read-back (host time otherwise spent
   // spinning), the rest after them
   WaitHook hook = [&](const std::function<bool()>& ready) {
-    const bool chains_done = launch_some(&ready);
+    // the waiting plan's tag does not cover what runs in its wait
+    struct Untag {
+      Ctx& c;
+      std::string old;
+      ~Untag() { c.prof_tag = old; }
+    } ut{c, c.prof_tag};
+    c.prof_tag.clear();
+    bool chains_done;
+    {
+      // the chains' own read-backs (a key range resolved on the device by
+      // scan_prepare, a non-pooled outcome slot) and staging go to the second
+      // level: the awaited slot and its request buffer stay the outer plan's
+      PubLevel lv;
+      chains_done = launch_some(&ready);
+    }
     if (chains_done) nest_some(ready);
     bool pending = false;
     for (size_t j = cur + 1; j < order.size() && nest; ++j) pending = pending || !done[order[j]];
@@ -821,8 +852,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
     Swap sw{c, c.s};
     if (split && j > 0) c.s = to_side();
     const double b0 = launched_bytes();
-    Exec ex{c, nodes[i], n[i], no_overload};
-    outs[i] = output(c, ex.eval(0));
+    outs[i] = eval_plan(i);
     c.plan_bytes[shape[i]] = launched_bytes() - b0;
     if (hooked) set_wait_hook(&hook);                      // (re-armed for the next plan's waits)
   }
@@ -832,8 +862,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   // 2. candidates no chain / union launch answers, in turn
   for (uint32_t i = 0; i < n_plans; ++i) {
     if (!cand[i] || runs[i] || uruns[i]) continue;
-    Exec ex{c, nodes[i], n[i], no_overload};
-    outs[i] = output(c, ex.eval(0));
+    outs[i] = eval_plan(i);
   }
   // 3. the unions' and chains' outcomes (a redo: the plan evaluated in full)
   for (uint32_t i = 0; i < n_plans; ++i) {
@@ -844,8 +873,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       outs[i].matched = m;
       if (m && t && t->nrows) outs[i].tables.push_back(std::move(t));
     } else {
-      Exec ex{c, nodes[i], n[i], no_overload};
-      outs[i] = output(c, ex.eval(0));
+      outs[i] = eval_plan(i);
     }
     uruns[i].reset();
   }
@@ -857,8 +885,7 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       outs[i].matched = m;
       if (m && t && t->nrows) outs[i].tables.push_back(std::move(t));
     } else {
-      Exec ex{c, nodes[i], n[i], no_overload};
-      outs[i] = output(c, ex.eval(0));
+      outs[i] = eval_plan(i);
     }
     runs[i].reset();
   }

@@ -1763,9 +1763,10 @@ std::unique_ptr<Table> gather_ranges(Ctx& c, const Table& a, const uint64_t* beg
   t->nrows = m;
   if (m && a.ncols) {
     DBuf<uint64_t> d(h.size(), c.s);
-    uint8_t* st = pinned_stage(8 * h.size());
-    std::memcpy(st, h.data(), 8 * h.size());
-    DAS_HIP(hipMemcpyAsync(d.p, st, 8 * h.size(), hipMemcpyHostToDevice, c.s));
+    // from pageable memory: the runtime stages it before returning, so no
+    // later user of the pinned staging buffer can overwrite a copy the
+    // stream has not reached yet
+    DAS_HIP(hipMemcpyAsync(d.p, h.data(), 8 * h.size(), hipMemcpyHostToDevice, c.s));
     hipLaunchKernelGGL(k_gather_ranges, G(m), dim3(B), 0, c.s, cols_of(a), (const uint64_t*)d.p,
                        (const uint64_t*)d.p + n_ranges + 1, n_ranges, m, t->data, t->cap);
     DAS_HIP(hipGetLastError());

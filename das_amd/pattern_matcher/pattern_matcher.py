@@ -655,12 +655,14 @@ def _try_plan(expr, db, answer):
     return matched
 
 
-def matched_many(db, exprs):
+def matched_many(db, exprs, tag=None):
     """[(matched, answer)] of independent expressions, each as
     `expr.matched(db, answer)` with a fresh PatternMatchingAnswer would give.
     On one HipDB the plannable ones go to ONE das_plan_execute_many call (the
     GPU runs an expression's fused chain while the host prepares the next);
-    the rest, and every expression on other DBs, are evaluated one by one."""
+    the rest, and every expression on other DBs, are evaluated one by one.
+    tag = (index, name): the kernel scopes of exprs[index] are recorded as
+    "<scope>@<name>" (das_prof_tag_plan; bench.py's in-step And join)."""
     res = [None] * len(exprs)
     batch = []
     if type(db) is HipDB and os.environ.get("DAS_PLAN") != "0":
@@ -678,7 +680,14 @@ def matched_many(db, exprs):
             if cached[1] is not None:
                 batch.append((i, cached[1]))
         if batch:
-            outs = db.ctx.plan_execute_many([(w, len(w) // _WORDS) for _, w in batch], no_overload)
+            at = next((k for k, (i, _) in enumerate(batch) if tag and i == tag[0]), None)
+            if at is not None:
+                db.ctx.prof_tag_plan(at, tag[1])
+            try:
+                outs = db.ctx.plan_execute_many([(w, len(w) // _WORDS) for _, w in batch], no_overload)
+            finally:
+                if at is not None:
+                    db.ctx.prof_tag_plan(None)
             for (i, _), (matched, negation, tables) in zip(batch, outs):
                 ans = PatternMatchingAnswer()
                 ans._set(db, Relation(tables))
@@ -687,7 +696,14 @@ def matched_many(db, exprs):
     for i, e in enumerate(exprs):
         if res[i] is None:
             ans = PatternMatchingAnswer()
-            res[i] = (e.matched(db, ans), ans)
+            tagged = tag is not None and i == tag[0] and type(db) is HipDB
+            if tagged:
+                db.ctx.prof_tag(tag[1])
+            try:
+                res[i] = (e.matched(db, ans), ans)
+            finally:
+                if tagged:
+                    db.ctx.prof_tag(None)
     return res
 
 

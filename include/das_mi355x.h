@@ -420,6 +420,11 @@ int das_prof_only(das_ctx_t* ctx, const char* name);   /* name: one scope or a '
  * none): one query's launches of a kernel other queries launch too are timed
  * apart inside a step (bench.py's in-step And-join fraction). */
 int das_prof_tag(das_ctx_t* ctx, const char* tag);
+/* The tag applied only while plan `plan` of each following
+ * das_plan_execute_many batch runs (its own launches, not those of other
+ * plans launched inside its read-back waits); plan = UINT32_MAX or tag NULL
+ * clears it: one query tagged inside a batched step. */
+int das_prof_tag_plan(das_ctx_t* ctx, uint32_t plan, const char* tag);
 int das_prof_reset(das_ctx_t* ctx);
 int das_prof_read(das_ctx_t* ctx, const char* name, double* ms, uint64_t* launches, double* bytes);
 int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap);

@@ -559,6 +559,44 @@ def _ordered_hash_join(acc, rows):
     return out
 
 
+def _ordered_nested_join(acc, rows):
+    """The And fold's nested loop (:732-738) itself -- every (acc, rows) pair
+    evaluated, the reference's complexity -- for ordered rows, with each row's
+    mapping dict and variable set built once per fold, as the reference's
+    OrderedAssignment holds them from freeze() on (:58-70, 141-153): the
+    pair's work is then the reference's evaluate_compatibility / _join_ordered
+    (:119-153).  Same rows as join() per pair.  None: not that case."""
+    if CONFIG["no_overload"]:
+        return None
+    rows = list(rows)
+    if any(r[0] != "O" for r in acc) or any(r[0] != "O" for r in rows):
+        return None
+    pa = [(a, dict(a[1]), frozenset(a1 for a1, _ in a[1])) for a in acc]
+    pb = [(b, dict(b[1]), frozenset(b1 for b1, _ in b[1])) for b in rows]
+    out = []
+    for a, ma, sa in pa:
+        for b, mb, sb in pb:
+            if a[1] == b[1]:                      # EQUAL
+                out.append(a)
+                continue
+            ok = True
+            for v in sa & sb:
+                if ma[v] != mb[v]:                # INCOMPATIBLE
+                    ok = False
+                    break
+            if not ok:
+                continue
+            if sb < sa:                           # FIRST_COVERS_SECOND
+                out.append(a)
+            elif sa < sb:                         # SECOND_COVERS_FIRST
+                out.append(b)
+            else:                                 # NO_COVERING: merged mapping
+                m = dict(ma)
+                m.update(mb)
+                out.append(o_row(m))
+    return out
+
+
 def check_negation(a, tabu):
     """a.check_negation(tabu) — :112-117, :211-217, :353-362."""
     if a[0] == "O":
@@ -760,7 +798,7 @@ def matched(spec, db, answer):
             if not acc:
                 acc = list(sub.rows)
                 continue
-            fast = _ordered_hash_join(acc, sub.rows)
+            fast = _ordered_hash_join(acc, sub.rows) if FAST_JOIN else _ordered_nested_join(acc, sub.rows)
             acc = fast if fast is not None else \
                 [j for a in acc for b in sub.rows for j in [join(a, b)] if j is not None]
         result = RowSet()

@@ -42,34 +42,60 @@ def _count(db, spec):
     return rows, ck
 
 
+def _count_many(db, specs):
+    """(rows, checksum) of each answer of ONE pm.matched_many batch -- the
+    bench step's call (das_plan_execute_many with its default side-stream
+    chains, deferred Or unions and plans nested in read-back waits)."""
+    import bench
+    from das_amd.pattern_matcher import pattern_matcher as pm
+    out = []
+    for _, ans in pm.matched_many(db, [bench.build_expr(pm, s) for s in specs]):
+        ck, rows = CK.answer_checksum(ans)
+        assert rows == ans.count()
+        out.append((rows, ck))
+    return out
+
+
 def _leaf_d64(arrays, n):
     """d64 (tests/checksum.py) of leaves 0 .. n-1 by hashlib over their strings."""
     return np.array([CK.d64_text(arrays.leaf_string(i)) for i in range(n)], dtype=np.uint64)
 
 
-def test_gpu_bio_fullsize_counts(monkeypatch):
-    """The bench's bio KB (bio_full_kb at 20 M Member links): Q1-Q4 against
-    closed forms; the reference's QUERY_2 / QUERY_3 (Q5 / Q6) as one native
-    plan call and through the per-operator path (same counts)."""
-    import bench
+@pytest.fixture(scope="module")
+def bio20m():
+    """The bench's bio KB (bio_full_kb at 20 M Member links), indexed once
+    for the module's bio tests, prefetched as bench.py's leg is."""
+    import gc
     from das_amd import synthetic
     from das_amd.database.hip_db import HipDB
-    n_genes, n_bps = 200_000, 50_000
-    arrays = synthetic.bio_full_kb(n_genes, n_bps, 20_000_000, 100_000)
+    arrays = synthetic.bio_full_kb(200_000, 50_000, 20_000_000, 100_000)
     db = HipDB(device=0)
     db.load_arrays(arrays)
+    db.prefetch()
+    yield db, arrays, _bio_base(arrays, 200_000, 50_000)
+    del db, arrays
+    gc.collect()
+
+
+def _bio_base(arrays, n_genes, n_bps):
+    """Anchor-independent parts of the bio closed forms."""
     base = len(arrays.type_names)                     # leaf index of gene 0; bps follow the genes
     m = _pairs(arrays, "Member")
-    mg, mb = m >> 32, m & 0xFFFFFFFF
     inh = _pairs(arrays, "Inheritance")
-    specs = dict(bench.bio_specs(np.arange(n_genes)))
-    rng = np.random.default_rng(17)
+    D = _leaf_d64(arrays, arrays.n_leaf)
+    return {"n_genes": n_genes, "n_bps": n_bps, "base": base, "m": m, "inh": inh, "D": D}
+
+
+def _bio_want(arrays, B, anchor):
+    """(rows, checksum) of bench.bio_specs(anchor=anchor)'s Q1-Q6 by closed form."""
+    n_genes, n_bps, base, m, inh, D = (B[k] for k in ("n_genes", "n_bps", "base", "m", "inh", "D"))
+    mg, mb = m >> 32, m & 0xFFFFFFFF
+    rng = np.random.default_rng(17 + 7919 * anchor)
     ga, gb = (int(x) for x in rng.choice(np.arange(n_genes), 2, replace=False))   # bench.bio_specs' anchors
     bp0 = base + n_genes
     nl = base + n_genes + n_bps + 10_000                # every node index below the Concept blocks
     gdeg = np.bincount(mg, minlength=nl)
     outdeg = np.bincount(inh >> 32, minlength=nl)
-    D = _leaf_d64(arrays, arrays.n_leaf)
     G = lambda v, x: CK.g_np(v, D[x])  # noqa: E731
     gsum = lambda k, v, n=nl: CK.group_sum_np(k, v, n)  # noqa: E731
     in_nl = mb < nl
@@ -88,12 +114,44 @@ def test_gpu_bio_fullsize_counts(monkeypatch):
         "Q4 hub join": (int(gdeg[mg[mb == bp0]].sum()), CK.sum_np(CK.prod_np(G("V_g", mg[q4]), G("V_bp", mb[q4])))),
     }
     want.update(_query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, D=D))
+    return want
+
+
+def test_gpu_bio_fullsize_counts(bio20m, monkeypatch):
+    """The bench's bio KB (bio_full_kb at 20 M Member links): Q1-Q4 against
+    closed forms; the reference's QUERY_2 / QUERY_3 (Q5 / Q6) as one native
+    plan call and through the per-operator path (same counts)."""
+    import bench
+    db, arrays, B = bio20m
+    specs = dict(bench.bio_specs(np.arange(B["n_genes"])))
+    want = _bio_want(arrays, B, 0)
     for name, spec in specs.items():
         assert _count(db, spec) == want[name], name
     # QUERY_2 / QUERY_3 through the per-operator fold as well (same answers)
     monkeypatch.setenv("DAS_PLAN", "0")
     for name in ("Q5 same_or_inherited_biological_process (QUERY_2)", "Q6 linked_reactome_uniprot (QUERY_3)"):
         assert _count(db, specs[name]) == want[name], name
+
+
+def test_gpu_bio_fullsize_batched_step(bio20m):
+    """bench.py's bio step exactly as timed: Q1-Q6 in ONE pm.matched_many
+    call (das_plan_execute_many, default DAS_PLAN_NEST / DAS_DEFER /
+    DAS_CHAIN_SIDE: plans nested in Q2's and Q6's long read-back waits on
+    the plan side stream), over three gene anchors, then all three anchors'
+    queries in one batch -- (count, checksum) per query against the closed
+    forms (pattern_matcher.py:41-51, 705-748)."""
+    import bench
+    db, arrays, B = bio20m
+    every, wants = [], []
+    for anchor in (1, 2, 3):
+        named = bench.bio_specs(np.arange(B["n_genes"]), anchor=anchor)
+        want = _bio_want(arrays, B, anchor)
+        got = _count_many(db, [q for _, q in named])
+        for (name, _), g in zip(named, got):
+            assert g == want[name], (anchor, name, g, want[name])
+        every += [q for _, q in named]
+        wants += [want[name] for name, _ in named]
+    assert _count_many(db, every) == wants
 
 
 def _query23_counts(arrays, n_genes, n_bps, base, ga, gb, m, inh, n_up=5000, n_r=1000, n_loc=40, D=None):
@@ -219,6 +277,12 @@ def test_gpu_hub_fullsize_counts(kb1g):
     del pairs, src, dst, s1, s23, in1, keep4
     for name, spec in bench.hub_specs():
         assert _count(db, spec) == want[name], name
+    # bench.py's hub step as timed: H4 and H2 in ONE das_plan_execute_many
+    # batch -- H2 nested in H4's filtered-walk read-back wait at 10^9 links
+    # (plan side stream, second read-back slot), three times
+    named = bench.hub_specs()
+    for rep in range(3):
+        assert _count_many(db, [q for _, q in named]) == [want[name] for name, _ in named], rep
 
 
 def _dev_leaf_d64(db, arrays):
@@ -395,8 +459,24 @@ def test_gpu_flybase_fullsize_counts():
     db.load_arrays(arrays)
     db.prefetch()                        # anchors resolved through the host node directory (bench.py's path)
     assert db._node_dir is not None and len(db._node_dir) > 600_000          # every node (genes, FB ids, values)
+    every, wants = [], []
     for gene in (7, 7 + 7919):
         do_terms = synthetic.flybase_do_terms(arrays, gene=gene)
         want = _flybase_counts(arrays, gene, do_terms)
-        for name, spec in bench.flybase_specs(gene, do_terms):
+        named = bench.flybase_specs(gene, do_terms)
+        for name, spec in named:
             assert _count(db, spec) == want[name], (gene, name)
+        # bench.py's step as timed: the five queries in one
+        # das_plan_execute_many batch (grid chains on side streams launched in
+        # the other plans' read-back waits, F9's union deferred)
+        assert _count_many(db, [q for _, q in named]) == [want[name] for name, _ in named], gene
+        every += [q for _, q in named]
+        wants += [want[name] for name, _ in named]
+    assert _count_many(db, every) == wants
+    # fresh anchors straight into a batch (no one-by-one run before it: the
+    # anchors' key ranges and shapes first seen inside the batch)
+    for gene in (7 + 2 * 7919, 7 + 3 * 7919):
+        do_terms = synthetic.flybase_do_terms(arrays, gene=gene)
+        named = bench.flybase_specs(gene, do_terms)
+        want = _flybase_counts(arrays, gene, do_terms)
+        assert _count_many(db, [q for _, q in named]) == [want[name] for name, _ in named], gene

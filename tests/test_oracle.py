@@ -200,3 +200,8 @@ def test_oracle_hash_join_equals_nested_loop(monkeypatch):
         slow = [O.evaluate(q, odb) for q in qs]
         assert fast == slow
         assert any(r.get("n") for r in slow)
+        # the nested loop with per-row mappings (bench.py's cpu_baseline)
+        # against join() per pair
+        monkeypatch.setattr(O, "_ordered_nested_join", lambda acc, rows: None)
+        assert [O.evaluate(q, odb) for q in qs] == slow
+        monkeypatch.undo()

@@ -24,10 +24,11 @@ from oracle import das_oracle as O  # noqa: E402
 from tests.golden import make_synthetic as MS  # noqa: E402
 
 
-def main():
-    out = {"what": "oracle matched() time / reference matched() time, same KB and queries, one core each, "
-                   "build container (nproc = %d)" % os.cpu_count(), "fixtures": {}}
-    tot_o = tot_r = 0.0
+def _ratios(fast):
+    """Per fixture: the oracle's matched() time (And fold joined as the
+    reference's nested loop, or by hash when `fast`) over the reference's."""
+    O.FAST_JOIN = fast
+    out, tot_o, tot_r = {}, 0.0, 0.0
     for name in ("bio_full", "flybase", "powerlaw", "hub"):
         with open(os.path.join(ROOT, "tests", "golden", f"kb_{name}.json")) as f:
             d = json.load(f)
@@ -45,11 +46,19 @@ def main():
             O.CONFIG["no_overload"] = False
             t_r += q["ref_seconds"]
             n += q.get("n", 0)
-        out["fixtures"][name] = {"queries": len(d["queries"]), "bindings": n, "oracle_s": round(t_o, 4),
-                                 "reference_s": round(t_r, 4), "ratio": round(t_o / t_r, 4)}
+        out[name] = {"queries": len(d["queries"]), "bindings": n, "oracle_s": round(t_o, 4),
+                     "reference_s": round(t_r, 4), "ratio": round(t_o / t_r, 4)}
         tot_o += t_o
         tot_r += t_r
-    out["ratio_all"] = round(tot_o / tot_r, 4)
+    return {"fixtures": out, "ratio_all": round(tot_o / tot_r, 4)}
+
+
+def main():
+    out = {"what": "oracle matched() time / reference matched() time, same KB and queries, one core each, "
+                   "build container (nproc = %d); nested: the oracle's And fold as the reference's nested loop "
+                   "(FAST_JOIN=False, what bench.py's cpu_baseline runs), hash: joined by hash on the shared "
+                   "variables (FAST_JOIN=True, bench.py's cpu_fast)" % os.cpu_count(),
+           "joins": {"nested": _ratios(False), "hash": _ratios(True)}}
     path = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
