@@ -1091,6 +1091,14 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
                 db.ctx.prof_tag(None)
         return out
 
+    # the KB's host arrays, query objects and caches are long-lived: moved to
+    # the collector's permanent generation, a full collection during the
+    # timed steps walks only what a step allocates (a multi-ms pause there
+    # added up to ~0.3 ms per bio step; DAS_BENCH_GC_FREEZE=0 off)
+    import gc
+    if os.environ.get("DAS_BENCH_GC_FREEZE") != "0":
+        gc.collect()
+        gc.freeze()
     log("warmup")
     # the warmup steps record every kernel scope (the "kernels" table); the
     # timed steps record events only around the dominant kernel, whose
@@ -1150,6 +1158,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     db.ctx.prof_only("|".join(k for k in ((dominant or {}).get("kernel"), join_k) if k) or None)
     tag_q2[0] = join_k is not None
     db.ctx.prof_enable(True)
+    db.ctx.prof_mark(1)                  # kernel-trace bracket of the timed steps (tools/step_split.py)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1163,6 +1172,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    db.ctx.prof_mark(2)
     bindings = sum(sum(c) for c in step_counts)
     coll_per_step = (engine.sdb.plan_stats["collectives"] - coll0) / args.steps if engine else 0
     db.ctx.prof_enable(False)
@@ -1302,6 +1312,7 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             out["join_probe_variants"] = variants
         if and_join:
             out["and_join_q2_in_step"] = and_join
+    gc.unfreeze()
     del engine, qsets, db
     return out
 
@@ -1505,7 +1516,21 @@ def main():
             r["leg_wall_s"] = round(time.perf_counter() - t_leg, 1)
             extra[w] = r
         _free_device()
+    # the card's 16-byte nontemporal store ceiling (k_cartesian's pattern),
+    # measured after the legs: write-bound fractions move with the card
+    box = None
+    try:
+        from das_amd.database.hip_db import HipDB
+        probe = HipDB(device=local_rank)
+        gbps = probe.ctx.box_store_bw(4 << 30, 5)
+        box = {"store16_nt_GBps": round(gbps, 1), "store16_nt_frac": round(gbps / HBM_PEAK_GBS, 4),
+               "how": "das_box_store_bw: 4 GiB as six columns of nontemporal dwordx4 stores, 5 launches"}
+        del probe
+    except Exception as e:                  # the line is still written
+        box = {"error": f"{type(e).__name__}: {e}"[:200]}
     if rank == 0:
+        if line is not None:
+            line["box"] = box
         if extra:
             line["workloads"] = extra
             line["headline_wall_s"] = round(time.perf_counter() - t_head, 1)

@@ -153,6 +153,8 @@ _SIGS = {
     "das_prof_only": (C.c_int, [P, C.c_char_p]),
     "das_prof_tag": (C.c_int, [P, C.c_char_p]),
     "das_prof_tag_plan": (C.c_int, [P, C.c_uint32, C.c_char_p]),
+    "das_box_store_bw": (C.c_int, [P, C.c_uint64, C.c_uint32, P]),
+    "das_prof_mark": (C.c_int, [P, C.c_uint32]),
     "das_prof_reset": (C.c_int, [P]),
     "das_prof_read": (C.c_int, [P, C.c_char_p, P, P, P]),
     "das_prof_names": (C.c_int, [P, P, C.c_uint64]),
@@ -764,6 +766,16 @@ class Context:
     def prof_tag(self, tag=None):
         """Name the scopes recorded from now on "<scope>@<tag>" (None: untagged)."""
         check(lib().das_prof_tag(self.h, tag.encode() if tag else None), self.h)
+
+    def box_store_bw(self, nbytes=4 << 30, reps=5):
+        """GB/s of the card's 16-byte nontemporal stores (das_box_store_bw)."""
+        g = C.c_double()
+        check(lib().das_box_store_bw(self.h, int(nbytes), int(reps), C.byref(g)), self.h)
+        return g.value
+
+    def prof_mark(self, mark_id):
+        """A k_prof_mark launch on the context stream (kernel-trace bracket)."""
+        check(lib().das_prof_mark(self.h, int(mark_id)), self.h)
 
     def prof_tag_plan(self, plan=None, tag=None):
         """Tag the launches of plan `plan` of each following plan_execute_many

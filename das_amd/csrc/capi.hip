@@ -682,6 +682,17 @@ int das_table_checksum(das_ctx_t* ctx, const das_table_t* t, const uint64_t* sal
   });
 }
 
+int das_box_store_bw(das_ctx_t* ctx, uint64_t bytes, uint32_t reps, double* gbps) {
+  return guarded(ctx, [&] {
+    DAS_CHECK(gbps, das::DAS_E_INVALID, "null argument");
+    *gbps = das::box_store_bw(ctx->c, bytes, reps);
+  });
+}
+
+int das_prof_mark(das_ctx_t* ctx, uint32_t id) {
+  return guarded(ctx, [&] { das::prof_mark(ctx->c, id); });
+}
+
 int das_table_get_bounds(const das_table_t* t, uint32_t* lo, uint32_t* hi) {
   if (!t || !lo || !hi) return fail(nullptr, DAS_ERR_INVALID, "null argument");
   for (int c = 0; c < t->t.ncols; ++c) {

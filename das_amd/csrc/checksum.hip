@@ -91,4 +91,48 @@ void table_checksum(Ctx& c, const Table& t, const uint64_t* salt, uint64_t out[2
   out[1] = h[1];
 }
 
+// ---- measurement: the box's 16-byte nontemporal store ceiling and trace marks
+// (bench.py records them next to every run: the write-bound kernels'
+// fractions move with the card, k_cartesian 0.73-0.87 over the same binary)
+namespace {
+// n4 uint4 per column over `ncol` columns, as k_cartesian writes them: one
+// nontemporal dwordx4 store per lane, grid-stride
+typedef uint32_t st_v4u __attribute__((ext_vector_type(4)));
+__global__ void k_store16_nt(st_v4u* out, uint64_t n4, uint64_t cap4, int ncol) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+    for (int c = 0; c < ncol; ++c)
+      __builtin_nontemporal_store(st_v4u{(uint32_t)i, (uint32_t)i + 1, (uint32_t)i + 2, (uint32_t)c}, &out[c * cap4 + i]);
+}
+__global__ void k_prof_mark(uint32_t* p, uint32_t id) {
+  if (threadIdx.x == 0) p[0] = id;
+}
+}  // namespace
+
+double box_store_bw(Ctx& c, uint64_t bytes, uint32_t reps) {
+  DAS_CHECK(bytes >= (1u << 20) && reps >= 1, DAS_E_INVALID, "store probe: bytes >= 1 MiB, reps >= 1");
+  const int ncol = 6;
+  const uint64_t cap4 = (bytes / 16 / ncol + 63) & ~63ull;
+  DBuf<st_v4u> buf(cap4 * ncol, c.s);
+  const unsigned g = grid_for(cap4, 256, 8192);
+  hipEvent_t a = c.take_event(), b = c.take_event();
+  hipLaunchKernelGGL(k_store16_nt, dim3(g), dim3(256), 0, c.s, buf.p, cap4, cap4, ncol);   // warm
+  DAS_HIP(hipEventRecord(a, c.s));
+  for (uint32_t r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(k_store16_nt, dim3(g), dim3(256), 0, c.s, buf.p, cap4, cap4, ncol);
+  DAS_HIP(hipGetLastError());
+  DAS_HIP(hipEventRecord(b, c.s));
+  DAS_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  DAS_HIP(hipEventElapsedTime(&ms, a, b));
+  c.ev_pool.push_back(a);
+  c.ev_pool.push_back(b);
+  return 16.0 * cap4 * ncol * reps / (ms * 1e-3) / 1e9;
+}
+
+void prof_mark(Ctx& c, uint32_t id) {
+  DBuf<uint32_t> m(1, c.s);
+  hipLaunchKernelGGL(k_prof_mark, dim3(1), dim3(64), 0, c.s, m.p, id);
+  DAS_HIP(hipGetLastError());
+}
+
 }  // namespace das

@@ -391,6 +391,8 @@ void export_rows(Ctx& c, const Table& t, uint32_t* dst);
 // over rows of the product over columns of g(salt[c], digest), out[1] = values
 // that are not atom ids.
 void table_checksum(Ctx& c, const Table& t, const uint64_t* salt, uint64_t out[2]);
+double box_store_bw(Ctx& c, uint64_t bytes, uint32_t reps);
+void prof_mark(Ctx& c, uint32_t id);
 std::unique_ptr<Table> import_rows(Ctx& c, int kind, int ncols, const int32_t* vars, const int32_t* member,
                                    const uint32_t* src, uint64_t n);
 

@@ -88,18 +88,64 @@ def _has_composite(tables):
     return any(t.kind == _lib.TABLE_COMPOSITE for t in tables)
 
 
+def _reference_pattern_keys(type_hash, elements):
+    """The `keys` list of canonical_parser.py:145-175 for one link, as
+    (type hash or '*', element or '*', ...) tuples: [*, e...] for every
+    arity, every mask with >= 1 wildcard for arities 1-3."""
+    keys = [(WILDCARD, *elements)]
+    a = len(elements)
+    if 1 <= a <= 3:
+        for mask in range(1, 1 << (a + 1)):
+            keys.append(tuple([WILDCARD if mask & 1 else type_hash] +
+                              [WILDCARD if mask >> (i + 1) & 1 else e for i, e in enumerate(elements)]))
+    return keys
+
+
+def _stale_entries(order, black_list):
+    """The reference's stale pattern entries (canonical_parser.py:144-178):
+    walking `order` (loader.canonical_pattern_order), a blacklisted link is
+    written under the keys of the last link that was not -- {key: {handle:
+    targets}} -- and one before any such link raises UnboundLocalError, as
+    the reference's load does."""
+    stale, keys = {}, None
+    for h, t, elements in order:
+        if t not in black_list:
+            keys = _reference_pattern_keys(ExpressionHasher.named_type_hash(t), elements)
+            continue
+        if keys is None:
+            raise UnboundLocalError("local variable 'keys' referenced before assignment")
+        for k in keys:
+            stale.setdefault(k, {})[h] = tuple(elements)
+    return stale
+
+
 class HipDB(RelationalDB):
 
     PREFETCH_MAX_ATOMS = 1 << 26            # host mirrors of prefetch() up to this many atoms
     HEX_DIRECT = 4096                       # hex_of: larger id arrays skip the per-id cache
     SEED_MAX = 1 << 16                      # _pairs: answers up to this size seed the handle cache
 
-    def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False):
+    def __init__(self, device: int = 0, stream=None, tuple_targets: bool = False,
+                 stale_pattern_keys: bool = False):
         """`tuple_targets=True` reproduces the reference DB path exactly,
         including returning targets as tuples from get_matched_links, which
         makes `Link._assign_variables` raise AttributeError for unordered links
         with a grounded target.  The default returns lists (the
-        semantics StubDB and service/README.md:356-363 show)."""
+        semantics StubDB and service/README.md:356-363 show).
+
+        `stale_pattern_keys=True` reproduces what the reference's canonical
+        loader does with a non-empty `pattern_black_list`
+        (canonical_parser.py:144-180): its pattern-key loop never resets
+        `keys` for a blacklisted link, so that link is written under the
+        PREVIOUS link's pattern keys in load order (links_1, links_2, links_n
+        collections, first occurrence in parse order), and a blacklisted first
+        link raises UnboundLocalError.  load_canonical then records those
+        stale entries and every pattern-key answer includes them (a Link
+        query hitting one binds the stale link's own targets, and raises
+        AssertionError when their count differs: _assign_variables :467).
+        Default: the intended semantics -- a blacklisted type's links get no
+        pattern keys at all.  (The MettaYacc loader walks a Python set
+        there, parser_threads.py:185-219: no order to reproduce.)"""
         if stream is None:
             try:
                 import torch
@@ -124,6 +170,8 @@ class HipDB(RelationalDB):
         self._outgoing = None
         self._node_dir = None
         self.pattern_black_list = []
+        self.stale_pattern_keys = stale_pattern_keys
+        self._stale = None              # stale_pattern_keys: pattern key -> {link handle: targets}
 
     def __repr__(self):
         return "<HipDB>"
@@ -150,13 +198,113 @@ class HipDB(RelationalDB):
         self._hstore = None
         self._outgoing = None
         self._node_dir = None
+        self._stale = None
 
     def load_metta(self, texts):
         self.load_arrays(_loader.parse_metta(texts).finish())
 
     def load_canonical(self, texts):
-        """Canonical MeTTa through the native reader (das_parse_canonical)."""
+        """Canonical MeTTa through the native reader (das_parse_canonical).
+        With stale_pattern_keys and a non-empty pattern_black_list, the
+        reference loader's stale pattern entries are recorded (see __init__)."""
+        stale = self.stale_from_canonical(texts)
         self.load_arrays(_lib.parse_canonical(texts))
+        self._stale = stale
+
+    def stale_from_canonical(self, texts):
+        """stale_pattern_keys with a non-empty pattern_black_list: the stale
+        entries the reference's loader would write for this canonical text
+        (raises UnboundLocalError where its load does); else None."""
+        if not (self.stale_pattern_keys and self.pattern_black_list):
+            return None
+        return _stale_entries(_loader.canonical_pattern_order(texts), set(self.pattern_black_list)) or None
+
+    # ----------------------------------------- stale_pattern_keys (compat)
+    def stale_values(self, link_type, target_handles):
+        """{link handle: targets} the reference's loader wrote under this
+        pattern key for blacklisted links (stale_pattern_keys), or None."""
+        if not self._stale:
+            return None
+        th = WILDCARD if link_type == WILDCARD else ExpressionHasher.named_type_hash(link_type)
+        hs = sorted(target_handles) if link_type in UNORDERED_LINK_TYPES else list(target_handles)
+        return self._stale.get((th, *hs))
+
+    def _stale_union(self, rel, link_type, handles, var_ids, ordered, no_overload, extra):
+        """match_link's answer with the stale entries of its key added, each
+        through Link._assign_variables (pattern_matcher.py:466-489) as the
+        reference evaluates every value of the key."""
+        arity = len(handles)
+        for tg in extra.values():
+            if len(tg) != arity:
+                raise AssertionError(f"link_targets = {list(tg)} self.targets = {handles}")
+        grounded = [h for h, v in zip(handles, var_ids) if v is None]
+        if not ordered and grounded and self.tuple_targets:
+            raise AttributeError("'tuple' object has no attribute 'remove'")
+        rows = []
+        for tg in extra.values():
+            if ordered:
+                m, vals, ok = {}, set(), True
+                for v, h in zip(var_ids, tg):
+                    if v is None:
+                        continue
+                    if v in m:
+                        ok = m[v] == h
+                    elif no_overload and h in vals:
+                        ok = False
+                    else:
+                        m[v] = h
+                        vals.add(h)
+                    if not ok:
+                        break
+                if ok:
+                    rows.append(m)
+            else:
+                left = list(tg)
+                for h in grounded:
+                    left.remove(h)                      # ValueError when absent, as list.remove
+                names = [v for v in var_ids if v is not None]
+                assert len(names) == len(left)
+                if len(set(names)) == len(names) and len(set(left)) == len(left):
+                    rows.append((names, left))           # UnorderedAssignment.freeze: counts agree
+        if not rows:
+            return rel
+        old = [t for t in rel.tables if t.nrows]
+        if ordered:
+            vars_ = list(old[0].vars) if old else list(dict.fromkeys(v for v in var_ids if v is not None))
+            ids = {h: i for h, i in zip(*self._ids_for([h for r in rows for h in r.values()]))}
+            cols = [[ids[r[v]] for r in rows] for v in vars_]
+            kind = _lib.TABLE_ORDERED
+        else:
+            vars_ = list(old[0].vars) if old else sorted(set(rows[0][0]))
+            ids = {h: i for h, i in zip(*self._ids_for([h for _, left in rows for h in left]))}
+            vals = [sorted(ids[h] for h in left) for _, left in rows]
+            cols = [list(c) for c in zip(*vals)]
+            kind = _lib.TABLE_UNORDERED
+        t = self.ctx.table_from_host(kind, vars_, np.array(cols, dtype=np.uint32).reshape(len(vars_), len(rows)))
+        merged = self.ctx.concat(old + [t]) if old else t
+        return Relation([self.ctx.dedup(merged)])
+
+    def _ids_for(self, handles):
+        hs = list(dict.fromkeys(handles))
+        return hs, self.ids_of(hs).tolist()
+
+    def touches_stale(self, expr) -> bool:
+        """Whether evaluating `expr` reads a pattern key that holds stale
+        entries (the plan executor then steps aside: the per-operator path
+        adds them at each Link)."""
+        if not self._stale:
+            return False
+        k = getattr(expr, '_k', None)
+        if k in ('a', 'o'):
+            return any(self.touches_stale(t) for t in expr.terms)
+        if k == 'x':
+            return self.touches_stale(expr.term)
+        if k == 'l':
+            if any(self.touches_stale(t) for t in expr.targets):
+                return True
+            hs = [t.get_handle(self) for t in expr.targets]
+            return None not in hs and WILDCARD in hs and self.stale_values(expr.atom_type, hs) is not None
+        return False
 
     def clear(self):
         b = _loader.AtomBuilder()
@@ -344,7 +492,11 @@ class HipDB(RelationalDB):
             h = self.get_link_handle(link_type, target_handles)
             return [h] if self._exists(h, len(target_handles)) else []
         t = self.matched_links_table(link_type, target_handles)
-        return self._pairs(t, len(target_handles)) if t is not None else []
+        out = self._pairs(t, len(target_handles)) if t is not None else []
+        extra = self.stale_values(link_type, target_handles)
+        if extra:
+            out = list(out) + [(h, tuple(tg) if self.tuple_targets else list(tg)) for h, tg in extra.items()]
+        return out
 
     # the (link, t0 .. t_{a-1}) id rows behind get_matched_links /
     # get_matched_type_template / get_matched_type, before formatting (a
@@ -439,6 +591,8 @@ class HipDB(RelationalDB):
         259-284), e.g. SimplePatternMiner's len(get_links(...)) counts."""
         if link_type != WILDCARD and WILDCARD not in target_handles:
             return self.get_matched_links(link_type, target_handles)
+        if self._stale and self.stale_values(link_type, target_handles):
+            return [h for h, _ in self.get_matched_links(link_type, target_handles)]
         t = self.matched_links_table(link_type, target_handles)
         if t is None or t.nrows == 0:
             return []
@@ -620,13 +774,17 @@ class HipDB(RelationalDB):
         order_var: the variable the caller will join on -- a typed scan then
         returns its rows sorted by it (same answer, join-friendly order)."""
         spec = self.link_scan_spec(link_type, handles, var_ids, ordered, no_overload, order_var)
-        if spec is None:
-            return Relation()
-        args, dedup = spec
-        t = self.ctx.scan_link(*args)
-        if dedup:
-            t = self.ctx.dedup(t)
-        return Relation([t])
+        rel = Relation()
+        if spec is not None:
+            args, dedup = spec
+            t = self.ctx.scan_link(*args)
+            if dedup:
+                t = self.ctx.dedup(t)
+            rel = Relation([t])
+        extra = self.stale_values(link_type, handles)
+        if extra:
+            rel = self._stale_union(rel, link_type, handles, var_ids, ordered, no_overload, extra)
+        return rel
 
     def link_scan_spec(self, link_type, handles, var_ids, ordered, no_overload=False, order_var=None):
         """(scan_link arguments, dedup) of match_link; None when the scan

@@ -42,7 +42,10 @@ class DistributedAtomSpace:
         device = int(kwargs.get("device", os.environ.get("DAS_DEVICE", 0)))
         # db: an existing DBInterface (a HipDB, or a parallel.ShardedDB over
         # one process per GPU); default: a HipDB on `device`
-        self.db = kwargs.get("db") or HipDB(device=device, tuple_targets=kwargs.get("tuple_targets", False))
+        # stale_pattern_keys: the reference canonical loader's pattern keys
+        # under a non-empty pattern_black_list, bug for bug (HipDB)
+        self.db = kwargs.get("db") or HipDB(device=device, tuple_targets=kwargs.get("tuple_targets", False),
+                                            stale_pattern_keys=kwargs.get("stale_pattern_keys", False))
         self.pattern_black_list = []
         self._metta_sources = []
         self._canonical_sources = []
@@ -71,11 +74,16 @@ class DistributedAtomSpace:
         # the loaders honour pattern_black_list (distributed_atom_space.py:346, 409)
         self.db.pattern_black_list = list(self.pattern_black_list)
         parts = []
+        stale = None
         if self._canonical_sources:
+            if not self._metta_sources and hasattr(self.db, "stale_from_canonical"):
+                stale = self.db.stale_from_canonical(self._canonical_sources)
             parts.append(_lib.parse_canonical(self._canonical_sources))
         if self._metta_sources or not parts:
             parts.append(_loader.parse_metta(self._metta_sources).finish())
         self.db.load_arrays(_loader.concat_arrays(parts))
+        if stale:
+            self.db._stale = stale
 
     def load_knowledge_base(self, source):
         """distributed_atom_space.py:336-363 (general MeTTa)."""

@@ -382,6 +382,59 @@ def parse_canonical(texts, builder=None):
     return b
 
 
+class _OrderRecorder:
+    """AtomBuilder stand-in for _canonical_expression: handles instead of
+    refs, and every link in the order CanonicalParser._add_expression sees
+    it (post-order: a nested link before the link holding it)."""
+
+    def __init__(self):
+        from .expression_hasher import ExpressionHasher
+        self.eh = ExpressionHasher
+        self.links = []
+
+    def terminal(self, stype, name, node=False):
+        return self.eh.terminal_hash(stype, name)
+
+    def expr(self, type_name, kids):
+        h = self.eh.expression_hash(self.eh.named_type_hash(type_name), kids)
+        self.links.append((h, type_name, list(kids)))
+        return h
+
+
+def canonical_pattern_order(texts):
+    """The links of canonical MeTTa text in the order the reference's
+    pattern-key loop walks them (canonical_parser.py:132-183): collection
+    links_1, then links_2, then links_n (_populate_mongo_links :185-206),
+    each in insertion order -- the first occurrence of each handle in parse
+    order (_add_expression :77-93 is called as an expression closes,
+    _mongo_insert_many :95-110 drops repeats).  [(handle, named_type,
+    [element handles])]."""
+    if isinstance(texts, str):
+        texts = [texts]
+    rec = _OrderRecorder()
+    for text in texts:
+        state = 0
+        for raw in _LINE_BREAK.split(text):
+            line = raw.strip()
+            if not line:
+                continue
+            words = line.split()
+            if state == 0 and words[0] == "(:" and not words[1].startswith('"'):
+                continue
+            if words[0] == "(:":
+                state = 1
+                continue
+            state = 2
+            _canonical_expression(line, rec)
+    seen, by_arity = set(), ([], [], [])
+    for h, t, kids in rec.links:
+        if h in seen:
+            continue
+        seen.add(h)
+        by_arity[0 if len(kids) == 1 else 1 if len(kids) == 2 else 2].append((h, t, kids))
+    return by_arity[0] + by_arity[1] + by_arity[2]
+
+
 def _nesting_levels(p):
     """1 + the deepest expression child, per expression (groups are children-first)."""
     lev = np.zeros(p.n_expr, dtype=np.int64)

@@ -640,6 +640,8 @@ def _try_plan(expr, db, answer):
         # a sharded DB (das_amd.parallel.ShardedDB) plans across its GPUs
         sharded = getattr(db, "plan_sharded", None)
         return sharded(expr, answer) if sharded is not None else None
+    if db._stale and db.touches_stale(expr):
+        return None                             # stale_pattern_keys: the per-operator path adds them
     no_overload = bool(CONFIG['no_overload'])
     key = (db.generation, no_overload)          # generation: unique per load, any HipDB
     cached = getattr(expr, '_plan', None)
@@ -672,6 +674,8 @@ def matched_many(db, exprs, tag=None):
             # the operators whose matched() tries a whole-expression plan
             # first, with its prelude (And.matched / Or.matched / Not.matched)
             if type(e) not in (And, Or, Not) or (type(e) is not Not and not e.terms):
+                continue
+            if db._stale and db.touches_stale(e):
                 continue
             cached = getattr(e, '_plan', None)
             if cached is None or cached[0] != key:
@@ -976,6 +980,8 @@ class Link(Atom):
         None when the shape does not allow it (And.matched scans instead)."""
         if not self.ordered or CONFIG['no_overload'] or not hasattr(db, 'rel_index_join'):
             return None
+        if getattr(db, '_stale', None) and db.touches_stale(self):
+            return None                         # the scan adds the stale entries (HipDB.match_link)
         if not all(isinstance(t, Variable) or type(t) is Node for t in self.targets):
             return None
         if any(isinstance(t, TypedVariable) for t in self.targets):

@@ -426,6 +426,13 @@ int das_prof_tag(das_ctx_t* ctx, const char* tag);
  * clears it: one query tagged inside a batched step. */
 int das_prof_tag_plan(das_ctx_t* ctx, uint32_t plan, const char* tag);
 int das_prof_reset(das_ctx_t* ctx);
+/* The card's 16-byte nontemporal store ceiling: `bytes` written as six
+ * columns of dwordx4 stores (k_cartesian's pattern), `reps` timed launches
+ * after one warm one; GB/s out.  bench.py records it beside every run. */
+int das_box_store_bw(das_ctx_t* ctx, uint64_t bytes, uint32_t reps, double* gbps);
+/* One tiny kernel (k_prof_mark) on the context stream: brackets a region in a
+ * rocprofv3 kernel trace (tools/step_split.py). */
+int das_prof_mark(das_ctx_t* ctx, uint32_t id);
 int das_prof_read(das_ctx_t* ctx, const char* name, double* ms, uint64_t* launches, double* bytes);
 int das_prof_names(das_ctx_t* ctx, char* buf, uint64_t cap);
 

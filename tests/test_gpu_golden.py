@@ -119,6 +119,81 @@ def _has_ordered_templates_below_root(spec):
     return spec[0] in ("And", "Or") and bool(ts) and all(t[2] for t in ts)
 
 
+@pytest.mark.parametrize("plan", ["1", "0", "many"])
+def test_gpu_pattern_black_list_reference_mode(golden, plan, monkeypatch, tmp_path):
+    """HipDB(stale_pattern_keys=True): the reference canonical loader's own
+    pattern_black_list behaviour (canonical_parser.py:144-180, stale `keys`),
+    for EVERY canonical-loader case of kb_blacklist.json -- every query and
+    every index probe equals the reference's recorded answer (including the
+    queries the stale entries touch and their AssertionErrors), and a
+    blacklisted first link fails the load with UnboundLocalError.  plan: 1 =
+    one query at a time (plans where no stale key is touched), 0 = the
+    per-operator path, many = the queries in one pm.matched_many batch; then
+    the same through the facade (load_canonical_knowledge_base)."""
+    import os
+    from das_amd.database.hip_db import HipDB
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    from tests.util import record_many
+    monkeypatch.setenv("DAS_PLAN", "0" if plan == "0" else "1")
+    d = golden("kb_blacklist.json")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
+    checked = touched = probes = failed_loads = 0
+    for case in d["cases"]:
+        if case["loader"] != "canonical":
+            continue
+        if case["source"] == "inline":
+            text = d["canonical_text"]
+        else:
+            with open(os.path.join(here, os.path.basename(case["source"]))) as f:
+                text = f.read()
+        db = HipDB(device=0, tuple_targets=True, stale_pattern_keys=True)
+        db.pattern_black_list = list(case["black_list"])
+        if case.get("load_error"):
+            with pytest.raises(UnboundLocalError):
+                db.load_canonical(text)
+            failed_loads += 1
+            continue
+        db.load_canonical(text)
+        assert list(db.count_atoms()) == case["count_atoms"]
+        qs = [q["query"] for q in case["queries"]]
+        got = record_many(qs, db) if plan == "many" else [record(q, db) for q in qs]
+        for q, g in zip(case["queries"], got):
+            assert same(g, q), (case["black_list"], q["query"], g, {k: q.get(k) for k in ("n", "error")})
+            checked += 1
+        touched += sum(1 for q in qs if db.touches_stale(_build(q)))
+        for p in case.get("index") or []:
+            args = p["args"]
+            try:
+                if p["kind"] == "links":
+                    r = db.get_matched_links(*args)
+                elif p["kind"] == "template":
+                    r = db.get_matched_type_template(args)
+                else:
+                    r = db.get_matched_type(args)
+            except (ValueError, AssertionError, AttributeError, KeyError) as e:
+                assert p.get("error") == type(e).__name__, (case["black_list"], p)
+                continue
+            assert "error" not in p, (case["black_list"], p)
+            assert sorted(x if isinstance(x, str) else x[0] for x in r) == p["handles"], (case["black_list"], p)
+            probes += 1
+        # the facade: DistributedAtomSpace(stale_pattern_keys=True)
+        f = tmp_path / "kb.metta"
+        f.write_text(text)
+        das = DistributedAtomSpace(tuple_targets=True, stale_pattern_keys=True)
+        das.pattern_black_list = list(case["black_list"])
+        das.load_canonical_knowledge_base(str(f))
+        for p in case.get("index") or []:
+            if p["kind"] == "links" and "error" not in p:
+                assert sorted(das.db.get_matched_links(*p["args"]), key=str) == \
+                    sorted(db.get_matched_links(*p["args"]), key=str)
+    assert failed_loads >= 2 and checked >= 70 and touched > 0 and probes >= 60, (failed_loads, checked, touched, probes)
+
+
+def _build(spec):
+    from tests.util import build
+    return build(spec)
+
+
 @pytest.mark.parametrize("plan", ["1", "0"])
 def test_gpu_pattern_black_list(golden, plan, monkeypatch):
     """pattern_black_list (kb_blacklist.json, reference-run with non-empty

@@ -205,3 +205,46 @@ def test_oracle_hash_join_equals_nested_loop(monkeypatch):
         monkeypatch.setattr(O, "_ordered_nested_join", lambda acc, rows: None)
         assert [O.evaluate(q, odb) for q in qs] == slow
         monkeypatch.undo()
+
+
+def test_stale_pattern_keys_host_restatement_matches_fixture(golden):
+    """HipDB(stale_pattern_keys=True)'s host side, for every canonical-loader
+    case of kb_blacklist.json (reference-run): the reference's pattern-loop
+    order recomputed from the canonical text (loader.canonical_pattern_order:
+    links_1 / links_2 / links_n, first occurrence in parse order) equals the
+    order the fixture recorded, the stale entries it derives equal the
+    oracle's (pinned against the reference's answers above), and a
+    blacklisted first link raises UnboundLocalError as the reference's load."""
+    import os
+    from das_amd import loader
+    from das_amd.database import hip_db
+    d = golden("kb_blacklist.json")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
+    n = 0
+    for case in d["cases"]:
+        if case["loader"] != "canonical":
+            continue
+        if case["source"] == "inline":
+            text = d["canonical_text"]
+        else:
+            with open(os.path.join(here, os.path.basename(case["source"]))) as f:
+                text = f.read()
+        order = loader.canonical_pattern_order(text)
+        assert [h for h, _, _ in order] == case["pattern_order"]
+        bl = set(case["black_list"])
+        if case.get("load_error"):
+            with pytest.raises(UnboundLocalError):
+                hip_db._stale_entries(order, bl)
+            n += 1
+            continue
+        stale = hip_db._stale_entries(order, bl)
+        kb = O.KB.from_tables(case["nodes"], case["links"])
+        odb = O.RedisMongoSemantics(kb, case["black_list"], tuple_targets=True, stale_key_order=case["pattern_order"])
+        want = {}
+        for k, vals in odb.patterns.items():
+            for h, tg in vals:
+                if kb.links[h][0] in bl:
+                    want.setdefault(k, {})[h] = tuple(tg)
+        assert stale == want and stale
+        n += 1
+    assert n >= 4

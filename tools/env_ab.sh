@@ -8,6 +8,6 @@ for rep in 1 2; do
     tag=$(echo "$cfg" | tr '=,' '__')
     if [ "$cfg" = "base" ]; then envs=""; else envs=$(echo "$cfg" | tr ',' ' '); fi
     env $envs timeout -k 10 300 python bench.py --workload $W --steps 20 --warmup 5 --no-cpu-baseline --no-materialise --detail gpurun_out/env_${W}_${tag}_$rep.json > gpurun_out/env_${W}_${tag}_$rep.out 2> gpurun_out/env_${W}_${tag}_$rep.err
-    echo "$W $cfg rep $rep: $(tail -1 gpurun_out/env_${W}_${tag}_$rep.out | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], {k: v['us'] for k, v in (d.get('latency') or {}).items()})")"
+    echo "$W $cfg rep $rep: $(tail -1 gpurun_out/env_${W}_${tag}_$rep.out | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], 'matched', d.get('step_ms_matched'), 'q2', (d.get('and_join_q2') or {}).get('us'), 'cart', (d.get('roofline') or {}).get('avg_launch_us'))")"
   done
 done
