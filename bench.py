@@ -245,7 +245,7 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
     levels, halo = [], []
     for lv in range(halo_length):
         t0 = time.perf_counter()
-        new_nodes, level_links, n_queries, bounded = set(), set(), 0, False
+        new_nodes, level_links, n_queries, bounded, rows = set(), set(), 0, False, 0
         t_log = t0
         for k, h in enumerate(node_handles):
             if progress and time.perf_counter() - t_log > 30:
@@ -253,6 +253,7 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
                 progress(f"halo level {lv}: node {k} of {len(node_handles)}, {n_queries} queries")
             for tpl in _halo_templates(h):
                 found = sorted(set(api.get_links(None, None, tpl)))
+                rows += len(found)
                 n_queries += 1                                    # the notebook's count (:411-413):
                 for link in found:                                # get_links + one per link found
                     if link not in level_links and len(level_links) >= max_level_links:
@@ -263,7 +264,7 @@ def miner_walk(api, seeds, rng, link_rate=0.01, max_pattern_links=2000, halo_len
                     new_nodes.update(api.get_link_targets(link))
         bounded = bounded or len(new_nodes) > max_level_nodes
         halo.append({"s": time.perf_counter() - t0, "queries": n_queries, "links": len(level_links),
-                     "nodes": len(node_handles), "bounded": bounded})
+                     "nodes": len(node_handles), "bounded": bounded, "rows": rows})
         if progress:
             progress(f"halo level {lv}: {len(node_handles)} nodes, {n_queries} queries, {len(level_links)} links")
         levels.append(level_links)
@@ -627,14 +628,25 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
     # the timed region stalled 1.4-1.9 s in ~1 of 3 processes (DAS_ALLOC_TRACE,
     # profiles/r5_build_alloc_stall.txt); --build-warmup small: round 4's
     # 10^4-link warm-up
+    # (the warm-up build is also the cold one: its wall time, driver
+    # allocations included, is reported as cold_build_ms; the timed build then
+    # runs as any rebuild does -- its idle blocks returned at its end, after
+    # its last kernel -- with the warm-up's blocks to reuse)
     keep_env = os.environ.get("DAS_BUILD_KEEP_GB")
     full_warm = args.build_warmup == "full" and world == 1
+    t_cold = time.perf_counter()
     if full_warm:
         os.environ["DAS_BUILD_KEEP_GB"] = "100000"
         db.load_arrays(arrays)
     else:
         db.load_arrays(synthetic.powerlaw_kb(1000, 10000, link_types=4))
     torch.cuda.synchronize()
+    cold_ms = (time.perf_counter() - t_cold) * 1e3
+    if full_warm:
+        if keep_env is None:
+            os.environ.pop("DAS_BUILD_KEEP_GB", None)
+        else:
+            os.environ["DAS_BUILD_KEEP_GB"] = keep_env
     db.ctx.prof_reset()
     db.ctx.prof_enable(True)
     if dist:
@@ -658,11 +670,6 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
     db.load_arrays(arrays)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t1
-    if full_warm:
-        if keep_env is None:
-            os.environ.pop("DAS_BUILD_KEEP_GB", None)
-        else:
-            os.environ["DAS_BUILD_KEEP_GB"] = keep_env
     db.ctx.prof_enable(False)
     stats = db.ctx.prof_stats()
     # device time of the timed region: owner hashing + row grouping + the
@@ -708,7 +715,9 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
                "config": {"workload": "config4 bulk ExpressionHasher + IncomingSet CSR build", "links": args.links,
                           "nodes": args.nodes, "link_types": 4, "arity": "70% 2 / 30% 3",
                           "distinct_links_indexed": links,
-                          "warmup_build": "same input, device blocks kept" if full_warm else "10^4-link KB",
+                          "warmup_build": ("same input, its device blocks kept for the timed build (a rebuild: "
+                                           "no driver allocation; it returns its idle blocks at its end)")
+                          if full_warm else "10^4-link KB",
                           "parallelism": (f"links hash-partitioned by handle x{world}: generated in ranges, "
                                           "regrouped on their owners by RCCL all-to-all" if world > 1 else "1 GPU")},
                # the build's roofline is SURVEY.md §8d's: algorithmic bytes of
@@ -726,6 +735,7 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
                         "md5_blocks": blocks_leaf + blocks_expr, "terminal_ms": round(hl["ms"], 3),
                         "valu": md5_valu(hash_ks)},
                "kernels": kernels_of(stats), "wall_incl_upload_s": round(wall, 3), "host_generate_s": round(t_gen, 2),
+               "cold_build_ms": round(cold_ms, 1) if full_warm else None,
                "atoms": int(st.n_atoms), "device_bytes": int(st.device_bytes)}
     del db, arrays
     return out
@@ -867,7 +877,14 @@ def _miner_totals(runs):
     pc = sum(r["pattern"]["get_links"] for r in runs)
     ps = sum(r["pattern"]["s"] for r in runs)
     pl = sum(r["pattern"]["links"] for r in runs)
+    hr = sum(h.get("rows", 0) for r in runs for h in r["halo"])
+    hg = sum(h["nodes"] * 5 for r in runs for h in r["halo"])         # get_links calls (5 templates per node)
+    pm_ = sum(r["pattern"]["matched"] for r in runs)
     return {"halo_queries": hq, "halo_s": hs, "halo_ms_per_query": 1e3 * hs / max(hq, 1),
+            # per returned row: answers differ in size between the GPU KB and the
+            # CPU's 1/300 sample (a hub's pattern key holds ~10^5 rows at full size)
+            "halo_rows_per_get_links": hr / max(hg, 1), "halo_us_per_row": 1e6 * hs / max(hr, 1),
+            "pattern_rows_per_get_links": pm_ / max(pc, 1), "pattern_us_per_row": 1e6 * ps / max(pm_, 1),
             "level_ms_per_query": [round(1e3 * sum(r["halo"][k]["s"] for r in runs) /
                                          max(sum(r["halo"][k]["queries"] for r in runs), 1), 5)
                                    for k in range(len(runs[0]["halo"]))] if runs else [],
@@ -947,10 +964,24 @@ def run_getlinks(args, rank, world, local_rank):
                          f"flybase_kb({g} genes, {args.fb_schema} schemas, {r} rows) = 1/{scale} of the GPU KB, "
                          f"{len(cruns)} seeds, one process",
                "halo_ms_per_query": round(ct["halo_ms_per_query"], 5),
-               "pattern_ms_per_get_links": round(ct["pattern_ms_per_get_links"], 5)}
+               "pattern_ms_per_get_links": round(ct["pattern_ms_per_get_links"], 5),
+               "rows": {k: round(ct[k], 4) for k in ("halo_rows_per_get_links", "halo_us_per_row",
+                                                     "pattern_rows_per_get_links", "pattern_us_per_row")}}
+    if cpu is not None:
+        # the two sides answer different KB sizes: rows per get_links and
+        # microseconds per returned row, side by side
+        cpu["rows_per_get_links"] = {"cpu_halo": round(ct["halo_rows_per_get_links"], 2),
+                                     "gpu_halo": round(tot["halo_rows_per_get_links"], 2),
+                                     "cpu_pattern": round(ct["pattern_rows_per_get_links"], 1),
+                                     "gpu_pattern": round(tot["pattern_rows_per_get_links"], 1)}
+        cpu["us_per_row"] = {"cpu_halo": round(ct["halo_us_per_row"], 4), "gpu_halo": round(tot["halo_us_per_row"], 4),
+                             "cpu_pattern": round(ct["pattern_us_per_row"], 4),
+                             "gpu_pattern": round(tot["pattern_us_per_row"], 4)}
     lat = {"halo_ms_per_query": round(tot["halo_ms_per_query"], 5), "level_ms_per_query": tot["level_ms_per_query"],
            "pattern_ms_per_get_links": round(tot["pattern_ms_per_get_links"], 5),
            "pattern_ms_per_notebook_query": round(tot["pattern_ms_per_notebook_query"], 5),
+           "rows": {k: round(tot[k], 4) for k in ("halo_rows_per_get_links", "halo_us_per_row",
+                                                  "pattern_rows_per_get_links", "pattern_us_per_row")},
            "published_ms_per_query": {"halo_level1": 2.289, "halo_level2": [0.097, 0.131],
                                       "pattern_count": [74, 104]}}
     out = {"metric": "DBInterface lookups/s (SimplePatternMiner halo walk: get_links + get_link_targets)",
@@ -1345,7 +1376,8 @@ def _compact_cpu(c, full=True):
     if not c:
         return None
     if not full:
-        return {k: _r(c.get(k), 1) for k in ("value", "join") if k in c}
+        return {k: (_r(c.get(k), 1) if k == "value" else c.get(k))
+                for k in ("value", "join", "rows_per_get_links", "us_per_row") if k in c}
     out = {k: _r(c.get(k), 1) for k in ("value", "unit", "cores", "kind", "join") if k in c}
     out["sample"] = (c.get("sample") or "")[:240]
     return out
@@ -1361,7 +1393,7 @@ def _compact_leg(d):
     out["cpu_baseline"] = _compact_cpu(d.get("cpu_baseline"), full=False)
     if d.get("cpu_fast"):
         out["cpu_fast"] = _compact_cpu(d.get("cpu_fast"), full=False)
-    for k in ("step_ms_matched", "latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
+    for k in ("step_ms_matched", "cold_build_ms", "latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
         if d.get(k) is not None:
             out[k] = d[k]
     return out

@@ -144,6 +144,7 @@ _SIGS = {
     "das_plan_execute": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32,
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "das_plan_execute_many": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P, P]),
+    "das_plan_execute_info": (C.c_int, [P, P, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P, P, P]),
     "das_plan_execute_sharded": (C.c_int, [P, C.POINTER(das_plan_node_t), C.c_uint32, C.c_uint32, P, C.c_uint32, P,
                                            C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
                                            C.POINTER(C.c_int32), P, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -544,18 +545,21 @@ class Context:
     def plan_execute(self, words, n_nodes, no_overload=False):
         """das_plan_execute over n_nodes das_plan_node_t records given as a
         u32 array (51 words each) -> (matched, negation, [Table])."""
-        cap = 64
-        nodes = C.cast(words.ctypes.data, C.POINTER(das_plan_node_t))
+        cap = 16
+        nodes = words.__array_interface__["data"][0]
         while True:
             out = (P * cap)()
             n_out, matched, neg = C.c_uint32(), C.c_int32(), C.c_int32()
-            rc = lib().das_plan_execute(self.h, nodes, n_nodes, 1 if no_overload else 0, out, cap, C.byref(n_out),
-                                        C.byref(matched), C.byref(neg))
+            info = (C.c_int64 * (20 * cap))()
+            rc = lib().das_plan_execute_info(self.h, nodes, n_nodes, 1 if no_overload else 0, out, cap,
+                                             C.byref(n_out), C.byref(matched), C.byref(neg), info)
             if rc == ERR_INVALID and n_out.value > cap:
                 cap = n_out.value          # more answer schemas than slots: run again with room for all
                 continue
             check(rc, self.h)
-            return bool(matched.value), bool(neg.value), [Table(self, out[i]) for i in range(n_out.value)]
+            k = n_out.value
+            return bool(matched.value), bool(neg.value), [Table(self, out[i], info[20 * i:20 * i + 20])
+                                                          for i in range(k)]
 
     def plan_execute_many(self, plans, no_overload=False):
         """das_plan_execute_many over [(words, n_nodes)] -> one (matched,

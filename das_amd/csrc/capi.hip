@@ -729,17 +729,35 @@ int das_set_minus(das_ctx_t* ctx, const das_table_t* const* a, uint32_t na, cons
   });
 }
 
-int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
-                     das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation) {
+int das_plan_execute_info(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                          das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation,
+                          int64_t* info) {
+  if (!ctx || !nodes || !n_out || !matched || !negation || (cap && !out)) return fail(ctx, DAS_ERR_INVALID, "null argument");
   return guarded(ctx, [&] {
     auto r = das::plan_execute(ctx->c, nodes, n, (int)no_overload);
     *n_out = (uint32_t)r.tables.size();     // on overflow: the capacity the caller needs
     DAS_CHECK(r.tables.size() <= cap, das::DAS_E_INVALID, "plan: more answer tables than `cap`");
-    for (size_t i = 0; i < r.tables.size(); ++i) out[i] = wrap(std::move(r.tables[i]));
-    *n_out = (uint32_t)r.tables.size();
+    for (size_t i = 0; i < r.tables.size(); ++i) {
+      if (info) {
+        // what das_table_info reports (das_plan_execute_many's layout)
+        int64_t* f = info + 20 * i;
+        const auto& t = *r.tables[i];
+        f[0] = t.kind;
+        f[1] = t.ncols;
+        f[2] = (int64_t)t.nrows;
+        f[3] = 0;
+        for (int k = 0; k < 16; ++k) f[4 + k] = k < t.ncols ? t.vars[k] : 0;
+      }
+      out[i] = wrap(std::move(r.tables[i]));
+    }
     *matched = r.matched ? 1 : 0;
     *negation = r.negation ? 1 : 0;
   });
+}
+
+int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                     das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation) {
+  return das_plan_execute_info(ctx, nodes, n, no_overload, out, cap, n_out, matched, negation, nullptr);
 }
 
 int das_plan_execute_many(das_ctx_t* ctx, uint32_t n_plans, const das_plan_node_t* const* nodes, const uint32_t* n,

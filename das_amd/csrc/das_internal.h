@@ -225,9 +225,12 @@ struct Ctx {
       // the batch's other plans (kPlanSide) run beside the lead plan's long
       // kernels: their queue gets the highest dispatch priority
       // (DAS_PLAN_PRIO=0: default priority, A/B)
+      // (DAS_CHAIN_PRIO=1: the chains' side streams too, A/B)
       int lo = 0, hi = 0;
       const char* pp = std::getenv("DAS_PLAN_PRIO");
-      if (i == kPlanSide && !(pp && pp[0] == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      const char* cp = std::getenv("DAS_CHAIN_PRIO");
+      const bool high = i == kPlanSide ? !(pp && pp[0] == '0') : (cp && cp[0] == '1');
+      if (high && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
         DAS_HIP(hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, hi));
       else
         DAS_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
@@ -238,12 +241,15 @@ struct Ctx {
   // grid kernel leaves its block zero again)
   static constexpr uint32_t kGscBlock = 64;               // words per block (>= the kernel's kGscWords)
   uint32_t* gsc_pool = nullptr;
+  // blocks 0 .. kPubPool-1: a batch's pooled chains; kPubPool + level: the
+  // one-at-a-time chain of each read-back level (fused_and)
+  static constexpr uint32_t kGscBlocks = 18;
   uint32_t* gsc_block(uint32_t k) {
     if (!gsc_pool) {
-      DAS_HIP(hipMalloc((void**)&gsc_pool, 4ull * kGscBlock * 16));
-      DAS_HIP(hipMemset(gsc_pool, 0, 4ull * kGscBlock * 16));
+      DAS_HIP(hipMalloc((void**)&gsc_pool, 4ull * kGscBlock * kGscBlocks));
+      DAS_HIP(hipMemset(gsc_pool, 0, 4ull * kGscBlock * kGscBlocks));
     }
-    return gsc_pool + (uint64_t)kGscBlock * (k % 16);
+    return gsc_pool + (uint64_t)kGscBlock * (k % kGscBlocks);
   }
   hipEvent_t fence_event(uint32_t i) {
     while (side_ev.size() <= i) {

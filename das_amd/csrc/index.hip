@@ -93,6 +93,7 @@ PubLevel::PubLevel() {
   t_pub_level = 1;
 }
 PubLevel::~PubLevel() { t_pub_level = 0; }
+int pub_level() { return t_pub_level; }
 
 uint8_t* pinned_stage(uint64_t bytes) {
   struct Stage {

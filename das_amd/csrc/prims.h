@@ -219,6 +219,7 @@ void set_wait_hook(WaitHook* hook);
 double bytes_since_wait();
 // While alive: pub_reserve / pinned_stage hand out this thread's second slot
 // and staging buffer (a plan run inside another plan's read-back wait)
+int pub_level();                 // 0, or 1 inside a PubLevel
 struct PubLevel {
   PubLevel();
   ~PubLevel();

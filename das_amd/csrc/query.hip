@@ -1258,6 +1258,11 @@ struct FiltKey {
 
 // NPC / NBC: the probe / build output column counts when specialised (the
 // pointers then live in registers), -1 = read from jc at run time
+// MODE 3 (MODE 2 staged): a chunk's kept outputs are collected in its wave's
+// LDS rows (stage: NPC + NBC columns of CH) and leave as 16-byte stores to
+// the chunk's scratch slots (+ its count, for k_chunk_compact) instead of
+// each lane's scattered 4-byte stores; with `kept` set, at a place reserved
+// by ONE atomic per chunk instead (no scratch, no compaction; unsorted).
 template <int MODE, int NPC, int NBC, int CH, int XU>
 __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
                                              uint32_t range, const uint2* __restrict__ lc, uint64_t units,
@@ -1265,7 +1270,9 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
                                              uint8_t* __restrict__ fl, uint32_t* __restrict__ ccnt,
                                              const uint32_t* __restrict__ coff, const JoinCols& jc,
                                              uint32_t* __restrict__ out, uint64_t cap, uint64_t wlo, uint64_t whi,
-                                             uint32_t* row) {
+                                             uint32_t* row, uint32_t* stage = nullptr,
+                                             unsigned long long* kept = nullptr,
+                                             const uint32_t* __restrict__ cunit = nullptr) {
   const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
   const int lane = __lane_id();
   const uint64_t lt = __lanemask_lt();
@@ -1274,18 +1281,26 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
   const uint32_t* bp[4];
   uint32_t* po[4];
   uint32_t* bo[4];
+  uint32_t* sp[4];                          // MODE 3: the LDS rows of the probe / build output columns
+  uint32_t* sb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     pp[i] = i < ncp ? jc.p[i] : nullptr;
     bp[i] = i < ncb ? jc.b[i] : nullptr;
-    po[i] = i < ncp && MODE >= 1 ? out + (uint64_t)jc.po[i] * cap : nullptr;
-    bo[i] = i < ncb && MODE >= 1 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+    po[i] = i < ncp && MODE >= 1 && MODE != 3 ? out + (uint64_t)jc.po[i] * cap : nullptr;
+    bo[i] = i < ncb && MODE >= 1 && MODE != 3 ? out + (uint64_t)jc.bo[i] * cap : nullptr;
+    sp[i] = i < ncp && MODE == 3 ? stage + (uint64_t)i * CH : nullptr;
+    sb[i] = i < ncb && MODE == 3 ? stage + (uint64_t)(ncp + i) * CH : nullptr;
   }
   // chunks [wlo, whi) of the virtual outputs
   for (uint64_t w = wlo + blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); w < whi; w += waves) {
     const uint64_t ob = w * CH;
     const uint64_t oe = ob + CH < total ? ob + CH : total;
     uint64_t lo = 0, hi = units;                       // last unit with unit_off[u] <= ob
+    if (cunit) {
+      lo = cunit[w];                                   // (k_chunk_units: one load, no search)
+      hi = lo + 1;
+    }
     while (hi - lo > 1) {
       const uint64_t step = (hi - lo + 63) / 64;
       const uint64_t idx = lo + (uint64_t)lane * step;
@@ -1296,7 +1311,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
       lo = nlo;
     }
     uint32_t run = 0;                                  // kept outputs of this chunk so far
-    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? (w - wlo) * CH : 0ull;
+    const uint64_t obase = MODE == 1 ? (uint64_t)coff[w] : MODE == 2 ? (w - wlo) * CH : 0ull;   // (MODE 3: LDS row 0)
     for (uint64_t u = lo; u < units; ++u) {
       uint64_t base = unit_off[u];
       if (base >= oe) break;
@@ -1305,7 +1320,9 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
 #pragma unroll
       for (int g = 0; g < kXGroups; ++g) {
         const uint64_t r = r0 + g * 64 + lane;
-        const uint32_t d = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+        // (pkey null: the probe rows' own (first, count), k_ij_lc's row ids
+        // are the identity -- one load instead of two dependent ones)
+        const uint32_t d = r < np ? (pkey ? pkey[r] - kmin : (uint32_t)r) : 0xFFFFFFFFu;
         e[g] = d < range ? lc[d] : make_uint2(0u, 0u);
       }
 #pragma unroll
@@ -1332,7 +1349,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
         // load and 4 bitmap words, and the kept ones leave compacted by a
         // wave prefix sum -- instead of 4 rounds of owner lanes, 4-byte
         // gathers and ballots (DAS_DJ_VEC=0: off)
-        const bool runs = MODE == 2 && ncb == 1 && fk.bcol == 0 && !(jc.search & 10) && (re - rs) > 256u;
+        const bool runs = MODE >= 2 && ncb == 1 && fk.bcol == 0 && !(jc.search & 10) && (re - rs) > 256u;
         for (uint32_t o0 = rs; o0 < re;) {
           if (runs && re - o0 >= 256u) {
             const uint64_t m0 = __ballot(pre <= o0);
@@ -1361,10 +1378,17 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
                 if (!f[k]) continue;
+                if constexpr (MODE == 3) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                  if (i < ncp) po[i][pos] = pvl[i];
-                bo[0][pos] = v[k] + fk.lo;
+                  for (int i = 0; i < 4; ++i)
+                    if (i < ncp) sp[i][pos] = pvl[i];
+                  sb[0][pos] = v[k] + fk.lo;
+                } else {
+#pragma unroll
+                  for (int i = 0; i < 4; ++i)
+                    if (i < ncp) po[i][pos] = pvl[i];
+                  bo[0][pos] = v[k] + fk.lo;
+                }
                 ++pos;
               }
               run += tot;
@@ -1415,7 +1439,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
           } else {
             bool f[XU];
             uint32_t v[XU];
-            if (MODE == 1) {
+            if constexpr (MODE == 1) {
 #pragma unroll
               for (int q = 0; q < XU; ++q) f[q] = q < nr && o[q] < re && fl[gb + o[q]] != 0;
             } else {
@@ -1434,7 +1458,7 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
             for (int q = 0; q < XU; ++q)
 #pragma unroll
               for (int i = 0; i < 4; ++i)
-                bv[q][i] = (i < ncb && f[q]) ? (MODE == 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
+                bv[q][i] = (i < ncb && f[q]) ? (MODE >= 2 && i == fk.bcol ? v[q] + fk.lo : bp[i][br[q]]) : 0u;
 #pragma unroll
             for (int q = 0; q < XU; ++q) {
               if (q >= nr) continue;
@@ -1446,12 +1470,18 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
                 if (i >= ncp) break;
                 const uint32_t x = un[q] ? (uint32_t)__builtin_amdgcn_readlane((int)pv[i], ll[q])
                                          : lane_get(pv[i], ll[q]);
-                if (f[q]) po[i][pos] = x;
+                if (f[q]) {
+                  if constexpr (MODE == 3) sp[i][pos] = x;
+                  else po[i][pos] = x;
+                }
               }
               if (f[q]) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                  if (i < ncb) bo[i][pos] = bv[q][i];
+                  if (i < ncb) {
+                    if constexpr (MODE == 3) sb[i][pos] = bv[q][i];
+                    else bo[i][pos] = bv[q][i];
+                  }
               }
             }
           }
@@ -1459,7 +1489,44 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
         }
       }
     }
-    if (MODE != 1 && lane == 0) ccnt[w] = run;
+    if constexpr (MODE == 3) {
+      // the chunk's kept rows, LDS -> the chunk's slots (or a reserved place)
+      // of the output: a head of <= 3 rows aligns the destination, 16-byte
+      // stores, a tail of <= 3
+      if (!kept && lane == 0) ccnt[w] = run;
+      if (run) {
+        // (LDS writes and reads of one wave stay in program order; the
+        // barrier keeps the compiler from moving them across each other)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        unsigned long long b = 0;
+        if (kept && lane == 0) b = atomicAdd(kept, (unsigned long long)run);
+        if (!kept) b = (unsigned long long)(w - wlo) * CH;
+        const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 0) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0);
+        const uint32_t h = (4u - (uint32_t)(base & 3u)) & 3u;
+        const uint32_t head = h < run ? h : run;
+        const uint32_t nq = (run - head) / 4u;
+        const uint32_t t0 = head + 4u * nq;
+        for (int k = 0; k < ncp + ncb; ++k) {
+          const uint32_t* sc = stage + (uint64_t)k * CH;
+          const int col = k < ncp ? jc.po[k] : jc.bo[k - ncp];
+          uint32_t* dc = out + (uint64_t)col * cap + base;
+          if ((uint32_t)lane < head) dc[lane] = sc[lane];
+          for (uint32_t q = (uint32_t)lane; q < nq; q += 64u) {
+            const uint32_t j = head + 4u * q;
+            store16<true>(dc + j, u32x4{sc[j], sc[j + 1], sc[j + 2], sc[j + 3]});
+          }
+          if (t0 + (uint32_t)lane < run) dc[t0 + lane] = sc[t0 + lane];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    } else if (MODE != 1 && lane == 0) {
+      ccnt[w] = run;
+    }
   }
 }
 
@@ -1476,17 +1543,41 @@ __global__ void __launch_bounds__(B) k_dj_filt(const uint32_t* __restrict__ pkey
                                        cap, wlo, whi, s_row[threadIdx.x >> 6]);
 }
 
-// the one walk at 8 waves per SIMD (<= 64 VGPRs; DAS_FILT_OCC=8, A/B): more
-// waves in flight for a walk whose waves spend ~80 % of their cycles waiting
-template <int NPC, int NBC, int XU>
-__global__ void __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(8, 8)))
-k_dj_filt_o8(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin, uint32_t range,
-             const uint2* __restrict__ lc, uint64_t units, const uint64_t* __restrict__ unit_off, uint64_t total,
-             FiltKey fk, uint32_t* __restrict__ ccnt, JoinCols jc, uint32_t* __restrict__ out, uint64_t cap,
-             uint64_t wlo, uint64_t whi) {
+// MODE 3: chunks of CH outputs, each wave's kept rows staged in LDS, then
+// written to the chunk's slots [(w - wlo) CH, + ccnt[w]) of `out` (a scratch
+// for k_chunk_compact), or -- kept non-null -- at a place reserved by one
+// atomic on *kept (A/B: DAS_FILT_STAGED=atomic)
+template <int NPC, int NBC, int CH>
+__global__ void __launch_bounds__(B) k_dj_filt_staged(const uint32_t* __restrict__ pkey, uint64_t np, uint32_t kmin,
+                                                      uint32_t range, const uint2* __restrict__ lc, uint64_t units,
+                                                      const uint64_t* __restrict__ unit_off, uint64_t total,
+                                                      FiltKey fk, JoinCols jc, uint32_t* __restrict__ out,
+                                                      uint64_t cap, uint64_t wlo, uint64_t whi,
+                                                      uint32_t* __restrict__ ccnt, unsigned long long* __restrict__ kept,
+                                                      const uint32_t* __restrict__ cunit) {
   __shared__ uint32_t s_row[B / 64][64];
-  dj_filt_body<2, NPC, NBC, 1024, XU>(pkey, np, kmin, range, lc, units, unit_off, total, fk, nullptr, ccnt, nullptr,
-                                      jc, out, cap, wlo, whi, s_row[threadIdx.x >> 6]);
+  __shared__ uint32_t s_stage[B / 64][(NPC + NBC) * CH];
+  dj_filt_body<3, NPC, NBC, CH, kXUnroll>(pkey, np, kmin, range, lc, units, unit_off, total, fk, nullptr, ccnt,
+                                          nullptr, jc, out, cap, wlo, whi, s_row[threadIdx.x >> 6],
+                                          s_stage[threadIdx.x >> 6], kept, cunit);
+}
+
+// For every CH-output chunk, the unit holding its first output (the last unit
+// u with unit_off[u] <= w CH), one thread per chunk: the walk's per-chunk
+// search (4 dependent rounds inside its latency chain) becomes one load
+template <int CH>
+__global__ void __launch_bounds__(B) k_chunk_units(const uint64_t* __restrict__ unit_off, uint64_t units,
+                                                   uint64_t chunks, uint32_t* __restrict__ cunit) {
+  for (uint64_t w = blockIdx.x * (uint64_t)B + threadIdx.x; w < chunks; w += (uint64_t)gridDim.x * B) {
+    const uint64_t ob = w * CH;
+    uint64_t lo = 0, hi = units;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (unit_off[mid] <= ob) lo = mid;
+      else hi = mid;
+    }
+    cunit[w] = (uint32_t)lo;
+  }
 }
 
 // MODE 2's second step: chunk w's kept rows [(w - wlo) CH, + cnt[w]) of the
@@ -3954,9 +4045,16 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               std::unique_ptr<Table>& out, uint32_t* consumed) {
   const int form = fused_and_form(c, terms, anti, no_overload);
   if (form < 0) return 0;
+  // DAS_CHAIN_PREP1=0: a grid chain's counters from this read-back level's
+  // pooled block (zeroed; the grid leaves it zero), no k_chain_prep launch,
+  // every workgroup reading the descriptor from the pinned stage -- FlyBase
+  // through matched() 0.284-0.301 vs 0.283-0.303 ms per step with the prep
+  // launch (round 6, one box): no gain, off by default
+  const char* cp = std::getenv("DAS_CHAIN_PREP1");
+  uint32_t* gsc = cp && cp[0] == '0' ? c.gsc_block(kPubPool + (uint32_t)pub_level()) : nullptr;
   for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
     ChainRun R;
-    const int r = chain_compile(c, terms, anti, attempt == 0, R);
+    const int r = chain_compile(c, terms, anti, attempt == 0, R, gsc);
     if (r < 0) continue;                                      // the grid form does not apply: one workgroup
     if (r == 0) return 0;
     // (the descriptor stages in this thread's pinned buffer, read by the
@@ -4910,59 +5008,100 @@ std::unique_ptr<Table> index_join_filtered(Ctx& c, const Table& A, const das_lin
     }
   }
   if (fits) {
-    DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);
+    // The one walk stages each chunk's kept rows in its wave's LDS rows and
+    // writes them to the chunk's slots of the scratch with 16-byte stores
+    // (k_dj_filt_staged, 512-output chunks): the walk itself 429 -> 228 us at
+    // config 5 (each lane's scattered 4-byte stores were the cost).
+    // DAS_FILT_STAGED=0: the unstaged walk (k_dj_filt<2>, 1024-output chunks);
+    // =atomic: the staged rows placed straight in the output by one atomic
+    // per chunk, no scratch, no compaction -- 1,600 us: 1.2 * 10^5 atomics on
+    // one address from 8 XCDs serialise (A/B record, output unsorted)
+    const char* se = std::getenv("DAS_FILT_STAGED");
     const bool spec = (jc.np == 1 && jc.nb == 1) || (jc.np == 2 && jc.nb == 1) || (jc.np == 1 && jc.nb == 2);
-    const std::string nm = spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
-                                : std::string("k_dj_filt<2,-1,-1,1024,4>");
+    const bool staged = !(se && se[0] == '0') && spec && nu == jc.np + jc.nb;
+    const bool atomic_place = staged && se && !std::strcmp(se, "atomic");
+    const uint64_t sch = staged ? 512 : 1024;
+    const uint64_t nch = (total + sch - 1) / sch;
+    const unsigned sgrid = grid_for(nch, B / 64, 65535u * 4u);
+    DBuf<uint32_t> ccnt(nch, c.s), coff(nch + 1, c.s);
+    DBuf<unsigned long long> kept;
+    std::unique_ptr<Table> direct_out;
+    if (atomic_place) {
+      direct_out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), total);
+      kept.alloc(1, c.s);
+      fill_dev(kept.p, 0, 8, c.s);
+    }
+    // the chunks' first units (DAS_FILT_CUNIT=0: the walk searches them)
+    const char* cue = std::getenv("DAS_FILT_CUNIT");
+    const bool cun = staged && !(cue && cue[0] == '0') && units < (1ull << 32);
+    DBuf<uint32_t> cunit;
+    if (cun) {
+      cunit.alloc(nch, c.s);
+      KScope ks("k_chunk_units", 4.0 * nch);
+      hipLaunchKernelGGL(k_chunk_units<512>, G(nch), dim3(B), 0, c.s, (const uint64_t*)toff.p, units, nch, cunit.p);
+      DAS_HIP(hipGetLastError());
+    }
+    const std::string nm = staged ? "k_dj_filt_staged<" + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",512>"
+                           : spec ? "k_dj_filt<2," + std::to_string(jc.np) + "," + std::to_string(jc.nb) + ",1024,4>"
+                                  : std::string("k_dj_filt<2,-1,-1,1024,4>");
     {
       // per probe row its row id, (first, count) and probe columns; per
       // output its build value (a P row); kept outputs' columns written
       ProfScope ps(c, nm, (12.0 + 4.0 * jc.np) * A.nrows + 4.0 * total);
+#define FILT_S(NPV, NBV)                                                                                         \
+  hipLaunchKernelGGL((k_dj_filt_staged<NPV, NBV, 512>), dim3(sgrid), dim3(B), 0, c.s, (const uint32_t*)nullptr,    \
+                     A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, \
+                     jc, atomic_place ? direct_out->data : scr.p, atomic_place ? direct_out->cap : total, 0ull, nch, \
+                     atomic_place ? (uint32_t*)nullptr : ccnt.p, atomic_place ? kept.p : nullptr, \
+                     cun ? (const uint32_t*)cunit.p : nullptr)
 #define FILT_L(NPV, NBV)                                                                                       \
-  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
+  hipLaunchKernelGGL((k_dj_filt<2, NPV, NBV, 1024>), dim3(sgrid), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, \
                      0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk,             \
-                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks)
-      // A/B variants of the (1, 1) walk: DAS_FILT_OCC=8 (8 waves per SIMD),
-      // DAS_FILT_XU=8 (8 rounds of 64 outputs per load batch)
-      static const int occ = std::getenv("DAS_FILT_OCC") ? std::atoi(std::getenv("DAS_FILT_OCC")) : 0;
-      static const int xu = std::getenv("DAS_FILT_XU") ? std::atoi(std::getenv("DAS_FILT_XU")) : 4;
-#define FILT_O8(XUV)                                                                                          \
-  hipLaunchKernelGGL((k_dj_filt_o8<1, 1, XUV>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p, A.nrows, 0u, \
-                     (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total, fk, ccnt.p, jc,    \
-                     scr.p, total, 0ull, fchunks)
-      if (jc.np == 1 && jc.nb == 1 && occ == 8) {
-        if (xu == 8) FILT_O8(8);
-        else FILT_O8(4);
-      } else if (jc.np == 1 && jc.nb == 1 && xu == 8) {
-        hipLaunchKernelGGL((k_dj_filt<2, 1, 1, 1024, 8>), dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)rowid.p,
-                           A.nrows, 0u, (uint32_t)A.nrows, (const uint2*)lc.p, units, (const uint64_t*)toff.p, total,
-                           fk, (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, fchunks);
+                     (uint8_t*)nullptr, ccnt.p, (const uint32_t*)nullptr, jc, scr.p, total, 0ull, nch)
+      if (staged) {
+        if (jc.np == 1 && jc.nb == 1) FILT_S(1, 1);
+        else if (jc.np == 2 && jc.nb == 1) FILT_S(2, 1);
+        else FILT_S(1, 2);
       } else if (jc.np == 1 && jc.nb == 1) FILT_L(1, 1);
       else if (jc.np == 2 && jc.nb == 1) FILT_L(2, 1);
       else if (jc.np == 1 && jc.nb == 2) FILT_L(1, 2);
       else FILT_L(-1, -1);
+#undef FILT_S
 #undef FILT_L
-#undef FILT_O8
       DAS_HIP(hipGetLastError());
     }
-    const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, fchunks, coff.p, c.s);
+    auto finish = [&](std::unique_ptr<Table> out, int sorted) {
+      out->sorted_col = sorted;
+      for (int k = 0; k < nu; ++k) {
+        out->lo[k] = pl.lo[k];
+        out->hi[k] = pl.hi[k];
+      }
+      out->lo[fo] = (uint32_t)lo;
+      out->hi[fo] = (uint32_t)hi;
+      return out;
+    };
+    if (atomic_place) {
+      const uint64_t m = read_u64(reinterpret_cast<const uint64_t*>(kept.p), c.s);
+      prof_add_bytes(c, nm, 4.0 * nu * m);
+      direct_out->nrows = m;
+      return finish(std::move(direct_out), -1);               // chunks land in completion order
+    }
+    const uint64_t m = scan_total<uint32_t>(SpanIn<uint32_t>{ccnt.p}, nch, coff.p, c.s);
     prof_add_bytes(c, nm, 4.0 * nu * m);
     auto out = new_table(c, DAS_TABLE_ORDERED, nu, pl.uni.data(), m);
     out->nrows = m;
     if (m) {
-      KScope ks("k_chunk_compact<1024>", 8.0 * nu * m + 8.0 * fchunks);
-      hipLaunchKernelGGL(k_chunk_compact<1024>, dim3(fgrid2), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
-                         (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, 0ull, fchunks, nu, out->data, out->cap);
+      KScope ks(staged ? "k_chunk_compact<512>" : "k_chunk_compact<1024>", 8.0 * nu * m + 8.0 * nch);
+      if (staged)
+        hipLaunchKernelGGL(k_chunk_compact<512>, dim3(sgrid), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
+                           (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, 0ull, nch, nu, out->data, out->cap);
+      else
+        hipLaunchKernelGGL(k_chunk_compact<1024>, dim3(sgrid), dim3(B), 0, c.s, (const uint32_t*)scr.p, total,
+                           (const uint32_t*)ccnt.p, (const uint32_t*)coff.p, 0ull, nch, nu, out->data, out->cap);
       DAS_HIP(hipGetLastError());
     }
-    out->sorted_col = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
-    for (int k = 0; k < nu; ++k) {
-      out->lo[k] = pl.lo[k];
-      out->hi[k] = pl.hi[k];
-    }
-    out->lo[fo] = (uint32_t)lo;
-    out->hi[fo] = (uint32_t)hi;
-    return out;
+    const int sorted = A.sorted_col >= 0 ? colof_t(*out, A.vars[A.sorted_col]) : -1;
+    return finish(std::move(out), sorted);
   }
   DBuf<uint8_t> fl(total, c.s);
   DBuf<uint32_t> ccnt(fchunks, c.s), coff(fchunks + 1, c.s);

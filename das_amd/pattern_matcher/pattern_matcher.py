@@ -673,7 +673,12 @@ def matched_many(db, exprs, tag=None):
         for i, e in enumerate(exprs):
             # the operators whose matched() tries a whole-expression plan
             # first, with its prelude (And.matched / Or.matched / Not.matched)
-            if type(e) not in (And, Or, Not) or (type(e) is not Not and not e.terms):
+            # (a root Link is one LINK / CONST plan node: Link.matched's scan
+            # or link_exists, :502-538 -- batched too, e.g. bench Q1)
+            if type(e) is Link:
+                if not e.ordered:
+                    continue
+            elif type(e) not in (And, Or, Not) or (type(e) is not Not and not e.terms):
                 continue
             if db._stale and db.touches_stale(e):
                 continue

@@ -346,6 +346,12 @@ typedef struct {
 } das_plan_node_t;
 int das_plan_execute(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
                      das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation);
+/* das_plan_execute + each answer table's (kind, ncols, nrows, 0, vars[16])
+ * in info[20 * i ..] (NULL: not written), as das_plan_execute_many reports
+ * them: the caller needs no das_table_info call per table. */
+int das_plan_execute_info(das_ctx_t* ctx, const das_plan_node_t* nodes, uint32_t n, uint32_t no_overload,
+                          das_table_t** out, uint32_t cap, uint32_t* n_out, int32_t* matched, int32_t* negation,
+                          int64_t* info);
 
 /* n_plans independent plans in one call (no reference counterpart: a batch of
  * the reference's Expression.matched calls, pattern_matcher.py:705-748 /

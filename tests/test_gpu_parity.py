@@ -873,7 +873,7 @@ def test_gpu_hub_four_clause_matches_oracle(semi, monkeypatch):
         assert same(got, want), (name, got.get("n"), want.get("n"))
 
 
-@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "1-capped", "0"])
+@pytest.mark.parametrize("multi", ["1", "1-twopass", "1-local", "1-unstaged", "1-atomic", "1-capped", "0"])
 def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     """Runs of one-variable hub clauses on one variable (T2(V2,a), T3(V2,b),
     ...) folded by ONE filter with the intersection of their key sets
@@ -886,10 +886,13 @@ def test_gpu_semi_join_multi_matches_oracle(multi, monkeypatch):
     from das_amd import synthetic
     monkeypatch.setenv("DAS_SEMI_MULTI", multi[0])
     # the filtered expansion in one pass with LDS flag tiles (unsorted) ...
-    monkeypatch.setenv("DAS_FILT_FUSED", "0" if multi in ("1-twopass", "1-local") else "1")
-    # ... as one walk writing chunk-locally + a compaction (k_dj_filt<2>,
-    # default) or as a flag pass and a second walk
+    monkeypatch.setenv("DAS_FILT_FUSED", "0" if multi in ("1-twopass", "1-local", "1-unstaged", "1-atomic") else "1")
+    # ... as one walk writing chunk-locally + a compaction -- the kept rows
+    # staged in LDS (k_dj_filt_staged, default), or stored lane by lane
+    # (k_dj_filt<2>, DAS_FILT_STAGED=0), or placed by one atomic per chunk
+    # (=atomic, no compaction) -- or as a flag pass and a second walk
     monkeypatch.setenv("DAS_FILT_LOCAL", "0" if multi == "1-twopass" else "1")
+    monkeypatch.setenv("DAS_FILT_STAGED", {"1-unstaged": "0", "1-atomic": "atomic"}.get(multi, "1"))
     # ... and the one walk's scratch over its budget: the two passes instead
     if multi == "1-capped":
         monkeypatch.setenv("DAS_FILT_SCRATCH_MAX", "0")
