@@ -920,8 +920,17 @@ void read_counters(uint64_t out[2]) {
   out[1] = g_readbacks.load(std::memory_order_relaxed);
 }
 
+void launch_gate(Ctx& c, double algorithmic_bytes) {
+  if (!c.gate_s || algorithmic_bytes < c.gate_min) return;
+  hipEvent_t e = c.fence_event(2 * kPubPool + 3);
+  DAS_HIP(hipEventRecord(e, c.gate_s));
+  DAS_HIP(hipStreamWaitEvent(c.s, e, 0));
+  c.gate_s = nullptr;                                  // once per nested plan
+}
+
 KScope::KScope(const char* name, double algorithmic_bytes) {
   Ctx* c = active_ctx();
+  if (c && c->gate_s) launch_gate(*c, algorithmic_bytes);
   if (c && c->prof) {
     impl = new ProfScope(*c, name, algorithmic_bytes);      // (counts the launch)
   } else {

@@ -169,6 +169,12 @@ struct Ctx {
   std::string prof_tag;              // non-empty: recorded scopes are named "<scope>@<tag>" (one query's launches)
   uint32_t tag_plan = ~0u;           // das_plan_execute_many: the plan whose launches carry tag_plan_name
   std::string tag_plan_name;
+  // a plan nested in another's read-back wait (das_plan_execute_many): its
+  // first kernel of >= gate_min algorithmic bytes waits for the work launched
+  // on gate_s (the outer plan's stream) so far -- latency-bound stages
+  // overlap, two HBM-bound floods do not (launch_gate)
+  hipStream_t gate_s = nullptr;
+  double gate_min = 0;
   bool prof_selected(const std::string& name) const {
     if (prof_only.empty()) return true;
     size_t b = 0;
@@ -286,12 +292,14 @@ void count_readback();
 void read_counters(uint64_t out[2]);
 void trace_dump(const char* title);
 
+void launch_gate(Ctx& c, double algorithmic_bytes);
 struct ProfScope {
   Ctx& c;
   std::string name;
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(Ctx& ctx, std::string n, double algorithmic_bytes) : c(ctx), name(std::move(n)), bytes(algorithmic_bytes) {
+    if (c.gate_s) launch_gate(c, algorithmic_bytes);
     count_launch();
     launched_bytes() += algorithmic_bytes;
     if (trace_on()) trace_mark("kernel", name + " " + std::to_string((uint64_t)algorithmic_bytes) + " B");

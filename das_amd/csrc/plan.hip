@@ -705,6 +705,8 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
   const bool nest = !(pn && pn[0] == '0') && n_plans - n_cand > 1;
   const char* nm = std::getenv("DAS_PLAN_NEST_MIN");             // tests: 0 = at every wait
   const double nest_min = nm ? std::atof(nm) : (double)(128u << 20);
+  const char* ng = std::getenv("DAS_NEST_GATE_MB");               // 0: no gate (A/B)
+  const double gate_min = (ng ? std::atof(ng) : 1024.0) * (1 << 20);
   if ((n_cand && side) || plan_side || nest) {
     // side streams are ordered after the context's stream as it stands when
     // the batch begins (their blocks' last readers), never after this batch's
@@ -795,6 +797,15 @@ std::vector<PlanOutput> plan_execute_many(Ctx& c, const das_plan_node_t* const* 
       PubLevel lv;
       Swap sw{c, c.s};
       c.s = to_side();
+      // its first flood of >= gate_min bytes (bio QUERY_3's 6.6 GB cross
+      // product) waits for the outer plan's launched kernels: running beside
+      // an HBM-bound join it slowed both (a 50 us join took 330 us beside it)
+      struct Ungate {
+        Ctx& c;
+        ~Ungate() { c.gate_s = nullptr; }
+      } ug{c};
+      c.gate_s = gate_min > 0 ? sw.old : nullptr;
+      c.gate_min = gate_min;
       outs[i] = eval_plan(i);
     }
   };
