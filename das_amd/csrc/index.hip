@@ -615,11 +615,15 @@ __global__ void k_remap_local(uint64_t n, const uint32_t* by_digest, uint32_t* l
     if (local2id[u] != kNone) local2id[u] = by_digest[local2id[u]];
 }
 
+// tkey (non-null): the id-order sort keys, already in final id order -- each
+// atom's named type is its key's high bits (k_temp_type looked it up once),
+// so the type's two dependent gathers (expr_child[expr_off[j]], then the type
+// table; leaf_ctype for nodes) are not repeated here
 __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, const Digest* dig,
                              const Digest* ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
                              const uint32_t* leaf_type_id, const uint64_t* expr_off, const uint32_t* expr_child,
                              Digest* a_dig, uint8_t* a_cat, uint32_t* a_type, uint32_t* a_arity, Digest* a_ct,
-                             uint32_t* a_name_leaf) {
+                             uint32_t* a_name_leaf, const uint32_t* tkey, uint32_t tshift, uint32_t n_types) {
   for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
        id += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = rep[id];
@@ -628,13 +632,17 @@ __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32
     a_ct[id] = ct[u];
     a_cat[id] = c;
     uint32_t ty = kNone, ar = 0, nl = kNone;
+    if (tkey) {
+      const uint32_t k = tkey[id] >> tshift;
+      ty = k == n_types ? kNone : k;
+    }
     if (u < n_leaf) {
-      ty = leaf_type_id[leaf_ctype[u]];
+      if (!tkey) ty = leaf_type_id[leaf_ctype[u]];
       if (c == CAT_NODE) nl = u;
     } else {
       const uint64_t j = u - n_leaf;
       if (c == CAT_LINK || c == CAT_LINK_REMOTE) {
-        ty = leaf_type_id[expr_child[expr_off[j]]];
+        if (!tkey) ty = leaf_type_id[expr_child[expr_off[j]]];
         ar = (uint32_t)(expr_off[j + 1] - expr_off[j] - 1);
       }
     }
@@ -1691,10 +1699,14 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   // then digest order), so the hot keys of a power-law KB share a few cache
   // lines of any id-indexed bitmap or directory.  by_digest keeps the digest
   // order for handle lookups.  DAS_DEGREE_ORDER=0: digest order inside a type.
+  // (the sorted id-order keys stay for k_fill_atoms: each atom's type)
+  DBuf<uint32_t> tkey(n_atoms ? n_atoms : 1, s);
+  uint32_t tshift = 0;
   {
-    DBuf<uint32_t> tkey(n_atoms ? n_atoms : 1, s), perm(n_atoms ? n_atoms : 1, s);
+    DBuf<uint32_t> perm(n_atoms ? n_atoms : 1, s);
     const char* dg = std::getenv("DAS_DEGREE_ORDER");
     const bool degree = !(dg && dg[0] == '0') && ne > 0;
+    tshift = degree ? 5u : 0u;
     if (n_atoms) {
       DBuf<uint32_t> cnt, slots;
       uint64_t n_slots = 0;
@@ -1772,9 +1784,11 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     hipLaunchKernelGGL(k_fill_atoms, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                        (const uint32_t*)catmax.p, (const Digest*)dig.p, (const Digest*)ct.p, nl,
                        (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)p_eoff,
-                       (const uint32_t*)p_child, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf);
+                       (const uint32_t*)p_child, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf,
+                       (const uint32_t*)tkey.p, tshift, (uint32_t)a.n_types);
     DAS_HIP(hipGetLastError());
   }
+  tkey.release();
   fill_dev(idx.ctype, 0xFF, 4 * (n_atoms ? n_atoms : 1), s);
   // outgoing CSR
   {
