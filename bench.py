@@ -43,6 +43,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# --batch -1: how a workload's timed step submits its queries -- the faster
+# mode in round 6's same-process pairs (the other is timed beside it, fresh
+# anchors): bio one by one 1.57-1.64 ms vs batched 1.67-1.73 (the batch's
+# up-front lowering leaves the GPU idle, and its nested plans contend with the
+# cross product; profiles/r6_bio_step_split.json); hub batched 0.77-0.79 vs
+# 0.84 (H2's expansion beside H4's latency-bound walk)
+BATCH_DEFAULT = {"bio": 0, "flybase": 0, "hub": 1}
 
 
 def parse():
@@ -60,9 +67,10 @@ def parse():
     ap.add_argument("--build-warmup", default="full", choices=["full", "small"],
                     help="config 4 warm-up build: the same input (default; the timed build then reuses every "
                          "device block) or a 10^4-link KB")
-    ap.add_argument("--batch", type=int, default=1, choices=[0, 1],
-                    help="1 (default): a step's queries in one das_plan_execute_many call (pm.matched_many); "
-                         "0: query.matched(db, answer) one by one")
+    ap.add_argument("--batch", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: a step's queries in one das_plan_execute_many call (pm.matched_many); 0: "
+                         "query.matched(db, answer) one by one, the reference's call pattern; -1 (default): per "
+                         "workload, the faster of the two as measured (BATCH_DEFAULT); the other is timed too")
     ap.add_argument("--events", default="dominant", choices=["dominant", "all"],
                     help="timed-step HIP events: around the dominant kernel only, or around every kernel scope")
     # bio (config 2)
@@ -725,8 +733,8 @@ def run_build(args, rank, world, dist, local_rank, backend="nccl"):
                # passes, scratch and intern traffic count against it)
                "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS * world,
                             "unit": "GB/s", "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
-                            "kernel": "whole build (SURVEY.md §8d bytes: hash (arity*16+16) in + 16 out, "
-                                      "CSR 2*arity*4 + 4 per link)",
+                            "kernel": "whole build (SURVEY.md §8d bytes)",
+                            "bytes_per_link": "hash (arity*16+16) in + 16 out, CSR 2*arity*4 + 4",
                             "algorithmic_bytes": algo},
                "dominant_kernel": roofline_of(stats, "build"),
                "cpu_baseline": cpu,
@@ -1052,6 +1060,8 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     from das_amd.database.hip_db import HipDB
     from das_amd.pattern_matcher import pattern_matcher as pm
     args = argparse.Namespace(**dict(vars(args), workload=workload))
+    if args.batch < 0:
+        args.batch = BATCH_DEFAULT.get(workload, 1)
     t_build = time.perf_counter()
     log(f"generating {workload} KB")
     # one non-null stream shared by torch (collectives, staging buffers) and
@@ -1215,24 +1225,27 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
     if and_join:
         and_join["note"] = "Q2's And join launches inside the timed steps (das_prof_tag)"
     stats = {k: v for k, v in stats.items() if "@" not in k}
-    # every timed step's answers against the same query set evaluated one
-    # query at a time through matched() (untimed): the batched executor's
-    # per-query answer sizes and the step's total must equal them
-    check = verify_steps(step_counts, [step(args.warmup + i, batch=False) for i in range(args.steps)],
+    # every timed step's answers against the same query set evaluated the
+    # other way (untimed): batched steps against matched() one query at a
+    # time, one-by-one steps against one das_plan_execute_many batch -- the
+    # per-query answer sizes and so the step's total must be equal
+    other = not args.batch
+    check = verify_steps(step_counts, [step(args.warmup + i, batch=other) for i in range(args.steps)],
                          [[name for name, _ in qsets[args.warmup + i]] for i in range(args.steps)], dist, stage_dev)
-    # the reference's call pattern, timed: one expr.matched(db, answer) per
-    # query (scripts/benchmark.py:231-239, QueryFlyBase.ipynb cells 5-9) over
-    # query sets no earlier step used
-    matched_ms = None
-    if engine is None and args.batch and not args.no_extras:
+    check["against"] = "pm.matched_many batches" if other else "matched() one query at a time"
+    # the other submission mode, timed over query sets no earlier step used:
+    # matched() per query is the reference's call pattern
+    # (scripts/benchmark.py:231-239, QueryFlyBase.ipynb cells 5-9)
+    other_ms = None
+    if engine is None and not args.no_extras:
         for i in range(2):                         # the extra sets' shapes warm (no new anchors timed cold)
-            step(args.warmup + i, batch=False)
+            step(args.warmup + i, batch=other)
         torch.cuda.synchronize()
         tm = time.perf_counter()
         for i in range(args.steps):
-            step(n_sets + i, batch=False)
+            step(n_sets + i, batch=other)
         torch.cuda.synchronize()
-        matched_ms = (time.perf_counter() - tm) * 1e3 / args.steps
+        other_ms = (time.perf_counter() - tm) * 1e3 / args.steps
     if args.cprofile and rank == 0:
         import cProfile
         import pstats
@@ -1332,9 +1345,13 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
             "kernels": kernels_of(warm_stats if dominant else stats),
             "kernels_from": "last warmup step (every scope)" if dominant else "timed steps (every scope)",
             "build_s": round(t_build, 2),
-            # the same workload through the reference's call pattern: one
-            # matched() per query (no batching), fresh anchors
-            "step_ms_matched": None if matched_ms is None else round(matched_ms, 4),
+            # both submission modes: the timed one's ms_per_step and the other
+            # timed beside it on fresh anchors (matched() per query = the
+            # reference's call pattern)
+            "step_ms_matched": round(ms_per_step, 4) if not args.batch else
+            (None if other_ms is None else round(other_ms, 4)),
+            "step_ms_batched": round(ms_per_step, 4) if args.batch else
+            (None if other_ms is None else round(other_ms, 4)),
         }
         if world > 1:
             out["sharded_plan_stats"] = dict(engine.sdb.plan_stats)
@@ -1387,15 +1404,21 @@ def _compact_leg(d):
     if "error" in d:
         return {"error": str(d["error"])[:200]}
     out = {k: _r(d.get(k)) for k in ("value", "unit", "ms_per_step") if k in d}
+    if (d.get("config") or {}).get("step_calls"):
+        out["step_calls"] = d["config"]["step_calls"]
     out["roofline"] = _compact_roofline(d.get("roofline"), full=False)
     sr = d.get("step_roofline")
     out["step_roofline"] = {"frac": sr.get("frac")} if sr else None
     out["cpu_baseline"] = _compact_cpu(d.get("cpu_baseline"), full=False)
     if d.get("cpu_fast"):
         out["cpu_fast"] = _compact_cpu(d.get("cpu_fast"), full=False)
-    for k in ("step_ms_matched", "cold_build_ms", "latency", "summary", "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
+    for k in ("step_ms_matched", "step_ms_batched", "cold_build_ms", "latency", "summary",
+              "collectives_per_step"):   # latency legs: per-query us, launches / read-backs
         if d.get(k) is not None:
             out[k] = d[k]
+    if isinstance(out.get("latency"), dict) and "rows" in out["latency"]:
+        # (getlinks: the per-row figures are in cpu_baseline, beside the CPU's)
+        out["latency"] = {k: v for k, v in out["latency"].items() if k not in ("rows", "level_ms_per_query")}
     return out
 
 
@@ -1409,15 +1432,17 @@ def compact_line(full):
     dropped, largest first, if a record ever grows past it."""
     line = {k: _r(full.get(k)) for k in HEAD_KEYS if k in full}
     cfg = full.get("config") or {}
-    line["config"] = {k: cfg[k] for k in ("workload", "parallelism") if k in cfg}
+    line["config"] = {k: cfg[k] for k in ("workload", "parallelism", "step_calls") if k in cfg}
     line["roofline"] = _compact_roofline(full.get("roofline"))
     line["step_roofline"] = _compact_roofline(full.get("step_roofline"))
     line["cpu_baseline"] = _compact_cpu(full.get("cpu_baseline"))
     if full.get("cpu_fast"):
         line["cpu_fast"] = _compact_cpu(full.get("cpu_fast"), full=False)
-    for k in ("step_ms_matched", "box", "latency", "summary", "collectives_per_step"):
+    for k in ("step_ms_matched", "step_ms_batched", "box", "latency", "summary", "collectives_per_step"):
         if full.get(k) is not None:
             line[k] = full[k]
+    if isinstance(line.get("box"), dict):
+        line["box"] = {k: v for k, v in line["box"].items() if k != "how"}
     jv = full.get("join_probe_variants") or {}
     ins = full.get("and_join_q2_in_step")
     if jv or ins:
