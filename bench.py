@@ -71,8 +71,9 @@ def parse():
                     help="1: a step's queries in one das_plan_execute_many call (pm.matched_many); 0: "
                          "query.matched(db, answer) one by one, the reference's call pattern; -1 (default): per "
                          "workload, the faster of the two as measured (BATCH_DEFAULT); the other is timed too")
-    ap.add_argument("--events", default="dominant", choices=["dominant", "all"],
-                    help="timed-step HIP events: around the dominant kernel only, or around every kernel scope")
+    ap.add_argument("--events", default="dominant", choices=["dominant", "all", "none"],
+                    help="timed-step HIP events: around the dominant kernel only, around every kernel scope, or none "
+                         "(A/B of the events' own cost; the roofline then comes from the profiled warmup step)")
     # bio (config 2)
     ap.add_argument("--genes", type=int, default=200_000)
     ap.add_argument("--bps", type=int, default=50_000)
@@ -1197,8 +1198,8 @@ def run_query(args, workload, rank, world, dist, local_rank, backend):
         join_k = q2_join_kernel()
     db.ctx.prof_reset()
     db.ctx.prof_only("|".join(k for k in ((dominant or {}).get("kernel"), join_k) if k) or None)
-    tag_q2[0] = join_k is not None
-    db.ctx.prof_enable(True)
+    tag_q2[0] = join_k is not None and args.events != "none"
+    db.ctx.prof_enable(args.events != "none")
     db.ctx.prof_mark(1)                  # kernel-trace bracket of the timed steps (tools/step_split.py)
     if dist:
         dist.barrier()

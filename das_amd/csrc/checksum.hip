@@ -113,7 +113,7 @@ double box_store_bw(Ctx& c, uint64_t bytes, uint32_t reps) {
   const int ncol = 6;
   const uint64_t cap4 = (bytes / 16 / ncol + 63) & ~63ull;
   DBuf<st_v4u> buf(cap4 * ncol, c.s);
-  const unsigned g = grid_for(cap4, 256, 8192);
+  const unsigned g = grid_for(cap4, 256);              // k_cartesian's launch: about one quad per thread and column
   hipEvent_t a = c.take_event(), b = c.take_event();
   hipLaunchKernelGGL(k_store16_nt, dim3(g), dim3(256), 0, c.s, buf.p, cap4, cap4, ncol);   // warm
   DAS_HIP(hipEventRecord(a, c.s));

@@ -188,10 +188,15 @@ struct Ctx {
   }
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;   // recycled timing events (creation is not cheap on ROCm)
+  // timing only: no system-scope fence when the event is recorded -- a default
+  // event writes back and invalidates the caches there, which the next
+  // kernels pay for (DAS_PROF_FENCE=1: default events, A/B)
   hipEvent_t take_event() {
     if (ev_pool.empty()) {
       hipEvent_t e;
-      DAS_HIP(hipEventCreate(&e));
+      const char* f = std::getenv("DAS_PROF_FENCE");
+      if (f && f[0] == '1') DAS_HIP(hipEventCreate(&e));
+      else DAS_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
       return e;
     }
     hipEvent_t e = ev_pool.back();
