@@ -4811,52 +4811,6 @@ __global__ void k_bits_set_sorted(const uint32_t* __restrict__ key, uint64_t n, 
   if (__ballot(d) && __lane_id() == 0) atomicOr(dup, 1u);
 }
 
-// A small key set's bitmap in ONE workgroup: its words zeroed, then the bits
-// set (duplicates flagged as in k_bits_set) -- one launch instead of a fill and
-// a set launch (bio QUERY_2 / QUERY_3's semi-joins: ~10^4 words, ~10^3 keys)
-constexpr uint64_t kBitsSmallWords = 1ull << 16, kBitsSmallKeys = 1ull << 16;
-__global__ void __launch_bounds__(1024) k_bits_small(const uint32_t* __restrict__ key, uint64_t n, uint32_t kmin,
-                                                     uint32_t range, uint64_t words, uint32_t* bits, bool zero_dup,
-                                                     uint32_t* dup) {
-  for (uint64_t w = threadIdx.x; w < words; w += 1024) bits[w] = 0u;
-  if (zero_dup && threadIdx.x == 0) *dup = 0u;
-  // the zeros reach L2 before any atomic of the set pass (atomics run there)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  uint32_t d = 0;
-  for (uint64_t i = threadIdx.x; i < n; i += 1024) {
-    const uint32_t k = key[i] - kmin;
-    if (k >= range) continue;
-    const uint32_t m = 1u << (k & 31);
-    if (atomicOr(&bits[k >> 5], m) & m) d = 1;
-  }
-  if (__ballot(d) && __lane_id() == 0) atomicOr(dup, 1u);
-}
-
-// bits[0 .. words) = the key set of `key` over [kmin, kmin + range); a
-// repeated key sets *dup (zeroed here first when zero_dup)
-void bits_build(Ctx& c, const uint32_t* key, uint64_t n, bool sorted, uint32_t kmin, uint64_t range, uint32_t* bits,
-                bool zero_dup, uint32_t* dup) {
-  const uint64_t words = (range + 31) / 32;
-  const char* e = std::getenv("DAS_BITS_SMALL");             // A/B: 0 = fill + set launches
-  if (words <= kBitsSmallWords && n <= kBitsSmallKeys && !(e && e[0] == '0')) {
-    ProfScope ps(c, "join_build", 4.0 * n + 4.0 * words);
-    hipLaunchKernelGGL(k_bits_small, dim3(1), dim3(1024), 0, c.s, key, n, kmin, (uint32_t)range, words, bits, zero_dup,
-                       dup);
-    DAS_HIP(hipGetLastError());
-    return;
-  }
-  const bool adjacent = zero_dup && dup == bits + words;        // (one fill covers the flag)
-  fill_dev(bits, 0, 4 * (words + (adjacent ? 1 : 0)), c.s);
-  if (zero_dup && !adjacent) fill_dev(dup, 0, 4, c.s);
-  ProfScope ps(c, "join_build", 4.0 * n + 4.0 * words);
-  if (sorted)
-    hipLaunchKernelGGL(k_bits_set_sorted, G(n), dim3(B), 0, c.s, key, n, kmin, (uint32_t)range, bits, dup);
-  else
-    hipLaunchKernelGGL(k_bits_set, G(n), dim3(B), 0, c.s, key, n, kmin, (uint32_t)range, bits, dup);
-  DAS_HIP(hipGetLastError());
-}
-
 struct BitsPred {
   const uint32_t* key;
   uint32_t kmin, range;
@@ -4883,7 +4837,13 @@ std::unique_ptr<Table> semi_join(Ctx& c, const Table& P, const Table& Q) {
   if (range > (1ull << 31)) return nullptr;
   const uint64_t words = (range + 31) / 32;
   DBuf<uint32_t> bits(words + 1, c.s);                     // + the duplicate flag
-  bits_build(c, (const uint32_t*)Q.col(0), Q.nrows, false, lo, range, bits.p, true, bits.p + words);
+  fill_dev(bits.p, 0, 4 * (words + 1), c.s);
+  {
+    ProfScope ps(c, "join_build", 4.0 * Q.nrows + 4.0 * words);
+    hipLaunchKernelGGL(k_bits_set, G(Q.nrows), dim3(B), 0, c.s, (const uint32_t*)Q.col(0), Q.nrows, lo, (uint32_t)range,
+                       bits.p, bits.p + words);
+    DAS_HIP(hipGetLastError());
+  }
   // the probe is the compaction's predicate: no flag array; duplicate keys
   // (counts matter: nullptr, the caller joins) are read back with the count
   return compact_pred(c, P, BitsPred{(const uint32_t*)P.col(pk), lo, (uint32_t)range, (const uint32_t*)bits.p},
@@ -4928,8 +4888,17 @@ bool key_bits(Ctx& c, const std::vector<const Table*>& Qs, int32_t var, uint64_t
   // every term's duplicate-key flag goes to acc[words]: one read-back at the end
   for (size_t i = 0; i < Qs.size(); ++i) {
     uint32_t* bits = i == 0 ? acc.p : one.p;
-    bits_build(c, (const uint32_t*)Qs[i]->col(0), Qs[i]->nrows, Qs[i]->sorted_col == 0, (uint32_t)lo, range, bits,
-               i == 0, acc.p + words);
+    fill_dev(bits, 0, 4 * (i == 0 ? words + 1 : words), c.s);
+    {
+      ProfScope ps(c, "join_build", 4.0 * Qs[i]->nrows + 4.0 * words);
+      if (Qs[i]->sorted_col == 0)
+        hipLaunchKernelGGL(k_bits_set_sorted, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, acc.p + words);
+      else
+        hipLaunchKernelGGL(k_bits_set, G(Qs[i]->nrows), dim3(B), 0, c.s, (const uint32_t*)Qs[i]->col(0),
+                           Qs[i]->nrows, (uint32_t)lo, (uint32_t)range, bits, acc.p + words);
+      DAS_HIP(hipGetLastError());
+    }
     if (i) {
       KScope ks("k_bits_and", 12.0 * words);
       hipLaunchKernelGGL(k_bits_and, G(words), dim3(B), 0, c.s, acc.p, (const uint32_t*)one.p, words);

@@ -767,21 +767,18 @@ def test_gpu_sparse_build_slots_cleared_between_joins(zlc, small, monkeypatch):
         _assert_same_rows(sorted(zip(*[c.tolist() for c in got])), want, (nk, nq, srt))
 
 
-@pytest.mark.parametrize("bits_small", ["1", "0"])
 @pytest.mark.parametrize("guard", ["1", "0"])
 @pytest.mark.parametrize("build", ["", "sparse", "dense"])
 @pytest.mark.parametrize("probe_rows", [5000, 40000])
-def test_gpu_key_join_duplicate_build_keys(probe_rows, build, guard, bits_small, monkeypatch):
+def test_gpu_key_join_duplicate_build_keys(probe_rows, build, guard, monkeypatch):
     """das_join of a two-column probe with a one-column build side: distinct
     build keys take the key-set filter (semi_join, the duplicate-key guard
     riding on the compaction's count read-back -- DAS_SMALL_GUARD=1, the
     one-launch compaction below kSmallScan = 16384 rows -- or read first, 0);
     repeated build keys void the filter and the direct join counts each
     repeat (dense or sparse build side).  Against a numpy join with
-    multiplicities.  bits_small: the key bitmap zeroed and set in one
-    workgroup (k_bits_small, default) or by a fill and a set launch."""
+    multiplicities."""
     monkeypatch.setenv("DAS_SMALL_GUARD", guard)
-    monkeypatch.setenv("DAS_BITS_SMALL", bits_small)
     if build:
         monkeypatch.setenv("DAS_DJ_BUILD", build)
     else:
