@@ -744,50 +744,6 @@ __global__ void __launch_bounds__(B) k_lc_clear(const uint32_t* key, uint64_t n,
   if (blockIdx.x == 0 && threadIdx.x == 0) lc[range] = make_uint2(0u, 0u);
 }
 
-// The unsorted sparse build in ONE workgroup (count, base, scatter as phases
-// between barriers) for build sides of at most kLcSmall rows: bio QUERY_2 /
-// QUERY_3's ~10^4-row sides were three launches of ~5 us each, with a host
-// launch gap between them, per join
-constexpr uint64_t kLcSmall = 1ull << 15;
-constexpr int kLcBlock = 1024;
-__global__ void __launch_bounds__(kLcBlock) k_lc_small(ColSet src, const uint32_t* __restrict__ key, uint64_t n,
-                                                       uint32_t kmin, uint32_t range, uint2* lc,
-                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ out,
-                                                       uint64_t cap) {
-  __shared__ uint32_t s_total;
-  if (threadIdx.x == 0) s_total = 0;
-  const uint64_t n_it = (n + kLcBlock - 1) / kLcBlock * kLcBlock;   // block-uniform trip count
-  for (uint64_t i = threadIdx.x; i < n_it; i += kLcBlock) {          // 1. counts, each row's rank in its key
-    const uint32_t d = i < n ? key[i] - kmin : range;
-    const bool act = d < range;
-    const uint32_t r = wave_agg_atomic_inc(reinterpret_cast<uint32_t*>(lc) + 1, act ? 2u * d : 0u, act);
-    if (act) rank[i] = r;
-  }
-  // (the counts live in L2 -- atomics -- and lc is read below with plain
-  // loads: an agent-scope acquire keeps the CU's L1 out of it)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n_it; i += kLcBlock) {          // 2. one row per key claims its run
-    const uint32_t d = i < n ? key[i] - kmin : range;
-    const uint32_t v = (d < range && rank[i] == 0u) ? __hip_atomic_load(&lc[d].y, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint32_t inc = wave_incl_sum_u32(v);
-    const uint32_t sum = __shfl(inc, 63, 64);
-    uint32_t base = 0;
-    if (__lane_id() == 63 && sum) base = atomicAdd(&s_total, sum);
-    base = __shfl(base, 63, 64);
-    if (v) __hip_atomic_store(&lc[d].x, base + inc - v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n; i += kLcBlock) {             // 3. rows to (base + rank)
-    const uint32_t d = key[i] - kmin;
-    if (d >= range) continue;
-    const uint64_t pos = (uint64_t)__hip_atomic_load(&lc[d].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + rank[i];
-    for (int c = 0; c < src.n; ++c) out[(uint64_t)c * cap + pos] = src.c[c][i];
-  }
-}
-
 __global__ void __launch_bounds__(B) k_lc_scatter(ColSet src, const uint32_t* key, const uint32_t* rank, uint64_t n,
                                                   uint32_t kmin, uint32_t range, const uint2* lc, uint32_t* out,
                                                   uint64_t cap) {
@@ -2778,19 +2734,9 @@ std::unique_ptr<Table> direct_join(Ctx& c, const Table& P, const Table& Q, int32
         lcp = lc.p;
       }
       DBuf<uint32_t> rk(srt ? 1 : Q.nrows, c.s);
-      // (DAS_LC_SMALL=0: the three launches below at every size, A/B)
-      const char* ls = std::getenv("DAS_LC_SMALL");
-      if (!srt && Q.nrows <= kLcSmall && !(ls && ls[0] == '0')) {
-        Qs = new_table_like(c, Q, Q.nrows);
-        Qs->nrows = Q.nrows;
-        hipLaunchKernelGGL(k_lc_small, dim3(1), dim3(kLcBlock), 0, c.s, cols_of(Q), qkey, Q.nrows, kmin,
-                           (uint32_t)range, lcp, rk.p, Qs->data, Qs->cap);
-        Qb = Qs.get();
-      } else {
-        hipLaunchKernelGGL(k_lc_count, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lcp, rk.p,
-                           srt ? 1 : 0);
-      }
-      if (!srt && !Qs) {
+      hipLaunchKernelGGL(k_lc_count, G(Q.nrows), dim3(B), 0, c.s, qkey, Q.nrows, kmin, (uint32_t)range, lcp, rk.p,
+                         srt ? 1 : 0);
+      if (!srt) {
         hipLaunchKernelGGL(k_lc_base, G(Q.nrows), dim3(B), 0, c.s, qkey, rk.p, Q.nrows, kmin, (uint32_t)range, lcp,
                            reinterpret_cast<uint32_t*>(lcp + range));
         Qs = new_table_like(c, Q, Q.nrows);

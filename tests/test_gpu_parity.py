@@ -724,26 +724,22 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     _assert_same_join(got, want)
 
 
-@pytest.mark.parametrize("small", ["1", "0"])
 @pytest.mark.parametrize("zlc", ["1", "0"])
-def test_gpu_sparse_build_slots_cleared_between_joins(zlc, small, monkeypatch):
+def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
     """The sparse direct-join build writes its (lo, cnt) slots into the
     context's descriptor array and clears them after the expansion (DAS_ZLC=1,
-    default; 0: a fresh array per join): six joins in a row on one context,
+    default; 0: a fresh array per join): five joins in a row on one context,
     over overlapping and growing key ranges (build keys in sorted order or
     not), each against a numpy join with multiplicities.  With the reused array, a
     join that unwinds between writing its slots and clearing them
-    (DAS_TEST_ZLC_THROW) must not leave them for the next join (advisor r4).
-    small=1: unsorted build sides up to 2^15 rows in one workgroup
-    (k_lc_small, default), 0: the three-launch build at every size."""
+    (DAS_TEST_ZLC_THROW) must not leave them for the next join (advisor r4)."""
     monkeypatch.setenv("DAS_DJ_BUILD", "sparse")
     monkeypatch.setenv("DAS_ZLC", zlc)
-    monkeypatch.setenv("DAS_LC_SMALL", small)
     from das_amd import _lib, synthetic
     db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
     rng = np.random.default_rng(11)
     for nk, nq, srt in ((20000, 300, False), (20000, 500, True), (90000, 800, False), (5000, 200, False),
-                        (90000, 1000, True), (900000, 30000, False), (900000, 40000, False)):
+                        (90000, 1000, True)):
         pk = rng.integers(0, nk, 30000)
         qk = rng.integers(0, nk, nq)
         if srt:
