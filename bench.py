@@ -47,9 +47,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # mode in round 6's same-process pairs (the other is timed beside it, fresh
 # anchors): bio one by one 1.57-1.64 ms vs batched 1.67-1.73 (the batch's
 # up-front lowering leaves the GPU idle, and its nested plans contend with the
-# cross product; profiles/r6_bio_step_split.json); hub batched 0.77-0.79 vs
-# 0.84 (H2's expansion beside H4's latency-bound walk)
-BATCH_DEFAULT = {"bio": 0, "flybase": 0, "hub": 1}
+# cross product; profiles/r6_bio_step_split.json); FlyBase batched 0.21-0.25 vs
+# 0.25-0.32 (chains on side streams launched in the other plans' waits); hub
+# batched 0.77-0.79 vs 0.84 (H2's expansion beside H4's latency-bound walk)
+BATCH_DEFAULT = {"bio": 0, "flybase": 1, "hub": 1}
 
 
 def parse():
