@@ -1010,6 +1010,60 @@ __global__ void __launch_bounds__(B) k_dj_count(const uint32_t* pkey, uint64_t n
   }
 }
 
+// k_dj_count + the count -> offsets scan in ONE launch for up to
+// kCountPubUnits units: every block writes its units' counts through to the
+// coherence point and arrives on a ticket; the last block scans the counts
+// into unit_off (unit_off[units] = total) and publishes (total, largest unit)
+// to the pinned read-back slot -- the scan launch and its launch gap are gone
+// (bio QUERY_2 / QUERY_3 run five such joins per step)
+constexpr uint64_t kCountPubUnits = 8192;
+__global__ void __launch_bounds__(B) k_dj_count_pub(const uint32_t* pkey, uint64_t np, uint32_t kmin, uint32_t range,
+                                                    const uint2* lc, uint64_t units, uint64_t* unit_tot,
+                                                    const uint32_t* warm0, const uint32_t* warm1, uint64_t* unit_off,
+                                                    unsigned long long* ctr, unsigned long long last, uint32_t* slot,
+                                                    uint32_t seq) {
+  __shared__ uint64_t s_sum[B / 64];
+  __shared__ uint64_t s_mx[B / 64];
+  __shared__ int s_last;
+  const uint64_t waves = (uint64_t)gridDim.x * (B / 64);
+  const int lane = __lane_id();
+  for (uint64_t u = blockIdx.x * (uint64_t)(B / 64) + (threadIdx.x >> 6); u < units; u += waves) {
+    const uint64_t r0 = u * kXRows;
+    uint32_t d[kXGroups];
+#pragma unroll
+    for (int g = 0; g < kXGroups; ++g) {
+      const uint64_t r = r0 + g * 64 + lane;
+      d[g] = r < np ? pkey[r] - kmin : 0xFFFFFFFFu;
+      if (warm0 && r < np) {
+        const uint32_t w0 = warm0[r];
+        asm volatile("" ::"v"(w0));
+      }
+      if (warm1 && r < np) {
+        const uint32_t w1 = warm1[r];
+        asm volatile("" ::"v"(w1));
+      }
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int g = 0; g < kXGroups; ++g)
+      if (d[g] < range) acc += lc[d[g]].y;
+    acc = wave_reduce_sum(acc);
+    if (lane == 0) __hip_atomic_store(&unit_tot[u], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // (write-through arrivals: no agent-scope release per block)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  uint64_t total, mx;
+  block_scan_loop<uint64_t>(SpanIn<uint64_t>{unit_tot}, units, unit_off, total, mx, s_sum, s_mx);
+  if (threadIdx.x == 0) unit_off[units] = total;
+  const uint32_t w[4] = {(uint32_t)total, (uint32_t)(total >> 32), (uint32_t)mx, (uint32_t)(mx >> 32)};
+  pub_store(slot, seq, w, 4);
+}
+
 // Output columns of a direct join, split by side so the kernel is
 // specialised on their counts (pointers stay in scalar registers).
 struct JoinCols {
@@ -2582,6 +2636,8 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
   const uint64_t units = (P.nrows + kXRows - 1) / kXRows;
   const unsigned grid = grid_for(units, B / 64, 65535u * 4u);
   DBuf<uint64_t> tot(units, c.s), toff(units + 1, c.s);
+  bool fused = false;
+  PubSlot ps_count{};
   {
     // a view's payload columns are read cold by the expansion: warm them here
     const uint32_t* w[2] = {nullptr, nullptr};
@@ -2590,13 +2646,32 @@ std::unique_ptr<Table> dj_expand(Ctx& c, const Table& P, const uint32_t* pkey, u
     if (P.view && !(wf && wf[0] == '0'))
       for (int i = 0; i < jc.np && nw < 2; ++i)
         if (jc.p[i] != pkey) w[nw++] = jc.p[i];
-    ProfScope ps(c, "k_dj_count", 4.0 * P.nrows);
-    hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
-                       lc, units, tot.p, w[0], w[1]);
+    // (DAS_COUNT_PUB=0: the count and the scan as two launches, A/B)
+    const char* cpe = std::getenv("DAS_COUNT_PUB");
+    fused = units <= kCountPubUnits && !(cpe && cpe[0] == '0');
+    ProfScope ps(c, fused ? "k_dj_count_pub" : "k_dj_count", 4.0 * P.nrows);
+    if (fused) {
+      ScanCtr& ct = scan_ctr(c.s);
+      ps_count = pub_reserve();
+      hipLaunchKernelGGL(k_dj_count_pub, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range, lc, units,
+                         tot.p, w[0], w[1], toff.p, ct.p, (unsigned long long)(ct.base + grid - 1), ps_count.p,
+                         ps_count.seq);
+      ct.base += grid;
+    } else {
+      hipLaunchKernelGGL(k_dj_count, dim3(grid), dim3(B), 0, c.s, pkey, P.nrows, kmin, (uint32_t)range,
+                         lc, units, tot.p, w[0], w[1]);
+    }
     DAS_HIP(hipGetLastError());
   }
   uint64_t tm[2];
-  tm[0] = scan_total<uint64_t>(SpanIn<uint64_t>{tot.p}, units, toff.p, c.s, &tm[1]);   // toff[units] = total
+  if (fused) {
+    uint32_t wv[4];
+    pub_wait(ps_count, c.s, wv, 4);
+    tm[0] = (uint64_t)wv[0] | ((uint64_t)wv[1] << 32);
+    tm[1] = (uint64_t)wv[2] | ((uint64_t)wv[3] << 32);
+  } else {
+    tm[0] = scan_total<uint64_t>(SpanIn<uint64_t>{tot.p}, units, toff.p, c.s, &tm[1]);   // toff[units] = total
+  }
   const uint64_t total = tm[0];
   // a unit owning far more outputs than a wave should expand alone (hub
   // keys) -> output-balanced expansion

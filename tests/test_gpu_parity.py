@@ -724,22 +724,27 @@ def test_gpu_direct_join_owner_lanes(shape, search, monkeypatch):
     _assert_same_join(got, want)
 
 
+@pytest.mark.parametrize("count_pub", ["1", "0"])
 @pytest.mark.parametrize("zlc", ["1", "0"])
-def test_gpu_sparse_build_slots_cleared_between_joins(zlc, monkeypatch):
+def test_gpu_sparse_build_slots_cleared_between_joins(zlc, count_pub, monkeypatch):
     """The sparse direct-join build writes its (lo, cnt) slots into the
     context's descriptor array and clears them after the expansion (DAS_ZLC=1,
     default; 0: a fresh array per join): five joins in a row on one context,
     over overlapping and growing key ranges (build keys in sorted order or
     not), each against a numpy join with multiplicities.  With the reused array, a
     join that unwinds between writing its slots and clearing them
-    (DAS_TEST_ZLC_THROW) must not leave them for the next join (advisor r4)."""
+    (DAS_TEST_ZLC_THROW) must not leave them for the next join (advisor r4).
+    count_pub: the expansion's per-unit counts and their offsets scan in one
+    launch (k_dj_count_pub, the last block scans and publishes; default) or
+    two (DAS_COUNT_PUB=0)."""
     monkeypatch.setenv("DAS_DJ_BUILD", "sparse")
     monkeypatch.setenv("DAS_ZLC", zlc)
+    monkeypatch.setenv("DAS_COUNT_PUB", count_pub)
     from das_amd import _lib, synthetic
     db = _hipdb(synthetic.powerlaw_kb(100, 500, link_types=2, seed=3))
     rng = np.random.default_rng(11)
     for nk, nq, srt in ((20000, 300, False), (20000, 500, True), (90000, 800, False), (5000, 200, False),
-                        (90000, 1000, True)):
+                        (90000, 1000, True), (90000, 20000, False)):
         pk = rng.integers(0, nk, 30000)
         qk = rng.integers(0, nk, nq)
         if srt:
