@@ -8,8 +8,8 @@
 #      (MI355X_MICROARCH.md "HBM": one TCC counter group per pass)
 #   4. tools/pmc_traffic.py -> per-kernel bytes per launch (gfx950 FETCH_SIZE
 #      correction), tools/roofline_check.py -> the roofline of the bench line
-#      printed UNDER rocprof (same process, --no-extras: the timed steps are
-#      the last launches) recomputed from the rocprof trace of those launches
+#      printed UNDER rocprof recomputed from the rocprof trace of the same
+#      process's timed launches (those between bench.py's k_prof_mark brackets)
 # WORKLOAD selects bench.py --workload (default bio); BENCH_ARGS adds flags;
 # TAG names the outputs gpurun_out/<TAG>_<workload>*, and <TAG>_<workload>_box.txt
 # records the card (serial, unique id, clocks).  Copy what is worth keeping

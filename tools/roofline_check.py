@@ -51,18 +51,27 @@ def main():
         trace = sys.argv[4]
     k_bench = bench.get("kernels", {}).get(name, {}).get("launches")
     if bench.get("unit") != "links/s" and rf.get("launches"):
-        # query workloads profiled with --no-extras: the timed steps' launches
-        # of the kernel are the process's last `launches` dispatches of it
+        # query workloads: the timed steps' launches of the kernel (picked by
+        # the k_prof_mark brackets, else the process's last `launches`)
         k_bench = rf["launches"]
     if k_bench:
         try:
             with open(trace) as f:
-                d = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-                           for r in csv.DictReader(f) if short(r["Kernel_Name"]) == name)
-            last = [x[1] for x in d[-k_bench:]]
+                allr = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
+                              for r in csv.DictReader(f))
+            d = [(s, e - s) for s, e, n in allr if n == name]
+            marks = [s for s, e, n in allr if n.endswith("k_prof_mark")]
+            if len(marks) >= 2 and bench.get("unit") != "links/s":
+                # bench.py brackets its timed steps with k_prof_mark launches:
+                # the kernel's dispatches between the first pair are the timed ones
+                last = [x[1] for x in d if marks[0] < x[0] < marks[1]]
+                how = "dispatches between the k_prof_mark brackets (the timed steps)"
+            else:
+                last = [x[1] for x in d[-k_bench:]]
+                how = "last dispatches (the timed region)"
             if last:
                 calls, tot = len(last), float(sum(last))
-                out["rocprof_launches"] = f"last {calls} dispatches (the timed region) of {len(d)} in {trace}"
+                out["rocprof_launches"] = f"{calls} {how} of {len(d)} in {trace}"
         except OSError:
             pass
     if calls:
