@@ -46,9 +46,9 @@ RANDOM = {"k_tile_count<BitsPred>", "k_ij_mid", "k_bits_probe", "k_ij_lc", "k_ij
 
 
 def fetch_factor(kernel):
-    # the filtered expansion's walk (flag pass <0>, one-walk <2>): one random
+    # the filtered expansion's walk (flag pass <0>, one-walk <2>, staged): one random
     # bitmap probe per output
-    return 1.0 if kernel in RANDOM or kernel.startswith(("k_dj_filt<0,", "k_dj_filt<2,")) else 2.0
+    return 1.0 if kernel in RANDOM or kernel.startswith(("k_dj_filt<0,", "k_dj_filt<2,", "k_dj_filt_staged<")) else 2.0
 
 
 def _last_counts():

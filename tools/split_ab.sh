@@ -1,6 +1,6 @@
 #!/bin/bash
 # The bio (or $W) step under rocprofv3 kernel traces, one run per setting of
-# $CFGS (space-separated; "base" = the default batch; "b0" = --batch 0; other
+# $CFGS (space-separated; "base" = the default batch; "b0" / "b1" = --batch 0 / 1; other
 # entries are comma-separated env settings), in the order given, then
 # tools/step_split.py over each trace -> gpurun_out/split_<W>_<SES>/<cfg>_<k>/split.json.
 # Every GPU step has its own time limit; a failure ends the script.
@@ -14,7 +14,7 @@ for cfg in $CFGS; do
   tag=$(echo "$cfg" | tr '=,' '__')_$k
   args="--workload $W --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-cpu-baseline --no-materialise --no-extras"
   envs=""
-  if [ "$cfg" = "b0" ]; then args="$args --batch 0"; elif [ "$cfg" != "base" ]; then envs=$(echo "$cfg" | tr ',' ' '); fi
+  if [ "$cfg" = "b0" ] || [ "$cfg" = "b1" ]; then args="$args --batch ${cfg#b}"; elif [ "$cfg" != "base" ]; then envs=$(echo "$cfg" | tr ',' ' '); fi
   D=gpurun_out/split_${W}_${SES:-s}/$tag
   mkdir -p $D
   env $envs timeout -k 10 ${PROF_TIMEOUT:-240} rocprofv3 --kernel-trace -f csv -d $D -o run -- python bench.py $args \
