@@ -271,24 +271,41 @@ __device__ __forceinline__ void block_sum_max(T& sum, uint64_t& mx, T* s_sum, ui
 }
 
 // One block scans rows [0, n) of `in` into out (block loop with carry),
-// accumulating the max; used for n <= one tile and for the tile sums.
+// accumulating the max; used for n <= one tile and for the tile sums.  Each
+// round takes kScanPre consecutive rows per thread, all loaded before the
+// round's scan: one memory latency per 4096 rows instead of one per 256 (the
+// last-block scans of the count / reduce kernels sit in a query's latency
+// chain).  In place (out == in's array) is fine: a thread writes only the rows
+// it loaded, after the round's loads.
+constexpr int kScanPre = 16;
 template <typename T, typename In>
 __device__ __forceinline__ void block_scan_loop(In in, uint64_t n, T* out, T& total, uint64_t& mx, T* s_wave,
                                                 uint64_t* s_mx) {
   const int wave = threadIdx.x >> 6;
   T carry = 0;
   uint64_t m = 0;
-  for (uint64_t base = 0; base < n; base += kScanBlock) {
-    const uint64_t i = base + threadIdx.x;
-    const T x = i < n ? (T)in(i) : (T)0;
-    m = (uint64_t)x > m ? (uint64_t)x : m;
-    const T inc = wave_inclusive_scan(x);
+  for (uint64_t base = 0; base < n; base += (uint64_t)kScanBlock * kScanPre) {
+    const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanPre;
+    T x[kScanPre];
+#pragma unroll
+    for (int k = 0; k < kScanPre; ++k) x[k] = i0 + k < n ? (T)in(i0 + k) : (T)0;
+    T sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPre; ++k) {
+      m = (uint64_t)x[k] > m ? (uint64_t)x[k] : m;
+      sum += x[k];
+    }
+    const T inc = wave_inclusive_scan(sum);
     if (__lane_id() == 63) s_wave[wave] = inc;
     __syncthreads();
-    T pre = carry;
+    T pre = carry + inc - sum;
     for (int w = 0; w < wave; ++w) pre += s_wave[w];
-    if (i < n) out[i] = pre + inc - x;
     for (int w = 0; w < kScanBlock / 64; ++w) carry += s_wave[w];
+#pragma unroll
+    for (int k = 0; k < kScanPre; ++k) {
+      if (i0 + k < n) out[i0 + k] = pre;
+      pre += x[k];
+    }
     __syncthreads();
   }
   T dummy = 0;
