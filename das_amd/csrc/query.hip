@@ -3937,40 +3937,47 @@ __device__ __forceinline__ void chain_body(const uint32_t* __restrict__ hdesc, u
       // (an arrival in two levels, per wg % 8 group then global, measured no
       // faster: FlyBase step 0.229 / 0.233 vs 0.229 / 0.219 ms one-level)
       const uint32_t prev = __hip_atomic_fetch_add(&d.gsc[kGscDone], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == G - 1) {
-        if (tstamp) {                                  // DAS_TRACE: the last workgroup's start and finish
-          tstamp[kChainStages + 2] = t_start;
-          tstamp[kChainStages + 3] = wall_clock64();
-        }
-        // every workgroup's counters and rows are in: the outcome
-        const uint32_t redo = __hip_atomic_load(&d.gsc[kGscRedo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t empty = 0;                            // a positive stage after the partition with no row anywhere
-        bool after = false;
-        for (uint32_t si = 0; si < d.nstage; ++si) {
-          if (after && d.st[si].op != CH_ANTI && d.st[si].op != CH_SCAN && d.st[si].done &&
-              __hip_atomic_load(&d.gsc[si], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            empty |= 1u << si;
-          after = after || d.st[si].part;
-        }
-        // a partitioned scan with no row on any workgroup: a failing term
-        bool failed = false;
-        for (uint32_t si = 0; si < d.nstage; ++si)
-          if (d.st[si].op == CH_SCAN && d.st[si].part && d.st[si].append == kChainNoStage && !d.st[si].empty_ok &&
-              __hip_atomic_load(&d.gsc[si], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            failed = true;
-        const uint32_t st = failed ? CHS_EMPTY_SCAN : redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
-        const uint32_t total = st == CHS_OK ? __hip_atomic_load(&d.gsc[kGscOut], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : s_cnt[s_acc];
-        // every workgroup is done with the counters: leave them zero for the
-        // next chain of a pooled counter block (no k_chain_prep launch)
-        for (uint32_t i = 0; i < kGscWords; ++i) __hip_atomic_store(&d.gsc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slot[0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&slot[1], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&slot[2], s_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&slot[3], empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_run = prev == G - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_run) return;
+    // the last workgroup: every counter read at once (one lane a word, one
+    // memory latency instead of a dependent load per stage), then left zero
+    // for the next chain of a pooled counter block (no k_chain_prep launch)
+    uint32_t* s_g = s_buf;
+    if (threadIdx.x < kGscWords) {
+      s_g[threadIdx.x] = __hip_atomic_load(&d.gsc[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&d.gsc[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (tstamp) {                                  // DAS_TRACE: the last workgroup's start and finish
+        tstamp[kChainStages + 2] = t_start;
+        tstamp[kChainStages + 3] = wall_clock64();
       }
+      // every workgroup's counters and rows are in: the outcome
+      const uint32_t redo = s_g[kGscRedo];
+      uint32_t empty = 0;                            // a positive stage after the partition with no row anywhere
+      bool after = false;
+      for (uint32_t si = 0; si < d.nstage; ++si) {
+        if (after && d.st[si].op != CH_ANTI && d.st[si].op != CH_SCAN && d.st[si].done && s_g[si] == 0)
+          empty |= 1u << si;
+        after = after || d.st[si].part;
+      }
+      // a partitioned scan with no row on any workgroup: a failing term
+      bool failed = false;
+      for (uint32_t si = 0; si < d.nstage; ++si)
+        if (d.st[si].op == CH_SCAN && d.st[si].part && d.st[si].append == kChainNoStage && !d.st[si].empty_ok &&
+            s_g[si] == 0)
+          failed = true;
+      const uint32_t st = failed ? CHS_EMPTY_SCAN : redo ? CHS_REDO : s_state;   // before the partition every workgroup agrees
+      const uint32_t total = st == CHS_OK ? s_g[kGscOut] : s_cnt[s_acc];
+      __hip_atomic_store(&slot[0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&slot[1], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&slot[2], s_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&slot[3], empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }
