@@ -622,14 +622,15 @@ static PyObject *shape_of(PyObject *e, PyObject *nodes, PyObject *unordered, int
 }
 
 /* plan_words(expr, shapes, no_overload, node_handles, handle_cache, node_dir,
- * unordered) -> a copy of the cached words of expr's query shape with its
+ * unordered[, get_node_handle]) -> a copy of the cached words of expr's query shape with its
  * nodes' atom ids patched in, or None: pattern_matcher._lower's shape-cache
  * hit, restated (the caller takes its Python path on None -- a shape not
- * cached yet, a node whose handle or id is not cached, a node absent). */
+ * cached yet, a node whose handle (without get_node_handle) or id is not
+ * cached, a node absent). */
 static PyObject *plan_words(PyObject *self, PyObject *args) {
-  PyObject *e, *shapes, *no_overload, *node_handles, *cache, *node_dir, *unordered;
-  if (!PyArg_ParseTuple(args, "OO!OO!O!OO", &e, &PyDict_Type, &shapes, &no_overload, &PyDict_Type, &node_handles,
-                        &PyDict_Type, &cache, &node_dir, &unordered))
+  PyObject *e, *shapes, *no_overload, *node_handles, *cache, *node_dir, *unordered, *hfun = NULL;
+  if (!PyArg_ParseTuple(args, "OO!OO!O!OO|O", &e, &PyDict_Type, &shapes, &no_overload, &PyDict_Type, &node_handles,
+                        &PyDict_Type, &cache, &node_dir, &unordered, &hfun))
     return NULL;
   if (!PyAnySet_Check(unordered)) { PyErr_SetString(PyExc_TypeError, "unordered: a set"); return NULL; }
   PyObject *nodes = PyList_New(0);
@@ -655,9 +656,14 @@ static PyObject *plan_words(PyObject *self, PyObject *args) {
         Py_XDECREF(t);
         Py_XDECREF(nm);
         h = tk ? PyDict_GetItemWithError(node_handles, tk) : NULL;
+        if (h) {
+          Py_INCREF(h);
+        } else if (tk && !PyErr_Occurred() && hfun && hfun != Py_None) {
+          /* a fresh anchor: its handle from the DB's own (memoising) get_node_handle */
+          h = PyObject_CallObject(hfun, tk);
+        }
         Py_XDECREF(tk);
         if (!h) { PyErr_Clear(); goto done; }
-        Py_INCREF(h);
         if (PyObject_SetAttr(n, s_handle, h) < 0) { Py_DECREF(h); PyErr_Clear(); goto done; }
       }
       PyObject *r = PyDict_GetItemWithError(cache, h);              /* (id, category, arity) */

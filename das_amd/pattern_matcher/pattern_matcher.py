@@ -533,6 +533,9 @@ def _node_ids(db, nodes):
     return out
 
 
+_UNORDERED = frozenset(UNORDERED_LINK_TYPES)
+
+
 def _lower(expr, db, no_overload):
     """The das_plan_node_t array (51 u32 words per node) of `expr`, or None.
 
@@ -550,7 +553,7 @@ def _lower(expr, db, no_overload):
         nh, hc = getattr(db, "_node_handles", None), getattr(db, "_handle_cache", None)
         if type(nh) is dict and type(hc) is dict:
             w = _assign.plan_words(expr, shapes, no_overload, nh, hc, getattr(db, "_node_dir", None),
-                                   frozenset(UNORDERED_LINK_TYPES))
+                                   _UNORDERED, db.get_node_handle)
             if w is not None:
                 return w
     nodes = []
