@@ -211,6 +211,26 @@ class HipDB(RelationalDB):
         self.load_arrays(_lib.parse_canonical(texts))
         self._stale = stale
 
+    def save_parsed(self, path):
+        """The loaded KB's parsed atom arrays, pattern_black_list and (with
+        stale_pattern_keys) the stale entries to one .npz, so a later
+        load_parsed rebuilds the device index without the parser -- what the
+        reference's kept key-value files do for its loader
+        (canonical_parser.py:28-29, 235, 317-319)."""
+        if self.arrays is None:
+            raise ValueError("nothing loaded")
+        stale = [[list(k), {h: list(t) for h, t in v.items()}] for k, v in (self._stale or {}).items()]
+        self.arrays.save(path, {"pattern_black_list": list(self.pattern_black_list), "stale": stale})
+
+    def load_parsed(self, path):
+        """Rebuilds the index from save_parsed's file (the black list it was
+        loaded with included); returns the AtomArrays."""
+        arrays, extra = _loader.AtomArrays.load(path)
+        self.pattern_black_list = list(extra.get("pattern_black_list", []))
+        self.load_arrays(arrays)
+        self._stale = {tuple(k): {h: tuple(t) for h, t in v.items()} for k, v in extra.get("stale", [])} or None
+        return arrays
+
     def stale_from_canonical(self, texts):
         """stale_pattern_keys with a non-empty pattern_black_list: the stale
         entries the reference's loader would write for this canonical text

@@ -49,6 +49,7 @@ class DistributedAtomSpace:
         self.pattern_black_list = []
         self._metta_sources = []
         self._canonical_sources = []
+        self._parsed = None          # arrays resumed by load_parsed_knowledge_base
 
     # -- loading -------------------------------------------------------------
     def _get_file_list(self, source):
@@ -73,7 +74,7 @@ class DistributedAtomSpace:
         # MeTTa through the Python MettaYacc restatement, one device index
         # the loaders honour pattern_black_list (distributed_atom_space.py:346, 409)
         self.db.pattern_black_list = list(self.pattern_black_list)
-        parts = []
+        parts = [self._parsed] if self._parsed is not None else []
         stale = None
         if self._canonical_sources:
             if not self._metta_sources and hasattr(self.db, "stale_from_canonical"):
@@ -81,6 +82,8 @@ class DistributedAtomSpace:
             parts.append(_lib.parse_canonical(self._canonical_sources))
         if self._metta_sources or not parts:
             parts.append(_loader.parse_metta(self._metta_sources).finish())
+        if self._parsed is not None and (self._canonical_sources or self._metta_sources):
+            stale = None        # stale entries are recorded for canonical-only loads
         self.db.load_arrays(_loader.concat_arrays(parts))
         if stale:
             self.db._stale = stale
@@ -99,6 +102,21 @@ class DistributedAtomSpace:
                 self._canonical_sources.append(fh.read())
         self._rebuild()
 
+    def save_parsed_knowledge_base(self, path):
+        """The loaded KB, parsed, to one .npz (HipDB.save_parsed): a later
+        load_parsed_knowledge_base skips the parser, as the reference's
+        loader does when it reuses its key-value files
+        (canonical_parser.py:28-29, 317-319)."""
+        self.db.save_parsed(path)
+
+    def load_parsed_knowledge_base(self, path):
+        """Replaces the KB with a saved one (its pattern_black_list
+        included); later loads and transactions add to it."""
+        self._metta_sources = []
+        self._canonical_sources = []
+        self._parsed = self.db.load_parsed(path)
+        self.pattern_black_list = list(self.db.pattern_black_list)
+
     def open_transaction(self) -> Transaction:
         return Transaction()
 
@@ -111,6 +129,7 @@ class DistributedAtomSpace:
     def clear_database(self):
         self._metta_sources = []
         self._canonical_sources = []
+        self._parsed = None
         self.db.clear()
 
     # -- API -----------------------------------------------------------------

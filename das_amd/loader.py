@@ -15,6 +15,7 @@ loaders:
                      CanonicalParser (das/canonical_parser.py:242-365): nodes
                      are the terminals declared by `(: "name" Type)` lines.
 """
+import json
 import re
 
 import numpy as np
@@ -73,6 +74,31 @@ class AtomArrays:
 
     def children(self, j):
         return [int(x) for x in self.expr_child[int(self.expr_off[j]):int(self.expr_off[j + 1])]]
+
+    # --- resume without the parser ------------------------------------------
+    _FIELDS = ("leaf_bytes", "leaf_off", "leaf_kind", "leaf_ctype", "leaf_type_id", "name_start", "expr_off",
+               "expr_child", "expr_kind", "expr_ctype_leaf", "level_off")
+
+    def save(self, path, extra=None):
+        """The parsed KB as one uncompressed .npz (plain arrays, no pickles):
+        the analogue of the reference loader's kept key-value files, which
+        let a later load skip the parser (canonical_parser.py:28-29, 235,
+        317-319).  `extra`: a JSON-serialisable dict stored beside them."""
+        meta = {"format": "das_amd.AtomArrays/1", "type_names": self.type_names, "extra": extra or {}}
+        fields = {k: getattr(self, k) for k in self._FIELDS}
+        fields["meta_json"] = np.frombuffer(json.dumps(meta).encode("utf-8"), dtype=np.uint8)
+        with open(path, "wb") as f:
+            np.savez(f, **fields)
+
+    @classmethod
+    def load(cls, path, mmap=False):
+        """(AtomArrays, extra) from save(); allow_pickle stays off."""
+        with np.load(path, allow_pickle=False, mmap_mode="r" if mmap else None) as z:
+            meta = json.loads(bytes(z["meta_json"]).decode("utf-8"))
+            if meta.get("format") != "das_amd.AtomArrays/1":
+                raise ValueError(f"{path}: not a saved das_amd KB")
+            a = cls(*[z[k] for k in cls._FIELDS], meta["type_names"])
+        return a, meta.get("extra", {})
 
 
 class AtomBuilder:

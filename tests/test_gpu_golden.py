@@ -189,6 +189,63 @@ def test_gpu_pattern_black_list_reference_mode(golden, plan, monkeypatch, tmp_pa
     assert failed_loads >= 2 and checked >= 70 and touched > 0 and probes >= 60, (failed_loads, checked, touched, probes)
 
 
+def test_gpu_resume_saved_kb(golden, tmp_path):
+    """save_parsed_knowledge_base / load_parsed_knowledge_base (the resume
+    without the parser, as the reference loader reuses its key-value files):
+    a KB reloaded from the saved file answers every reference-recorded query
+    of kb_bio_full.json and equals the first load's atom tables; a
+    stale_pattern_keys KB keeps its black list and its stale entries (every
+    query of a kb_blacklist.json canonical case the stale keys touch); a
+    transaction after the resume adds to the resumed KB."""
+    import os
+    from das_amd.distributed_atom_space import DistributedAtomSpace
+    from das_amd.database.hip_db import HipDB
+    d = golden("kb_bio_full.json")
+    f = tmp_path / "bio.metta"
+    f.write_text(MS.text_of("bio_full"))
+    das = DistributedAtomSpace(tuple_targets=True)
+    das.load_canonical_knowledge_base(str(f))
+    saved = tmp_path / "bio.npz"
+    das.save_parsed_knowledge_base(str(saved))
+    das2 = DistributedAtomSpace(tuple_targets=True)
+    das2.load_parsed_knowledge_base(str(saved))
+    assert list(das2.count_atoms()) == d["count_atoms"]
+    assert _atom_tables(das2.db) == _atom_tables(das.db)
+    bad = [q["query"] for q in d["queries"] if not q.get("no_overload") and not same(record(q["query"], das2.db), q)]
+    assert not bad, bad
+    n0, l0 = das2.count_atoms()
+    tr = das2.open_transaction()
+    for line in ("(: Concept Type)", "(: Inheritance Type)", '(: "resumed_a" Concept)', '(: "resumed_b" Concept)',
+                 '(Inheritance "resumed_a" "resumed_b")'):
+        tr.add(line)
+    das2.commit_transaction(tr)
+    assert tuple(das2.count_atoms()) == (n0 + 2, l0 + 1)
+    # stale_pattern_keys: the black list and the stale entries travel
+    b = golden("kb_blacklist.json")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
+    done = 0
+    for case in b["cases"]:
+        if case["loader"] != "canonical" or case.get("load_error") or not case["black_list"]:
+            continue
+        if case["source"] == "inline":
+            text = b["canonical_text"]
+        else:
+            with open(os.path.join(here, os.path.basename(case["source"]))) as fh:
+                text = fh.read()
+        db = HipDB(device=0, tuple_targets=True, stale_pattern_keys=True)
+        db.pattern_black_list = list(case["black_list"])
+        db.load_canonical(text)
+        p = tmp_path / f"bl{done}.npz"
+        db.save_parsed(str(p))
+        db2 = HipDB(device=0, tuple_targets=True, stale_pattern_keys=True)
+        db2.load_parsed(str(p))
+        assert db2.pattern_black_list == list(case["black_list"]) and db2._stale == db._stale
+        for q in case["queries"]:
+            assert same(record(q["query"], db2), q), (case["black_list"], q["query"])
+        done += 1
+    assert done >= 2
+
+
 def _build(spec):
     from tests.util import build
     return build(spec)

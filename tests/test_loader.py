@@ -61,3 +61,27 @@ def test_levels_are_grouped_by_arity():
         s, e = int(arr.level_off[g]), int(arr.level_off[g + 1])
         ks = {int(arr.expr_off[j + 1] - arr.expr_off[j]) for j in range(s, e)}
         assert len(ks) == 1
+
+
+def test_saved_kb_roundtrip(golden, tmp_path):
+    """AtomArrays.save / load (the resume-without-parser file): every array,
+    the type names and the extra metadata come back unchanged, through plain
+    np.load (allow_pickle off), and the reloaded arrays still hash to the
+    atoms the reference stored."""
+    import numpy as np
+    with open(os.path.join(DATA, "animals.metta")) as f:
+        arrays = loader.parse_metta(f.read()).finish()
+    p = tmp_path / "kb.npz"
+    arrays.save(p, {"pattern_black_list": ["Similarity"], "stale": [[["a", "b"], {"h": ["x", "y"]}]]})
+    back, extra = loader.AtomArrays.load(p)
+    for k in loader.AtomArrays._FIELDS:
+        a, b = getattr(arrays, k), getattr(back, k)
+        assert a.dtype == b.dtype and np.array_equal(a, b), k
+    assert back.type_names == arrays.type_names and back.type_id == arrays.type_id
+    assert extra == {"pattern_black_list": ["Similarity"], "stale": [[["a", "b"], {"h": ["x", "y"]}]]}
+    _tables_equal(O.KB.from_arrays(back), golden("kb_animals.json"))
+    bad = tmp_path / "bad.npz"
+    np.savez(bad, meta_json=np.frombuffer(b'{"format": "other"}', dtype=np.uint8))
+    import pytest
+    with pytest.raises(ValueError):
+        loader.AtomArrays.load(bad)
