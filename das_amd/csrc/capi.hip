@@ -254,7 +254,7 @@ int das_composite_digest(const uint32_t* digests, uint32_t k, uint32_t out[4]) {
 }
 
 int das_hash_strings_dev(das_ctx_t* ctx, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_out) {
-  return guarded(ctx, [&] { das::hash_strings(d_bytes, d_off, n, (Digest*)d_out, ctx->c.s); });
+  return guarded(ctx, [&] { das::hash_strings(d_bytes, d_off, n, dig_s((Digest*)d_out), ctx->c.s); });
 }
 
 int das_hash_fixed_dev(das_ctx_t* ctx, const uint32_t* d_elems, uint32_t k, uint64_t n, uint32_t* d_out) {

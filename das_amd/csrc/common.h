@@ -104,6 +104,16 @@ struct Digest {
     return ((uint64_t)__builtin_bswap32(w[2]) << 32) | __builtin_bswap32(w[3]);
   }
 };
+// A digest table with an element stride: 1 = a plain Digest[]; 2 = one half
+// of the build's interleaved {digest, composite digest} records, so a random
+// gather of both (a child's two digests in the hash pass, an atom's in
+// k_fill_atoms) touches one 64-byte line instead of two.
+struct DigS {
+  Digest* p;
+  uint32_t st;
+  __host__ __device__ Digest& operator[](uint64_t i) const { return p[i * st]; }
+};
+inline DigS dig_s(const Digest* p, uint32_t st = 1) { return DigS{const_cast<Digest*>(p), st}; }
 
 // Shard that owns a handle when links are hash-partitioned by handle across
 // `world` GPUs: the handle's first 8 hex characters as a

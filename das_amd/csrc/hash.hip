@@ -16,7 +16,7 @@ namespace das {
 
 __global__ void __launch_bounds__(256) k_hash_strings(const uint8_t* __restrict__ bytes,
                                                       const uint64_t* __restrict__ off, uint64_t n,
-                                                      Digest* __restrict__ out) {
+                                                      DigS out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t b = off[i];
@@ -92,7 +92,7 @@ __device__ __forceinline__ void md5_composite(const uint32_t (&d)[K][4], uint32_
 }
 
 // Generic K (> 9 elements): runtime byte loop, still one lane per message.
-__device__ void md5_composite_dyn(const Digest* tab, const uint32_t* child, uint32_t K, uint32_t st[4]) {
+__device__ void md5_composite_dyn(DigS tab, const uint32_t* child, uint32_t K, uint32_t st[4]) {
   const uint64_t L = 33ull * K - 1;
   const uint64_t NB = (L + 9 + 63) / 64;
   md5::init(st);
@@ -127,7 +127,7 @@ __device__ void md5_composite_dyn(const Digest* tab, const uint32_t* child, uint
 // composite types the same way (canonical_parser.py:276, base_yacc.py:92-98),
 // unless `ctype_leaf[j] >= 0` (typedef used as a symbol: md5(name)).
 template <int K>
-__global__ void __launch_bounds__(256) k_hash_group(Digest* __restrict__ table, Digest* __restrict__ ctab,
+__global__ void __launch_bounds__(256) k_hash_group(DigS table, DigS ctab,
                                                     const uint32_t* __restrict__ child,
                                                     const uint64_t* __restrict__ child_off,
                                                     const int32_t* __restrict__ ctype_leaf, uint64_t n_leaf,
@@ -135,12 +135,21 @@ __global__ void __launch_bounds__(256) k_hash_group(Digest* __restrict__ table, 
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t j = begin + t;
     const uint32_t* ch = child + child_off[j];
-    uint32_t d[K][4];
+    const int32_t cl = ctab.p && ctype_leaf ? ctype_leaf[j] : -1;
+    // both digests of every child loaded up front: with the interleaved
+    // records (DigS stride 2) they share a line, and the composite digests
+    // are in registers when the second MD5 starts
+    uint32_t d[K][4], cd[K][4];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
       const Digest x = table[ch[e]];
 #pragma unroll
       for (int q = 0; q < 4; ++q) d[e][q] = x.w[q];
+      if (ctab.p && cl < 0) {
+        const Digest y = ctab[ch[e]];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cd[e][q] = y.w[q];
+      }
     }
     uint32_t st[4];
     if (K == 1) {
@@ -150,17 +159,14 @@ __global__ void __launch_bounds__(256) k_hash_group(Digest* __restrict__ table, 
       md5_composite<K>(d, st);
     }
     table[n_leaf + j] = Digest{{st[0], st[1], st[2], st[3]}};
-    if (ctab) {
-      const int32_t cl = ctype_leaf ? ctype_leaf[j] : -1;
+    if (ctab.p) {
       if (cl >= 0) {
         ctab[n_leaf + j] = table[cl];
       } else {
 #pragma unroll
-        for (int e = 0; e < K; ++e) {
-          const Digest x = ctab[ch[e]];
+        for (int e = 0; e < K; ++e)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) d[e][q] = x.w[q];
-        }
+          for (int q = 0; q < 4; ++q) d[e][q] = cd[e][q];
         if (K == 1) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) st[q] = d[0][q];
@@ -173,7 +179,7 @@ __global__ void __launch_bounds__(256) k_hash_group(Digest* __restrict__ table, 
   }
 }
 
-__global__ void k_hash_group_dyn(Digest* table, Digest* ctab, const uint32_t* child, const uint64_t* child_off,
+__global__ void k_hash_group_dyn(DigS table, DigS ctab, const uint32_t* child, const uint64_t* child_off,
                                  const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n) {
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t j = begin + t;
@@ -182,7 +188,7 @@ __global__ void k_hash_group_dyn(Digest* table, Digest* ctab, const uint32_t* ch
     uint32_t st[4];
     md5_composite_dyn(table, ch, K, st);
     table[n_leaf + j] = Digest{{st[0], st[1], st[2], st[3]}};
-    if (ctab) {
+    if (ctab.p) {
       const int32_t cl = ctype_leaf ? ctype_leaf[j] : -1;
       if (cl >= 0) {
         ctab[n_leaf + j] = table[cl];
@@ -212,13 +218,13 @@ __global__ void __launch_bounds__(256) k_hash_fixed(const Digest* __restrict__ e
   }
 }
 
-void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, Digest* out, hipStream_t s) {
+void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, DigS out, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_hash_strings, dim3(grid_for(n, 256, 256 * 64)), dim3(256), 0, s, bytes, off, n, out);
   DAS_HIP(hipGetLastError());
 }
 
-void hash_group(Digest* table, Digest* ctab, const uint32_t* child, const uint64_t* child_off,
+void hash_group(DigS table, DigS ctab, const uint32_t* child, const uint64_t* child_off,
                 const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n, uint32_t K,
                 hipStream_t s) {
   if (!n) return;

@@ -257,7 +257,7 @@ DBuf<T> upload(const T* h, uint64_t n, hipStream_t s) {
   return d;
 }
 
-__global__ void k_leaf_ctype(const Digest* dig, const uint32_t* leaf_ctype, Digest* ct, uint64_t n) {
+__global__ void k_leaf_ctype(DigS dig, const uint32_t* leaf_ctype, DigS ct, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     ct[i] = dig[leaf_ctype[i]];
 }
@@ -265,7 +265,7 @@ __global__ void k_leaf_ctype(const Digest* dig, const uint32_t* leaf_ctype, Dige
 // flag/catl over unified indices: nodes, links, and anything a link targets.
 // world > 1: a link's category comes from its handle's owner (indexed here iff
 // handle_owner == rank), so every copy of one handle agrees on every shard.
-__global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, const Digest* dig, uint64_t n_leaf,
+__global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, DigS dig, uint64_t n_leaf,
                            uint64_t n_expr, uint32_t rank, uint32_t world, uint8_t* catl, uint32_t* flag) {
   const uint64_t n = n_leaf + n_expr;
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x) {
@@ -286,7 +286,7 @@ __global__ void k_init_cat(const uint8_t* leaf_kind, const uint8_t* expr_kind, c
   }
 }
 
-__global__ void k_expr_owner(const Digest* dig, uint64_t n_leaf, uint64_t n_expr, uint32_t world, uint8_t* owner) {
+__global__ void k_expr_owner(DigS dig, uint64_t n_leaf, uint64_t n_expr, uint32_t world, uint8_t* owner) {
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_expr; j += (uint64_t)gridDim.x * blockDim.x)
     owner[j] = (uint8_t)handle_owner(dig[n_leaf + j], world);
 }
@@ -349,7 +349,7 @@ __global__ void k_compact_index(const uint32_t* flag, const uint32_t* scan, uint
     if (flag[i]) out[scan[i]] = (uint32_t)i;
 }
 
-__global__ void k_digest_key(const Digest* dig, const uint32_t* idx, uint64_t n, uint64_t* key, bool hi) {
+__global__ void k_digest_key(DigS dig, const uint32_t* idx, uint64_t n, uint64_t* key, bool hi) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Digest d = dig[idx[i]];
     key[i] = hi ? d.hi() : d.lo();
@@ -358,7 +358,7 @@ __global__ void k_digest_key(const Digest* dig, const uint32_t* idx, uint64_t n,
 
 // Counts adjacent entries whose 64-bit high halves tie but whose digests differ
 // (then the hi-only sort is not a full 128-bit order and we redo it).
-__global__ void k_hi_ties(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+__global__ void k_hi_ties(DigS dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
   for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Digest a = dig[idx[i - 1]], b = dig[idx[i]];
     if (a.hi() == b.hi() && a.lo() != b.lo()) atomicAdd(bad, 1u);
@@ -382,14 +382,14 @@ __global__ void k_prefix_ties(const uint64_t* key, uint64_t n, int shift, uint32
 // of the high half's two lowest bits: equal digests stay adjacent (ordered by
 // category inside their run); entries whose keys agree above those bits but
 // whose digests differ are caught by k_prio_ties (then the exact sort runs).
-__global__ void k_digest_key_prio(const Digest* dig, const uint32_t* idx, const uint8_t* prio, uint64_t n,
+__global__ void k_digest_key_prio(DigS dig, const uint32_t* idx, const uint8_t* prio, uint64_t n,
                                   uint64_t* key) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = idx[i];
     key[i] = (dig[u].hi() & ~3ull) | (uint64_t)(prio[u] & 3u);
   }
 }
-__global__ void k_prio_ties(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+__global__ void k_prio_ties(const uint64_t* key, DigS dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
   uint32_t b = 0;
   for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     if ((key[i] >> 2) == (key[i - 1] >> 2)) {
@@ -404,13 +404,13 @@ __global__ void k_first_flags_prio(const uint64_t* key, uint64_t n, uint32_t* fi
     first[i] = i == 0 || (key[i] >> 2) != (key[i - 1] >> 2);
 }
 
-__global__ void k_hi_ties_key(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
+__global__ void k_hi_ties_key(const uint64_t* key, DigS dig, const uint32_t* idx, uint64_t n, uint32_t* bad) {
   uint32_t b = 0;
   for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     if (key[i] == key[i - 1]) b |= dig[idx[i - 1]].lo() != dig[idx[i]].lo();
   if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
 }
-__global__ void k_first_flags_key(const uint64_t* key, const Digest* dig, const uint32_t* idx, uint64_t n,
+__global__ void k_first_flags_key(const uint64_t* key, DigS dig, const uint32_t* idx, uint64_t n,
                                   uint32_t* first) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t f = 1;
@@ -419,7 +419,7 @@ __global__ void k_first_flags_key(const uint64_t* key, const Digest* dig, const 
   }
 }
 
-__global__ void k_first_flags(const Digest* dig, const uint32_t* idx, uint64_t n, uint32_t* first) {
+__global__ void k_first_flags(DigS dig, const uint32_t* idx, uint64_t n, uint32_t* first) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t f = 1;
     if (i > 0) {
@@ -619,8 +619,8 @@ __global__ void k_remap_local(uint64_t n, const uint32_t* by_digest, uint32_t* l
 // atom's named type is its key's high bits (k_temp_type looked it up once),
 // so the type's two dependent gathers (expr_child[expr_off[j]], then the type
 // table; leaf_ctype for nodes) are not repeated here
-__global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, const Digest* dig,
-                             const Digest* ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
+__global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, DigS dig,
+                             DigS ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
                              const uint32_t* leaf_type_id, const uint64_t* expr_off, const uint32_t* expr_child,
                              Digest* a_dig, uint8_t* a_cat, uint32_t* a_type, uint32_t* a_arity, Digest* a_ct,
                              uint32_t* a_name_leaf, const uint32_t* tkey, uint32_t tshift, uint32_t n_types) {
@@ -1197,7 +1197,7 @@ bool fix_prefix_runs(uint64_t* key, uint32_t* idx, uint64_t n, int shift, hipStr
 // `prio` (category per unified index) the fast path carries it in the key's
 // two lowest bits and returns true: then key >> 2 separates digests and
 // key & 3 is the entry's category.  false: exact order, key = high halves.
-bool sort_by_digest(const Digest* dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>& key, hipStream_t s,
+bool sort_by_digest(DigS dig, uint32_t* idx, uint64_t n, DBuf<uint64_t>& key, hipStream_t s,
                     const uint8_t* prio = nullptr) {
   key.alloc(n ? n : 1, s);
   if (n <= 1) {
@@ -1451,7 +1451,7 @@ bool keys_sorted(const uint32_t* key, uint64_t n, hipStream_t s) {
 // expression level by level (children first), and the composite types.
 void hash_all(Ctx& c, const das_atoms_t& a, bool dev_expr, const uint8_t* d_bytes, const uint64_t* d_loff,
               const uint32_t* d_lct, const uint32_t* p_child, const uint64_t* p_eoff, const int32_t* p_ectl,
-              Digest* dig, Digest* ct) {
+              DigS dig, DigS ct) {
   hipStream_t s = c.s;
   const uint64_t nl = a.n_leaf;
   {
@@ -1460,7 +1460,7 @@ void hash_all(Ctx& c, const das_atoms_t& a, bool dev_expr, const uint8_t* d_byte
   }
   if (nl) {
     KScope ks("k_leaf_ctype", 36.0 * nl);
-    hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, (const Digest*)dig, d_lct, ct, nl);
+    hipLaunchKernelGGL(k_leaf_ctype, G(nl), dim3(B), 0, s, dig, d_lct, ct, nl);
   }
   for (uint32_t g = 0; g < a.n_levels; ++g) {
     const uint64_t b = a.level_off[g], e = a.level_off[g + 1];
@@ -1501,11 +1501,12 @@ void hash_owners(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t world, u
     d_ectl = upload(a.expr_ctype_leaf, ne, s);
   }
   ProfScope whole(c, "hash_owners", 0.0);
-  DBuf<Digest> dig(nu, s), ct(nu, s);
+  DBuf<Digest> dc(2 * nu, s);                  // interleaved {digest, composite digest} per unified index
+  const DigS dig{dc.p, 2}, ct{dc.p + 1, 2};
   hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, dev_expr ? a.expr_child : d_child.p,
-           dev_expr ? a.expr_off : d_eoff.p, dev_expr ? a.expr_ctype_leaf : d_ectl.p, dig.p, ct.p);
+           dev_expr ? a.expr_off : d_eoff.p, dev_expr ? a.expr_ctype_leaf : d_ectl.p, dig, ct);
   KScope ks("k_expr_owner", 17.0 * ne);
-  hipLaunchKernelGGL(k_expr_owner, G(ne), dim3(B), 0, s, (const Digest*)dig.p, nl, ne, world, d_owner);
+  hipLaunchKernelGGL(k_expr_owner, G(ne), dim3(B), 0, s, dig, nl, ne, world, d_owner);
   DAS_HIP(hipGetLastError());
 }
 
@@ -1609,10 +1610,13 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   ProfScope whole(c, "build_device", 0.0);
 
   // 1. digests + composite types of every unified index
-  DBuf<Digest> dig(nu, s), ct(nu, s);
+  // interleaved {digest, composite digest} records: the hash pass's child
+  // gathers and k_fill_atoms' per-atom gathers read both from one line
+  DBuf<Digest> dc(2 * nu, s);
+  const DigS dig{dc.p, 2}, ct{dc.p + 1, 2};
   {
     ProfScope ph(c, "phase_hash", 0.0);
-    hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig.p, ct.p);
+    hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig, ct);
   }
   // (phase_* scopes: the build's steps as the bench's kernel table lists them)
   std::optional<ProfScope> phase(std::in_place, c, "phase_intern", 0.0);
@@ -1623,7 +1627,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   {
     KScope ks("k_init_cat", 1.0 * nu + 5.0 * nu);
     hipLaunchKernelGGL(k_init_cat, G(nu), dim3(B), 0, s, (const uint8_t*)d_lkind.p, (const uint8_t*)p_ekind,
-                       (const Digest*)dig.p, nl, ne, shard_rank, shard_world, catl.p, flag.p);
+                       dig, nl, ne, shard_rank, shard_world, catl.p, flag.p);
   }
   if (ne) {
     KScope ks("k_mark_targets", 9.0 * ne + 8.0 * n_child);
@@ -1637,7 +1641,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
 
   // 3. intern: sort by digest, one id per distinct digest
   DBuf<uint64_t> skey;
-  const bool prio_key = sort_by_digest(dig.p, list.p, nc, skey, s, catl.p);
+  const bool prio_key = sort_by_digest(dig, list.p, nc, skey, s, catl.p);
   DBuf<uint32_t> first(nc ? nc : 1, s), scan(nc ? nc : 1, s);
   uint64_t n_atoms = 0;
   if (nc) {
@@ -1646,7 +1650,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
       hipLaunchKernelGGL(k_first_flags_prio, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, nc, first.p);
     } else {
       KScope ks("k_first_flags_key", 12.0 * nc);   // sorted keys in, flags out; digests only where keys tie
-      hipLaunchKernelGGL(k_first_flags_key, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, (const Digest*)dig.p,
+      hipLaunchKernelGGL(k_first_flags_key, G(nc), dim3(B), 0, s, (const uint64_t*)skey.p, dig,
                          (const uint32_t*)list.p, nc, first.p);
     }
     exclusive_scan<uint32_t>(first.p, nc, scan.p, s);
@@ -1782,7 +1786,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     // cat, type, arity, ctype digest, name leaf out
     KScope ks("k_fill_atoms", 8.0 * n_atoms + 32.0 * n_atoms + 8.0 * n_atoms + 16.0 * n_atoms + 29.0 * n_atoms);
     hipLaunchKernelGGL(k_fill_atoms, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
-                       (const uint32_t*)catmax.p, (const Digest*)dig.p, (const Digest*)ct.p, nl,
+                       (const uint32_t*)catmax.p, dig, ct, nl,
                        (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)p_eoff,
                        (const uint32_t*)p_child, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf,
                        (const uint32_t*)tkey.p, tshift, (uint32_t)a.n_types);
@@ -1803,7 +1807,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
                          (const uint32_t*)p_child, (const uint32_t*)local2id.p, idx.tgt);
     DAS_HIP(hipGetLastError());
   }
-  dig.release(); ct.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
+  dc.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
   d_child.release(); d_bytes.release();
   phase.reset();
 
@@ -1878,7 +1882,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
       DBuf<uint32_t> bad(1, s);
       fill_dev(bad.p, 0, 4, s);
       hipLaunchKernelGGL(k_prefix_ties, G(nlk), dim3(B), 0, s, (const uint64_t*)key.p, nlk, 48, bad.p);
-      hipLaunchKernelGGL(k_hi_ties, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, bad.p);
+      hipLaunchKernelGGL(k_hi_ties, G(nlk), dim3(B), 0, s, dig_s(a_ct.p), (const uint32_t*)lids.p, nlk, bad.p);
       if (read_u32(bad.p, s)) {
         hipLaunchKernelGGL(k_ct_key, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, key.p, false);
         radix_sort_pairs<uint64_t>(key.p, lids.p, nlk, 0, 64, s);
@@ -1888,7 +1892,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
       DBuf<uint32_t> f(nlk, s), sc(nlk, s);
       {
         KScope ks("k_first_flags", 24.0 * nlk);
-        hipLaunchKernelGGL(k_first_flags, G(nlk), dim3(B), 0, s, (const Digest*)a_ct.p, (const uint32_t*)lids.p, nlk, f.p);
+        hipLaunchKernelGGL(k_first_flags, G(nlk), dim3(B), 0, s, dig_s(a_ct.p), (const uint32_t*)lids.p, nlk, f.p);
       }
       exclusive_scan<uint32_t>(f.p, nlk, sc.p, s);
       n_ctypes = (uint64_t)read_u32(sc.p + nlk - 1, s) + read_u32(f.p + nlk - 1, s);
