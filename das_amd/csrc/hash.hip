@@ -127,7 +127,7 @@ __device__ void md5_composite_dyn(DigS tab, const uint32_t* child, uint32_t K, u
 // composite types the same way (canonical_parser.py:276, base_yacc.py:92-98),
 // unless `ctype_leaf[j] >= 0` (typedef used as a symbol: md5(name)).
 template <int K>
-__global__ void __launch_bounds__(256) k_hash_group(DigS table, DigS ctab,
+__global__ void __launch_bounds__(256, K <= 6 ? 6 : 1) k_hash_group(DigS table, DigS ctab,
                                                     const uint32_t* __restrict__ child,
                                                     const uint64_t* __restrict__ child_off,
                                                     const int32_t* __restrict__ ctype_leaf, uint64_t n_leaf,

@@ -3,7 +3,7 @@
 set -e
 W=${W:-flybase}
 CFGS=${CFGS:-base}
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for cfg in $CFGS; do
     tag=$(echo "$cfg" | tr '=,' '__')
     if [ "$cfg" = "base" ]; then envs=""; else envs=$(echo "$cfg" | tr ',' ' '); fi
