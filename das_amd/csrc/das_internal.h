@@ -331,7 +331,7 @@ Ctx*& active_ctx();
 void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, DigS out, hipStream_t s);
 void hash_group(DigS table, DigS ctab, const uint32_t* child, const uint64_t* child_off,
                 const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n, uint32_t K,
-                hipStream_t s);
+                hipStream_t s, uint32_t* etype = nullptr);   // etype: each expression's type leaf (nullable)
 void hash_fixed(const Digest* elems, uint32_t k, uint64_t n, Digest* out, hipStream_t s);
 
 // index.hip

@@ -131,10 +131,11 @@ __global__ void __launch_bounds__(256, K <= 6 ? 6 : 1) k_hash_group(DigS table, 
                                                     const uint32_t* __restrict__ child,
                                                     const uint64_t* __restrict__ child_off,
                                                     const int32_t* __restrict__ ctype_leaf, uint64_t n_leaf,
-                                                    uint64_t begin, uint64_t n) {
+                                                    uint64_t begin, uint64_t n, uint32_t* __restrict__ etype) {
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t j = begin + t;
     const uint32_t* ch = child + child_off[j];
+    if (etype) etype[j] = ch[0];                       // the expression's first element: its type leaf
     const int32_t cl = ctab.p && ctype_leaf ? ctype_leaf[j] : -1;
     // both digests of every child loaded up front: with the interleaved
     // records (DigS stride 2) they share a line, and the composite digests
@@ -180,10 +181,12 @@ __global__ void __launch_bounds__(256, K <= 6 ? 6 : 1) k_hash_group(DigS table, 
 }
 
 __global__ void k_hash_group_dyn(DigS table, DigS ctab, const uint32_t* child, const uint64_t* child_off,
-                                 const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n) {
+                                 const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n,
+                                 uint32_t* etype) {
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t j = begin + t;
     const uint32_t* ch = child + child_off[j];
+    if (etype) etype[j] = ch[0];
     const uint32_t K = (uint32_t)(child_off[j + 1] - child_off[j]);
     uint32_t st[4];
     md5_composite_dyn(table, ch, K, st);
@@ -226,18 +229,19 @@ void hash_strings(const uint8_t* bytes, const uint64_t* off, uint64_t n, DigS ou
 
 void hash_group(DigS table, DigS ctab, const uint32_t* child, const uint64_t* child_off,
                 const int32_t* ctype_leaf, uint64_t n_leaf, uint64_t begin, uint64_t n, uint32_t K,
-                hipStream_t s) {
+                hipStream_t s, uint32_t* etype) {
   if (!n) return;
   const dim3 g(grid_for(n, 256, 256 * 64)), b(256);
 #define DAS_HG(KK)                                                                                  \
   case KK:                                                                                          \
     hipLaunchKernelGGL((k_hash_group<KK>), g, b, 0, s, table, ctab, child, child_off, ctype_leaf, \
-                       n_leaf, begin, n);                                                           \
+                       n_leaf, begin, n, etype);                                                    \
     break;
   switch (K) {
     DAS_HG(1) DAS_HG(2) DAS_HG(3) DAS_HG(4) DAS_HG(5) DAS_HG(6) DAS_HG(7) DAS_HG(8) DAS_HG(9)
     default:
-      hipLaunchKernelGGL(k_hash_group_dyn, g, b, 0, s, table, ctab, child, child_off, ctype_leaf, n_leaf, begin, n);
+      hipLaunchKernelGGL(k_hash_group_dyn, g, b, 0, s, table, ctab, child, child_off, ctype_leaf, n_leaf, begin, n,
+                         etype);
   }
 #undef DAS_HG
   DAS_HIP(hipGetLastError());

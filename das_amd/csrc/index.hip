@@ -524,15 +524,15 @@ __global__ void k_scatter_pairs(const uint32_t* __restrict__ key, const uint32_t
 
 // named-type cluster key of a temp (digest-order) id; kNone types last
 __global__ void k_temp_type(uint64_t n_atoms, const uint32_t* rep, const uint32_t* catmax, uint64_t n_leaf,
-                            const uint32_t* leaf_ctype, const uint32_t* leaf_type_id, const uint64_t* expr_off,
-                            const uint32_t* expr_child, uint32_t n_types, uint32_t degree_bits, uint32_t* key) {
+                            const uint32_t* leaf_ctype, const uint32_t* leaf_type_id, const uint32_t* etype,
+                            uint32_t n_types, uint32_t degree_bits, uint32_t* key) {
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n_atoms; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = rep[t];
     uint32_t ty = kNone;
     if (u < n_leaf) {
       ty = leaf_type_id[leaf_ctype[u]];
     } else if (catmax[t] == PRIO_LINK || catmax[t] == PRIO_REMOTE) {
-      ty = leaf_type_id[expr_child[expr_off[u - n_leaf]]];
+      ty = leaf_type_id[etype[u - n_leaf]];
     }
     const uint32_t k = ty == kNone ? n_types : ty;
     // degree_bits = 5: (type, 31) -- the bucket of an atom with no sampled
@@ -1451,7 +1451,7 @@ bool keys_sorted(const uint32_t* key, uint64_t n, hipStream_t s) {
 // expression level by level (children first), and the composite types.
 void hash_all(Ctx& c, const das_atoms_t& a, bool dev_expr, const uint8_t* d_bytes, const uint64_t* d_loff,
               const uint32_t* d_lct, const uint32_t* p_child, const uint64_t* p_eoff, const int32_t* p_ectl,
-              DigS dig, DigS ct) {
+              DigS dig, DigS ct, uint32_t* etype = nullptr) {
   hipStream_t s = c.s;
   const uint64_t nl = a.n_leaf;
   {
@@ -1476,7 +1476,7 @@ void hash_all(Ctx& c, const das_atoms_t& a, bool dev_expr, const uint8_t* d_byte
     // per expression: K child ids, K child digests + ctypes, offset, ctype leaf, two digests out
     ProfScope ps(c, K <= 9 ? "k_hash_group<" + std::to_string(K) + ">" : std::string("k_hash_group_dyn"),
                  (double)(e - b) * (4.0 * K + 32.0 * K + 8.0 + 4.0 + 32.0));
-    hash_group(dig, ct, p_child, p_eoff, p_ectl, nl, b, e - b, K, s);
+    hash_group(dig, ct, p_child, p_eoff, p_ectl, nl, b, e - b, K, s, etype);
   }
 }
 }  // namespace
@@ -1614,9 +1614,13 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   // gathers and k_fill_atoms' per-atom gathers read both from one line
   DBuf<Digest> dc(2 * nu, s);
   const DigS dig{dc.p, 2}, ct{dc.p + 1, 2};
+  // each expression's type leaf, written in order by the hash pass (which
+  // reads it anyway): k_temp_type's type lookup is one gather, not the two
+  // dependent ones through expr_off / expr_child
+  DBuf<uint32_t> etype(ne ? ne : 1, s);
   {
     ProfScope ph(c, "phase_hash", 0.0);
-    hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig, ct);
+    hash_all(c, a, dev_expr, d_bytes.p, d_loff.p, d_lct.p, p_child, p_eoff, p_ectl, dig, ct, etype.p);
   }
   // (phase_* scopes: the build's steps as the bench's kernel table lists them)
   std::optional<ProfScope> phase(std::in_place, c, "phase_intern", 0.0);
@@ -1739,7 +1743,8 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
         KScope ks("k_temp_type", 24.0 * n_atoms);    // rep, catmax, a type lookup, key out
         hipLaunchKernelGGL(k_temp_type, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
                            (const uint32_t*)catmax.p, nl, (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p,
-                           (const uint64_t*)p_eoff, (const uint32_t*)p_child, a.n_types, degree ? 5u : 0u, tkey.p);
+                           (const uint32_t*)etype.p, a.n_types, degree ? 5u : 0u, tkey.p);
+        etype.release();
       }
       if (degree) {
         KScope ks("k_run_bucket", 8.0 * n_slots);
