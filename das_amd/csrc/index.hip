@@ -623,7 +623,8 @@ __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32
                              DigS ct, uint64_t n_leaf, const uint32_t* leaf_ctype,
                              const uint32_t* leaf_type_id, const uint64_t* expr_off, const uint32_t* expr_child,
                              Digest* a_dig, uint8_t* a_cat, uint32_t* a_type, uint32_t* a_arity, Digest* a_ct,
-                             uint32_t* a_name_leaf, const uint32_t* tkey, uint32_t tshift, uint32_t n_types) {
+                             uint32_t* a_name_leaf, const uint32_t* tkey, uint32_t tshift, uint32_t n_types,
+                             uint64_t* a_eoff) {
   for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
        id += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = rep[id];
@@ -642,8 +643,10 @@ __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32
     } else {
       const uint64_t j = u - n_leaf;
       if (c == CAT_LINK || c == CAT_LINK_REMOTE) {
-        if (!tkey) ty = leaf_type_id[expr_child[expr_off[j]]];
-        ar = (uint32_t)(expr_off[j + 1] - expr_off[j] - 1);
+        const uint64_t b0 = expr_off[j];
+        if (!tkey) ty = leaf_type_id[expr_child[b0]];
+        ar = (uint32_t)(expr_off[j + 1] - b0 - 1);
+        if (a_eoff) a_eoff[id] = b0;                   // k_fill_targets reads it in id order
       }
     }
     a_type[id] = ty;
@@ -652,16 +655,19 @@ __global__ void k_fill_atoms(uint64_t n_atoms, const uint32_t* rep, const uint32
   }
 }
 
-__global__ void k_fill_targets(uint64_t n_atoms, const uint32_t* rep, const uint8_t* a_cat, const uint64_t* tgt_off,
-                               uint64_t n_leaf, const uint64_t* expr_off, const uint32_t* expr_child,
-                               const uint32_t* local2id, uint32_t* tgt) {
+// a_eoff[id]: the link's expression offset, written in id order by
+// k_fill_atoms (no random expr_off gather through rep here); its targets
+// are the expression's elements after the type, tgt_off[id + 1] - tgt_off[id]
+// of them
+__global__ void k_fill_targets(uint64_t n_atoms, const uint8_t* a_cat, const uint64_t* tgt_off,
+                               const uint64_t* a_eoff, const uint32_t* expr_child, const uint32_t* local2id,
+                               uint32_t* tgt) {
   for (uint64_t id = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; id < n_atoms;
        id += (uint64_t)gridDim.x * blockDim.x) {
     if (a_cat[id] != CAT_LINK && a_cat[id] != CAT_LINK_REMOTE) continue;
-    const uint64_t j = rep[id] - n_leaf;
-    const uint64_t b = expr_off[j] + 1, e = expr_off[j + 1];
-    uint64_t o = tgt_off[id];
-    for (uint64_t k = b; k < e; ++k) tgt[o++] = local2id[expr_child[k]];
+    const uint64_t b = a_eoff[id] + 1;
+    const uint64_t o = tgt_off[id], m = tgt_off[id + 1] - o;
+    for (uint64_t k = 0; k < m; ++k) tgt[o + k] = local2id[expr_child[b + k]];
   }
 }
 
@@ -1786,6 +1792,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
   idx.ctype = dalloc<uint32_t>(idx, n_atoms);
   idx.name_leaf = dalloc<uint32_t>(idx, n_atoms);
   DBuf<Digest> a_ct(n_atoms ? n_atoms : 1, s);
+  DBuf<uint64_t> a_eoff(n_atoms ? n_atoms : 1, s);
   if (n_atoms) {
     // rep + catmax in, digest + ctype digest gathered, type lookup; digest,
     // cat, type, arity, ctype digest, name leaf out
@@ -1794,7 +1801,7 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
                        (const uint32_t*)catmax.p, dig, ct, nl,
                        (const uint32_t*)d_lct.p, (const uint32_t*)d_ltype.p, (const uint64_t*)p_eoff,
                        (const uint32_t*)p_child, idx.digest, idx.cat, idx.type, idx.arity, a_ct.p, idx.name_leaf,
-                       (const uint32_t*)tkey.p, tshift, (uint32_t)a.n_types);
+                       (const uint32_t*)tkey.p, tshift, (uint32_t)a.n_types, a_eoff.p);
     DAS_HIP(hipGetLastError());
   }
   tkey.release();
@@ -1807,11 +1814,12 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
     idx.tgt = dalloc<uint32_t>(idx, total);
     KScope ks("k_fill_targets", 13.0 * n_atoms + 12.0 * total);     // per target: child in, id lookup, target out
     if (n_atoms)
-      hipLaunchKernelGGL(k_fill_targets, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint32_t*)rep.p,
-                         (const uint8_t*)idx.cat, (const uint64_t*)idx.tgt_off, nl, (const uint64_t*)p_eoff,
-                         (const uint32_t*)p_child, (const uint32_t*)local2id.p, idx.tgt);
+      hipLaunchKernelGGL(k_fill_targets, G(n_atoms), dim3(B), 0, s, n_atoms, (const uint8_t*)idx.cat,
+                         (const uint64_t*)idx.tgt_off, (const uint64_t*)a_eoff.p, (const uint32_t*)p_child,
+                         (const uint32_t*)local2id.p, idx.tgt);
     DAS_HIP(hipGetLastError());
   }
+  a_eoff.release();
   dc.release(); catl.release(); local2id.release(); catmax.release(); rep.release();
   d_child.release(); d_bytes.release();
   phase.reset();
