@@ -929,9 +929,25 @@ __global__ void k_owner_fill(const uint64_t* tgt_off, uint64_t n_atoms, uint32_t
 
 // sorted keys in [0, n_keys) -> off[k] = first index with key >= k, k in [0, n_keys]
 // (one binary search per k: runs of absent keys can be long)
-__global__ void k_bounds_u32(const uint32_t* key, uint64_t n, uint32_t n_keys, uint32_t* off) {
+// Two levels: the search first runs over every kBoundStep-th key (samp, a
+// few MB that stay in L2 / MALL across the threads' searches), then inside
+// one kBoundStep-key block -- ~8 cold loads per search instead of ~31.
+constexpr uint64_t kBoundStep = 256;
+__global__ void k_bound_sample(const uint32_t* key, uint64_t n, uint32_t* samp, uint64_t ns) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < ns; j += (uint64_t)gridDim.x * blockDim.x)
+    samp[j] = key[j * kBoundStep];
+}
+__global__ void k_bounds_u32(const uint32_t* key, uint64_t n, uint32_t n_keys, uint32_t* off, const uint32_t* samp,
+                             uint64_t ns) {
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t lo = 0, hi = n;
+    // first sample >= k: the answer lies in ((j - 1) * step, j * step]
+    uint64_t lo = 0, hi = ns;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (samp[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    hi = lo < ns ? lo * kBoundStep : n;
+    lo = lo ? (lo - 1) * kBoundStep + 1 : 0;
     while (lo < hi) {
       const uint64_t mid = (lo + hi) >> 1;
       if (key[mid] < k) lo = mid + 1; else hi = mid;
@@ -1841,9 +1857,12 @@ void build_index(Ctx& c, const das_atoms_t& a, uint32_t flags, uint32_t shard_ra
       }
       copy_dev(key.p, idx.tgt, 4 * total, s);
       radix_sort_pairs<uint32_t>(key.p, idx.in_link, total, 0, std::max(1, bits_for(n_atoms ? n_atoms - 1 : 0)), s);
+      const uint64_t ns = (total + kBoundStep - 1) / kBoundStep;
+      DBuf<uint32_t> samp(ns, s);
+      hipLaunchKernelGGL(k_bound_sample, G(ns), dim3(B), 0, s, (const uint32_t*)key.p, total, samp.p, ns);
       KScope ks("k_bounds_u32", 4.0 * total + 4.0 * (n_atoms + 1));
       hipLaunchKernelGGL(k_bounds_u32, G(n_atoms + 1), dim3(B), 0, s, (const uint32_t*)key.p, total,
-                         (uint32_t)n_atoms, idx.in_off);
+                         (uint32_t)n_atoms, idx.in_off, (const uint32_t*)samp.p, ns);
     } else {
       fill_dev(idx.in_off, 0, 4 * (n_atoms + 1), s);
     }
