@@ -339,7 +339,10 @@ __global__ void k_mark_targets(const uint8_t* expr_kind, const uint64_t* off, co
                                uint32_t* flag) {
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_expr; j += (uint64_t)gridDim.x * blockDim.x) {
     if (expr_kind[j] != 1 && expr_kind[j] != 3) continue;
-    for (uint64_t k = off[j] + 1; k < off[j + 1]; ++k) flag[child[k]] = 1;
+    // (read first: nodes and links are flagged by k_init_cat already, and a
+    // hub's flag line would otherwise take ~10^8 stores)
+    for (uint64_t k = off[j] + 1; k < off[j + 1]; ++k)
+      if (!flag[child[k]]) flag[child[k]] = 1;
   }
 }
 
