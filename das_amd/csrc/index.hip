@@ -1040,6 +1040,18 @@ void scatter_partitioned(uint32_t* keys, uint32_t* vals, uint64_t n, uint64_t ke
   if (!n) return;
   DAS_CHECK(n < (1ull << 32), DAS_E_UNSUPPORTED, "scatter_partitioned: more than 2^32 pairs");
   const int bits = std::max(1, bits_for(key_range ? key_range - 1 : 0));
+  // DAS_L2I_BITS=16 (A/B): two LSD passes on the keys' top 16 bits, so the
+  // scatter's windows are key_range / 2^16 slots (L2-sized) instead of / 2^8:
+  // k_scatter_pairs 29 -> 15 ms at 10^9 links, but the second pass costs as
+  // much (build 650-658 vs 649-653 ms, one box), so one pass stays
+  static const int pbits = std::getenv("DAS_L2I_BITS") && std::atoi(std::getenv("DAS_L2I_BITS")) == 16 ? 16 : 8;
+  if (pbits == 16 && bits > 16) {
+    radix_sort_pairs<uint32_t>(keys, vals, n, bits - 16, bits, s);
+    KScope ks("k_scatter_pairs", 12.0 * n);
+    hipLaunchKernelGGL(k_scatter_pairs, G(n), dim3(B), 0, s, (const uint32_t*)keys, (const uint32_t*)vals, n, dst);
+    DAS_HIP(hipGetLastError());
+    return;
+  }
   const int shift = std::max(0, bits - 8);
   const uint32_t tiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
   DBuf<uint32_t> hist((uint64_t)tiles * 256, s), offs((uint64_t)tiles * 256, s), k2(n, s), v2(n, s);
