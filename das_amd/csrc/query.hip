@@ -1568,9 +1568,17 @@ __device__ __forceinline__ void dj_filt_body(const uint32_t* __restrict__ pkey, 
           const int col = k < ncp ? jc.po[k] : jc.bo[k - ncp];
           uint32_t* dc = out + (uint64_t)col * cap + base;
           if ((uint32_t)lane < head) dc[lane] = sc[lane];
-          for (uint32_t q = (uint32_t)lane; q < nq; q += 64u) {
-            const uint32_t j = head + 4u * q;
-            store16<true>(dc + j, u32x4{sc[j], sc[j + 1], sc[j + 2], sc[j + 3]});
+          if (head == 0) {
+            // chunk slots (CH-aligned, the default): the LDS quads are 16-byte
+            // aligned too -- one conflict-free ds_read_b128 per lane instead
+            // of four dword reads 16 bytes apart (4-way bank conflicts)
+            for (uint32_t q = (uint32_t)lane; q < nq; q += 64u)
+              store16<true>(dc + 4u * q, *reinterpret_cast<const u32x4*>(sc + 4u * q));
+          } else {
+            for (uint32_t q = (uint32_t)lane; q < nq; q += 64u) {
+              const uint32_t j = head + 4u * q;
+              store16<true>(dc + j, u32x4{sc[j], sc[j + 1], sc[j + 2], sc[j + 3]});
+            }
           }
           if (t0 + (uint32_t)lane < run) dc[t0 + lane] = sc[t0 + lane];
         }
@@ -1610,7 +1618,7 @@ __global__ void __launch_bounds__(B) k_dj_filt_staged(const uint32_t* __restrict
                                                       uint32_t* __restrict__ ccnt, unsigned long long* __restrict__ kept,
                                                       const uint32_t* __restrict__ cunit) {
   __shared__ uint32_t s_row[B / 64][64];
-  __shared__ uint32_t s_stage[B / 64][(NPC + NBC) * CH];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[B / 64][(NPC + NBC) * CH];
   dj_filt_body<3, NPC, NBC, CH, kXUnroll>(pkey, np, kmin, range, lc, units, unit_off, total, fk, nullptr, ccnt,
                                           nullptr, jc, out, cap, wlo, whi, s_row[threadIdx.x >> 6],
                                           s_stage[threadIdx.x >> 6], kept, cunit);
