@@ -4137,13 +4137,16 @@ int fused_and(Ctx& c, const std::vector<const das_plan_node_t*>& terms,
               std::unique_ptr<Table>& out, uint32_t* consumed) {
   const int form = fused_and_form(c, terms, anti, no_overload);
   if (form < 0) return 0;
-  // DAS_CHAIN_PREP1=0: a grid chain's counters from this read-back level's
-  // pooled block (zeroed; the grid leaves it zero), no k_chain_prep launch,
-  // every workgroup reading the descriptor from the pinned stage -- FlyBase
-  // through matched() 0.284-0.301 vs 0.283-0.303 ms per step with the prep
-  // launch (round 6, one box): no gain, off by default
+  // One at a time (matched()), a grid chain takes its counters from this
+  // read-back level's pooled block (zeroed; the grid's last workgroup leaves
+  // it zero) and every workgroup reads the descriptor from the pinned stage:
+  // no k_chain_prep launch -- FlyBase F5 / F6 / F7 46.7 / 39.4 / 56.8 vs
+  // 50.2 / 43.7 / 61.4 us per query, the matched() step 0.236-0.251 vs
+  // 0.257-0.280 ms (round 6, one box, 9 of 10 alternating pairs).
+  // DAS_CHAIN_PREP1=1: the prep launch (fresh counters, the descriptor
+  // copied to device memory once).
   const char* cp = std::getenv("DAS_CHAIN_PREP1");
-  uint32_t* gsc = cp && cp[0] == '0' ? c.gsc_block(kPubPool + (uint32_t)pub_level()) : nullptr;
+  uint32_t* gsc = cp && cp[0] == '1' ? nullptr : c.gsc_block(kPubPool + (uint32_t)pub_level());
   for (int attempt = form == 1 ? 0 : 1; attempt < 2; ++attempt) {
     ChainRun R;
     const int r = chain_compile(c, terms, anti, attempt == 0, R, gsc);
